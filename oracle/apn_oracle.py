@@ -1,0 +1,579 @@
+"""TEST INFRASTRUCTURE ONLY -- CPU restatement of the articulated-point render/deform path.
+
+Each function cites the reference file:line it restates (paths relative to the reference
+repository root). Floating-point conventions are fixed so that the HIP kernels can be
+checked bit-exactly where the path produces indices:
+
+* float32 everywhere the reference kernel uses ``float``; no fused multiply-add (numpy and
+  torch-CPU elementwise ops round every operation; the HIP kernels that produce indices are
+  compiled with ``-ffp-contract=off``);
+* squared distances are ``(dx*dx + dy*dy) + dz*dz`` in float32 -- the reference recomputes
+  ``to_nn = (rel_p**2).sum(-1)`` with exactly this association (temporalpoints.py:446-447);
+* the double-precision promotions of the CUDA source are reproduced
+  (render_utils_kernel.cu:47 and 450-451);
+* kNN ties are broken by point index (pykeops leaves tie order unspecified).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use this module.
+"""
+from __future__ import annotations
+
+import colorsys
+import math
+
+import numpy as np
+import torch
+
+F32 = np.float32
+
+
+# ----------------------------------------------------------------------------------------
+# Positional encoding -- tineuvox.py:872-878
+# ----------------------------------------------------------------------------------------
+
+def poc_fre(x: torch.Tensor, freqs: torch.Tensor) -> torch.Tensor:
+    """[x, sin(x (x) f), cos(x (x) f)], dim-major flatten (x0f0..x0f{F-1}, x1f0, ...)."""
+    emb = (x.unsqueeze(-1) * freqs).flatten(-2)
+    return torch.cat([x, emb.sin(), emb.cos()], -1)
+
+
+# ----------------------------------------------------------------------------------------
+# render_utils_cuda restatement -- lib/cuda/render_utils_kernel.cu
+# ----------------------------------------------------------------------------------------
+
+def infer_t_minmax(rays_o, rays_d, xyz_min, xyz_max, near, far):
+    """render_utils_kernel.cu:11-35. Zero direction components become (float)1e-6."""
+    o = np.asarray(rays_o, F32); d = np.asarray(rays_d, F32)
+    lo = np.asarray(xyz_min, F32); hi = np.asarray(xyz_max, F32)
+    v = np.where(d == 0, F32(1e-6), d).astype(F32)
+    a = ((hi[None, :] - o) / v).astype(F32)
+    b = ((lo[None, :] - o) / v).astype(F32)
+    mn = np.minimum(a, b); mx = np.maximum(a, b)
+    near = F32(near); far = F32(far)
+    t_min = np.maximum(np.minimum(np.maximum(np.maximum(mn[:, 0], mn[:, 1]), mn[:, 2]), far), near)
+    t_max = np.maximum(np.minimum(np.minimum(np.minimum(mx[:, 0], mx[:, 1]), mx[:, 2]), far), near)
+    return t_min.astype(F32), t_max.astype(F32)
+
+
+def infer_n_samples(t_min, t_max, stepdist):
+    """render_utils_kernel.cu:37-49: max(ceil((t_max-t_min)/stepdist), 1.) -> int64."""
+    q = ((t_max - t_min).astype(F32) / F32(stepdist)).astype(F32)
+    return np.maximum(np.ceil(q).astype(np.float64), 1.0).astype(np.int64)
+
+
+def infer_ray_start_dir(rays_o, rays_d, t_min):
+    """render_utils_kernel.cu:51-73: start = o + d*t_min; dir = d / |d|."""
+    o = np.asarray(rays_o, F32); d = np.asarray(rays_d, F32)
+    rnorm = np.sqrt(((d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2]).astype(F32)).astype(F32)
+    start = (o + (d * t_min[:, None]).astype(F32)).astype(F32)
+    direc = (d / rnorm[:, None]).astype(F32)
+    return start, direc
+
+
+def sample_pts_on_rays(rays_o, rays_d, xyz_min, xyz_max, near, far, stepdist):
+    """render_utils_kernel.cu:190-236 (host) + 138-188 (kernels).
+
+    Returns [rays_pts (M,3) f32, mask_outbbox (M,) bool, ray_id (M,) i64, step_id (M,) i64,
+    N_steps (R,) i64, t_min (R,) f32, t_max (R,) f32], M = sum(N_steps).
+    """
+    t_min, t_max = infer_t_minmax(rays_o, rays_d, xyz_min, xyz_max, near, far)
+    n_steps = infer_n_samples(t_min, t_max, stepdist)
+    R = len(n_steps)
+    ray_id = np.repeat(np.arange(R, dtype=np.int64), n_steps)
+    starts = np.concatenate([[0], np.cumsum(n_steps)[:-1]]).astype(np.int64)
+    step_id = np.arange(len(ray_id), dtype=np.int64) - starts[ray_id]
+    start, direc = infer_ray_start_dir(rays_o, rays_d, t_min)
+    dist = (F32(stepdist) * step_id.astype(F32)).astype(F32)
+    pts = (start[ray_id] + (direc[ray_id] * dist[:, None]).astype(F32)).astype(F32)
+    lo = np.asarray(xyz_min, F32); hi = np.asarray(xyz_max, F32)
+    mask_out = np.any(lo[None, :] > pts, axis=1) | np.any(hi[None, :] < pts, axis=1)
+    return [pts, mask_out, ray_id, step_id, n_steps, t_min, t_max]
+
+
+def raw2alpha(density, shift, interval):
+    """render_utils_kernel.cu:357-393: e = exp(d+shift); alpha = 1 - (1+e)^(-interval)."""
+    d = np.asarray(density, F32)
+    with np.errstate(over="ignore"):
+        e = np.exp((d + F32(shift)).astype(F32)).astype(F32)
+        alpha = (F32(1) - np.power((F32(1) + e).astype(F32), F32(-F32(interval)))).astype(F32)
+    return e, alpha
+
+
+def alpha2weight(alpha, ray_id, n_rays):
+    """render_utils_kernel.cu:430-505.
+
+    Per ray (segments of the sorted ``ray_id``): T[i] = T_cum; w[i] = T_cum*alpha[i] (float);
+    T_cum = (float)((double)T_cum * (1. - (double)alpha[i])); break after the sample whose
+    update drops T_cum below 1e-3 (double compare). alphainv_last = T_cum (1 for empty rays).
+    Vectorised over rays, sequential over the step within a ray.
+    Returns [weight, T, alphainv_last, i_start, i_end].
+    """
+    a = np.asarray(alpha, F32); rid = np.asarray(ray_id, np.int64)
+    n = len(a)
+    weight = np.zeros(n, F32); T = np.ones(n, F32)
+    last = np.ones(n_rays, F32)
+    i_start = np.zeros(n_rays, np.int64); i_end = np.zeros(n_rays, np.int64)
+    if n == 0:
+        return [weight, T, last, i_start, i_end]
+    chg = np.nonzero(rid[1:] != rid[:-1])[0] + 1
+    i_start[rid[chg]] = chg
+    i_end[rid[chg - 1]] = chg
+    i_end[rid[n - 1]] = n
+    rays = np.unique(rid)
+    s = i_start[rays].copy(); e = i_end[rays].copy()
+    Tc = np.ones(len(rays), F32)
+    active = s < e
+    pos = s.copy()
+    while active.any():
+        idx = pos[active]
+        al = a[idx]
+        tc = Tc[active]
+        T[idx] = tc
+        weight[idx] = (tc * al).astype(F32)
+        tc_new = (tc.astype(np.float64) * (1.0 - al.astype(np.float64))).astype(F32)
+        Tc[active] = tc_new
+        pos[active] = idx + 1
+        stop = tc_new.astype(np.float64) < 1e-3
+        act_idx = np.nonzero(active)[0]
+        active[act_idx[stop]] = False
+        active &= pos < e
+    i_end[rays] = pos
+    last[rays] = Tc
+    return [weight, T, last, i_start, i_end]
+
+
+def segment_sum(src, index, n):
+    """torch_scatter.segment_coo(reduce='sum') over sorted ``index``: sequential in-order
+    float32 accumulation into a zero output (temporalpoints.py:653-677)."""
+    src = np.asarray(src, F32); index = np.asarray(index, np.int64)
+    out = np.zeros((n,) + src.shape[1:], F32)
+    np.add.at(out, index, src)
+    return out
+
+
+# ----------------------------------------------------------------------------------------
+# kNN -- pykeops LazyTensor.Kmin_argKmin semantics (temporalpoints.py:433-437, 106-111)
+# ----------------------------------------------------------------------------------------
+
+def sqdist(q: np.ndarray, p: np.ndarray) -> np.ndarray:
+    """Float32 squared distance (dx*dx + dy*dy) + dz*dz, broadcasting q[...,3] vs p[...,3]."""
+    dx = (q[..., 0] - p[..., 0]).astype(F32)
+    dy = (q[..., 1] - p[..., 1]).astype(F32)
+    dz = (q[..., 2] - p[..., 2]).astype(F32)
+    return ((dx * dx + dy * dy).astype(F32) + dz * dz).astype(F32)
+
+
+def _finalize_topk(q, pts, cand, K):
+    """Exact (d2, idx) lexicographic top-K among candidate indices cand (Q, C)."""
+    d2 = sqdist(q[:, None, :], pts[cand])
+    order = np.lexsort((cand, d2), axis=1)[:, :K]
+    idx = np.take_along_axis(cand, order, 1)
+    return np.take_along_axis(d2, order, 1), idx
+
+
+def knn_kmin(query, points, K, chunk=2048, use_tree=None):
+    """K smallest float32 squared distances (ascending, ties by index) and their indices.
+
+    Brute force for small problems; a scipy cKDTree candidate search (K+6 candidates in
+    float64, re-ranked in float32) for large ones.
+    """
+    q = np.ascontiguousarray(query, F32); p = np.ascontiguousarray(points, F32)
+    Q, N = len(q), len(p)
+    Kc = min(N, K + 6)
+    if use_tree is None:
+        use_tree = Q * N > 4e8
+    d_out = np.empty((Q, K), F32); i_out = np.empty((Q, K), np.int64)
+    if Q == 0:
+        return d_out, i_out
+    if use_tree:
+        from scipy.spatial import cKDTree
+        tree = cKDTree(p.astype(np.float64))
+        for s in range(0, Q, 1 << 18):
+            qq = q[s:s + (1 << 18)]
+            _, cand = tree.query(qq.astype(np.float64), k=Kc, workers=-1)
+            cand = np.asarray(cand, np.int64).reshape(len(qq), Kc)
+            d_out[s:s + len(qq)], i_out[s:s + len(qq)] = _finalize_topk(qq, p, cand, K)
+        return d_out, i_out
+    pt = torch.from_numpy(p)
+    for s in range(0, Q, chunk):
+        qq = q[s:s + chunk]
+        qt = torch.from_numpy(qq)
+        dx = qt[:, None, 0] - pt[None, :, 0]
+        dy = qt[:, None, 1] - pt[None, :, 1]
+        dz = qt[:, None, 2] - pt[None, :, 2]
+        d2 = (dx * dx + dy * dy) + dz * dz
+        cand = torch.topk(d2, Kc, dim=1, largest=False).indices.numpy().astype(np.int64)
+        d_out[s:s + len(qq)], i_out[s:s + len(qq)] = _finalize_topk(qq, p, cand, K)
+    return d_out, i_out
+
+
+def mean_min_distance(canonical_pcd, K=8, eps=1e-6):
+    """temporalpoints.py:104-111: argKmin over the cloud itself (self-inclusive);
+    nn_distance = sqrt(sum(delta^2) + eps); mean of column 1."""
+    p = np.asarray(canonical_pcd, F32)
+    _, idx = knn_kmin(p, p, K)
+    pt = torch.from_numpy(p)
+    nn_d = torch.sqrt(((pt[:, None, :] - pt[torch.from_numpy(idx), :]) ** 2).sum(-1) + torch.tensor(eps))
+    return nn_d[:, 1].mean()
+
+
+# ----------------------------------------------------------------------------------------
+# seaborn.color_palette("hls", n) restatement (temporalpoints.py:692) -- parity unpinned
+# ----------------------------------------------------------------------------------------
+
+def hls_palette(n, h=0.01, l=0.6, s=0.65):
+    hues = np.linspace(0, 1, n + 1)[:-1]
+    hues += h
+    hues %= 1
+    hues -= hues.astype(int)
+    return [colorsys.hls_to_rgb(hh, l, s) for hh in hues]
+
+
+# ----------------------------------------------------------------------------------------
+# PointWarper -- lib/pointwarper.py
+# ----------------------------------------------------------------------------------------
+
+def rodrigues(rvec: torch.Tensor):
+    """pointwarper.py:118-143 (3-vector and 4-vector branches)."""
+    if rvec.shape[-1] == 3:
+        theta = torch.sqrt(1e-5 + torch.sum(rvec ** 2, dim=1))
+        r = rvec / theta[:, None]
+    elif rvec.shape[-1] == 4:
+        theta = rvec[:, -1]
+        r = rvec[:, :3]
+        r = r / torch.sqrt(1e-5 + torch.sum(r ** 2, dim=1))[:, None]
+    else:
+        raise ValueError(rvec.shape)
+    c = torch.cos(theta); s = torch.sin(theta)
+    x, y, z = r[:, 0], r[:, 1], r[:, 2]
+    R = torch.stack((
+        x ** 2 + (1. - x ** 2) * c, x * y * (1. - c) - z * s, x * z * (1. - c) + y * s,
+        x * y * (1. - c) + z * s, y ** 2 + (1. - y ** 2) * c, y * z * (1. - c) - x * s,
+        x * z * (1. - c) - y * s, y * z * (1. - c) + x * s, z ** 2 + (1. - z ** 2) * c), dim=1)
+    return R.view(-1, 3, 3), theta
+
+
+def chain_product(m: torch.Tensor) -> torch.Tensor:
+    """pointwarper.py:145-153: recursive halving product over dim 1."""
+    L = m.shape[1]
+    if L == 1:
+        return m
+    return chain_product(m[:, :L // 2]) @ chain_product(m[:, L // 2:])
+
+
+def skeleton_tree(bones, J):
+    """pointwarper.py:94-116 (``old=False``): parent_indices (J, depth) padded with -1 at
+    the end, and parent_joint_ex (root -> 0)."""
+    parent = {b[1]: b[0] for b in bones}
+    paths = [[0]]
+    for i in range(len(bones)):
+        j = i + 1
+        inds = []
+        while j >= 0:
+            inds.append(j)
+            j = parent.get(j, -1)
+        paths.append(inds[::-1])
+    depth = max(len(x) for x in paths)
+    pi = torch.full((len(paths), depth), -1, dtype=torch.long)
+    for i, inds in enumerate(paths):
+        pi[i, :len(inds)] = torch.tensor(inds)
+    pex = torch.tensor([parent.get(i, 0) for i in range(len(paths))], dtype=torch.long)
+    return pi, pex
+
+
+def bone_transforms(R_t: torch.Tensor, joints: torch.Tensor, parent_indices, parent_joint_ex):
+    """pointwarper.py:156-193 (``calc_rec_abs_T_fast``, the ``old`` formulation it returns)."""
+    J = R_t.shape[0]
+    joints_old = torch.cat((torch.zeros(1, 3), joints), 0)[parent_joint_ex + 1]
+    hom = torch.tensor([0., 0., 0., 1.])
+    M = torch.cat((torch.cat((R_t, joints_old[..., None] + R_t @ -joints_old[..., None]), -1),
+                   hom[None, None].repeat(J, 1, 1)), -2)
+    M = torch.cat((torch.eye(4)[None], M), 0)
+    return chain_product(M[parent_indices + 1])[:, 0]
+
+
+def transform_net(t_embed: torch.Tensor, tn: dict, J: int) -> torch.Tensor:
+    """pointwarper.py:5-37: Linear/ReLU x4, final Linear without bias -> (J+1, 4)."""
+    h = t_embed
+    for li in range(4):
+        h = torch.relu(torch.nn.functional.linear(h, tn[f"net.{2 * li}.weight"], tn[f"net.{2 * li}.bias"]))
+    out = torch.nn.functional.linear(h, tn["net.8.weight"])
+    return out.reshape(J + 1, 4)
+
+
+def pointwarper_forward(st: dict, weights, joints, t_embed=None, rot_params=None):
+    """pointwarper.py:213-279 with get_frames=True, get_skeleton=True, avg_procrustes=False.
+
+    Returns (xyz (N,3), joints_rel (J,3), G (N,4,4), joints_warped (J,3)).
+    """
+    J = joints.shape[0]
+    if rot_params is None:
+        params = transform_net(t_embed.unsqueeze(0), st["transform_net"], J)
+        global_t = params[-1, :3]
+        R_t, _ = rodrigues(params[:J, :])
+    else:
+        R_t, _ = rodrigues(rot_params)
+        global_t = torch.zeros(3)
+    R_t = R_t[st["sibling_mask"]]
+    R_t[st["rot_mask"]] = torch.eye(3)
+    bone_Ts = bone_transforms(R_t, joints, st["parent_indices"], st["parent_joint_ex"])
+    G = (bone_Ts * weights[:, :, None, None]).sum(dim=1)
+    xyz = st["canonical_pcd"]
+    xyzh = torch.cat([xyz, torch.ones((len(xyz), 1))], -1)
+    xyz = torch.bmm(G, xyzh.unsqueeze(-1)).squeeze(-1)[:, :3]
+    jh = torch.cat([joints, torch.ones((J, 1))], -1)
+    joints_rel = torch.bmm(bone_Ts, jh.unsqueeze(-1)).squeeze(-1)[:, :3]
+    return (xyz + global_t).contiguous(), joints_rel, G, joints_rel + global_t, bone_Ts, global_t
+
+
+# ----------------------------------------------------------------------------------------
+# TemporalPoints -- lib/temporalpoints.py
+# ----------------------------------------------------------------------------------------
+
+def get_weights(W: torch.Tensor, theta_weight: torch.Tensor, flat_merging_rules, eps=1e-6):
+    """temporalpoints.py:401-414: softmax(W/max(eps,theta)) then column merge
+    out[:, i] = sum_{k: rules[k]==i} sm[:, k] (sequential in k)."""
+    th = torch.max(torch.tensor(eps), theta_weight)
+    sm = torch.softmax(W / th, dim=-1)
+    rules = torch.as_tensor(flat_merging_rules).long()
+    J = sm.shape[1]
+    if torch.equal(rules, torch.arange(J)):
+        return sm
+    out = torch.zeros_like(sm)
+    for k in range(J):
+        out[:, rules[k]] += sm[:, k]
+    return out
+
+
+def project_point_to_image_plane(points, pose, K):
+    """utils.py:435-450."""
+    pts = torch.repeat_interleave(points.unsqueeze(0), len(pose), 0)
+    pose = pose.inverse()
+    pts = torch.bmm(pose[:, :3, :3], pts.transpose(1, 2)).transpose(1, 2) + pose[:, :3, 3:].transpose(1, 2)
+    pts = torch.bmm(K, pts.transpose(1, 2)).transpose(1, 2)
+    return pts[:, :, :2] / pts[:, :, 2:]
+
+
+def _lin(x, st, name):
+    return torch.nn.functional.linear(x, st[name + ".weight"], st.get(name + ".bias"))
+
+
+def feat_net(x, st):
+    """temporalpoints.py:123-130 (feat_depth=4): 4 x [Linear + LeakyReLU(0.01)]."""
+    for nm in ["feat_net.0", "feat_net.2.0", "feat_net.3.0", "feat_net.4"]:
+        x = torch.nn.functional.leaky_relu(_lin(x, st, nm), 0.01)
+    return x
+
+
+def rgbnet(h, views, st):
+    """tineuvox.py:65-88: feature_linears (no activation) -> cat views -> Linear/ReLU/Linear."""
+    f = _lin(h, st, "rgbnet.feature_linears")
+    if views is not None:
+        f = torch.cat([f, views], -1)
+    f = torch.relu(_lin(f, st, "rgbnet.views_linears.0"))
+    return _lin(f, st, "rgbnet.views_linears.2")
+
+
+def pose_embedding_net(x, st):
+    for nm in ["pose_embedding_net.0", "pose_embedding_net.2.0", "pose_embedding_net.3.0",
+               "pose_embedding_net.4"]:
+        x = torch.nn.functional.leaky_relu(_lin(x, st, nm), 0.01)
+    return x
+
+
+class OracleModel:
+    """CPU restatement of ``TemporalPoints`` built from a state dict (keys as in the
+    reference) plus the non-state constructor arguments."""
+
+    def __init__(self, state: dict, canonical_pcd, bones, *, stepsize=0.5, voxel_size=0.034,
+                 fast_color_thres=1e-4, pose_embedding_dim=0, neighbours=8, eps=1e-6,
+                 act_shift=None, voxel_size_ratio=1.0, frozen_view_dir=None,
+                 mean_min_distance_value=None, merging_rules=None, sibling_mask=None,
+                 rot_mask=None):
+        g = lambda k: state[k].detach().cpu().float() if torch.is_tensor(state[k]) else state[k]
+        self.st = {k: (v.detach().cpu() if torch.is_tensor(v) else v) for k, v in state.items()}
+        self.canonical_pcd = torch.as_tensor(canonical_pcd).float().cpu()
+        self.bones = [list(map(int, b)) for b in bones]
+        self.joints = g("joints")
+        self.J = self.joints.shape[0]
+        self.W = g("weights")
+        self.theta_weight = g("theta_weight")
+        self.feat = g("canonical_feat")
+        self.alpha_c = g("canonical_alpha")
+        self.rgb_c = g("canonical_rgbs")
+        self.direct_eps = g("direct_eps")
+        self.rules = merging_rules if merging_rules is not None else torch.arange(self.J)
+        self.stepsize = stepsize
+        self.voxel_size = voxel_size
+        self.fast_color_thres = fast_color_thres
+        self.pose_embedding_dim = pose_embedding_dim
+        self.K = neighbours
+        self.eps = torch.tensor(eps)
+        self.act_shift = math.log(1 / (1 - 1e-3) - 1) if act_shift is None else act_shift
+        self.voxel_size_ratio = voxel_size_ratio
+        self.frozen_view_dir = frozen_view_dir
+        self.time_poc = torch.tensor([2.0 ** i for i in range(8)])
+        self.pos_poc = torch.tensor([2.0 ** i for i in range(10)])
+        self.view_poc = torch.tensor([2.0 ** i for i in range(4)])
+        pi, pex = skeleton_tree(self.bones, self.J)
+        self.pw = {
+            "transform_net": {k[len("forward_warp.transform_net."):]: g(k) for k in state
+                              if k.startswith("forward_warp.transform_net.net")},
+            "sibling_mask": sibling_mask if sibling_mask is not None else torch.arange(self.J),
+            "rot_mask": rot_mask if rot_mask is not None else torch.zeros(self.J, dtype=torch.bool),
+            "parent_indices": pi, "parent_joint_ex": pex, "canonical_pcd": self.canonical_pcd,
+        }
+        self.nets = {k: g(k) for k in state if k.split(".")[0] in
+                     ("feat_net", "rgbnet", "densitynet", "pose_embedding_net")}
+        self.mmd = (mean_min_distance(self.canonical_pcd, neighbours, eps)
+                    if mean_min_distance_value is None else torch.as_tensor(mean_min_distance_value))
+        self.trace = {}
+
+    # temporalpoints.py:401-414
+    def get_weights(self):
+        return get_weights(self.W, self.theta_weight, self.rules, float(self.eps))
+
+    # temporalpoints.py:370-371
+    def repose(self, rot_params):
+        xyz, joints_rel, *_ = pointwarper_forward(self.pw, self.get_weights(), self.joints, rot_params=rot_params)
+        return xyz, joints_rel
+
+    def warp(self, t=None, rot_params=None):
+        t_embed = poc_fre(torch.as_tensor(t).reshape(1).float(), self.time_poc) if rot_params is None else None
+        weights = self.get_weights()
+        return weights, pointwarper_forward(self.pw, weights, self.joints, t_embed, rot_params)
+
+    # temporalpoints.py:373-399
+    def sample_ray(self, rays_o, rays_d, near, far, stepsize, xyz_min, xyz_max):
+        stepdist = stepsize * self.voxel_size
+        pts, mask_out, ray_id, step_id, *_ = sample_pts_on_rays(
+            rays_o.numpy(), rays_d.numpy(), xyz_min.numpy(), xyz_max.numpy(), near, far, stepdist)
+        m = ~mask_out
+        return pts[m], ray_id[m], step_id[m], m
+
+    # temporalpoints.py:416-521
+    def aggregate_pts(self, t_hat_pcd, Rinv, query_radius, render_kwargs, pose_embedding,
+                      calc_min_max=True, knn_tree=None):
+        R = len(render_kwargs["rays_o"])
+        K = self.K
+        if calc_min_max:
+            xyz_min = torch.min(t_hat_pcd, dim=0)[0] - query_radius
+            xyz_max = torch.max(t_hat_pcd, dim=0)[0] + query_radius
+        else:
+            raise NotImplementedError("calc_min_max=False needs the TiNeuVox bbox")
+        pts, ray_id, step_id, _ = self.sample_ray(render_kwargs["rays_o"], render_kwargs["rays_d"],
+                                                  render_kwargs["near"], render_kwargs["far"],
+                                                  render_kwargs["stepsize"], xyz_min, xyz_max)
+        self.trace.update(xyz_min=xyz_min, xyz_max=xyz_max, n_inbbox=len(pts))
+        if len(pts) == 0:
+            return None
+        tp = t_hat_pcd.numpy()
+        d2, s_i = knn_kmin(pts, tp, K, use_tree=knn_tree)
+        keep = np.nonzero(d2[:, -1] <= F32(query_radius))[0]
+        s_i = s_i[keep]; ray_id = ray_id[keep]; step_id = step_id[keep]; pts = pts[keep]
+        self.trace.update(s_i=s_i, ray_id=ray_id, step_id=step_id, keep=keep)
+        if len(s_i) == 0:
+            return None
+        s_i_t = torch.from_numpy(s_i)
+        ray_pts = torch.from_numpy(pts)
+        rel_p = ray_pts[:, None, :] - t_hat_pcd[s_i_t, :]
+        to_nn = (rel_p ** 2).sum(-1)
+        features_k = self.feat[s_i_t, :]
+        Rk = Rinv[s_i_t, :, :]
+        # direct render (459-470), forced on at 592
+        sig = self.mmd * torch.max(self.direct_eps, torch.tensor(0.))
+        w_direct = torch.exp(-(to_nn ** 2) / (2 * (sig[s_i_t]) ** 2 + 1e-12))
+        w_dd = (torch.tensor(1. / K) * w_direct).unsqueeze(-1)
+        w_direct = (w_direct / (w_direct.sum(dim=-1) + 1e-12)[:, None]).unsqueeze(-1)
+        rgbs_direct = (w_direct * self.rgb_c.clip(0, 1)[s_i_t, :]).sum(dim=1)
+        alpha_direct = (w_dd * self.alpha_c.clip(0, 1)[s_i_t].unsqueeze(-1)).sum(dim=1).squeeze(-1)
+        # point-NeRF aggregation (472-494)
+        w = 1 / (to_nn + self.eps)
+        w = (w / w.sum(dim=-1)[:, None]).unsqueeze(-1)
+        rel_c = torch.bmm(Rk[..., :3, :3].reshape(-1, 3, 3), rel_p.reshape(-1, 3).unsqueeze(-1)).squeeze(-1)
+        x = [poc_fre(rel_c, self.pos_poc), features_k.reshape(-1, features_k.shape[-1])]
+        if pose_embedding is not None:
+            x.append(pose_embedding.expand(len(x[0]), -1))
+        out = feat_net(torch.cat(x, -1), self.nets)
+        h = (out.reshape(len(s_i), K, -1) * w).sum(dim=1)
+        density = _lin(h, self.nets, "densitynet").squeeze(-1)
+        interval = render_kwargs["stepsize"] * self.voxel_size_ratio
+        _, alpha = raw2alpha(density.numpy(), self.act_shift, interval)
+        alpha = torch.from_numpy(alpha)
+        if self.frozen_view_dir is not None:
+            views = poc_fre(torch.as_tensor(self.frozen_view_dir).float(), self.view_poc)[None].expand(len(ray_id), -1)
+        else:
+            views = poc_fre(render_kwargs["viewdirs"], self.view_poc)[torch.from_numpy(ray_id)]
+        rgbs = torch.sigmoid(rgbnet(h, views, self.nets))
+        lbsw = (self._last_weights[s_i_t, :] * w).sum(dim=1)
+        self.trace.update(to_nn=to_nn, h=h, density=density, alpha=alpha, rgbs=rgbs,
+                          alpha_direct=alpha_direct, rgbs_direct=rgbs_direct, lbsw=lbsw)
+        return rgbs, alpha, rgbs_direct, alpha_direct, lbsw, ray_id, step_id, R
+
+    # temporalpoints.py:540-712
+    @torch.no_grad()
+    def forward(self, t, render_depth=False, render_kwargs=None, query_radius=0.01,
+                render_weights=False, rot_params=None, poses=None, Ks=None, get_skeleton=False,
+                calc_min_max=True, perm=None, knn_tree=None):
+        assert (t is None) ^ (rot_params is None)
+        rk = {k: (v.detach().cpu() if torch.is_tensor(v) else v) for k, v in render_kwargs.items()}
+        weights, (t_hat, joints_rel, G, joints_w, bone_Ts, global_t) = self.warp(t, rot_params)
+        self._last_weights = weights
+        Rinv = torch.inverse(G)
+        self.trace = dict(t_hat_pcd=t_hat, G=G, Rinv=Rinv, bone_Ts=bone_Ts, weights=weights,
+                          joints_rel=joints_rel, global_t=global_t)
+        delta = (self.joints - joints_rel)
+        pose_embedding = (pose_embedding_net(poc_fre(delta, self.pos_poc).view(1, -1), self.nets)
+                          if self.pose_embedding_dim > 0 else None)
+        joints = bones = None
+        if get_skeleton:
+            joints = project_point_to_image_plane(joints_w, poses.cpu(), Ks.cpu().float())
+            bones = self.bones
+        R = len(rk["rays_o"])
+        bg = rk["bg"]
+        res = self.aggregate_pts(t_hat, Rinv, query_radius, rk, pose_embedding, calc_min_max, knn_tree)
+        if res is None:  # NoPointsException fallback (598-609)
+            return {"rgb_marched": torch.ones(R, 3) * bg, "rgb_marched_direct": torch.ones(R, 3) * bg,
+                    "depth": torch.zeros(R), "weights": torch.ones(R, 3) * bg, "t_hat_pcd": t_hat,
+                    "alphainv_last": None, "grid": None, "joints": joints, "bones": bones}
+        rgbs, alpha, rgbs_d, alpha_d, lbsw, ray_id, step_id, N = res
+        thr = F32(self.fast_color_thres)
+        ray_id_d = ray_id.copy()
+        a = alpha.numpy(); ad = alpha_d.numpy()
+        rgbs = rgbs.numpy(); rgbs_d = rgbs_d.numpy(); lbsw = lbsw.numpy()
+        if self.fast_color_thres > 0:
+            m = a > thr
+            ray_id, step_id, a, rgbs, lbsw = ray_id[m], step_id[m], a[m], rgbs[m], lbsw[m]
+            md = ad > thr
+            ray_id_d, ad, rgbs_d = ray_id_d[md], ad[md], rgbs_d[md]
+        w, _, last, *_ = alpha2weight(a, ray_id, N)
+        wd, _, last_d, *_ = alpha2weight(ad, ray_id_d, N)
+        if self.fast_color_thres > 0:
+            m = w > thr
+            w, a, ray_id, step_id, rgbs, lbsw = w[m], a[m], ray_id[m], step_id[m], rgbs[m], lbsw[m]
+            md = wd > thr
+            ray_id_d, ad, rgbs_d, wd = ray_id_d[md], ad[md], rgbs_d[md], wd[md]
+        rgb_marched = segment_sum((w[:, None] * rgbs).astype(F32), ray_id, N)
+        rgb_marched = (rgb_marched + (last[:, None] * F32(bg)).astype(F32)).astype(F32)
+        rgb_marched_d = segment_sum((wd[:, None] * rgbs_d).astype(F32), ray_id_d, N)
+        rgb_marched_d = (rgb_marched_d + (last_d[:, None] * F32(bg)).astype(F32)).astype(F32)
+        ret = {"t_hat_pcd": t_hat, "rgb_marched": torch.from_numpy(rgb_marched),
+               "alphainv_last": torch.from_numpy(last), "alphainv_last_direct": torch.from_numpy(last_d),
+               "grid": None, "rgb_marched_direct": torch.from_numpy(rgb_marched_d),
+               "joints": joints, "bones": bones}
+        if render_depth:
+            ret["depth"] = torch.from_numpy(segment_sum((w * step_id.astype(F32)).astype(F32), ray_id, N))
+        if render_weights:
+            wmask = weights.sum(dim=0) > 0
+            cols = torch.tensor(hls_palette(int(wmask.sum())))
+            if perm is None:
+                gen = torch.Generator(); gen.manual_seed(0)
+                perm = torch.randperm(cols.shape[0], generator=gen)
+            cols = cols[perm]
+            col = 0
+            lb = torch.from_numpy(lbsw)
+            for ci, wi in enumerate(torch.where(wmask)[0]):
+                col = col + cols[ci, None] * lb[:, wi, None]
+            col = torch.as_tensor(col).float().numpy() if torch.is_tensor(col) else np.zeros((len(w), 3), F32)
+            wm = segment_sum((w[:, None] * col).astype(F32), ray_id, N)
+            ret["weights"] = torch.from_numpy((wm + (last[:, None] * F32(bg)).astype(F32)).astype(F32))
+        return ret

@@ -1,0 +1,86 @@
+"""Known-answer tests for the oracle's restatement of render_utils_kernel.cu, derived by
+hand from the kernel source; these pin the parts no reference run can."""
+import numpy as np
+
+from oracle import apn_oracle as O
+
+F32 = np.float32
+LO = np.array([-1, -1, -1], F32)
+HI = np.array([1, 1, 1], F32)
+
+
+def test_axis_parallel_ray_zero_components():
+    # d = (1,0,0): y/z components replaced by 1e-6 (render_utils_kernel.cu:23-25)
+    o = np.array([[-3, 0, 0]], F32); d = np.array([[1, 0, 0]], F32)
+    t_min, t_max = O.infer_t_minmax(o, d, LO, HI, 0.0, 10.0)
+    assert t_min[0] == F32(2) and t_max[0] == F32(4)
+    n = O.infer_n_samples(t_min, t_max, 0.5)
+    assert n[0] == 4          # exact multiple: ceil(2/0.5) = 4
+
+
+def test_missing_ray_gets_one_masked_sample():
+    o = np.array([[-3, 5, 0]], F32); d = np.array([[1, 0, 0]], F32)
+    pts, mo, rid, sid, n, t_min, t_max = O.sample_pts_on_rays(o, d, LO, HI, 0.5, 10.0, 0.1)
+    assert n[0] == 1 and len(pts) == 1 and mo[0]
+    assert rid[0] == 0 and sid[0] == 0
+
+
+def test_step_ids_and_positions():
+    o = np.array([[-3, 0, 0], [0, -3, 0.5]], F32); d = np.array([[2, 0, 0], [0, 1, 0]], F32)
+    pts, mo, rid, sid, n, t_min, t_max = O.sample_pts_on_rays(o, d, LO, HI, 0.0, 100.0, 0.25)
+    assert list(n) == [4, 8]
+    assert list(rid) == [0] * 4 + [1] * 8
+    assert list(sid) == list(range(4)) + list(range(8))
+    # start = o + d*t_min (unnormalised d), dir = d/|d|
+    assert np.allclose(pts[:4, 0], [-1, -0.75, -0.5, -0.25])
+    assert np.allclose(pts[4:, 1], np.arange(8) * 0.25 - 1)
+
+
+def test_raw2alpha_overflow_gives_one():
+    e, a = O.raw2alpha(np.array([1e4, -1e4, 0.0], F32), -6.9, 0.5)
+    assert np.isinf(e[0]) and a[0] == F32(1)
+    assert a[1] == F32(0)
+    assert np.isclose(a[2], 1 - (1 + np.exp(np.float32(-6.9))) ** -0.5, rtol=1e-6)
+
+
+def test_alpha2weight_early_exit_and_empty_rays():
+    alpha = np.array([0.5, 0.9, 0.99, 0.5, 0.5, 0.3], F32)
+    rid = np.array([1, 1, 1, 1, 1, 3], np.int64)
+    w, T, last, i_s, i_e = O.alpha2weight(alpha, rid, 5)
+    # ray 1: T = 1, .5, .05, 5e-4 (<1e-3 -> break after the 3rd sample, which is written)
+    assert np.allclose(T[:3], [1, 0.5, 0.05], rtol=1e-6)
+    assert np.allclose(w[:3], [0.5, 0.45, 0.0495], rtol=1e-6)
+    assert w[3] == 0 and w[4] == 0 and T[3] == 1 and T[4] == 1
+    assert i_s[1] == 0 and i_e[1] == 3
+    assert np.isclose(last[1], np.float32(np.float64(np.float32(0.05)) * (1 - np.float64(np.float32(0.99)))))
+    # empty rays keep alphainv_last = 1
+    assert last[0] == 1 and last[2] == 1 and last[4] == 1
+    assert np.isclose(last[3], 0.7)
+    assert i_s[3] == 5 and i_e[3] == 6
+
+
+def test_alpha2weight_double_precision_update():
+    # T_cum is updated in double and narrowed (render_utils_kernel.cu:450)
+    alpha = np.full(50, 0.1, F32)
+    rid = np.zeros(50, np.int64)
+    w, T, last, *_ = O.alpha2weight(alpha, rid, 1)
+    tc = F32(1)
+    for i in range(50):
+        assert T[i] == tc
+        tc = F32(np.float64(tc) * (1.0 - np.float64(F32(0.1))))
+        if np.float64(tc) < 1e-3:
+            break
+    assert last[0] == tc
+
+
+def test_segment_sum_sequential():
+    src = np.array([1e8, 1, -1e8, 1], F32)
+    out = O.segment_sum(src, np.array([0, 0, 0, 1]), 2)
+    # sequential float32: (1e8 + 1) - 1e8 = 0
+    assert out[0] == F32(0) and out[1] == F32(1)
+
+
+def test_knn_ties_broken_by_index():
+    pts = np.array([[1, 0, 0], [-1, 0, 0], [0, 1, 0], [0, 0, 0.5]], F32)
+    d2, idx = O.knn_kmin(np.zeros((1, 3), F32), pts, 3)
+    assert list(idx[0]) == [3, 0, 1] and d2[0, 0] == F32(0.25)
