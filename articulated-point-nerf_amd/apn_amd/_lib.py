@@ -1,0 +1,108 @@
+"""ctypes binding of libapn_hip.so (C-ABI declared in include/apn_hip.h).
+
+The product path has no CPU fallback: importing an op that needs the library raises
+``RuntimeError`` when libapn_hip.so is missing or cannot be loaded, and every C call that
+returns a non-zero status raises as well.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("APN_HIP_LIB", os.path.join(_HERE, "libapn_hip.so"))
+
+P = C.c_void_p
+I64 = C.c_int64
+I32 = C.c_int32
+F32 = C.c_float
+SZ = C.c_size_t
+
+# name -> (restype, argtypes); must match include/apn_hip.h
+SIGNATURES = {
+    "apn_sample_pts_on_rays_workspace_bytes": (SZ, [I64]),
+    "apn_sample_pts_on_rays_count": (C.c_int, [P, P, P, P, F32, F32, F32, I64, P, P, P, P, P, P]),
+    "apn_sample_pts_on_rays_fill": (C.c_int, [P, P, P, P, F32, F32, F32, I64, P, P, P, P, P, P]),
+    "apn_raw2alpha": (C.c_int, [P, F32, F32, I64, P, P, P]),
+    "apn_alpha2weight": (C.c_int, [P, P, I64, I64, P, P, P, P, P, P]),
+    "apn_segment_sum": (C.c_int, [P, P, I64, I64, I64, P, P, P]),
+    "apn_lbs_skin": (C.c_int, [P, P, I64, I32, P, F32, P, P, P, P, P, P, P, F32, I32, P, P, P, P, P, P, P]),
+    "apn_bbox_unpack": (C.c_int, [P, F32, P, P]),
+    "apn_inbbox_count": (C.c_int, [P, P, P, F32, F32, F32, I64, P, P, P]),
+    "apn_inbbox_fill": (C.c_int, [P, P, P, F32, F32, F32, I64, P, P, P, P]),
+    "apn_grid_workspace_bytes": (SZ, [I64, I32]),
+    "apn_grid_build": (C.c_int, [P, I64, P, F32, I32, P, P, P]),
+    "apn_knn_workspace_bytes": (SZ, [I64]),
+    "apn_knn_radius": (C.c_int, [P, P, I64, P, P, I64, I32, P, F32, P, P, P, P, P, P]),
+    "apn_nn1_distance": (C.c_int, [P, I64, F32, I32, P, P, P, P, P]),
+    "apn_mlp_weight_layout": (C.c_int, [P]),
+    "apn_point_mlp": (C.c_int, [P, P, P, I64, P, P, P, P, I32, P, P, P, F32, F32, F32, I32, P, P]),
+    "apn_composite": (C.c_int, [P, P, P, I64, P, I64, F32, F32, P, P, P, P, P, P, P, P]),
+    "apn_scan_workspace_bytes": (SZ, [I64]),
+    "apn_scan_exclusive_i32": (C.c_int, [P, P, I64, P, P]),
+    "apn_version": (C.c_char_p, []),
+}
+
+_lib = None
+_load_error = None
+
+
+def load():
+    """Load libapn_hip.so once; raise RuntimeError (no fallback) if it is unavailable."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    if _load_error is not None:
+        raise RuntimeError(_load_error)
+    if not os.path.exists(LIB_PATH):
+        _load_error = (f"libapn_hip.so not found at {LIB_PATH}; build it with "
+                       f"`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
+        raise RuntimeError(_load_error)
+    try:
+        lib = C.CDLL(LIB_PATH)
+    except OSError as e:  # pragma: no cover
+        _load_error = f"failed to load {LIB_PATH}: {e}"
+        raise RuntimeError(_load_error)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def exported_symbols():
+    return list(SIGNATURES)
+
+
+class APNError(RuntimeError):
+    pass
+
+
+_STATUS = {1: "invalid argument (shape/pointer)", 2: "HIP launch failure"}
+
+
+def call(name, *args):
+    rc = getattr(load(), name)(*args)
+    if rc != 0:
+        raise APNError(f"{name} failed: {_STATUS.get(rc, rc)}")
+    return rc
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return C.c_void_p(t.data_ptr())
+
+
+def stream_ptr(device=None):
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_cuda(*tensors, what="apn op"):
+    for t in tensors:
+        if t is not None and torch.is_tensor(t) and not t.is_cuda:
+            raise RuntimeError(f"{what}: expected a device (HIP) tensor, got {t.device}")

@@ -1,0 +1,65 @@
+"""Render harness: the counterpart of the reference's ``render_viewpoints`` /
+``render_repose`` (run.py:80-239, 241-356) for synthetic scenes, minus file I/O and metrics
+that need ground-truth images.
+
+A frame is rendered with a single ``TemporalPoints.forward`` over all H*W rays (chunking is
+optional and bit-identical); ``render_pcd_direct`` substitutes ``rgb_marched_direct`` for
+``rgb_marched`` as run.py:162-163 does.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import synthetic as S
+from .temporalpoints import TemporalPoints
+from .tineuvox import TiNeuVoxHeads
+
+
+def build_model(scene: S.Scene, device="cuda") -> TemporalPoints:
+    """TemporalPoints(**scene.ctor, tineuvox=heads) with the scene's network weights loaded."""
+    c = scene.ctor
+    heads = TiNeuVoxHeads(c["xyz_min"], c["xyz_max"], num_voxels=160 ** 3, num_voxels_base=160 ** 3,
+                          net_width=S.NET_WIDTH, alpha_init=S.ALPHA_INIT, posbase_pe=S.POSBASE_PE,
+                          viewbase_pe=S.VIEWBASE_PE, timebase_pe=S.TIMEBASE_PE, no_view_dir=False)
+    model = TemporalPoints(**c, tineuvox=heads)
+    missing, unexpected = model.load_state_dict(scene.params, strict=False)
+    if unexpected:
+        raise KeyError(f"unexpected state-dict keys: {unexpected}")
+    return model.to(device)
+
+
+def render_kwargs_for(scene: S.Scene, device="cuda"):
+    return scene.render_kwargs(device)
+
+
+@torch.no_grad()
+def render_frame(model, scene: S.Scene, t=None, rot_params=None, render_kwargs=None, chunk=None,
+                 render_pcd_direct=False, device="cuda"):
+    """One frame -> dict of (H, W, C) images: rgb, depth, weights (+ joints)."""
+    rk = render_kwargs if render_kwargs is not None else scene.render_kwargs(device)
+    H, W = scene.cfg.H, scene.cfg.W
+    R = rk["rays_o"].shape[0]
+    chunk = chunk or R
+    outs = []
+    t_arg = None if rot_params is not None else torch.tensor([scene.cfg.t if t is None else t], device=device)
+    for s in range(0, R, chunk):
+        sub = dict(rk)
+        for k in ("rays_o", "rays_d", "viewdirs"):
+            sub[k] = rk[k][s:s + chunk]
+        out = model(t_arg, render_depth=True, render_kwargs=sub, render_weights=True, rot_params=rot_params,
+                    render_pcd_direct=render_pcd_direct, poses=scene.c2w[None].to(device),
+                    Ks=scene.K[None].to(device), get_skeleton=True)
+        if render_pcd_direct:
+            out["rgb_marched"] = out["rgb_marched_direct"]
+        outs.append(out)
+    res = {k: torch.cat([o[k] for o in outs]).reshape(H, W, -1) for k in ("rgb_marched", "depth", "weights")}
+    res["joints"] = outs[0]["joints"]
+    return res
+
+
+def psnr(a: torch.Tensor, b: torch.Tensor) -> float:
+    """run.py:186: -10 log10(mean((a-b)^2))."""
+    mse = float(((a.float() - b.float()) ** 2).mean())
+    return float("inf") if mse == 0 else -10.0 * math.log10(mse)

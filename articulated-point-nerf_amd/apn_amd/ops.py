@@ -1,0 +1,157 @@
+"""Torch-facing wrappers over the C-ABI: allocation, stream plumbing, shape checks.
+
+Every function here launches HIP kernels from libapn_hip.so on the current stream; none
+has a CPU path.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _lib as L
+from ._lib import call, ptr, stream_ptr
+
+
+def _f32c(t):
+    return t.detach().to(torch.float32).contiguous()
+
+
+class Workspace:
+    """Grow-only device scratch buffers keyed by name (reused across forward calls)."""
+
+    def __init__(self):
+        self.bufs = {}
+
+    def get(self, name, numel, dtype, device):
+        b = self.bufs.get(name)
+        if b is None or b.numel() < numel or b.dtype != dtype or b.device != torch.device(device):
+            b = torch.empty(max(int(numel), 1), dtype=dtype, device=device)
+            self.bufs[name] = b
+        return b[:max(int(numel), 1)]
+
+    def bytes(self, name, nbytes, device):
+        return self.get(name, (int(nbytes) + 255) // 256 * 256, torch.uint8, device)
+
+
+# ----------------------------------------------------------------------------------------
+# render_utils_cuda drop-ins (render_utils.cpp:144-155)
+# ----------------------------------------------------------------------------------------
+
+def sample_pts_on_rays(rays_o, rays_d, xyz_min, xyz_max, near, far, stepdist):
+    """Returns [rays_pts, mask_outbbox, ray_id, step_id, N_steps, t_min, t_max] like
+    render_utils_cuda.sample_pts_on_rays (render_utils_kernel.cu:190-236)."""
+    L.require_cuda(rays_o, rays_d, xyz_min, xyz_max, what="sample_pts_on_rays")
+    if not (rays_o.is_contiguous() and rays_d.is_contiguous()):
+        raise RuntimeError("rays_o / rays_d must be contiguous")
+    dev = rays_o.device
+    ro, rd = _f32c(rays_o), _f32c(rays_d)
+    lo, hi = _f32c(xyz_min), _f32c(xyz_max)
+    R = ro.shape[0]
+    t_min = torch.empty(R, device=dev); t_max = torch.empty(R, device=dev)
+    n_steps = torch.empty(R, dtype=torch.int64, device=dev)
+    offs = torch.empty(R + 1, dtype=torch.int32, device=dev)
+    ws = torch.empty(int(L.load().apn_sample_pts_on_rays_workspace_bytes(R)) + 256, dtype=torch.uint8, device=dev)
+    s = stream_ptr(dev)
+    call("apn_sample_pts_on_rays_count", ptr(ro), ptr(rd), ptr(lo), ptr(hi), float(near), float(far),
+         float(stepdist), R, ptr(t_min), ptr(t_max), ptr(n_steps), ptr(offs), ptr(ws), s)
+    total = int(offs[R].item())
+    pts = torch.empty(total, 3, device=dev)
+    mask = torch.empty(total, dtype=torch.bool, device=dev)
+    ray_id = torch.empty(total, dtype=torch.int64, device=dev)
+    step_id = torch.empty(total, dtype=torch.int64, device=dev)
+    call("apn_sample_pts_on_rays_fill", ptr(ro), ptr(rd), ptr(lo), ptr(hi), float(near), float(far),
+         float(stepdist), R, ptr(offs), ptr(pts), ptr(mask), ptr(ray_id), ptr(step_id), s)
+    return [pts, mask, ray_id, step_id, n_steps, t_min, t_max]
+
+
+def raw2alpha(density, shift, interval):
+    """render_utils_kernel.cu:357-393 -> (exp_d, alpha)."""
+    L.require_cuda(density, what="raw2alpha")
+    d = _f32c(density)
+    e = torch.empty_like(d); a = torch.empty_like(d)
+    call("apn_raw2alpha", ptr(d), float(shift), float(interval), d.numel(), ptr(e), ptr(a), stream_ptr(d.device))
+    return e, a
+
+
+def alpha2weight(alpha, ray_id, n_rays):
+    """render_utils_kernel.cu:430-505 -> (weight, T, alphainv_last, i_start, i_end)."""
+    L.require_cuda(alpha, ray_id, what="alpha2weight")
+    a = _f32c(alpha); rid = ray_id.to(torch.int64).contiguous()
+    n = a.numel(); dev = a.device
+    w = torch.empty(n, device=dev); T = torch.empty(n, device=dev)
+    last = torch.empty(int(n_rays), device=dev)
+    i_s = torch.empty(int(n_rays), dtype=torch.int64, device=dev)
+    i_e = torch.empty(int(n_rays), dtype=torch.int64, device=dev)
+    call("apn_alpha2weight", ptr(a), ptr(rid), n, int(n_rays), ptr(w), ptr(T), ptr(last), ptr(i_s), ptr(i_e),
+         stream_ptr(dev))
+    return w, T, last, i_s, i_e
+
+
+def segment_coo_sum(src, index, n_out):
+    """torch_scatter.segment_coo(src, index, out=zeros, reduce='sum') for sorted index."""
+    L.require_cuda(src, index, what="segment_coo")
+    s2 = _f32c(src)
+    C = math.prod(s2.shape[1:]) if s2.dim() > 1 else 1
+    idx = index.to(torch.int64).contiguous()
+    out = torch.empty((int(n_out),) + tuple(s2.shape[1:]), device=s2.device)
+    ws = torch.empty(2 * max(int(n_out), 1), dtype=torch.int64, device=s2.device)
+    call("apn_segment_sum", ptr(s2), ptr(idx), s2.shape[0], C, int(n_out), ptr(out), ptr(ws), stream_ptr(s2.device))
+    return out
+
+
+# ----------------------------------------------------------------------------------------
+# packed MLP weights
+# ----------------------------------------------------------------------------------------
+
+_LAYOUT = None
+
+
+def mlp_layout():
+    global _LAYOUT
+    if _LAYOUT is None:
+        import ctypes as C
+        arr = (C.c_int32 * 32)()
+        n = L.load().apn_mlp_weight_layout(arr)
+        names = ["W1", "B1", "W2", "B2", "W3", "B3", "W4", "B4", "WD", "BD", "WF", "BF", "WV0", "BV0",
+                 "WV2", "BV2", "TOTAL", "K1", "KV"]
+        _LAYOUT = dict(zip(names, list(arr)[:n]))
+    return _LAYOUT
+
+
+def pack_mlp_weights(feat_net_layers, densitynet, rgbnet, pose_embedding=None, out=None):
+    """Pack feat_net / densitynet / rgbnet weights (nn.Linear (out,in) layout, zero-padded K)
+    into the buffer apn_point_mlp reads. The pose-embedding columns of feat_net.0
+    (temporalpoints.py:487-488) are folded into the layer-1 bias: b1 + W1[:,191:] @ pe."""
+    lay = mlp_layout()
+    l1, l2, l3, l4 = feat_net_layers
+    dev = l1.weight.device
+    buf = out if out is not None else torch.zeros(lay["TOTAL"], device=dev)
+    K1, KV = lay["K1"], lay["KV"]
+
+    def put(name, t):
+        t = t.detach().float().reshape(-1)
+        buf[lay[name]:lay[name] + t.numel()].copy_(t)
+
+    w1 = l1.weight.detach().float()
+    base = 63 + 128
+    w1p = torch.zeros(128, K1, device=dev)
+    w1p[:, :base] = w1[:, :base]
+    put("W1", w1p)
+    b1 = l1.bias.detach().float()
+    if pose_embedding is not None:
+        b1 = b1 + (w1[:, base:] @ pose_embedding.reshape(-1, 1).float()).reshape(-1)
+    elif w1.shape[1] != base:
+        raise ValueError(f"feat_net.0 expects {w1.shape[1]} inputs but no pose embedding was given")
+    put("B1", b1)
+    for nm, l in (("2", l2), ("3", l3), ("4", l4)):
+        put("W" + nm, l.weight); put("B" + nm, l.bias)
+    put("WD", densitynet.weight); put("BD", densitynet.bias)
+    put("WF", rgbnet.feature_linears.weight); put("BF", rgbnet.feature_linears.bias)
+    v0 = rgbnet.views_linears[0]
+    wv0 = torch.zeros(64, KV, device=dev)
+    wv0[:, :v0.weight.shape[1]] = v0.weight.detach().float()
+    put("WV0", wv0); put("BV0", v0.bias)
+    v2 = rgbnet.views_linears[2]
+    put("WV2", v2.weight); put("BV2", v2.bias)
+    return buf

@@ -1,0 +1,187 @@
+"""PointWarper / TransformNet with the reference's API and state-dict names
+(lib/pointwarper.py). The skeleton stage -- TransformNet (1x17 -> (J+1)x4), Rodrigues, the
+kinematic chain -- is a handful of J-sized tensor ops and runs as torch ops on the device;
+the per-point LBS blend + apply (the hot part, pointwarper.py:241-266) runs in the HIP kernel
+``apn_lbs_skin``.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from ._lib import call, ptr, stream_ptr
+
+
+class TransformNet(torch.nn.Module):
+    """pointwarper.py:5-37."""
+
+    def __init__(self, input_dim, num_components, num_params_per_component, num_layers=3, hidden_dim=256):
+        super().__init__()
+        self.hidden_dim = hidden_dim
+        self.num_components = num_components
+        self.num_params_per_component = num_params_per_component
+        self.out_dim = num_components * num_params_per_component
+        self.register_buffer("rotation_switch_mask", torch.arange(0, num_components).long())
+        layers = []
+        for i in range(num_layers - 1):
+            layers.append(torch.nn.Linear(input_dim if i == 0 else hidden_dim, hidden_dim))
+            layers.append(torch.nn.ReLU())
+        layers.append(torch.nn.Linear(hidden_dim, self.out_dim, bias=False))
+        self.net = torch.nn.Sequential(*layers)
+
+    def forward(self, x):
+        b = x.shape[0]
+        out = self.net(x)
+        if b > 1:
+            return out.reshape(b, self.num_components, self.num_params_per_component)
+        return out.reshape(self.num_components, self.num_params_per_component)
+
+
+def rodrigues(rvec: torch.Tensor):
+    """pointwarper.py:118-143 (Neural Volumes form; 3- or 4-vector)."""
+    if rvec.shape[-1] == 3:
+        theta = torch.sqrt(1e-5 + torch.sum(rvec ** 2, dim=1))
+        r = rvec / theta[:, None]
+    elif rvec.shape[-1] == 4:
+        theta = rvec[:, -1]
+        r = rvec[:, :3]
+        r = r / torch.sqrt(1e-5 + torch.sum(r ** 2, dim=1))[:, None]
+    else:
+        raise ValueError(rvec.shape)
+    c, s = torch.cos(theta), torch.sin(theta)
+    x, y, z = r[:, 0], r[:, 1], r[:, 2]
+    R = torch.stack((x ** 2 + (1. - x ** 2) * c, x * y * (1. - c) - z * s, x * z * (1. - c) + y * s,
+                     x * y * (1. - c) + z * s, y ** 2 + (1. - y ** 2) * c, y * z * (1. - c) - x * s,
+                     x * z * (1. - c) - y * s, y * z * (1. - c) + x * s, z ** 2 + (1. - z ** 2) * c), dim=1)
+    return R.view(-1, 3, 3), theta
+
+
+class PointWarper(torch.nn.Module):
+    """pointwarper.py:39-279. ``forward`` keeps the reference signature and return list."""
+
+    def __init__(self, t_dim, canonical_pcd, joints, bones, num_layers=5, over_parameterized_rot=True):
+        super().__init__()
+        self.t_dim = t_dim
+        self.params_per_compoent = 4
+        self.register_buffer("canonical_pcd", torch.as_tensor(canonical_pcd).float(), persistent=False)
+        self.num_layers = num_layers
+        self.over_parameterized_rot = over_parameterized_rot
+        self.init_tree(joints, bones)
+        self.register_buffer("hom_row", torch.tensor([0, 0, 0, 1], dtype=torch.float32), persistent=False)
+        self.transform_net = TransformNet(t_dim, len(joints) + 1, self.params_per_compoent, num_layers=num_layers)
+        self.register_buffer("rot_mask", torch.zeros(len(joints), dtype=torch.bool))
+        self.register_buffer("sibling_mask", torch.arange(0, len(joints)).long())
+
+    def init_tree(self, joints, bones, old=False):
+        """pointwarper.py:94-116 (the ``old=False`` tree used at construction)."""
+        self.bones = bones
+        self.parent_joint = {b[1]: b[0] for b in bones}
+        self.child_joints = {k: [] for k in range(len(joints))}
+        for k, p in self.parent_joint.items():
+            self.child_joints[p].append(k)
+        paths = [[0]]
+        for i in range(len(bones)):
+            j, inds = i + 1, []
+            while j >= 0:
+                inds.append(j)
+                j = self.parent_joint.get(j, -1)
+            paths.append(inds[::-1])
+        depth = int(np.max([len(x) for x in paths]))
+        pi = torch.full((len(paths), depth), -1, dtype=torch.long)
+        for i, inds in enumerate(paths):
+            pi[i, :len(inds)] = torch.tensor(inds)
+        self.register_buffer("parent_indices", pi, persistent=False)
+        self.register_buffer("parent_joint_ex", torch.tensor([self.parent_joint.get(i, 0) for i in range(len(paths))],
+                                                             dtype=torch.long), persistent=False)
+
+    Rodrigues = staticmethod(rodrigues)
+
+    @classmethod
+    def matrix_chain_product(cls, m):
+        """pointwarper.py:145-153: recursive halving (binary-tree) product over dim 1."""
+        L_ = m.shape[1]
+        if L_ == 1:
+            return m
+        return cls.matrix_chain_product(m[:, :L_ // 2]) @ cls.matrix_chain_product(m[:, L_ // 2:])
+
+    def calc_rec_abs_T_fast(self, R_t, joints):
+        """pointwarper.py:156-193: M_j = [R_j | p - R_j p] about the parent joint p, chained
+        root->joint; returns bone_Ts [J,4,4]."""
+        J = R_t.shape[0]
+        dev = R_t.device
+        joints_old = torch.cat((self.hom_row[None, :3].to(dev), joints), 0)[self.parent_joint_ex + 1]
+        M = torch.cat((torch.cat((R_t, joints_old[..., None] + R_t @ -joints_old[..., None]), -1),
+                       self.hom_row[None, None].to(dev).repeat(J, 1, 1)), -2)
+        M = torch.cat((torch.eye(4, device=dev)[None], M), 0)
+        return self.matrix_chain_product(M[self.parent_indices + 1])[:, 0]
+
+    def get_thetas(self, ts_embed):
+        params = self.transform_net(ts_embed)
+        rot = params[:, :-1, :3]
+        shape = rot.shape[:2]
+        _, thetas = self.Rodrigues(rot.reshape(shape[0] * shape[1], 3))
+        return thetas.reshape(shape)
+
+    def set_rotation_mask(self, rotations_to_keep):
+        mask = ~rotations_to_keep
+        if self.rot_mask is not None:
+            mask = torch.logical_or(mask, self.rot_mask)
+        self.rot_mask = mask
+
+    def set_sibling_mask(self, sibling_mask):
+        self.sibling_mask = sibling_mask.long()
+
+    def pose(self, joints, t=None, rot_params=None, global_t=None):
+        """Skeleton stage of forward (pointwarper.py:216-239): returns bone_Ts [J,4,4],
+        global_t [3] and joints_rel [J,3]. Sets prev_params / prev_thetas / prev_global_t."""
+        assert (t is None) ^ (rot_params is None)
+        if rot_params is None:
+            params = self.transform_net(t.unsqueeze(0))
+            self.prev_params = params
+            global_t = params[-1, :3]
+            R_t, self.prev_thetas = self.Rodrigues(params[:len(joints), :])
+            self.prev_global_t = global_t
+        else:
+            R_t, self.prev_thetas = self.Rodrigues(rot_params)
+        R_t = R_t[self.sibling_mask]
+        if self.rot_mask is not None:
+            R_t[self.rot_mask] = torch.eye(3, device=R_t.device)
+        bone_Ts = self.calc_rec_abs_T_fast(R_t, joints)
+        if global_t is None:
+            global_t = torch.zeros(3, dtype=torch.float32, device=bone_Ts.device)
+        jh = torch.cat([joints, torch.ones((len(joints), 1), device=joints.device)], -1)
+        joints_rel = torch.bmm(bone_Ts, jh.unsqueeze(-1)).squeeze(-1)[:, :3]
+        return bone_Ts, global_t, joints_rel
+
+    def forward(self, weights, joints, t=None, rot_params=None, global_t=None, get_frames=False,
+                avg_procrustes=False, get_skeleton=False):
+        """pointwarper.py:213-279 -> [xyz, joints_warped_rel, (weighted_G_tw), (joints_warped, bones)].
+        The per-point blend and transform run in ``apn_lbs_skin`` (weights taken as given)."""
+        if avg_procrustes:
+            raise NotImplementedError("avg_procrustes needs roma.special_procrustes (out of scope)")
+        bone_Ts, global_t, joints_rel = self.pose(joints, t, rot_params, global_t)
+        xyz, G = lbs_apply(self.canonical_pcd, weights, bone_Ts, global_t, get_frames=get_frames)
+        out = [xyz, joints_rel]
+        if get_frames:
+            out.append(G)
+        if get_skeleton:
+            out.append(joints_rel + global_t)
+            out.append(self.bones)
+        return out
+
+
+def lbs_apply(pcd, weights, bone_Ts, global_t, get_frames=False):
+    """Blend + apply with given per-point weights (HIP); returns (xyz [N,3], G [N,4,4] or None)."""
+    L.require_cuda(pcd, weights, bone_Ts, what="PointWarper.forward")
+    N, J = weights.shape
+    dev = pcd.device
+    xyz = torch.empty(N, 3, device=dev)
+    G = torch.empty(N, 4, 4, device=dev) if get_frames else None
+    bbox = torch.empty(8, dtype=torch.int32, device=dev)
+    T34 = bone_Ts[:, :3, :].detach().float().reshape(J, 12).contiguous()
+    gt = global_t.detach().float().reshape(3).contiguous()
+    w = weights.detach().float().contiguous()
+    call("apn_lbs_skin", ptr(pcd.contiguous()), ptr(w), N, J, None, 0.0, None, ptr(T34), ptr(gt), None, None, None,
+         None, 0.0, 1, ptr(xyz), None, ptr(G), None, None, ptr(bbox), stream_ptr(dev))
+    return xyz, G

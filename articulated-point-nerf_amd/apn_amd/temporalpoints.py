@@ -1,0 +1,406 @@
+"""TemporalPoints with the reference's constructor, ``forward()``, ``repose()``,
+``get_weights()``, ``sample_ray()`` signatures and return dicts (lib/temporalpoints.py),
+rendering through the fused HIP pipeline of libapn_hip.so:
+
+    skeleton stage (torch, J-sized) -> apn_lbs_skin -> apn_grid_build -> apn_inbbox_count/fill
+    -> apn_knn_radius -> apn_point_mlp -> apn_composite
+
+One forward renders any number of rays in a single pass (the reference's 8192-ray chunking
+is bit-identical to a single pass), so LBS, the 4x4 inverse and the kNN grid
+are built once per call instead of once per chunk.
+"""
+from __future__ import annotations
+
+import colorsys
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from ._lib import call, ptr, stream_ptr
+from .ops import Workspace, pack_mlp_weights
+from .pointwarper import PointWarper
+from .tineuvox import poc_fre
+
+CELL_CAP = 1 << 20
+
+
+class NoPointsException(Exception):
+    """temporalpoints.py:26-28."""
+
+
+def hls_palette(n, h=0.01, l=0.6, s=0.65):
+    """seaborn.color_palette('hls', n) (temporalpoints.py:692)."""
+    hues = np.linspace(0, 1, n + 1)[:-1]
+    hues += h
+    hues %= 1
+    hues -= hues.astype(int)
+    return [colorsys.hls_to_rgb(x, l, s) for x in hues]
+
+
+def project_point_to_image_plane(points, pose, intrinsic):
+    """utils.py:435-450."""
+    points = torch.repeat_interleave(points.unsqueeze(0), len(pose), 0)
+    pose = pose.inverse()
+    points = torch.bmm(pose[:, :3, :3], points.transpose(1, 2)).transpose(1, 2) + pose[:, :3, 3:].transpose(1, 2)
+    points = torch.bmm(intrinsic, points.transpose(1, 2)).transpose(1, 2)
+    return points[:, :, :2] / points[:, :, 2:]
+
+
+def _bone_distances(p, a, b):
+    """Point-to-segment distances [B, N] (temporalpoints.py:206-233)."""
+    s = b - a
+    w = p[None, :, :] - a[:, None, :]
+    ps = (w * s[:, None, :]).sum(-1)
+    l2 = (s * s).sum(-1)
+    d_lo = torch.norm(w, dim=-1)
+    d_hi = torch.norm(p[None, :, :] - b[:, None, :], dim=-1)
+    proj = a[:, None, :] + (ps / l2[:, None]).unsqueeze(-1) * s[:, None, :]
+    d_in = torch.norm(p[None, :, :] - proj, dim=-1)
+    lower = ps <= 0
+    upper = (~lower) & (ps >= l2[:, None])
+    return torch.where(lower, d_lo, torch.where(upper, d_hi, d_in))
+
+
+class TemporalPoints(torch.nn.Module):
+    def __init__(self, canonical_pcd, canonical_alpha, canonical_feat, canonical_rgbs, skeleton_pcd, joints, bones,
+                 xyz_min, xyz_max, tineuvox, neighbours=8, timebase_pe=8, eps=1e-6, stepsize=None, voxel_size=None,
+                 fast_color_thres=0, embedding='full', frozen_view_dir=None, over_parameterized_rot=True,
+                 re_init_feat=False, re_init_mlps=False, feat_depth=4, pose_embedding_dim=0, **kwargs):
+        super().__init__()
+        canonical_pcd = torch.as_tensor(canonical_pcd).float()
+        joints = torch.as_tensor(joints)
+        self.register_buffer("canonical_pcd", canonical_pcd, persistent=False)
+        self.skeleton_pcd = skeleton_pcd
+        self.bones = bones
+        self.bone_arap_mask = torch.tensor(bones).reshape(-1)
+        self.register_buffer("xyz_min", torch.Tensor(np.asarray(xyz_min, dtype=np.float32)))
+        self.register_buffer("xyz_max", torch.Tensor(np.asarray(xyz_max, dtype=np.float32)))
+        self.eps = torch.tensor(eps)
+        self._eps = float(eps)
+        self.feat_depth = feat_depth
+        self.timebase_pe = timebase_pe
+        self.t_dim = 1 + timebase_pe * 2
+        self.stepsize = stepsize
+        self.voxel_size = voxel_size
+        self.fast_color_thres = fast_color_thres
+        self.embedding = embedding
+        self.over_parameterized_rot = over_parameterized_rot
+        self.joints_to_keep = None
+        self.forward_warp_t_dim = self.t_dim
+        self.weights = torch.nn.Parameter(self._weights_from_bones(joints.float(), bones, canonical_pcd))
+        self.forward_warp = PointWarper(canonical_pcd=canonical_pcd, t_dim=self.forward_warp_t_dim, joints=joints,
+                                        bones=bones, over_parameterized_rot=over_parameterized_rot)
+        self.original_joints = torch.nn.Parameter(joints.to(torch.float32), requires_grad=False)
+        self.joints = torch.nn.Parameter(joints.to(torch.float32))
+        self.canonical_feat = torch.nn.Parameter(torch.as_tensor(canonical_feat).float())
+        if re_init_feat:
+            self.canonical_feat.data = torch.randn_like(self.canonical_feat)
+        self.theta_weight = torch.nn.Parameter(torch.tensor([0.1]))
+        self.merging_dict = None
+        self.merging_mat = None
+        gammas = torch.ones(len(canonical_pcd))
+        self.gammas = torch.nn.Parameter(gammas + torch.randn_like(gammas) * 1e-2)
+        self.pruned_joints = torch.zeros(len(joints), dtype=bool)
+        self.register_buffer("flat_merging_rules", torch.arange(0, len(joints)))
+        self.register_buffer("sibling_merging_rules", torch.zeros(len(joints), dtype=bool))
+        self.canonical_rgbs = torch.nn.Parameter(torch.as_tensor(canonical_rgbs).float())
+        self.canonical_alpha = torch.nn.Parameter(torch.as_tensor(canonical_alpha).float())
+        self.direct_eps = torch.nn.Parameter(torch.tensor([0.05] * len(canonical_alpha)))
+        self.register_buffer("time_poc", torch.FloatTensor([(2 ** i) for i in range(timebase_pe)]))
+        self.neighbours = neighbours
+        if neighbours != 8:
+            raise NotImplementedError("the HIP kNN / MLP kernels are specialised for K=8 neighbours")
+        self._mmd = None  # mean_min_distance, computed on the device on first use (temporalpoints.py:104-111)
+        self.og_joint_distance = (self.original_joints[self.bone_arap_mask][0::2, :]
+                                  - self.original_joints[self.bone_arap_mask][1::2, :])
+        feat_in = self.canonical_feat.shape[-1] + 3 + 3 * tineuvox.posbase_pe * 2 + pose_embedding_dim
+        width = self.canonical_feat.shape[-1]
+        self.feat_net = torch.nn.Sequential(
+            torch.nn.Linear(feat_in, width), torch.nn.LeakyReLU(inplace=True),
+            *[torch.nn.Sequential(torch.nn.Linear(width, width), torch.nn.LeakyReLU(inplace=True))
+              for _ in range(feat_depth - 2)],
+            torch.nn.Linear(width, width), torch.nn.LeakyReLU(inplace=True))
+        self.rgbnet = tineuvox.rgbnet
+        self.densitynet = tineuvox.densitynet
+        self.timenet = tineuvox.timenet
+        if re_init_mlps:
+            for m in (self.rgbnet, self.densitynet, self.timenet):
+                m.apply(lambda x: x.reset_parameters() if hasattr(x, "reset_parameters") else None)
+        self.view_poc = tineuvox.view_poc
+        self.time_poc = tineuvox.time_poc
+        self.pos_poc = tineuvox.pos_poc
+        self.no_view_dir = tineuvox.no_view_dir
+        self.tineuvox = tineuvox
+        self.register_buffer("xyz_max_canonical", canonical_pcd.max(dim=0)[0])
+        self.register_buffer("xyz_min_canonical", canonical_pcd.min(dim=0)[0])
+        self.frozen_view_dir = frozen_view_dir
+        if frozen_view_dir is not None:
+            vemb = poc_fre(torch.as_tensor(frozen_view_dir).float(), self.view_poc)
+            self.viewdirs_emb = torch.nn.Parameter(vemb[None], requires_grad=False)
+        self.pose_embedding_dim = pose_embedding_dim
+        if pose_embedding_dim > 0:
+            pin = len(self.joints) * (3 * len(self.pos_poc) * 2 + 3)
+            self.pose_embedding_net = torch.nn.Sequential(
+                torch.nn.Linear(pin, pin // 2), torch.nn.LeakyReLU(inplace=True),
+                *[torch.nn.Sequential(torch.nn.Linear(pin // 2, pin // 2), torch.nn.LeakyReLU(inplace=True))
+                  for _ in range(feat_depth - 2)],
+                torch.nn.Linear(pin // 2, pose_embedding_dim), torch.nn.LeakyReLU(inplace=True))
+        self.beta = torch.nn.Parameter(torch.tensor([0.5]))
+        self.beta_min = torch.nn.Parameter(torch.tensor([0.0001]), requires_grad=False)
+        self._ws = Workspace()
+        self._palette_cache = {}
+        self.timing = None          # set to {} to record HIP-event timings of the MLP launch
+        self.last_stats = {}
+
+    # ------------------------------------------------------------------ construction helpers
+    def _weights_from_bones(self, joints, bones, pcd, soft_weights=True):
+        """temporalpoints.py:235-254 with add_noise=True, noise_var=0, add_zero_weight=True."""
+        a = torch.stack([joints[b[0]] for b in bones])
+        b = torch.stack([joints[b[1]] for b in bones])
+        d = _bone_distances(pcd, a, b)
+        w = (1 / (0.5 * torch.e ** d + self.eps)).T.contiguous()
+        return torch.cat([torch.zeros((len(w), 1)), w], dim=-1)
+
+    def get_kwargs(self):
+        """temporalpoints.py:176-200."""
+        return {'canonical_pcd': self.canonical_pcd, 'skeleton_pcd': self.skeleton_pcd,
+                'canonical_alpha': self.canonical_alpha, 'canonical_feat': self.canonical_feat,
+                'canonical_rgbs': self.canonical_rgbs, 'joints': self.joints, 'bones': self.bones,
+                'neighbours': self.neighbours, 'timebase_pe': self.timebase_pe, 'eps': self.eps,
+                'stepsize': self.stepsize, 'weights': self.weights, 'xyz_min': self.xyz_min.cpu().numpy(),
+                'xyz_max': self.xyz_max.cpu().numpy(), 'tineuvox': self.tineuvox, 'voxel_size': self.voxel_size,
+                'fast_color_thres': self.fast_color_thres, 'embedding': self.embedding,
+                'frozen_view_dir': self.frozen_view_dir, 'over_parameterized_rot': self.over_parameterized_rot,
+                'feat_depth': self.feat_depth, 'pose_embedding_dim': self.pose_embedding_dim}
+
+    @property
+    def mean_min_distance(self):
+        """temporalpoints.py:104-111, computed with the HIP grid search (apn_nn1_distance)."""
+        if self._mmd is None or self._mmd.device != self.canonical_pcd.device:
+            pcd = self.canonical_pcd.contiguous()
+            L.require_cuda(pcd, what="mean_min_distance")
+            N, dev = pcd.shape[0], pcd.device
+            nn = torch.empty(N, device=dev)
+            sorted4 = torch.empty(N, 4, device=dev)
+            bbox = torch.empty(8, dtype=torch.int32, device=dev)
+            gws = torch.empty(int(L.load().apn_grid_workspace_bytes(N, CELL_CAP)), dtype=torch.uint8, device=dev)
+            call("apn_nn1_distance", ptr(pcd), N, self._eps, CELL_CAP, ptr(nn), ptr(sorted4), ptr(bbox), ptr(gws),
+                 stream_ptr(dev))
+            self._mmd = nn.double().mean().float()
+            self._mmd_f = float(self._mmd)
+        return self._mmd
+
+    # ------------------------------------------------------------------ reference API
+    def _merge_rules(self):
+        J = self.weights.shape[1]
+        if self.merging_mat is None:
+            return None
+        rules = self.flat_merging_rules.to(torch.int64)
+        if torch.equal(rules.cpu(), torch.arange(J)):
+            return None
+        return rules
+
+    def get_weights(self):
+        """temporalpoints.py:401-414: softmax(W / max(eps, theta)), columns merged by rule."""
+        th = torch.max(self.eps.to(self.theta_weight.device), self.theta_weight)
+        sm = torch.softmax(self.weights / th, dim=-1)
+        rules = self._merge_rules()
+        if rules is None:
+            return sm
+        out = torch.zeros_like(sm)
+        out.index_add_(1, rules.to(sm.device), sm)
+        return out
+
+    def repose(self, rot_params):
+        """temporalpoints.py:370-371 -> [xyz (N,3), joints_rel (J,3)] via the fused LBS kernel."""
+        bone_Ts, global_t, joints_rel = self.forward_warp.pose(self.joints, rot_params=rot_params)
+        xyz, _, _ = self._lbs(bone_Ts, global_t, records=False)
+        return [xyz, joints_rel]
+
+    def sample_ray(self, rays_o, rays_d, near, far, stepsize, xyz_min=None, xyz_max=None, **render_kwargs):
+        """temporalpoints.py:373-399 through the render_utils drop-in."""
+        from .ops import sample_pts_on_rays
+        xyz_min = self.xyz_min if xyz_min is None else xyz_min
+        xyz_max = self.xyz_max if xyz_max is None else xyz_max
+        pts, mask_out, ray_id, step_id, *_ = sample_pts_on_rays(rays_o.contiguous(), rays_d.contiguous(), xyz_min,
+                                                                xyz_max, near, far, stepsize * self.voxel_size)
+        m = ~mask_out
+        return pts[m], ray_id[m], step_id[m], m
+
+    # ------------------------------------------------------------------ fused pipeline
+    def _joint_colors(self, dev):
+        """Weight-visualisation colours per LBS column (temporalpoints.py:690-699): seaborn hls
+        palette over the columns with non-zero total weight, permuted by randperm(seed 0) on
+        the weights' device. Softmax weights are > 0, so those columns are the merge targets."""
+        rules = self._merge_rules()
+        J = self.weights.shape[1]
+        key = (str(dev), None if rules is None else tuple(rules.tolist()))
+        if key not in self._palette_cache:
+            wmask = torch.zeros(J, dtype=torch.bool)
+            if rules is None:
+                wmask[:] = True
+            else:
+                wmask[rules.cpu()] = True
+            m = int(wmask.sum())
+            cols = torch.tensor(hls_palette(m), dtype=torch.float64)
+            gen = torch.Generator(device=dev)
+            gen.manual_seed(0)
+            perm = torch.randperm(m, generator=gen, device=dev).cpu()
+            colors = torch.zeros(J, 3, dtype=torch.float64)
+            colors[torch.where(wmask)[0]] = cols[perm]
+            self._palette_cache[key] = colors.float().to(dev)
+        return self._palette_cache[key]
+
+    def _lbs(self, bone_Ts, global_t, records=True, colors=None):
+        pcd = self.canonical_pcd.contiguous()
+        L.require_cuda(pcd, self.weights, what="TemporalPoints")
+        N, J = self.weights.shape
+        dev = pcd.device
+        ws = self._ws
+        xyz = torch.empty(N, 3, device=dev)
+        wout = torch.empty(N, J, device=dev) if records else None
+        recA = ws.get("recA", N * 16, torch.float32, dev) if records else None
+        recB = ws.get("recB", N * 8, torch.float32, dev) if records else None
+        bbox = ws.get("bbox_ord", 8, torch.int32, dev)
+        T34 = bone_Ts[:, :3, :].detach().float().reshape(J, 12).contiguous()
+        gt = global_t.detach().float().reshape(3).contiguous()
+        rules = self._merge_rules()
+        rules32 = rules.to(device=dev, dtype=torch.int32).contiguous() if rules is not None else None
+        mmd = 0.0
+        if records:
+            self.mean_min_distance
+            mmd = self._mmd_f
+        call("apn_lbs_skin", ptr(pcd), ptr(self.weights.detach().contiguous()), N, J, ptr(self.theta_weight.detach()),
+             self._eps, ptr(rules32), ptr(T34), ptr(gt), ptr(colors),
+             ptr(self.canonical_alpha.detach().contiguous()) if records else None,
+             ptr(self.canonical_rgbs.detach().contiguous()) if records else None,
+             ptr(self.direct_eps.detach().contiguous()) if records else None, mmd, 0, ptr(xyz), ptr(wout), None,
+             ptr(recA), ptr(recB), ptr(bbox), stream_ptr(dev))
+        return xyz, wout, (recA, recB, bbox)
+
+    def _packed_weights(self, pose_embedding, dev):
+        layers = [self.feat_net[0], self.feat_net[2][0], self.feat_net[3][0], self.feat_net[4]]
+        if len(self.feat_net) != 6:
+            raise NotImplementedError("the fused MLP kernel implements feat_depth=4 (the reference default)")
+        from .ops import mlp_layout
+        buf = self._ws.get("mlp_w", mlp_layout()["TOTAL"], torch.float32, dev)
+        return pack_mlp_weights(layers, self.densitynet, self.rgbnet, pose_embedding, out=buf)
+
+    @torch.no_grad()
+    def forward(self, t, render_depth=False, render_kwargs=None, query_radius=0.01, render_weights=False,
+                rot_params=None, render_pcd_direct=False, poses=None, Ks=None, cam_per_ray=None, calc_min_max=True,
+                get_skeleton=False):
+        """temporalpoints.py:540-712."""
+        assert (t is None) ^ (rot_params is None)
+        dev = self.canonical_feat.device
+        L.require_cuda(self.canonical_feat, what="TemporalPoints.forward")
+        t_embed = poc_fre(t, self.time_poc) if rot_params is None else None
+        bone_Ts, global_t, joints_rel = self.forward_warp.pose(self.joints, t_embed, rot_params)
+        colors = self._joint_colors(dev) if render_weights else None
+        t_hat_pcd, weights, recs = self._lbs(bone_Ts, global_t, records=True, colors=colors)
+        self._last_weights = weights
+        delta_joint = (self.joints - joints_rel).clone().detach()
+        pose_embedding = (self.pose_embedding_net(poc_fre(delta_joint, self.pos_poc).view(1, -1))
+                          if self.pose_embedding_dim > 0 else None)
+        joints = bones = None
+        if get_skeleton:
+            joints = project_point_to_image_plane(joints_rel + global_t, poses.to(dev), Ks.to(dev, torch.float32))
+            bones = self.bones
+            if self.joints_to_keep is not None:
+                joints = joints[:, self.joints_to_keep]
+                bones = self.new_bones
+        R = len(render_kwargs['rays_o'])
+        try:
+            out = self._render(t_hat_pcd, recs, query_radius, render_kwargs, pose_embedding, calc_min_max)
+        except NoPointsException:
+            bg = render_kwargs['bg']
+            return {'rgb_marched': torch.ones(R, 3, device=dev) * bg,
+                    'rgb_marched_direct': torch.ones(R, 3, device=dev) * bg,
+                    'depth': torch.zeros(R, device=dev), 'weights': torch.ones(R, 3, device=dev) * bg,
+                    't_hat_pcd': t_hat_pcd, 'alphainv_last': None, 'grid': None, 'joints': joints, 'bones': bones}
+        rgb, rgb_d, depth, wvis, last, last_d = out
+        ret = {'t_hat_pcd': t_hat_pcd, 'rgb_marched': rgb, 'alphainv_last': last, 'alphainv_last_direct': last_d,
+               'grid': None, 'rgb_marched_direct': rgb_d, 'joints': joints, 'bones': bones}
+        if render_depth:
+            ret['depth'] = depth
+        if render_weights:
+            ret['weights'] = wvis
+        return ret
+
+    def _render(self, xyz, recs, query_radius, rk, pose_embedding, calc_min_max):
+        recA, recB, bbox_ord = recs
+        dev = xyz.device
+        lib = L.load()
+        ws = self._ws
+        s = stream_ptr(dev)
+        N = xyz.shape[0]
+        ro = rk['rays_o'].detach().float().contiguous()
+        rd = rk['rays_d'].detach().float().contiguous()
+        vd = rk['viewdirs'].detach().float().contiguous()
+        L.require_cuda(ro, rd, vd, what="render_kwargs")
+        R = ro.shape[0]
+        qr = float(query_radius)
+        stepdist = float(rk['stepsize']) * float(self.voxel_size)
+        interval = float(rk['stepsize']) * float(self.tineuvox.voxel_size_ratio)
+        bg = float(rk['bg'])
+        near, far = float(rk['near']), float(rk['far'])
+        # sampling bbox (temporalpoints.py:423-427)
+        if calc_min_max:
+            bbox6 = ws.get("bbox6", 6, torch.float32, dev)
+            call("apn_bbox_unpack", ptr(bbox_ord), qr, ptr(bbox6), s)
+        else:
+            bbox6 = torch.cat([self.xyz_min, self.xyz_max]).float().contiguous()
+        # kNN grid over the warped cloud
+        gws = ws.bytes("grid_ws", lib.apn_grid_workspace_bytes(N, CELL_CAP), dev)
+        sorted4 = ws.get("sorted4", N * 4, torch.float32, dev)
+        call("apn_grid_build", ptr(xyz), N, ptr(bbox_ord), qr, CELL_CAP, ptr(sorted4), ptr(gws), s)
+        # in-bbox samples
+        offs = ws.get("offs", R + 1, torch.int32, dev)
+        sws = ws.bytes("samp_ws", lib.apn_sample_pts_on_rays_workspace_bytes(R), dev)
+        call("apn_inbbox_count", ptr(ro), ptr(rd), ptr(bbox6), near, far, stepdist, R, ptr(offs), ptr(sws), s)
+        n_bbox = int(offs[R].item())
+        self.last_stats = {"rays": R, "inbbox_samples": n_bbox}
+        if n_bbox == 0:
+            raise NoPointsException("No points.")
+        q_pos = ws.get("q_pos", n_bbox * 4, torch.float32, dev)
+        q_ray = ws.get("q_ray", n_bbox, torch.int32, dev)
+        call("apn_inbbox_fill", ptr(ro), ptr(rd), ptr(bbox6), near, far, stepdist, R, ptr(offs), ptr(q_pos),
+             ptr(q_ray), s)
+        # radius kNN + compaction of survivors
+        s_pos = ws.get("s_pos", n_bbox * 4, torch.float32, dev)
+        s_ray = ws.get("s_ray", n_bbox, torch.int32, dev)
+        s_nbr = ws.get("s_nbr", n_bbox * 8, torch.int32, dev)
+        nsurv = ws.get("nsurv", 1, torch.int32, dev)
+        kws = ws.bytes("knn_ws", lib.apn_knn_workspace_bytes(n_bbox), dev)
+        call("apn_knn_radius", ptr(q_pos), ptr(q_ray), n_bbox, C.c_void_p(offs.data_ptr() + 4 * R), ptr(gws), N,
+             CELL_CAP, ptr(sorted4), qr, ptr(s_pos), ptr(s_ray), ptr(s_nbr), ptr(nsurv), ptr(kws), s)
+        S = int(nsurv.item())
+        self.last_stats["kept_samples"] = S
+        if S == 0:
+            raise NoPointsException("No points.")
+        # neighbour MLP + heads + direct blend
+        wbuf = self._packed_weights(pose_embedding, dev)
+        out12 = ws.get("out12", S * 12, torch.float32, dev)
+        feat = self.canonical_feat.detach().contiguous()
+        vemb = self.viewdirs_emb.detach().reshape(-1).float().contiguous() if self.frozen_view_dir is not None else None
+        if self.no_view_dir:
+            raise NotImplementedError("no_view_dir=True breaks the reference forward (viewdirs_emb_reshape undefined)")
+        if self.timing is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        call("apn_point_mlp", ptr(s_pos), ptr(s_ray), ptr(s_nbr), S, ptr(nsurv), ptr(recA), ptr(recB), ptr(feat),
+             feat.shape[1], ptr(vd), ptr(vemb), ptr(wbuf), self._eps, float(self.tineuvox.act_shift), interval, 0,
+             ptr(out12), s)
+        if self.timing is not None:
+            e1.record()
+            self.timing.setdefault("mlp_events", []).append((e0, e1, S))
+        # compositing
+        rgb = torch.empty(R, 3, device=dev); rgb_d = torch.empty(R, 3, device=dev)
+        depth = torch.empty(R, device=dev); wvis = torch.empty(R, 3, device=dev)
+        last = torch.empty(R, device=dev); last_d = torch.empty(R, device=dev)
+        rws = ws.get("ray_ws", 2 * R, torch.int32, dev)
+        call("apn_composite", ptr(out12), ptr(s_pos), ptr(s_ray), S, ptr(nsurv), R, float(self.fast_color_thres), bg,
+             ptr(rgb), ptr(rgb_d), ptr(depth), ptr(wvis), ptr(last), ptr(last_d), ptr(rws), s)
+        return rgb, rgb_d, depth, wvis, last, last_d

@@ -1,0 +1,89 @@
+// Per-ray compositing of the kept samples, one ray per thread (temporalpoints.py:611-710):
+//   pre-mask  alpha > fast_color_thres                         (611-626)
+//   Alphas2Weights: T_i = prod_{j<i}(1 - a_j), w_i = T_i a_i,    (629-632 -> render_utils_kernel.cu:430-459)
+//                   T updated in double, break once T < 1e-3 (the crossing sample is kept)
+//   post-mask w > fast_color_thres                             (634-651)
+//   segment sums: rgb (+ alphainv_last*bg), depth = sum w*step_id, weight-vis colour (+bg)
+// for the Point-NeRF path and, independently masked, the direct path (alpha_d, rgb_d).
+// Sequential per-ray accumulation in sample order reproduces segment_coo's sum order.
+#include "apn_common.h"
+
+namespace apn {
+
+__global__ void k_ray_bounds(const int* __restrict__ s_ray, const int* __restrict__ n_dev, int* __restrict__ beg,
+                             int* __restrict__ end) {
+  const int n = *n_dev;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int r = s_ray[i];
+  if (i == 0 || s_ray[i - 1] != r) beg[r] = i;
+  if (i == n - 1 || s_ray[i + 1] != r) end[r] = i + 1;
+}
+
+__global__ void k_composite(const float4* __restrict__ smp, const float4* __restrict__ s_pos,
+                            const int* __restrict__ beg, const int* __restrict__ end, int64_t n_rays, float thr,
+                            int use_mask, float bg, float* __restrict__ rgb_out, float* __restrict__ rgb_d_out,
+                            float* __restrict__ depth_out, float* __restrict__ wvis_out, float* __restrict__ last_out,
+                            float* __restrict__ last_d_out) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rays) return;
+  const int b = beg[r], e = end[r];
+  // Point-NeRF path
+  float T = 1.f, cr = 0.f, cg = 0.f, cb = 0.f, dep = 0.f, wr = 0.f, wg = 0.f, wb = 0.f;
+  for (int i = b; i < e; ++i) {
+    const float4 v = smp[3 * (size_t)i];
+    const float a = v.w;
+    if (use_mask && !(a > thr)) continue;
+    const float w = T * a;
+    if (!use_mask || w > thr) {
+      cr += w * v.x; cg += w * v.y; cb += w * v.z;
+      dep += w * (float)__float_as_int(s_pos[i].w);
+      const float4 c = smp[3 * (size_t)i + 2];
+      wr += w * c.x; wg += w * c.y; wb += w * c.z;
+    }
+    T = (float)((double)T * (1.0 - (double)a));
+    if ((double)T < 1e-3) break;
+  }
+  rgb_out[3 * r] = cr + T * bg; rgb_out[3 * r + 1] = cg + T * bg; rgb_out[3 * r + 2] = cb + T * bg;
+  depth_out[r] = dep;
+  wvis_out[3 * r] = wr + T * bg; wvis_out[3 * r + 1] = wg + T * bg; wvis_out[3 * r + 2] = wb + T * bg;
+  last_out[r] = T;
+  // direct path
+  float Td = 1.f, dr = 0.f, dg = 0.f, db = 0.f;
+  for (int i = b; i < e; ++i) {
+    const float4 v = smp[3 * (size_t)i + 1];
+    const float a = v.w;
+    if (use_mask && !(a > thr)) continue;
+    const float w = Td * a;
+    if (!use_mask || w > thr) { dr += w * v.x; dg += w * v.y; db += w * v.z; }
+    Td = (float)((double)Td * (1.0 - (double)a));
+    if ((double)Td < 1e-3) break;
+  }
+  rgb_d_out[3 * r] = dr + Td * bg; rgb_d_out[3 * r + 1] = dg + Td * bg; rgb_d_out[3 * r + 2] = db + Td * bg;
+  last_d_out[r] = Td;
+}
+
+}  // namespace apn
+
+using namespace apn;
+
+// ray_ws: 2 * n_rays int32 scratch (segment bounds).
+extern "C" int apn_composite(const float* smp12, const float* s_pos4, const int32_t* s_ray, int64_t max_samples,
+                             const int32_t* n_samples_dev, int64_t n_rays, float fast_color_thres, float bg,
+                             float* rgb_marched, float* rgb_marched_direct, float* depth, float* weights_vis,
+                             float* alphainv_last, float* alphainv_last_direct, int32_t* ray_ws, void* stream) {
+  if (n_rays <= 0 || !ray_ws || !rgb_marched || !rgb_marched_direct || !depth || !weights_vis || !alphainv_last ||
+      !alphainv_last_direct)
+    return APN_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  int* beg = ray_ws;
+  int* end = ray_ws + n_rays;
+  APN_HIP_TRY(hipMemsetAsync(ray_ws, 0, (size_t)n_rays * 2 * sizeof(int), s));
+  if (max_samples > 0)
+    hipLaunchKernelGGL(k_ray_bounds, dim3(ceil_div(max_samples, 256)), dim3(256), 0, s, s_ray, n_samples_dev, beg,
+                       end);
+  hipLaunchKernelGGL(k_composite, dim3(ceil_div(n_rays, 256)), dim3(256), 0, s, (const float4*)smp12,
+                     (const float4*)s_pos4, beg, end, n_rays, fast_color_thres, fast_color_thres > 0.f ? 1 : 0, bg,
+                     rgb_marched, rgb_marched_direct, depth, weights_vis, alphainv_last, alphainv_last_direct);
+  return launch_status();
+}

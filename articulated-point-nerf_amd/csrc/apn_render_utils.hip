@@ -1,0 +1,300 @@
+// Ray sampling and compositing ops: the drop-in for the reference's `render_utils_cuda`
+// module (lib/cuda/render_utils.cpp:144-155) plus the fused-pipeline sampling stage.
+//
+// Index-producing arithmetic follows render_utils_kernel.cu op-for-op and this file is
+// compiled with -ffp-contract=off, so ray_id / step_id / in-bbox masks / sample positions
+// are bit-identical to the CPU oracle (oracle/apn_oracle.py).
+#include "apn_common.h"
+
+namespace apn {
+
+struct RayGeom {
+  float sx, sy, sz;   // start = o + d * t_min
+  float dx, dy, dz;   // normalised direction
+  int n;              // number of steps (>= 1)
+};
+
+// render_utils_kernel.cu:11-73 for one ray.
+__device__ __forceinline__ RayGeom ray_geom(const float* __restrict__ o3, const float* __restrict__ d3,
+                                            const float lo[3], const float hi[3], float near, float far,
+                                            float stepdist, float* tmin_out = nullptr,
+                                            float* tmax_out = nullptr) {
+  const float ox = o3[0], oy = o3[1], oz = o3[2];
+  const float rdx = d3[0], rdy = d3[1], rdz = d3[2];
+  const float vx = (rdx == 0.f) ? 1e-6f : rdx;
+  const float vy = (rdy == 0.f) ? 1e-6f : rdy;
+  const float vz = (rdz == 0.f) ? 1e-6f : rdz;
+  const float ax = (hi[0] - ox) / vx, ay = (hi[1] - oy) / vy, az = (hi[2] - oz) / vz;
+  const float bx = (lo[0] - ox) / vx, by = (lo[1] - oy) / vy, bz = (lo[2] - oz) / vz;
+  const float tmin = fmaxf(fminf(fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz)), far), near);
+  const float tmax = fmaxf(fminf(fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz)), far), near);
+  if (tmin_out) *tmin_out = tmin;
+  if (tmax_out) *tmax_out = tmax;
+  const float q = ceilf((tmax - tmin) / stepdist);
+  RayGeom g;
+  g.n = q > 1.f ? (int)q : 1;
+  const float rn = sqrtf((rdx * rdx + rdy * rdy) + rdz * rdz);
+  g.sx = ox + rdx * tmin; g.sy = oy + rdy * tmin; g.sz = oz + rdz * tmin;
+  g.dx = rdx / rn; g.dy = rdy / rn; g.dz = rdz / rn;
+  return g;
+}
+
+__device__ __forceinline__ bool sample_at(const RayGeom& g, int k, float stepdist, const float lo[3],
+                                          const float hi[3], float& px, float& py, float& pz) {
+  const float dist = stepdist * (float)k;
+  px = g.sx + g.dx * dist; py = g.sy + g.dy * dist; pz = g.sz + g.dz * dist;
+  const bool out = (lo[0] > px) | (lo[1] > py) | (lo[2] > pz) | (hi[0] < px) | (hi[1] < py) | (hi[2] < pz);
+  return !out;
+}
+
+// ---------------------------------------------------------------- reference-mirror ops
+__global__ void k_sample_count(const float* __restrict__ ro, const float* __restrict__ rd,
+                               const float* __restrict__ xyz_min, const float* __restrict__ xyz_max,
+                               float near, float far, float stepdist, int64_t n_rays,
+                               float* __restrict__ t_min, float* __restrict__ t_max,
+                               int64_t* __restrict__ n_steps, int* __restrict__ cnt) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rays) return;
+  const float lo[3] = {xyz_min[0], xyz_min[1], xyz_min[2]};
+  const float hi[3] = {xyz_max[0], xyz_max[1], xyz_max[2]};
+  float a, b;
+  RayGeom g = ray_geom(ro + 3 * r, rd + 3 * r, lo, hi, near, far, stepdist, &a, &b);
+  t_min[r] = a; t_max[r] = b;
+  n_steps[r] = g.n;
+  cnt[r] = g.n;
+}
+
+__global__ void k_sample_fill(const float* __restrict__ ro, const float* __restrict__ rd,
+                              const float* __restrict__ xyz_min, const float* __restrict__ xyz_max,
+                              float near, float far, float stepdist, int64_t n_rays,
+                              const int* __restrict__ off, float* __restrict__ pts,
+                              uint8_t* __restrict__ mask_out, int64_t* __restrict__ ray_id,
+                              int64_t* __restrict__ step_id) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rays) return;
+  const float lo[3] = {xyz_min[0], xyz_min[1], xyz_min[2]};
+  const float hi[3] = {xyz_max[0], xyz_max[1], xyz_max[2]};
+  RayGeom g = ray_geom(ro + 3 * r, rd + 3 * r, lo, hi, near, far, stepdist);
+  const int64_t base = off[r];
+  for (int k = 0; k < g.n; ++k) {
+    float px, py, pz;
+    bool in = sample_at(g, k, stepdist, lo, hi, px, py, pz);
+    const int64_t i = base + k;
+    pts[3 * i] = px; pts[3 * i + 1] = py; pts[3 * i + 2] = pz;
+    mask_out[i] = in ? 0 : 1;
+    ray_id[i] = r;
+    step_id[i] = k;
+  }
+}
+
+// render_utils_kernel.cu:357-393
+__global__ void k_raw2alpha(const float* __restrict__ density, float shift, float interval, int64_t n,
+                            float* __restrict__ exp_d, float* __restrict__ alpha) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float e = expf(density[i] + shift);
+  exp_d[i] = e;
+  alpha[i] = 1.f - powf(1.f + e, -interval);
+}
+
+// render_utils_kernel.cu:461-471 + host fix at 489 (i_end of the last ray = n_pts)
+__global__ void k_segment_bounds(const int64_t* __restrict__ ray_id, int64_t n, int64_t* __restrict__ i_start,
+                                 int64_t* __restrict__ i_end) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (i > 0 && ray_id[i] != ray_id[i - 1]) {
+    i_start[ray_id[i]] = i;
+    i_end[ray_id[i - 1]] = i;
+  }
+  if (i == n - 1) i_end[ray_id[i]] = n;
+}
+
+// render_utils_kernel.cu:430-459: one ray per thread, T_cum update in double.
+__global__ void k_alpha2weight(const float* __restrict__ alpha, int64_t n_rays, float* __restrict__ weight,
+                               float* __restrict__ T, float* __restrict__ last,
+                               const int64_t* __restrict__ i_start, int64_t* __restrict__ i_end) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rays) return;
+  const int64_t s = i_start[r], e = i_end[r];
+  float tc = 1.f;
+  int64_t i;
+  for (i = s; i < e; ++i) {
+    const float a = alpha[i];
+    T[i] = tc;
+    weight[i] = tc * a;
+    tc = (float)((double)tc * (1.0 - (double)a));
+    if ((double)tc < 1e-3) { ++i; break; }
+  }
+  i_end[r] = i;
+  last[r] = tc;
+}
+
+__global__ void k_a2w_init(int64_t n, int64_t n_rays, float* __restrict__ weight, float* __restrict__ T,
+                           float* __restrict__ last, int64_t* __restrict__ i_start, int64_t* __restrict__ i_end) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) { weight[i] = 0.f; T[i] = 1.f; }
+  if (i < n_rays) { last[i] = 1.f; i_start[i] = 0; i_end[i] = 0; }
+}
+
+// torch_scatter.segment_coo(reduce='sum') into a zero output, sequential per segment.
+__global__ void k_segment_sum(const float* __restrict__ src, int64_t C, int64_t n_out,
+                              const int64_t* __restrict__ i_start, const int64_t* __restrict__ i_end,
+                              float* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_out * C) return;
+  const int64_t r = t / C, c = t % C;
+  float acc = 0.f;
+  for (int64_t i = i_start[r]; i < i_end[r]; ++i) acc += src[i * C + c];
+  out[t] = acc;
+}
+
+__global__ void k_zero_i64(int64_t* p, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = 0;
+}
+
+// ---------------------------------------------------------------- fused pipeline sampling
+// bbox6 = {lo x,y,z, hi x,y,z} of the sampling box (apn_bbox_unpack or the model bbox).
+__global__ void k_inbbox_count(const float* __restrict__ ro, const float* __restrict__ rd,
+                               const float* __restrict__ bbox6, float near, float far,
+                               float stepdist, int64_t n_rays, int* __restrict__ cnt) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rays) return;
+  const float lo[3] = {bbox6[0], bbox6[1], bbox6[2]}, hi[3] = {bbox6[3], bbox6[4], bbox6[5]};
+  RayGeom g = ray_geom(ro + 3 * r, rd + 3 * r, lo, hi, near, far, stepdist);
+  int c = 0;
+  for (int k = 0; k < g.n; ++k) {
+    float px, py, pz;
+    c += sample_at(g, k, stepdist, lo, hi, px, py, pz) ? 1 : 0;
+  }
+  cnt[r] = c;
+}
+
+// q_pos[i] = (x, y, z, bits(step_id)); q_ray[i] = ray id. Sorted by ray, then step.
+__global__ void k_inbbox_fill(const float* __restrict__ ro, const float* __restrict__ rd,
+                              const float* __restrict__ bbox6, float near, float far,
+                              float stepdist, int64_t n_rays, const int* __restrict__ off,
+                              float4* __restrict__ q_pos, int* __restrict__ q_ray) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rays) return;
+  int o = off[r];
+  if (off[r + 1] == o) return;
+  const float lo[3] = {bbox6[0], bbox6[1], bbox6[2]}, hi[3] = {bbox6[3], bbox6[4], bbox6[5]};
+  RayGeom g = ray_geom(ro + 3 * r, rd + 3 * r, lo, hi, near, far, stepdist);
+  for (int k = 0; k < g.n; ++k) {
+    float px, py, pz;
+    if (sample_at(g, k, stepdist, lo, hi, px, py, pz)) {
+      q_pos[o] = make_float4(px, py, pz, __int_as_float(k));
+      q_ray[o] = (int)r;
+      ++o;
+    }
+  }
+}
+
+// bbox_ord: ordered-int encoded [min x,y,z, max x,y,z] of the warped cloud (apn_lbs.hip);
+// padded by query_radius exactly as temporalpoints.py:424 (float32 subtract / add).
+__global__ void k_bbox_unpack(const int* __restrict__ bbox_ord, float qr, float* __restrict__ out6) {
+  if (threadIdx.x < 3) out6[threadIdx.x] = ordered_to_float(bbox_ord[threadIdx.x]) - qr;
+  else if (threadIdx.x < 6) out6[threadIdx.x] = ordered_to_float(bbox_ord[threadIdx.x]) + qr;
+}
+
+}  // namespace apn
+
+using namespace apn;
+
+// ---------------------------------------------------------------- C-ABI
+extern "C" int apn_sample_pts_on_rays_count(const float* rays_o, const float* rays_d, const float* xyz_min,
+                                            const float* xyz_max, float near, float far, float stepdist,
+                                            int64_t n_rays, float* t_min, float* t_max, int64_t* n_steps,
+                                            int32_t* offsets, void* workspace, void* stream) {
+  if (n_rays < 0 || !offsets || (n_rays > 0 && (!rays_o || !rays_d || !xyz_min || !xyz_max))) return APN_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  if (n_rays == 0) return scan_exclusive_i32(nullptr, offsets, 0, workspace, s);
+  // counts are staged in offsets[] itself? no: scan needs a separate input -> use the tail of workspace
+  int* cnt = (int*)((char*)workspace + scan_workspace_bytes(n_rays));
+  hipLaunchKernelGGL(k_sample_count, dim3(ceil_div(n_rays, 256)), dim3(256), 0, s, rays_o, rays_d, xyz_min,
+                     xyz_max, near, far, stepdist, n_rays, t_min, t_max, n_steps, cnt);
+  if (launch_status()) return APN_ERR_HIP;
+  return scan_exclusive_i32(cnt, offsets, n_rays, workspace, s);
+}
+
+extern "C" size_t apn_sample_pts_on_rays_workspace_bytes(int64_t n_rays) {
+  return scan_workspace_bytes(n_rays) + (size_t)(n_rays + 1) * sizeof(int);
+}
+
+extern "C" int apn_sample_pts_on_rays_fill(const float* rays_o, const float* rays_d, const float* xyz_min,
+                                           const float* xyz_max, float near, float far, float stepdist,
+                                           int64_t n_rays, const int32_t* offsets, float* rays_pts,
+                                           uint8_t* mask_outbbox, int64_t* ray_id, int64_t* step_id,
+                                           void* stream) {
+  if (n_rays <= 0) return APN_OK;
+  hipLaunchKernelGGL(k_sample_fill, dim3(ceil_div(n_rays, 256)), dim3(256), 0, (hipStream_t)stream, rays_o,
+                     rays_d, xyz_min, xyz_max, near, far, stepdist, n_rays, offsets, rays_pts, mask_outbbox,
+                     ray_id, step_id);
+  return launch_status();
+}
+
+extern "C" int apn_raw2alpha(const float* density, float shift, float interval, int64_t n_pts, float* exp_d,
+                             float* alpha, void* stream) {
+  if (n_pts < 0) return APN_ERR_ARG;
+  if (n_pts == 0) return APN_OK;
+  hipLaunchKernelGGL(k_raw2alpha, dim3(ceil_div(n_pts, 256)), dim3(256), 0, (hipStream_t)stream, density, shift,
+                     interval, n_pts, exp_d, alpha);
+  return launch_status();
+}
+
+extern "C" int apn_alpha2weight(const float* alpha, const int64_t* ray_id, int64_t n_pts, int64_t n_rays,
+                                float* weight, float* T, float* alphainv_last, int64_t* i_start, int64_t* i_end,
+                                void* stream) {
+  if (n_pts < 0 || n_rays < 0) return APN_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  int64_t m = n_pts > n_rays ? n_pts : n_rays;
+  if (m == 0) return APN_OK;
+  hipLaunchKernelGGL(k_a2w_init, dim3(ceil_div(m, 256)), dim3(256), 0, s, n_pts, n_rays, weight, T,
+                     alphainv_last, i_start, i_end);
+  if (n_pts == 0) return launch_status();
+  hipLaunchKernelGGL(k_segment_bounds, dim3(ceil_div(n_pts, 256)), dim3(256), 0, s, ray_id, n_pts, i_start, i_end);
+  hipLaunchKernelGGL(k_alpha2weight, dim3(ceil_div(n_rays, 256)), dim3(256), 0, s, alpha, n_rays, weight, T,
+                     alphainv_last, i_start, i_end);
+  return launch_status();
+}
+
+extern "C" int apn_segment_sum(const float* src, const int64_t* index, int64_t n_pts, int64_t channels,
+                               int64_t n_out, float* out, int64_t* seg_workspace, void* stream) {
+  if (n_pts < 0 || channels <= 0 || n_out < 0) return APN_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  if (n_out == 0) return APN_OK;
+  int64_t* i_start = seg_workspace;
+  int64_t* i_end = seg_workspace + n_out;
+  hipLaunchKernelGGL(k_zero_i64, dim3(ceil_div(2 * n_out, 256)), dim3(256), 0, s, seg_workspace, 2 * n_out);
+  if (n_pts > 0)
+    hipLaunchKernelGGL(k_segment_bounds, dim3(ceil_div(n_pts, 256)), dim3(256), 0, s, index, n_pts, i_start, i_end);
+  hipLaunchKernelGGL(k_segment_sum, dim3(ceil_div(n_out * channels, 256)), dim3(256), 0, s, src, channels, n_out,
+                     i_start, i_end, out);
+  return launch_status();
+}
+
+extern "C" int apn_inbbox_count(const float* rays_o, const float* rays_d, const float* bbox6, float near, float far,
+                                float stepdist, int64_t n_rays, int32_t* offsets, void* workspace, void* stream) {
+  if (n_rays <= 0) return APN_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  int* cnt = (int*)((char*)workspace + scan_workspace_bytes(n_rays));
+  hipLaunchKernelGGL(k_inbbox_count, dim3(ceil_div(n_rays, 256)), dim3(256), 0, s, rays_o, rays_d, bbox6, near,
+                     far, stepdist, n_rays, cnt);
+  if (launch_status()) return APN_ERR_HIP;
+  return scan_exclusive_i32(cnt, offsets, n_rays, workspace, s);
+}
+
+extern "C" int apn_inbbox_fill(const float* rays_o, const float* rays_d, const float* bbox6, float near, float far,
+                               float stepdist, int64_t n_rays, const int32_t* offsets, float* q_pos4, int32_t* q_ray,
+                               void* stream) {
+  if (n_rays <= 0) return APN_ERR_ARG;
+  hipLaunchKernelGGL(k_inbbox_fill, dim3(ceil_div(n_rays, 256)), dim3(256), 0, (hipStream_t)stream, rays_o, rays_d,
+                     bbox6, near, far, stepdist, n_rays, offsets, (float4*)q_pos4, q_ray);
+  return launch_status();
+}
+
+extern "C" int apn_bbox_unpack(const int32_t* bbox_ord, float query_radius, float* out6, void* stream) {
+  hipLaunchKernelGGL(k_bbox_unpack, dim3(1), dim3(64), 0, (hipStream_t)stream, bbox_ord, query_radius, out6);
+  return launch_status();
+}

@@ -1,0 +1,126 @@
+// Device-wide exclusive prefix sum of int32 counts (rays, grid cells, kNN blocks).
+// Three launches: per-block totals -> one-workgroup scan of the totals -> per-block scan.
+// Deterministic (no atomics), so every consumer sees the same offsets run to run.
+#include "apn_common.h"
+
+namespace apn {
+
+constexpr int SCAN_THREADS = 256;
+constexpr int SCAN_ITEMS = 8;
+constexpr int SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;  // 2048 elements per block
+
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+// Block-wide exclusive scan of one value per thread; returns exclusive prefix, *total set.
+__device__ __forceinline__ int block_excl_scan(int v, int* lds_waves, int* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int inc = wave_incl_scan(v);
+  if (lane == 63) lds_waves[wid] = inc;
+  __syncthreads();
+  int base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < SCAN_THREADS / 64; ++w) {
+    int x = lds_waves[w];
+    base += (w < wid) ? x : 0;
+    tot += x;
+  }
+  __syncthreads();
+  *total = tot;
+  return base + inc - v;
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void scan_block_totals(const int* __restrict__ in, int64_t n,
+                                                                  int* __restrict__ totals) {
+  __shared__ int lw[SCAN_THREADS / 64];
+  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_ITEMS;
+  int s = 0;
+#pragma unroll
+  for (int i = 0; i < SCAN_ITEMS; ++i) s += (base + i < n) ? in[base + i] : 0;
+  int tot;
+  block_excl_scan(s, lw, &tot);
+  if (threadIdx.x == 0) totals[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(1024) void scan_totals_single(int* __restrict__ totals, int nb) {
+  // exclusive scan in place over nb block totals, one workgroup, chunks of 1024
+  __shared__ int lw[16];
+  __shared__ int carry_s;
+  if (threadIdx.x == 0) carry_s = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int c = 0; c < nb; c += 1024) {
+    int i = c + threadIdx.x;
+    int v = i < nb ? totals[i] : 0;
+    int inc = wave_incl_scan(v);
+    if (lane == 63) lw[wid] = inc;
+    __syncthreads();
+    int base = 0, tot = 0;
+    for (int w = 0; w < 16; ++w) {
+      base += (w < wid) ? lw[w] : 0;
+      tot += lw[w];
+    }
+    int carry = carry_s;
+    if (i < nb) totals[i] = carry + base + inc - v;
+    __syncthreads();
+    if (threadIdx.x == 0) carry_s = carry + tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) totals[nb] = carry_s;
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void scan_block_apply(const int* __restrict__ in, int64_t n,
+                                                                 const int* __restrict__ totals,
+                                                                 int* __restrict__ out, int nb) {
+  __shared__ int lw[SCAN_THREADS / 64];
+  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_ITEMS;
+  int v[SCAN_ITEMS];
+  int s = 0;
+#pragma unroll
+  for (int i = 0; i < SCAN_ITEMS; ++i) {
+    v[i] = (base + i < n) ? in[base + i] : 0;
+    s += v[i];
+  }
+  int tot;
+  int run = block_excl_scan(s, lw, &tot) + totals[blockIdx.x];
+#pragma unroll
+  for (int i = 0; i < SCAN_ITEMS; ++i) {
+    if (base + i < n) out[base + i] = run;
+    run += v[i];
+  }
+  if (blockIdx.x == nb - 1 && threadIdx.x == 0) out[n] = totals[nb];
+}
+
+size_t scan_workspace_bytes(int64_t n) {
+  int64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+  return (size_t)(nb + 1) * sizeof(int);
+}
+
+int scan_exclusive_i32(const int* in, int* out, int64_t n, void* ws, hipStream_t s) {
+  if (n <= 0) {
+    APN_HIP_TRY(hipMemsetAsync(out, 0, sizeof(int), s));
+    return launch_status();
+  }
+  int nb = ceil_div(n, SCAN_TILE);
+  int* totals = (int*)ws;
+  hipLaunchKernelGGL(scan_block_totals, dim3(nb), dim3(SCAN_THREADS), 0, s, in, n, totals);
+  hipLaunchKernelGGL(scan_totals_single, dim3(1), dim3(1024), 0, s, totals, nb);
+  hipLaunchKernelGGL(scan_block_apply, dim3(nb), dim3(SCAN_THREADS), 0, s, in, n, totals, out, nb);
+  return launch_status();
+}
+
+}  // namespace apn
+
+extern "C" size_t apn_scan_workspace_bytes(int64_t n) { return apn::scan_workspace_bytes(n); }
+
+extern "C" int apn_scan_exclusive_i32(const int32_t* in, int32_t* out, int64_t n, void* workspace,
+                                      void* stream) {
+  return apn::scan_exclusive_i32(in, out, n, workspace, (hipStream_t)stream);
+}

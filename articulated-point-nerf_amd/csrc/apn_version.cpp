@@ -1,0 +1,3 @@
+// Library identification string (apn_version in include/apn_hip.h).
+#include "../../include/apn_hip.h"
+extern "C" const char* apn_version(void) { return "apn_hip 0.1 gfx950"; }

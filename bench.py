@@ -1,0 +1,184 @@
+"""Benchmark: rendered rays/s of the articulated-point render path on MI355X.
+
+Workload (BASELINE.json configs[1]): dnerf/jumpingjacks-like synthetic scene,
+800x800 rays, 300k canonical points, 24 bones (SMPL topology), t = 0.3, D-NeRF camera.
+A step = one full frame: TemporalPoints.forward over all 640k rays (skeleton, LBS, grid,
+sampling, radius kNN, neighbour MLP, compositing), inputs resident in HBM.
+
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process per GPU, each
+rank renders its own frame (different time t) per step -- frames are independent units, no
+data-path collective (weak scaling); the timing is barrier + synchronize bracketed and the
+max over ranks (RCCL all-reduce MAX of the elapsed time).
+
+Rank 0 prints ONE JSON line. Diagnostics go to stderr.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "articulated-point-nerf_amd"))
+sys.path.insert(0, ROOT)
+
+from apn_amd import harness, synthetic as S  # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
+HBM_PEAK_GBS = 8000.0
+
+
+def flop_per_kept_sample(d_in=191, width=128):
+    """K*2*(D_in*128 + 3*128^2) + 2*(128 + 128^2 + 155*64 + 64*3)."""
+    return 8 * 2 * (d_in * width + 3 * width * width) + 2 * (128 + 128 * 128 + 155 * 64 + 64 * 3)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(model, scene, rows, threads):
+    """The oracle (CPU restatement, pure PyTorch + scipy cKDTree kNN) on a bounded sample:
+    a band of ``rows`` image rows through the object centre of the same frame."""
+    from oracle.apn_oracle import OracleModel
+    torch.set_num_threads(threads)
+    st = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    orc = OracleModel(st, model.canonical_pcd.cpu(), model.bones, stepsize=S.STEPSIZE, voxel_size=S.VOXEL_SIZE,
+                      fast_color_thres=S.FAST_COLOR_THRES, pose_embedding_dim=model.pose_embedding_dim,
+                      act_shift=float(model.tineuvox.act_shift),
+                      voxel_size_ratio=float(model.tineuvox.voxel_size_ratio),
+                      mean_min_distance_value=float(model.mean_min_distance))
+    rk = scene.render_kwargs("cpu")
+    H, W = scene.cfg.H, scene.cfg.W
+    r0 = H // 2 - rows // 2
+    sub = dict(rk)
+    for k in ("rays_o", "rays_d", "viewdirs"):
+        sub[k] = rk[k][r0 * W:(r0 + rows) * W]
+    t = torch.tensor([scene.cfg.t])
+    orc.forward(t, render_depth=True, render_kwargs=sub, render_weights=True, knn_tree=True)  # warm-up
+    n_rep, t0 = 0, time.perf_counter()
+    while n_rep < 2 or time.perf_counter() - t0 < 10.0:
+        orc.forward(t, render_depth=True, render_kwargs=sub, render_weights=True, knn_tree=True)
+        n_rep += 1
+        if n_rep >= 6:
+            break
+    dt = (time.perf_counter() - t0) / n_rep
+    nrays = rows * W
+    return {"value": nrays / dt, "unit": "rays/s", "cores": threads, "kind": "port",
+            "sample": f"{rows} central rows x {W} = {nrays} rays of the same frame, {n_rep} timed frames "
+                      f"(oracle: torch-CPU MLP, scipy cKDTree kNN), {dt:.2f} s/band"}
+
+
+def read_traffic(path):
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--cpu-rows", type=int, default=16, help="image rows in the CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")   # RCCL over xGMI
+    dev = torch.device("cuda", local)
+
+    scene = S.make_scene(args.config)
+    # weak scaling: every rank renders its own frame time
+    scene.cfg.t = scene.cfg.t + 0.05 * rank
+    t_setup = time.perf_counter()
+    model = harness.build_model(scene, dev)
+    rk = scene.render_kwargs(dev)
+    R = rk["rays_o"].shape[0]
+    t_arg = torch.tensor([scene.cfg.t], device=dev)
+    _ = model.mean_min_distance
+    torch.cuda.synchronize(dev)
+    log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.2f}s, rays/frame {R}")
+
+    def step():
+        return model(t_arg, render_depth=True, render_kwargs=rk, render_weights=True,
+                     poses=scene.c2w[None].to(dev), Ks=scene.K[None].to(dev), get_skeleton=True)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    stats = dict(model.last_stats)
+    log(f"[rank {rank}] scene: {stats}")
+
+    model.timing = {}
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t)
+    ev = model.timing.get("mlp_events", [])
+    mlp_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / max(len(ev), 1)
+    S_kept = ev[-1][2] if ev else stats.get("kept_samples", 0)
+    model.timing = None
+
+    if rank != 0:
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
+
+    d_in = 191  # pose embedding folded into the bias for ZJU; F_alg still counts the reference D_in
+    if model.pose_embedding_dim > 0:
+        d_in = 191 + model.pose_embedding_dim
+    flop = S_kept * flop_per_kept_sample(d_in)
+    achieved = flop / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else 0.0
+    traffic = read_traffic(os.path.join(ROOT, "profiles", "r01_point_mlp_traffic.json"))
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * args.steps * R / elapsed
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(model, scene, args.cpu_rows, torch.get_num_threads())
+        except Exception as e:  # never lose the GPU line over the baseline leg
+            log(f"cpu baseline failed: {e!r}")
+    line = {
+        "metric": "rendered rays/sec at 800x800, 300k pts, 24 bones",
+        "value": value, "unit": "rays/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "fp32", "data": "synthetic (procedural SMPL-24 capsule cloud, random-init networks)",
+        "config": {"workload": S.CONFIGS[args.config].name + f" ({args.config})", "rays_per_frame": R,
+                   "points": scene.cfg.N, "bones": scene.cfg.J, "inbbox_samples": stats.get("inbbox_samples"),
+                   "kept_samples": S_kept, "parallelism": f"frames x{world}" if world > 1 else "single"},
+        "roofline": {"bound": "mfma", "kernel": "k_point_mlp", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
+                     "traffic": traffic.get("bytes_per_launch") if traffic else None,
+                     "flop_per_launch": flop, "avg_launch_ms": mlp_ms},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,146 @@
+/*
+ * apn_hip.h -- C-ABI of libapn_hip.so, the MI355X (gfx950) implementation of the
+ * articulated-point render/deform hot path of Articulated-Point-NeRF.
+ *
+ * Conventions
+ *   - every pointer is a device pointer unless noted; arrays are dense row-major;
+ *   - `stream` is a hipStream_t passed as void* (the caller's current stream);
+ *   - functions only enqueue work (no host synchronisation) and return APN_OK or an error
+ *     code; APN_ERR_ARG = invalid shape/pointer (the reference raises RuntimeError via
+ *     TORCH_CHECK / assert, render_utils.cpp:40-42), APN_ERR_HIP = launch failure;
+ *   - scratch memory is caller-provided (`*_workspace_bytes` queries), outputs are
+ *     caller-allocated: no allocation happens inside the library.
+ * Reference locations are relative to the reference repository root.
+ */
+#ifndef APN_HIP_H
+#define APN_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define APN_OK 0
+#define APN_ERR_ARG 1
+#define APN_ERR_HIP 2
+
+/* ---------------------------------------------------------------------------------------
+ * Drop-in for the `render_utils_cuda` pybind module (lib/cuda/render_utils.cpp:144-155).
+ * ------------------------------------------------------------------------------------- */
+
+/* sample_pts_on_rays (render_utils.cpp:67-78, render_utils_kernel.cu:190-236), phase 1:
+ * per-ray t_min/t_max/N_steps and the exclusive prefix sum of N_steps in offsets[0..n_rays]
+ * (offsets[n_rays] = total_len). The caller reads total_len, allocates, then calls _fill. */
+size_t apn_sample_pts_on_rays_workspace_bytes(int64_t n_rays);
+int apn_sample_pts_on_rays_count(const float* rays_o, const float* rays_d, const float* xyz_min,
+                                 const float* xyz_max, float near, float far, float stepdist,
+                                 int64_t n_rays, float* t_min, float* t_max, int64_t* n_steps,
+                                 int32_t* offsets, void* workspace, void* stream);
+/* phase 2: rays_pts [total_len,3], mask_outbbox [total_len] (1 = outside), ray_id, step_id. */
+int apn_sample_pts_on_rays_fill(const float* rays_o, const float* rays_d, const float* xyz_min,
+                                const float* xyz_max, float near, float far, float stepdist,
+                                int64_t n_rays, const int32_t* offsets, float* rays_pts,
+                                uint8_t* mask_outbbox, int64_t* ray_id, int64_t* step_id, void* stream);
+
+/* raw2alpha (render_utils.cpp:80-85, render_utils_kernel.cu:357-393):
+ * exp_d = exp(density + shift); alpha = 1 - (1 + exp_d)^(-interval). */
+int apn_raw2alpha(const float* density, float shift, float interval, int64_t n_pts, float* exp_d,
+                  float* alpha, void* stream);
+
+/* alpha2weight (render_utils.cpp:95-102, render_utils_kernel.cu:430-505); ray_id sorted. */
+int apn_alpha2weight(const float* alpha, const int64_t* ray_id, int64_t n_pts, int64_t n_rays,
+                     float* weight, float* T, float* alphainv_last, int64_t* i_start, int64_t* i_end,
+                     void* stream);
+
+/* torch_scatter.segment_coo(src, index, out=zeros(n_out, C), reduce='sum')
+ * (temporalpoints.py:653-677); index sorted; seg_workspace: 2*n_out int64. */
+int apn_segment_sum(const float* src, const int64_t* index, int64_t n_pts, int64_t channels,
+                    int64_t n_out, float* out, int64_t* seg_workspace, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Fused render pipeline stages (TemporalPoints.forward, temporalpoints.py:540-712).
+ * ------------------------------------------------------------------------------------- */
+
+/* LBS skinning: get_weights (temporalpoints.py:401-414) + PointWarper blend/apply
+ * (pointwarper.py:241-266) + torch.inverse(G)[:3,:3] (temporalpoints.py:569) + per-point
+ * records for the kNN/MLP stages + bbox of the warped cloud (temporalpoints.py:424).
+ *   bone_T34 [J,12]: rows 0..2 of each bone 4x4; merge_rules [J] int32 or NULL (identity);
+ *   joint_colors [J,3] or NULL; weights_out [N,J] or NULL;
+ *   recA16 [N,16] = {x,y,z, 2*(mmd*max(eps_n,0))^2+1e-12, Rinv(9), clip(alpha), 0,0};
+ *   recB8 [N,8] = {clip(rgb), 0, sum_j col_j w_j, 0}; bbox_ord [6] ordered-int min/max. */
+int apn_lbs_skin(const float* canonical_pcd, const float* raw_weights, int64_t n_points,
+                 int32_t n_joints, const float* theta_weight, float eps, const int32_t* merge_rules,
+                 const float* bone_T34, const float* global_t, const float* joint_colors,
+                 const float* canonical_alpha, const float* canonical_rgbs, const float* direct_eps,
+                 float mean_min_distance, int32_t weights_final, float* xyz_out, float* weights_out,
+                 float* G_out, float* recA16, float* recB8, int32_t* bbox_ord, void* stream);
+/* weights_final = 1: raw_weights already are the per-point LBS weights (PointWarper.forward
+ * input, pointwarper.py:213) -- softmax/merge skipped. G_out [N,16] (weighted_G_tw) or NULL. */
+
+/* Padded sampling bbox = bbox_ord -/+ query_radius (temporalpoints.py:424) as 6 floats. */
+int apn_bbox_unpack(const int32_t* bbox_ord, float query_radius, float* out6, void* stream);
+
+/* In-bbox ray samples (sample_ray, temporalpoints.py:373-399, with the boolean compaction
+ * done on device): per-ray counts -> offsets [n_rays+1]; then q_pos4 {x,y,z,bits(step)},
+ * q_ray, sorted by (ray, step). bbox6 = {lo xyz, hi xyz} (device).
+ * Workspace: apn_sample_pts_on_rays_workspace_bytes. */
+int apn_inbbox_count(const float* rays_o, const float* rays_d, const float* bbox6, float near,
+                     float far, float stepdist, int64_t n_rays, int32_t* offsets, void* workspace,
+                     void* stream);
+int apn_inbbox_fill(const float* rays_o, const float* rays_d, const float* bbox6, float near,
+                    float far, float stepdist, int64_t n_rays, const int32_t* offsets,
+                    float* q_pos4, int32_t* q_ray, void* stream);
+
+/* Uniform grid over the warped cloud (cell >= sqrt(query_radius)): counting sort into
+ * sorted_pts4 [N,4] {x,y,z,bits(idx)}. cell_cap bounds the number of cells. */
+size_t apn_grid_workspace_bytes(int64_t n_points, int32_t cell_cap);
+int apn_grid_build(const float* xyz, int64_t n_points, const int32_t* bbox_ord, float query_radius,
+                   int32_t cell_cap, float* sorted_pts4, void* workspace, void* stream);
+
+/* Radius-bounded exact kNN (K=8), replacing pykeops Kmin_argKmin + the radius filter
+ * (temporalpoints.py:433-447): survivors (8th-NN squared distance <= query_radius) in
+ * query order -> s_pos4, s_ray, s_nbr [S,8]; S written to *n_survivors_dev. */
+size_t apn_knn_workspace_bytes(int64_t n_queries);
+int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t n_queries,
+                   const int32_t* n_queries_dev, const void* grid_workspace, int64_t n_points,
+                   int32_t cell_cap, const float* sorted_pts4, float query_radius, float* s_pos4,
+                   int32_t* s_ray, int32_t* s_nbr, int32_t* n_survivors_dev, void* workspace,
+                   void* stream);
+
+/* mean_min_distance support (temporalpoints.py:104-111): per-point sqrt(d2_nn + eps) to the
+ * nearest other point. Uses grid_workspace/sorted_pts4/bbox_ord as scratch. */
+int apn_nn1_distance(const float* xyz, int64_t n_points, float eps, int32_t cell_cap, float* nn_dist,
+                     float* sorted_pts4, int32_t* bbox_ord, void* grid_workspace, void* stream);
+
+/* Packed MLP weight layout: writes 19 int32 offsets (W1,B1,W2,B2,W3,B3,W4,B4,WD,BD,WF,BF,
+ * WV0,BV0,WV2,BV2,TOTAL,K1,KV) and returns their count. */
+int apn_mlp_weight_layout(int32_t* offsets);
+
+/* Fused neighbour MLP + heads + direct blend (temporalpoints.py:452-519) for the kept
+ * samples; out12 [S,12] = {r,g,b,alpha, r_d,g_d,b_d,alpha_d, wr,wg,wb,0}. feat_dim must be
+ * 128. vemb_const [27] (frozen_view_dir) or NULL to embed viewdirs[ray]. */
+int apn_point_mlp(const float* s_pos4, const int32_t* s_ray, const int32_t* s_nbr,
+                  int64_t max_samples, const int32_t* n_samples_dev, const float* recA16,
+                  const float* recB8, const float* canonical_feat, int32_t feat_dim,
+                  const float* viewdirs, const float* vemb_const, const float* wbuf, float eps,
+                  float act_shift, float interval, int32_t grid_blocks, float* out12, void* stream);
+
+/* Masks + Alphas2Weights + segment sums for both paths (temporalpoints.py:611-710).
+ * ray_ws: 2*n_rays int32 scratch. */
+int apn_composite(const float* smp12, const float* s_pos4, const int32_t* s_ray,
+                  int64_t max_samples, const int32_t* n_samples_dev, int64_t n_rays,
+                  float fast_color_thres, float bg, float* rgb_marched, float* rgb_marched_direct,
+                  float* depth, float* weights_vis, float* alphainv_last,
+                  float* alphainv_last_direct, int32_t* ray_ws, void* stream);
+
+/* Utilities */
+size_t apn_scan_workspace_bytes(int64_t n);
+int apn_scan_exclusive_i32(const int32_t* in, int32_t* out, int64_t n, void* workspace, void* stream);
+const char* apn_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* APN_HIP_H */

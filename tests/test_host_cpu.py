@@ -1,0 +1,122 @@
+"""CPU-only checks of the product host side: the C-ABI library loads and exports every
+symbol include/apn_hip.h declares, the ctypes table matches the header, and the
+reference-shaped modules are state-dict compatible with the reference (golden fixtures)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from golden_io import CASES, Golden
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "apn_hip.h")
+
+
+def header_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(apn_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    from apn_amd import _lib
+    lib = _lib.load()
+    fns = header_functions()
+    assert len(fns) >= 20
+    for name in fns:
+        assert hasattr(lib, name), name
+    assert set(fns) == set(_lib.SIGNATURES), set(fns) ^ set(_lib.SIGNATURES)
+    assert lib.apn_version().startswith(b"apn_hip")
+
+
+def test_ctypes_arity_matches_header():
+    from apn_amd import _lib
+    txt = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    for name, (_, args) in _lib.SIGNATURES.items():
+        m = re.search(name + r"\s*\(([^;]*)\)\s*;", txt)
+        assert m, name
+        params = [p for p in m.group(1).split(",") if p.strip() and p.strip() != "void"]
+        assert len(params) == len(args), (name, len(params), len(args))
+
+
+def test_workspace_queries_need_no_gpu():
+    from apn_amd import _lib
+    lib = _lib.load()
+    assert lib.apn_scan_workspace_bytes(10_000) > 0
+    assert lib.apn_grid_workspace_bytes(300_000, 1 << 20) > 4 * (1 << 20)
+    assert lib.apn_knn_workspace_bytes(8_000_000) > 8_000_000 * 32
+    arr = (ctypes.c_int32 * 32)()
+    n = lib.apn_mlp_weight_layout(arr)
+    assert n == 19 and arr[17] == 192 and arr[18] == 160
+
+
+def test_invalid_arguments_rejected_without_gpu():
+    from apn_amd import _lib
+    lib = _lib.load()
+    assert lib.apn_point_mlp(*([None] * 3), 10, *([None] * 4), 64, *([None] * 3), 0.0, 0.0, 0.0, 0, None,
+                             None) == 1  # feat_dim != 128
+    assert lib.apn_lbs_skin(None, None, 0, 0, None, 0.0, None, None, None, None, None, None, None, 0.0, 0,
+                            None, None, None, None, None, None, None) == 1
+
+
+def test_missing_library_fails_loudly(monkeypatch):
+    from apn_amd import _lib
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "_load_error", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", "/nonexistent/libapn_hip.so")
+    with pytest.raises(RuntimeError):
+        _lib.load()
+
+
+def test_product_ops_refuse_cpu_tensors():
+    from apn_amd import render_utils
+    with pytest.raises(RuntimeError):
+        render_utils.raw2alpha(torch.zeros(4), -6.9, 0.5)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_state_dict_compatible_with_reference(name):
+    from model_io import model_from_golden
+    g = Golden(name)
+    model = model_from_golden(g, "cpu")
+    ours = model.state_dict()
+    for k, v in g.state().items():
+        assert k in ours, k
+        assert tuple(ours[k].shape) == tuple(v.shape), k
+        assert torch.equal(ours[k].float(), v.float()), k
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_constructor_lbs_weights_match_reference(name):
+    """_weights_from_bones (temporalpoints.py:235-254) reproduces the reference's init."""
+    from model_io import model_from_golden
+    g = Golden(name)
+    model = model_from_golden(g, "cpu")
+    w = model._weights_from_bones(g.t("joints") if "joints" in g.z else g.state()["joints"], g.bones,
+                                  g.t("in_canonical_pcd"))
+    assert (w - g.state()["weights"]).abs().max() < 1e-6
+
+
+def test_synthetic_scenes_satisfy_bone_invariant():
+    from apn_amd import synthetic as S
+    for J in (8, 24, 32, 48):
+        joints, bones = S.skeleton_for(J)
+        assert len(joints) == J and len(bones) == J - 1
+        for k, (p, c) in enumerate(bones):
+            assert c == k + 1 and 0 <= p < J and p != c
+    sc = S.make_scene("C1")
+    assert sc.ctor["canonical_pcd"].shape == (10_000, 3)
+    ro, rd, vd = sc.rays()
+    assert ro.shape == (64 * 64, 3) and torch.allclose(vd.norm(dim=-1), torch.ones(64 * 64))
+
+
+def test_get_rays_matches_synthetic_rays():
+    from apn_amd import synthetic as S
+    from apn_amd.tineuvox import get_rays_of_a_view
+    sc = S.make_scene("G2")
+    ro, rd, vd = get_rays_of_a_view(sc.cfg.H, sc.cfg.W, sc.K, sc.c2w, inverse_y=True)
+    ro2, rd2, vd2 = sc.rays()
+    assert torch.equal(rd.reshape(-1, 3), rd2) and torch.equal(vd.reshape(-1, 3), vd2)
