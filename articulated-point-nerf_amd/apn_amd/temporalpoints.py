@@ -128,9 +128,7 @@ class TemporalPoints(torch.nn.Module):
         if re_init_mlps:
             for m in (self.rgbnet, self.densitynet, self.timenet):
                 m.apply(lambda x: x.reset_parameters() if hasattr(x, "reset_parameters") else None)
-        self.view_poc = tineuvox.view_poc
-        self.time_poc = tineuvox.time_poc
-        self.pos_poc = tineuvox.pos_poc
+        self.time_poc = tineuvox.time_poc          # buffer (same values as the TiNeuVox one)
         self.no_view_dir = tineuvox.no_view_dir
         self.tineuvox = tineuvox
         self.register_buffer("xyz_max_canonical", canonical_pcd.max(dim=0)[0])
@@ -151,8 +149,19 @@ class TemporalPoints(torch.nn.Module):
         self.beta_min = torch.nn.Parameter(torch.tensor([0.0001]), requires_grad=False)
         self._ws = Workspace()
         self._palette_cache = {}
+        self.palette_perm_device = None   # None: the weights' device (reference behaviour)
         self.timing = None          # set to {} to record HIP-event timings of the MLP launch
         self.last_stats = {}
+
+    # view_poc / pos_poc alias the TiNeuVox buffers (temporalpoints.py:148-150); as properties
+    # they follow .to(device) (the reference relies on a CUDA default tensor type instead).
+    @property
+    def view_poc(self):
+        return self.tineuvox.view_poc
+
+    @property
+    def pos_poc(self):
+        return self.tineuvox.pos_poc
 
     # ------------------------------------------------------------------ construction helpers
     def _weights_from_bones(self, joints, bones, pcd, soft_weights=True):
@@ -236,7 +245,10 @@ class TemporalPoints(torch.nn.Module):
         the weights' device. Softmax weights are > 0, so those columns are the merge targets."""
         rules = self._merge_rules()
         J = self.weights.shape[1]
-        key = (str(dev), None if rules is None else tuple(rules.tolist()))
+        # the reference draws the permutation from a generator on the weights' device; a CPU
+        # reference run draws a different one, so the device is selectable for comparisons
+        perm_dev = torch.device(self.palette_perm_device) if self.palette_perm_device else dev
+        key = (str(dev), str(perm_dev), None if rules is None else tuple(rules.tolist()))
         if key not in self._palette_cache:
             wmask = torch.zeros(J, dtype=torch.bool)
             if rules is None:
@@ -245,13 +257,14 @@ class TemporalPoints(torch.nn.Module):
                 wmask[rules.cpu()] = True
             m = int(wmask.sum())
             cols = torch.tensor(hls_palette(m), dtype=torch.float64)
-            gen = torch.Generator(device=dev)
+            gen = torch.Generator(device=perm_dev)
             gen.manual_seed(0)
-            perm = torch.randperm(m, generator=gen, device=dev).cpu()
+            perm = torch.randperm(m, generator=gen, device=perm_dev).cpu()
             colors = torch.zeros(J, 3, dtype=torch.float64)
             colors[torch.where(wmask)[0]] = cols[perm]
-            self._palette_cache[key] = colors.float().to(dev)
-        return self._palette_cache[key]
+            self._palette_cache[key] = (colors.float().to(dev), perm)
+        self.last_palette_perm = self._palette_cache[key][1]
+        return self._palette_cache[key][0]
 
     def _lbs(self, bone_Ts, global_t, records=True, colors=None):
         pcd = self.canonical_pcd.contiguous()

@@ -167,7 +167,10 @@ __global__ __launch_bounds__(MLP_THREADS, 3) void k_point_mlp(
         }
       } else {
         for (int c = p; c < K1; c += 4) xr[c] = 0.f;
-        if (p == 0) { sTo[r] = 1.f; sNbr[r] = -1; }
+        if (p == 0) {
+          sTo[r] = 1.f; sNbr[r] = -1;
+          if (k == 0) sRay[s] = 0;   // padding sample: keep the view-embedding gather in bounds
+        }
       }
     }
     __syncthreads();

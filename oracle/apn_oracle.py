@@ -470,7 +470,7 @@ class OracleModel:
         d2, s_i = knn_kmin(pts, tp, K, use_tree=knn_tree)
         keep = np.nonzero(d2[:, -1] <= F32(query_radius))[0]
         s_i = s_i[keep]; ray_id = ray_id[keep]; step_id = step_id[keep]; pts = pts[keep]
-        self.trace.update(s_i=s_i, ray_id=ray_id, step_id=step_id, keep=keep)
+        self.trace.update(s_i=s_i, ray_id=ray_id, step_id=step_id, keep=keep, pts=pts)
         if len(s_i) == 0:
             return None
         s_i_t = torch.from_numpy(s_i)
@@ -513,10 +513,14 @@ class OracleModel:
     @torch.no_grad()
     def forward(self, t, render_depth=False, render_kwargs=None, query_radius=0.01,
                 render_weights=False, rot_params=None, poses=None, Ks=None, get_skeleton=False,
-                calc_min_max=True, perm=None, knn_tree=None):
+                calc_min_max=True, perm=None, knn_tree=None, t_hat_override=None):
+        """``t_hat_override``: render against a given warped cloud (e.g. the GPU's) so that a
+        1-ulp difference in the warp cannot flip a borderline kNN-radius decision."""
         assert (t is None) ^ (rot_params is None)
         rk = {k: (v.detach().cpu() if torch.is_tensor(v) else v) for k, v in render_kwargs.items()}
         weights, (t_hat, joints_rel, G, joints_w, bone_Ts, global_t) = self.warp(t, rot_params)
+        if t_hat_override is not None:
+            t_hat = torch.as_tensor(t_hat_override).detach().cpu().float().contiguous()
         self._last_weights = weights
         Rinv = torch.inverse(G)
         self.trace = dict(t_hat_pcd=t_hat, G=G, Rinv=Rinv, bone_Ts=bone_Ts, weights=weights,
@@ -524,6 +528,7 @@ class OracleModel:
         delta = (self.joints - joints_rel)
         pose_embedding = (pose_embedding_net(poc_fre(delta, self.pos_poc).view(1, -1), self.nets)
                           if self.pose_embedding_dim > 0 else None)
+        self.trace["pose_embedding"] = pose_embedding
         joints = bones = None
         if get_skeleton:
             joints = project_point_to_image_plane(joints_w, poses.cpu(), Ks.cpu().float())
@@ -536,20 +541,35 @@ class OracleModel:
                     "depth": torch.zeros(R), "weights": torch.ones(R, 3) * bg, "t_hat_pcd": t_hat,
                     "alphainv_last": None, "grid": None, "joints": joints, "bones": bones}
         rgbs, alpha, rgbs_d, alpha_d, lbsw, ray_id, step_id, N = res
+        col_all = None
+        if render_weights:
+            # weight-visualisation colour per kept sample (temporalpoints.py:690-701)
+            wmask = weights.sum(dim=0) > 0
+            cols = torch.tensor(hls_palette(int(wmask.sum())))
+            if perm is None:
+                gen = torch.Generator(); gen.manual_seed(0)
+                perm = torch.randperm(cols.shape[0], generator=gen)
+            cols = cols[perm]
+            col = 0
+            for ci, wi in enumerate(torch.where(wmask)[0]):
+                col = col + cols[ci, None] * lbsw[:, wi, None]
+            col_all = torch.as_tensor(col).float().numpy()
+            self.trace.update(col=col_all, perm=perm)
         thr = F32(self.fast_color_thres)
         ray_id_d = ray_id.copy()
         a = alpha.numpy(); ad = alpha_d.numpy()
-        rgbs = rgbs.numpy(); rgbs_d = rgbs_d.numpy(); lbsw = lbsw.numpy()
+        rgbs = rgbs.numpy(); rgbs_d = rgbs_d.numpy()
+        col = col_all if col_all is not None else np.zeros((len(a), 3), F32)
         if self.fast_color_thres > 0:
             m = a > thr
-            ray_id, step_id, a, rgbs, lbsw = ray_id[m], step_id[m], a[m], rgbs[m], lbsw[m]
+            ray_id, step_id, a, rgbs, col = ray_id[m], step_id[m], a[m], rgbs[m], col[m]
             md = ad > thr
             ray_id_d, ad, rgbs_d = ray_id_d[md], ad[md], rgbs_d[md]
         w, _, last, *_ = alpha2weight(a, ray_id, N)
         wd, _, last_d, *_ = alpha2weight(ad, ray_id_d, N)
         if self.fast_color_thres > 0:
             m = w > thr
-            w, a, ray_id, step_id, rgbs, lbsw = w[m], a[m], ray_id[m], step_id[m], rgbs[m], lbsw[m]
+            w, a, ray_id, step_id, rgbs, col = w[m], a[m], ray_id[m], step_id[m], rgbs[m], col[m]
             md = wd > thr
             ray_id_d, ad, rgbs_d, wd = ray_id_d[md], ad[md], rgbs_d[md], wd[md]
         rgb_marched = segment_sum((w[:, None] * rgbs).astype(F32), ray_id, N)
@@ -563,17 +583,6 @@ class OracleModel:
         if render_depth:
             ret["depth"] = torch.from_numpy(segment_sum((w * step_id.astype(F32)).astype(F32), ray_id, N))
         if render_weights:
-            wmask = weights.sum(dim=0) > 0
-            cols = torch.tensor(hls_palette(int(wmask.sum())))
-            if perm is None:
-                gen = torch.Generator(); gen.manual_seed(0)
-                perm = torch.randperm(cols.shape[0], generator=gen)
-            cols = cols[perm]
-            col = 0
-            lb = torch.from_numpy(lbsw)
-            for ci, wi in enumerate(torch.where(wmask)[0]):
-                col = col + cols[ci, None] * lb[:, wi, None]
-            col = torch.as_tensor(col).float().numpy() if torch.is_tensor(col) else np.zeros((len(w), 3), F32)
             wm = segment_sum((w[:, None] * col).astype(F32), ray_id, N)
             ret["weights"] = torch.from_numpy((wm + (last[:, None] * F32(bg)).astype(F32)).astype(F32))
         return ret

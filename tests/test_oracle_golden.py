@@ -93,3 +93,25 @@ def test_alpha2weight_matches_reference_inputs(golden):
     w, T, last, _, _ = O.alpha2weight(a, rid, R)
     assert np.all(np.isfinite(w)) and np.all((last >= 0) & (last <= 1))
     assert np.allclose(last, golden.z["out_alphainv_last"], atol=1e-5)
+
+
+def test_bbox_sensitivity_of_reference_sampling():
+    """Documents a property of the reference path itself: with the sampling bbox fixed, a
+    3e-7 perturbation of the warped cloud leaves every kNN survivor unchanged, while letting
+    the bbox follow the perturbed cloud (calc_min_max=True) changes the in-bbox sample set."""
+    g = Golden("G1")
+    t = g.z["out_t_hat_pcd"].astype(np.float32)
+    rk = g.render_kwargs()
+    sd = rk["stepsize"] * g.cfg("voxel_size")
+
+    def survivors(cloud, lo, hi):
+        pts, mo, *_ = O.sample_pts_on_rays(rk["rays_o"].numpy(), rk["rays_d"].numpy(), lo, hi, rk["near"],
+                                           rk["far"], sd)
+        d2, _ = O.knn_kmin(pts[~mo], cloud, 8)
+        return int((d2[:, -1] <= np.float32(0.01)).sum()), int((~mo).sum())
+
+    lo, hi = g.z["trace_xyz_min"], g.z["trace_xyz_max"]
+    tp = (t + np.random.default_rng(0).uniform(-3e-7, 3e-7, t.shape)).astype(np.float32)
+    assert survivors(tp, lo, hi) == survivors(t, lo, hi)
+    lo2 = (tp.min(0) - np.float32(0.01)).astype(np.float32); hi2 = (tp.max(0) + np.float32(0.01)).astype(np.float32)
+    assert survivors(tp, lo2, hi2)[1] != survivors(t, lo, hi)[1]
