@@ -2,15 +2,21 @@
 // pykeops brute-force `Kmin_argKmin(K=8)` + radius filter (temporalpoints.py:433-447).
 //
 // Exactness: a sample survives the reference filter iff its 8th-nearest squared distance
-// is <= query_radius. Every neighbour of a survivor therefore lies within r = sqrt(qr).
-// The uniform grid has cells of side >= r * (1 + 2^-10), so all points within r of a query
-// lie in the 27 cells around it, and the top-8 (by float32 (dx*dx+dy*dy)+dz*dz, ties by
-// index) over those cells equals the global top-8 for every survivor. Non-survivors are
-// discarded by the reference anyway. Distances use -ffp-contract=off arithmetic, so they
-// equal the reference's recomputed `to_nn` bit-for-bit.
+// is <= query_radius = r^2. Every neighbour of a survivor lies within r, so a search that has
+// seen every point within r returns the reference's top-8 (by float32 (dx*dx+dy*dy)+dz*dz,
+// ties by index; pykeops leaves tie order unspecified). Non-survivors are discarded by the
+// reference anyway. Distances use -ffp-contract=off arithmetic, so they equal the reference's
+// recomputed `to_nn` bit-for-bit.
 //
-// Grid build: counting sort (count -> scan -> scatter) of float4 {x,y,z,bits(idx)}; the
-// cells of one x-row are contiguous, so a query scans 9 contiguous ranges.
+// Data structure: a fine uniform grid (cell h = r / KNN_SUBDIV, bounded by a cell cap) built by
+// counting sort into float4 {x,y,z,bits(idx)} -- the cells of one x-row are contiguous -- plus
+// a coarse count grid (cell side cf*h >= r).
+// Query (two passes):
+//   classify: < 8 points in the 27 coarse cells around the sample => < 8 within r => reject
+//             (55% of the in-bbox samples at C2); the rest are compacted in query order;
+//   search:   cubes of Chebyshev radius k in {1, 2, 4, kmax} (kmax*h >= r), each scanned as
+//             (2k+1)^2 contiguous x-rows; after cube k every point closer than k*h has been
+//             seen, so the search stops exactly when the 8th best is closer than k*h(1-1e-4).
 #include "apn_common.h"
 
 namespace apn {
@@ -20,7 +26,7 @@ struct GridParams {
   float inv_h, r, r2, pad0;   // search radius r = sqrt(query_radius), r2 = query_radius
   int dx, dy, dz, nf;         // fine grid dims and cell count
   int cf, cdx, cdy, cdz;      // fine cells per coarse cell (coarse side >= r), coarse dims
-  int nc, kmax, pad1, pad2;   // coarse cell count, ring limit (kmax * h >= r)
+  int nc, kmax, pad1, pad2;   // coarse cell count, search limit (kmax * h >= r)
 };
 
 constexpr int KNN_K = 8;
@@ -108,27 +114,75 @@ __device__ __forceinline__ void knn_insert(float d, int id, float (&bd)[K], int 
   }
 }
 
-// Scan fine cells [x0,x1] of row (y,z) (contiguous in the sorted array) into the top-K.
 template <int K, bool EXCL>
-__device__ __forceinline__ void scan_cells(const int* __restrict__ cell_start, const float4* __restrict__ sorted,
-                                           int c0, int c1, float qx, float qy, float qz, float dmax2, int excl,
-                                           float (&bd)[K], int (&bi)[K]) {
-  const int b = cell_start[c0], e = cell_start[c1 + 1];
-  for (int p = b; p < e; ++p) {
-    const float4 P = sorted[p];
-    const float ddx = qx - P.x, ddy = qy - P.y, ddz = qz - P.z;
-    const float d = (ddx * ddx + ddy * ddy) + ddz * ddz;
-    const int id = __float_as_int(P.w);
-    if (d <= dmax2 && (!EXCL || id != excl)) knn_insert<K>(d, id, bd, bi);
-  }
+__device__ __forceinline__ void consider(const float4& P, float qx, float qy, float qz, float dmax2, int excl,
+                                         float (&bd)[K], int (&bi)[K]) {
+  const float ddx = qx - P.x, ddy = qy - P.y, ddz = qz - P.z;
+  const float d = (ddx * ddx + ddy * ddy) + ddz * ddz;
+  const int id = __float_as_int(P.w);
+  if (d <= dmax2 && (!EXCL || id != excl)) knn_insert<K>(d, id, bd, bi);
 }
 
-// Cells at Chebyshev ring distance exactly k around fine cell (fx,fy,fz), clamped to the grid.
+// Scan points [b, e) of the sorted array into the top-K, 4 independent loads per step.
 template <int K, bool EXCL>
-__device__ __forceinline__ void scan_ring(const GridParams& g, const int* __restrict__ cell_start,
+__device__ __forceinline__ void scan_range(const float4* __restrict__ sorted, int b, int e, float qx, float qy,
+                                           float qz, float dmax2, int excl, float (&bd)[K], int (&bi)[K]) {
+  int p = b;
+  for (; p + 4 <= e; p += 4) {
+    const float4 P0 = sorted[p], P1 = sorted[p + 1], P2 = sorted[p + 2], P3 = sorted[p + 3];
+    consider<K, EXCL>(P0, qx, qy, qz, dmax2, excl, bd, bi);
+    consider<K, EXCL>(P1, qx, qy, qz, dmax2, excl, bd, bi);
+    consider<K, EXCL>(P2, qx, qy, qz, dmax2, excl, bd, bi);
+    consider<K, EXCL>(P3, qx, qy, qz, dmax2, excl, bd, bi);
+  }
+  for (; p < e; ++p) consider<K, EXCL>(sorted[p], qx, qy, qz, dmax2, excl, bd, bi);
+}
+
+// All points in the cube of Chebyshev radius k (fine cells) around (fx,fy,fz), clamped to the
+// grid, as (2k+1)^2 contiguous x-rows. The next row's bounds are fetched before the current
+// row is scanned.
+template <int K, bool EXCL>
+__device__ __forceinline__ void scan_cube(const GridParams& g, const int* __restrict__ cell_start,
                                           const float4* __restrict__ sorted, int fx, int fy, int fz, int k,
                                           float qx, float qy, float qz, float dmax2, int excl, float (&bd)[K],
                                           int (&bi)[K]) {
+  const int x0 = max(fx - k, 0), x1 = min(fx + k, g.dx - 1);
+  const int y0 = max(fy - k, 0), y1 = min(fy + k, g.dy - 1);
+  const int z0 = max(fz - k, 0), z1 = min(fz + k, g.dz - 1);
+  if (x0 > x1 || y0 > y1 || z0 > z1) return;
+  const int ny = y1 - y0 + 1, nrows = ny * (z1 - z0 + 1);
+  int row = (z0 * g.dy + y0) * g.dx;
+  int b = cell_start[row + x0], e = cell_start[row + x1 + 1];
+  for (int j = 0; j < nrows; ++j) {
+    int nb = 0, ne = 0;
+    if (j + 1 < nrows) {
+      const int jj = j + 1;
+      const int nrow = ((z0 + jj / ny) * g.dy + (y0 + jj % ny)) * g.dx;
+      nb = cell_start[nrow + x0];
+      ne = cell_start[nrow + x1 + 1];
+    }
+    scan_range<K, EXCL>(sorted, b, e, qx, qy, qz, dmax2, excl, bd, bi);
+    b = nb; e = ne;
+  }
+}
+
+__device__ __forceinline__ int next_level(int k, int kmax) { return k >= kmax ? kmax + 1 : min(2 * k, kmax); }
+
+// Squared distance from coordinate v to the slab of cells [c0, c1] along one axis.
+__device__ __forceinline__ float slab_d2(float v, float o, float h, int c0, int c1) {
+  const float lo = o + (float)c0 * h, hi = o + (float)(c1 + 1) * h;
+  const float d = v < lo ? lo - v : (v > hi ? v - hi : 0.f);
+  return d * d;
+}
+
+// Ring k (Chebyshev distance exactly k) around (fx,fy,fz) as row segments; a segment is
+// skipped when its box is farther than the current K-th best (or r), which only removes
+// points that could not enter the top-K (box distance is a lower bound, with 1e-4 slack).
+template <int K, bool EXCL>
+__device__ __forceinline__ void scan_ring_culled(const GridParams& g, const int* __restrict__ cell_start,
+                                                 const float4* __restrict__ sorted, int fx, int fy, int fz, int k,
+                                                 float qx, float qy, float qz, float dmax2, int excl,
+                                                 float (&bd)[K], int (&bi)[K]) {
   const int z0 = max(fz - k, 0), z1 = min(fz + k, g.dz - 1);
   const int y0 = max(fy - k, 0), y1 = min(fy + k, g.dy - 1);
   const int xa = fx - k, xb = fx + k;
@@ -136,61 +190,102 @@ __device__ __forceinline__ void scan_ring(const GridParams& g, const int* __rest
   if (x0 > x1) return;
   for (int z = z0; z <= z1; ++z) {
     const bool zs = (z == fz - k) || (z == fz + k);
+    const float dz2 = slab_d2(qz, g.oz, g.h, z, z);
     for (int y = y0; y <= y1; ++y) {
+      const float tau = fminf(bd[K - 1], dmax2) * 1.0001f;
+      const float dyz2 = dz2 + slab_d2(qy, g.oy, g.h, y, y);
+      if (dyz2 > tau) continue;
       const int row = (z * g.dy + y) * g.dx;
       if (zs || y == fy - k || y == fy + k) {
-        scan_cells<K, EXCL>(cell_start, sorted, row + x0, row + x1, qx, qy, qz, dmax2, excl, bd, bi);
+        if (dyz2 + slab_d2(qx, g.ox, g.h, x0, x1) <= tau)
+          scan_range<K, EXCL>(sorted, cell_start[row + x0], cell_start[row + x1 + 1], qx, qy, qz, dmax2, excl, bd, bi);
       } else {
-        if (xa >= 0) scan_cells<K, EXCL>(cell_start, sorted, row + xa, row + xa, qx, qy, qz, dmax2, excl, bd, bi);
-        if (xb < g.dx && k > 0)
-          scan_cells<K, EXCL>(cell_start, sorted, row + xb, row + xb, qx, qy, qz, dmax2, excl, bd, bi);
+        if (xa >= 0 && dyz2 + slab_d2(qx, g.ox, g.h, xa, xa) <= tau)
+          scan_range<K, EXCL>(sorted, cell_start[row + xa], cell_start[row + xa + 1], qx, qy, qz, dmax2, excl, bd, bi);
+        if (xb < g.dx && k > 0 && dyz2 + slab_d2(qx, g.ox, g.h, xb, xb) <= tau)
+          scan_range<K, EXCL>(sorted, cell_start[row + xb], cell_start[row + xb + 1], qx, qy, qz, dmax2, excl, bd, bi);
       }
     }
   }
 }
 
-// One in-bbox sample per thread.
-//  1. coarse rejection: fewer than K points in the 27 coarse cells (side >= r) around the
-//     sample => fewer than K points within r => not a survivor;
-//  2. ring search over fine cells, k = 0..kmax: after ring k every point closer than k*h is
-//     found, so the search stops exactly once the K-th best is closer than k*h(1-1e-4), and at
-//     kmax (kmax*h >= r) every point within r has been seen.
-// Survivors are compacted per block (order preserved) into the block's slot range
-// [blockIdx*256, ...); blk_cnt[blockIdx] = survivors in the block.
-__global__ __launch_bounds__(KNN_THREADS) void k_knn_radius(
-    const float4* __restrict__ q_pos, const int* __restrict__ q_ray, const int* __restrict__ n_q_dev,
-    const GridParams* __restrict__ gp, const int* __restrict__ cell_start, const int* __restrict__ ccount,
-    const float4* __restrict__ sorted, float4* __restrict__ t_pos, int* __restrict__ t_ray,
-    int* __restrict__ t_nbr, int* __restrict__ blk_cnt) {
+// Pass 1: coarse rejection. Queries with >= 8 points in the 27 coarse cells around them are
+// compacted (in query order) per block into cand[blockIdx*256 ...]; blk_cnt[block] = count.
+__global__ __launch_bounds__(KNN_THREADS) void k_knn_classify(const float4* __restrict__ q_pos,
+                                                              const int* __restrict__ n_q_dev,
+                                                              const GridParams* __restrict__ gp,
+                                                              const int* __restrict__ ccount,
+                                                              int* __restrict__ cand, int* __restrict__ blk_cnt) {
   __shared__ int wave_cnt[KNN_THREADS / 64];
   const int nq = *n_q_dev;
   const int i = blockIdx.x * KNN_THREADS + threadIdx.x;
+  const GridParams g = *gp;
+  bool keep = false;
+  if (i < nq) {
+    const float4 q = q_pos[i];
+    const int cx = floor_div((int)floorf((q.x - g.ox) * g.inv_h), g.cf);
+    const int cy = floor_div((int)floorf((q.y - g.oy) * g.inv_h), g.cf);
+    const int cz = floor_div((int)floorf((q.z - g.oz) * g.inv_h), g.cf);
+    int cnt = 0;
+    for (int z = max(cz - 1, 0); z <= min(cz + 1, g.cdz - 1); ++z)
+      for (int y = max(cy - 1, 0); y <= min(cy + 1, g.cdy - 1); ++y)
+        for (int x = max(cx - 1, 0); x <= min(cx + 1, g.cdx - 1); ++x) cnt += ccount[(z * g.cdy + y) * g.cdx + x];
+    keep = cnt >= KNN_K;
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const unsigned long long bal = __ballot(keep);
+  const int before = __popcll(bal & ((1ull << lane) - 1ull));
+  if (lane == 0) wave_cnt[wid] = __popcll(bal);
+  __syncthreads();
+  int base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < KNN_THREADS / 64; ++w) {
+    base += (w < wid) ? wave_cnt[w] : 0;
+    tot += wave_cnt[w];
+  }
+  if (keep) cand[blockIdx.x * KNN_THREADS + base + before] = i;
+  if (threadIdx.x == 0) blk_cnt[blockIdx.x] = tot;
+}
+
+// Compact per-block int lists into a dense list (order preserved).
+__global__ __launch_bounds__(KNN_THREADS) void k_compact_i32(const int* __restrict__ src,
+                                                             const int* __restrict__ blk_cnt,
+                                                             const int* __restrict__ blk_off,
+                                                             int* __restrict__ dst) {
+  const int t = threadIdx.x;
+  if (t < blk_cnt[blockIdx.x]) dst[blk_off[blockIdx.x] + t] = src[blockIdx.x * KNN_THREADS + t];
+}
+
+// Pass 2: exact search for the compacted candidates. Survivors are compacted per block (order
+// preserved) into slots [blockIdx*256, ...) of t_*; blk_cnt[block] = survivors.
+__global__ __launch_bounds__(KNN_THREADS) void k_knn_search(
+    const float4* __restrict__ q_pos, const int* __restrict__ q_ray, const int* __restrict__ cand,
+    const int* __restrict__ n_cand_dev, const GridParams* __restrict__ gp, const int* __restrict__ cell_start,
+    const float4* __restrict__ sorted, float4* __restrict__ t_pos, int* __restrict__ t_ray,
+    int* __restrict__ t_nbr, int* __restrict__ blk_cnt) {
+  __shared__ int wave_cnt[KNN_THREADS / 64];
+  const int nc = *n_cand_dev;
+  const int c = blockIdx.x * KNN_THREADS + threadIdx.x;
   float bd[KNN_K];
   int bi[KNN_K];
 #pragma unroll
   for (int k = 0; k < KNN_K; ++k) { bd[k] = INFINITY; bi[k] = 0x7fffffff; }
   float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+  int qi = 0;
   const GridParams g = *gp;
-  if (i < nq) {
-    q = q_pos[i];
+  if (c < nc) {
+    qi = cand[c];
+    q = q_pos[qi];
     const int fx = (int)floorf((q.x - g.ox) * g.inv_h);
     const int fy = (int)floorf((q.y - g.oy) * g.inv_h);
     const int fz = (int)floorf((q.z - g.oz) * g.inv_h);
-    const int cx = floor_div(fx, g.cf), cy = floor_div(fy, g.cf), cz = floor_div(fz, g.cf);
-    int cnt = 0;
-    for (int z = max(cz - 1, 0); z <= min(cz + 1, g.cdz - 1); ++z)
-      for (int y = max(cy - 1, 0); y <= min(cy + 1, g.cdy - 1); ++y)
-        for (int x = max(cx - 1, 0); x <= min(cx + 1, g.cdx - 1); ++x) cnt += ccount[(z * g.cdy + y) * g.cdx + x];
-    if (cnt >= KNN_K) {
-      for (int k = 0; k <= g.kmax; ++k) {
-        scan_ring<KNN_K, false>(g, cell_start, sorted, fx, fy, fz, k, q.x, q.y, q.z, g.r2, -1, bd, bi);
-        const float gk = (float)k * g.h * (1.f - 1e-4f);
-        if (bd[KNN_K - 1] < gk * gk) break;
-      }
+    for (int k = 0; k <= g.kmax; ++k) {
+      scan_ring_culled<KNN_K, false>(g, cell_start, sorted, fx, fy, fz, k, q.x, q.y, q.z, g.r2, -1, bd, bi);
+      const float gk = (float)k * g.h * (1.f - 1e-4f);
+      if (bd[KNN_K - 1] < gk * gk) break;
     }
   }
-  const bool surv = (i < nq) && (bd[KNN_K - 1] <= g.r2);
-  // block-level order-preserving compaction
+  const bool surv = (c < nc) && (bd[KNN_K - 1] <= g.r2);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const unsigned long long bal = __ballot(surv);
   const int before = __popcll(bal & ((1ull << lane) - 1ull));
@@ -205,7 +300,7 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_radius(
   if (surv) {
     const int slot = blockIdx.x * KNN_THREADS + base + before;
     t_pos[slot] = q;
-    t_ray[slot] = q_ray[i];
+    t_ray[slot] = q_ray[qi];
     int4* nb = (int4*)(t_nbr + (int64_t)slot * KNN_K);
     nb[0] = make_int4(bi[0], bi[1], bi[2], bi[3]);
     nb[1] = make_int4(bi[4], bi[5], bi[6], bi[7]);
@@ -230,9 +325,9 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_compact(
 }
 
 // Nearest *other* point for every canonical point (temporalpoints.py:104-111: column 1 of the
-// self-inclusive argKmin is the nearest other point, or a duplicate at distance 0). Ring
-// search over the whole grid with the same exact stopping rule; brute force if the grid runs
-// out. Output: sqrt(d2 + eps) per point.
+// self-inclusive argKmin is the nearest other point, or a duplicate at distance 0). Cube search
+// with the same exact stopping rule, radius doubling over the whole grid; brute force if the
+// grid runs out. Output: sqrt(d2 + eps) per point.
 __global__ void k_nn1(const float* __restrict__ xyz, int64_t N, const GridParams* __restrict__ gp,
                       const int* __restrict__ cell_start, const float4* __restrict__ sorted, float eps,
                       float* __restrict__ nn_dist) {
@@ -244,10 +339,11 @@ __global__ void k_nn1(const float* __restrict__ xyz, int64_t N, const GridParams
   const int fz = cell_coord(qz, g.oz, g.inv_h, g.dz);
   float bd[1] = {INFINITY};
   int bi[1] = {0x7fffffff};
-  const int kend = max(g.dx, max(g.dy, g.dz));
+  const int kend = min(max(g.dx, max(g.dy, g.dz)), 64);
   bool done = false;
-  for (int k = 0; k <= kend && k <= 64; ++k) {
-    scan_ring<1, true>(g, cell_start, sorted, fx, fy, fz, k, qx, qy, qz, INFINITY, (int)n, bd, bi);
+  for (int k = 1; k <= kend; k *= 2) {
+    bd[0] = INFINITY; bi[0] = 0x7fffffff;
+    scan_cube<1, true>(g, cell_start, sorted, fx, fy, fz, k, qx, qy, qz, INFINITY, (int)n, bd, bi);
     const float gk = (float)k * g.h * (1.f - 1e-4f);
     if (bd[0] < gk * gk) { done = true; break; }
   }
@@ -334,11 +430,12 @@ extern "C" int apn_grid_build(const float* xyz, int64_t n_points, const int32_t*
   return launch_status();
 }
 
+// kNN workspace: per-slot candidate / survivor staging + block counts/offsets + scan scratch.
 extern "C" size_t apn_knn_workspace_bytes(int64_t n_queries) {
   int64_t nb = (n_queries + KNN_THREADS - 1) / KNN_THREADS;
   size_t slots = (size_t)nb * KNN_THREADS;
-  return al256(slots * 16) + al256(slots * 4) + al256(slots * 4 * KNN_K) + al256((size_t)(nb + 1) * 4) +
-         al256((size_t)(nb + 1) * 4) + al256(scan_workspace_bytes(nb));
+  return al256(slots * 4) * 2 + al256((size_t)(nb + 2) * 4) * 2 + al256(slots * 16) + al256(slots * 4) +
+         al256(slots * 4 * KNN_K) + al256((size_t)(nb + 1) * 4) * 2 + al256(scan_workspace_bytes(nb));
 }
 
 // Queries: q_pos4[n_queries] {x,y,z,bits(step)} and q_ray. n_queries is an upper bound used for
@@ -349,6 +446,7 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
                               int32_t cell_cap, const float* sorted_pts4, float query_radius, float* s_pos4,
                               int32_t* s_ray, int32_t* s_nbr, int32_t* n_survivors_dev, void* workspace,
                               void* stream) {
+  (void)query_radius;  // the grid was built for it (GridParams.r2)
   if (n_queries < 0 || !grid_workspace || !workspace) return APN_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   if (n_queries == 0) {
@@ -359,15 +457,25 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
   const int nb = ceil_div(n_queries, KNN_THREADS);
   const size_t slots = (size_t)nb * KNN_THREADS;
   char* p = (char*)workspace;
+  int* cand_blk = (int*)p; p += al256(slots * 4);
+  int* cand = (int*)p; p += al256(slots * 4);
+  int* cblk_cnt = (int*)p; p += al256((size_t)(nb + 2) * 4);
+  int* cblk_off = (int*)p; p += al256((size_t)(nb + 2) * 4);
   float4* t_pos = (float4*)p; p += al256(slots * 16);
   int* t_ray = (int*)p; p += al256(slots * 4);
   int* t_nbr = (int*)p; p += al256(slots * 4 * KNN_K);
   int* blk_cnt = (int*)p; p += al256((size_t)(nb + 1) * 4);
   int* blk_off = (int*)p; p += al256((size_t)(nb + 1) * 4);
   void* sws = p;
-  hipLaunchKernelGGL(k_knn_radius, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, q_ray, n_queries_dev,
-                     g.gp, g.cell_start, g.ccount, (const float4*)sorted_pts4, t_pos, t_ray, t_nbr, blk_cnt);
-  int st = scan_exclusive_i32(blk_cnt, blk_off, nb, sws, s);
+  hipLaunchKernelGGL(k_knn_classify, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, n_queries_dev, g.gp,
+                     g.ccount, cand_blk, cblk_cnt);
+  int st = scan_exclusive_i32(cblk_cnt, cblk_off, nb, sws, s);
+  if (st) return st;
+  hipLaunchKernelGGL(k_compact_i32, dim3(nb), dim3(KNN_THREADS), 0, s, cand_blk, cblk_cnt, cblk_off, cand);
+  // candidates: count at cblk_off[nb]; launch over the upper bound nb blocks
+  hipLaunchKernelGGL(k_knn_search, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, q_ray, cand,
+                     cblk_off + nb, g.gp, g.cell_start, (const float4*)sorted_pts4, t_pos, t_ray, t_nbr, blk_cnt);
+  st = scan_exclusive_i32(blk_cnt, blk_off, nb, sws, s);
   if (st) return st;
   hipLaunchKernelGGL(k_knn_compact, dim3(nb), dim3(KNN_THREADS), 0, s, t_pos, t_ray, t_nbr, blk_cnt, blk_off,
                      (float4*)s_pos4, s_ray, s_nbr);
@@ -382,7 +490,6 @@ extern "C" int apn_nn1_distance(const float* xyz, int64_t n_points, float eps, i
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(k_bbox_init2, dim3(1), dim3(64), 0, s, bbox_ord);
   hipLaunchKernelGGL(k_bbox_from_points, dim3(ceil_div(n_points, 256)), dim3(256), 0, s, xyz, n_points, bbox_ord);
-  // cell side sqrt(0.01) unless the cap forces it larger
   int st = apn_grid_build(xyz, n_points, bbox_ord, 0.01f, cell_cap, sorted_pts4, grid_workspace, stream);
   if (st) return st;
   GridWs g = grid_ws(grid_workspace, n_points, cell_cap);
