@@ -105,6 +105,8 @@ def segment_coo_sum(src, index, n_out):
 # ----------------------------------------------------------------------------------------
 
 _LAYOUT = None
+_LAYOUT_NAMES = ["W1E", "B1", "W2", "B2", "W3", "B3", "W4", "B4", "WD", "BD", "WH", "BH", "WV2", "BV2", "W1F",
+                 "TOTAL", "KE", "KV"]
 
 
 def mlp_layout():
@@ -113,45 +115,66 @@ def mlp_layout():
         import ctypes as C
         arr = (C.c_int32 * 32)()
         n = L.load().apn_mlp_weight_layout(arr)
-        names = ["W1", "B1", "W2", "B2", "W3", "B3", "W4", "B4", "WD", "BD", "WF", "BF", "WV0", "BV0",
-                 "WV2", "BV2", "TOTAL", "K1", "KV"]
-        _LAYOUT = dict(zip(names, list(arr)[:n]))
+        if n != len(_LAYOUT_NAMES):
+            raise RuntimeError(f"apn_mlp_weight_layout returned {n} offsets, expected {len(_LAYOUT_NAMES)}")
+        _LAYOUT = dict(zip(_LAYOUT_NAMES, list(arr)[:n]))
     return _LAYOUT
 
 
 def pack_mlp_weights(feat_net_layers, densitynet, rgbnet, pose_embedding=None, out=None):
-    """Pack feat_net / densitynet / rgbnet weights (nn.Linear (out,in) layout, zero-padded K)
-    into the buffer apn_point_mlp reads. The pose-embedding columns of feat_net.0
-    (temporalpoints.py:487-488) are folded into the layer-1 bias: b1 + W1[:,191:] @ pe."""
+    """Pack feat_net / densitynet / rgbnet (nn.Linear (out,in) layout, zero-padded K) into the
+    buffer apn_point_mlp / apn_feat_project read (layout: apn_mlp_weight_layout):
+      * feat_net.0 split into its posenc columns (W1E) and feature columns (W1F);
+      * the pose-embedding columns (temporalpoints.py:487-488) folded into b1: b1 + W1p @ pe;
+      * rgbnet.feature_linears folded into views_linears.0 (no activation in between):
+        WH = [Wv0[:, :128] @ Wf | Wv0[:, 128:]], BH = Wv0[:, :128] @ bf + bv0 (float64 fold)."""
     lay = mlp_layout()
     l1, l2, l3, l4 = feat_net_layers
     dev = l1.weight.device
     buf = out if out is not None else torch.zeros(lay["TOTAL"], device=dev)
-    K1, KV = lay["K1"], lay["KV"]
+    KE, KV = lay["KE"], lay["KV"]
 
     def put(name, t):
         t = t.detach().float().reshape(-1)
         buf[lay[name]:lay[name] + t.numel()].copy_(t)
 
     w1 = l1.weight.detach().float()
-    base = 63 + 128
-    w1p = torch.zeros(128, K1, device=dev)
-    w1p[:, :base] = w1[:, :base]
-    put("W1", w1p)
+    n_emb, n_feat = 63, 128
+    if w1.shape[1] < n_emb + n_feat:
+        raise ValueError(f"feat_net.0 has {w1.shape[1]} inputs; expected >= {n_emb + n_feat}")
+    w1e = torch.zeros(128, KE, device=dev)
+    w1e[:, :n_emb] = w1[:, :n_emb]
+    put("W1E", w1e)
+    put("W1F", w1[:, n_emb:n_emb + n_feat].contiguous())
     b1 = l1.bias.detach().float()
     if pose_embedding is not None:
-        b1 = b1 + (w1[:, base:] @ pose_embedding.reshape(-1, 1).float()).reshape(-1)
-    elif w1.shape[1] != base:
+        b1 = b1 + (w1[:, n_emb + n_feat:] @ pose_embedding.reshape(-1, 1).float()).reshape(-1)
+    elif w1.shape[1] != n_emb + n_feat:
         raise ValueError(f"feat_net.0 expects {w1.shape[1]} inputs but no pose embedding was given")
     put("B1", b1)
     for nm, l in (("2", l2), ("3", l3), ("4", l4)):
         put("W" + nm, l.weight); put("B" + nm, l.bias)
     put("WD", densitynet.weight); put("BD", densitynet.bias)
-    put("WF", rgbnet.feature_linears.weight); put("BF", rgbnet.feature_linears.bias)
+    wf = rgbnet.feature_linears.weight.detach().double()
+    bf = rgbnet.feature_linears.bias.detach().double()
     v0 = rgbnet.views_linears[0]
-    wv0 = torch.zeros(64, KV, device=dev)
-    wv0[:, :v0.weight.shape[1]] = v0.weight.detach().float()
-    put("WV0", wv0); put("BV0", v0.bias)
+    wv0 = v0.weight.detach().double()
+    nh = wf.shape[0]
+    wh = torch.zeros(64, KV, dtype=torch.float64, device=dev)
+    wh[:, :nh] = wv0[:, :nh] @ wf
+    wh[:, nh:wv0.shape[1]] = wv0[:, nh:]
+    put("WH", wh)
+    put("BH", wv0[:, :nh] @ bf + v0.bias.detach().double())
     v2 = rgbnet.views_linears[2]
     put("WV2", v2.weight); put("BV2", v2.bias)
     return buf
+
+
+def feat_project(canonical_feat, wbuf, out=None):
+    """apn_feat_project: per-point layer-1 feature projection [N,128]."""
+    L.require_cuda(canonical_feat, wbuf, what="feat_project")
+    f = canonical_feat.detach().float().contiguous()
+    N = f.shape[0]
+    P = out if out is not None else torch.empty(N, 128, device=f.device)
+    call("apn_feat_project", ptr(f), N, f.shape[1], ptr(wbuf), ptr(P), stream_ptr(f.device))
+    return P

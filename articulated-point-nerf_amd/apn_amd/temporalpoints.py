@@ -294,12 +294,23 @@ class TemporalPoints(torch.nn.Module):
         return xyz, wout, (recA, recB, bbox)
 
     def _packed_weights(self, pose_embedding, dev):
-        layers = [self.feat_net[0], self.feat_net[2][0], self.feat_net[3][0], self.feat_net[4]]
+        """Packed MLP weights + the per-point layer-1 projection, cached on parameter versions
+        (only the pose-embedding bias fold changes per frame)."""
         if len(self.feat_net) != 6:
             raise NotImplementedError("the fused MLP kernel implements feat_depth=4 (the reference default)")
-        from .ops import mlp_layout
+        from .ops import feat_project, mlp_layout
+        layers = [self.feat_net[0], self.feat_net[2][0], self.feat_net[3][0], self.feat_net[4]]
+        params = [p for l in layers for p in (l.weight, l.bias)] + list(self.densitynet.parameters()) + \
+            list(self.rgbnet.parameters()) + [self.canonical_feat]
+        key = tuple((p.data_ptr(), p._version) for p in params)
         buf = self._ws.get("mlp_w", mlp_layout()["TOTAL"], torch.float32, dev)
-        return pack_mlp_weights(layers, self.densitynet, self.rgbnet, pose_embedding, out=buf)
+        if key != getattr(self, "_pack_key", None) or pose_embedding is not None:
+            pack_mlp_weights(layers, self.densitynet, self.rgbnet, pose_embedding, out=buf)
+        if key != getattr(self, "_pack_key", None):
+            proj = self._ws.get("feat_proj", self.canonical_feat.shape[0] * 128, torch.float32, dev)
+            feat_project(self.canonical_feat, buf, out=proj.view(-1, 128))
+            self._pack_key = key
+        return buf, self._ws.bufs["feat_proj"]
 
     @torch.no_grad()
     def forward(self, t, render_depth=False, render_kwargs=None, query_radius=0.01, render_weights=False,
@@ -394,9 +405,9 @@ class TemporalPoints(torch.nn.Module):
         if S == 0:
             raise NoPointsException("No points.")
         # neighbour MLP + heads + direct blend
-        wbuf = self._packed_weights(pose_embedding, dev)
+        wbuf, proj = self._packed_weights(pose_embedding, dev)
         out12 = ws.get("out12", S * 12, torch.float32, dev)
-        feat = self.canonical_feat.detach().contiguous()
+        feat = proj
         vemb = self.viewdirs_emb.detach().reshape(-1).float().contiguous() if self.frozen_view_dir is not None else None
         if self.no_view_dir:
             raise NotImplementedError("no_view_dir=True breaks the reference forward (viewdirs_emb_reshape undefined)")
@@ -404,7 +415,7 @@ class TemporalPoints(torch.nn.Module):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
         call("apn_point_mlp", ptr(s_pos), ptr(s_ray), ptr(s_nbr), S, ptr(nsurv), ptr(recA), ptr(recB), ptr(feat),
-             feat.shape[1], ptr(vd), ptr(vemb), ptr(wbuf), self._eps, float(self.tineuvox.act_shift), interval, 0,
+             128, ptr(vd), ptr(vemb), ptr(wbuf), self._eps, float(self.tineuvox.act_shift), interval, 0,
              ptr(out12), s)
         if self.timing is not None:
             e1.record()

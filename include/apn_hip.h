@@ -114,16 +114,25 @@ int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t n_queries,
 int apn_nn1_distance(const float* xyz, int64_t n_points, float eps, int32_t cell_cap, float* nn_dist,
                      float* sorted_pts4, int32_t* bbox_ord, void* grid_workspace, void* stream);
 
-/* Packed MLP weight layout: writes 19 int32 offsets (W1,B1,W2,B2,W3,B3,W4,B4,WD,BD,WF,BF,
- * WV0,BV0,WV2,BV2,TOTAL,K1,KV) and returns their count. */
+/* Packed MLP weight layout: writes 18 int32 offsets (W1E,B1,W2,B2,W3,B3,W4,B4,WD,BD,WH,BH,
+ * WV2,BV2,W1F,TOTAL,KE,KV) and returns their count. W1E = feat_net.0 columns 0..62 (posenc),
+ * W1F = feat_net.0 columns 63..190 (features), WH/BH = rgbnet feature_linears folded into
+ * views_linears.0 (no activation between them), see apn_mlp.hip. */
 int apn_mlp_weight_layout(int32_t* offsets);
 
+/* Per-point layer-1 feature projection proj [N,128] = canonical_feat [N,128] x W1F^T
+ * (temporalpoints.py:483-491 reassociated: W1 [emb; feat] = W1e emb + W1f feat). Computed once
+ * per model; feat_dim must be 128. */
+int apn_feat_project(const float* canonical_feat, int64_t n_points, int32_t feat_dim,
+                     const float* wbuf, float* proj, void* stream);
+
 /* Fused neighbour MLP + heads + direct blend (temporalpoints.py:452-519) for the kept
- * samples; out12 [S,12] = {r,g,b,alpha, r_d,g_d,b_d,alpha_d, wr,wg,wb,0}. feat_dim must be
- * 128. vemb_const [27] (frozen_view_dir) or NULL to embed viewdirs[ray]. */
+ * samples; out12 [S,12] = {r,g,b,alpha, r_d,g_d,b_d,alpha_d, wr,wg,wb,0}. feat_proj is the
+ * apn_feat_project output (feat_dim 128). vemb_const [27] (frozen_view_dir) or NULL to embed
+ * viewdirs[ray]. */
 int apn_point_mlp(const float* s_pos4, const int32_t* s_ray, const int32_t* s_nbr,
                   int64_t max_samples, const int32_t* n_samples_dev, const float* recA16,
-                  const float* recB8, const float* canonical_feat, int32_t feat_dim,
+                  const float* recB8, const float* feat_proj, int32_t feat_dim,
                   const float* viewdirs, const float* vemb_const, const float* wbuf, float eps,
                   float act_shift, float interval, int32_t grid_blocks, float* out12, void* stream);
 

@@ -202,7 +202,8 @@ def test_mlp_stage_vs_oracle(dev, name):
     layers = [m.feat_net[0], m.feat_net[2][0], m.feat_net[3][0], m.feat_net[4]]
     wbuf = pack_mlp_weights(layers, m.densitynet, m.rgbnet, pe)
     out12 = torch.empty(S, 12, device=dev)
-    feat = m.canonical_feat.detach().contiguous()
+    from apn_amd.ops import feat_project
+    feat = feat_project(m.canonical_feat, wbuf)
     vd = g.t("in_viewdirs").to(dev)
     recA_d, recB_d = recA.to(dev), recB.to(dev)   # keep device copies alive across the async launch
     L.call("apn_point_mlp", L.ptr(args[0]), L.ptr(args[1]), L.ptr(args[2]), S, L.ptr(ns), L.ptr(recA_d),
