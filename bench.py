@@ -53,7 +53,8 @@ def log(*a):
 
 def cpu_baseline(model, scene, rows, threads):
     """The oracle (CPU restatement, pure PyTorch + scipy cKDTree kNN) on a bounded sample:
-    a band of ``rows`` image rows through the object centre of the same frame."""
+    ``rows`` image rows spread evenly over the same frame (every H/rows-th row), so the
+    object-hit fraction matches the full frame."""
     from oracle.apn_oracle import OracleModel
     torch.set_num_threads(threads)
     st = {k: v.detach().cpu() for k, v in model.state_dict().items()}
@@ -64,10 +65,11 @@ def cpu_baseline(model, scene, rows, threads):
                       mean_min_distance_value=float(model.mean_min_distance))
     rk = scene.render_kwargs("cpu")
     H, W = scene.cfg.H, scene.cfg.W
-    r0 = H // 2 - rows // 2
+    stride = max(1, H // rows)
+    sel = torch.cat([torch.arange(r * W, (r + 1) * W) for r in range(stride // 2, H, stride)][:rows])
     sub = dict(rk)
     for k in ("rays_o", "rays_d", "viewdirs"):
-        sub[k] = rk[k][r0 * W:(r0 + rows) * W]
+        sub[k] = rk[k][sel].contiguous()
     t = torch.tensor([scene.cfg.t])
     orc.forward(t, render_depth=True, render_kwargs=sub, render_weights=True, knn_tree=True)  # warm-up
     n_rep, t0 = 0, time.perf_counter()
@@ -79,7 +81,7 @@ def cpu_baseline(model, scene, rows, threads):
     dt = (time.perf_counter() - t0) / n_rep
     nrays = rows * W
     return {"value": nrays / dt, "unit": "rays/s", "cores": threads, "kind": "port",
-            "sample": f"{rows} central rows x {W} = {nrays} rays of the same frame, {n_rep} timed frames "
+            "sample": f"{rows} evenly spaced rows x {W} = {nrays} rays of the same frame, {n_rep} timed repeats "
                       f"(oracle: torch-CPU MLP, scipy cKDTree kNN), {dt:.2f} s/band"}
 
 

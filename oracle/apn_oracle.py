@@ -189,7 +189,7 @@ def knn_kmin(query, points, K, chunk=2048, use_tree=None):
         tree = cKDTree(p.astype(np.float64))
         for s in range(0, Q, 1 << 18):
             qq = q[s:s + (1 << 18)]
-            _, cand = tree.query(qq.astype(np.float64), k=Kc, workers=-1)
+            _, cand = tree.query(qq.astype(np.float64), k=Kc, workers=torch.get_num_threads())
             cand = np.asarray(cand, np.int64).reshape(len(qq), Kc)
             d_out[s:s + len(qq)], i_out[s:s + len(qq)] = _finalize_topk(qq, p, cand, K)
         return d_out, i_out
