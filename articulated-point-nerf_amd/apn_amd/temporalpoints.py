@@ -21,6 +21,7 @@ from . import _lib as L
 from ._lib import call, ptr, stream_ptr
 from .ops import Workspace, pack_mlp_weights
 from .pointwarper import PointWarper
+from .shard import balanced_ray_split
 from .tineuvox import poc_fre
 
 CELL_CAP = 1 << 20
@@ -315,8 +316,12 @@ class TemporalPoints(torch.nn.Module):
     @torch.no_grad()
     def forward(self, t, render_depth=False, render_kwargs=None, query_radius=0.01, render_weights=False,
                 rot_params=None, render_pcd_direct=False, poses=None, Ks=None, cam_per_ray=None, calc_min_max=True,
-                get_skeleton=False):
-        """temporalpoints.py:540-712."""
+                get_skeleton=False, ray_shard=None):
+        """temporalpoints.py:540-712.
+
+        ``ray_shard=(rank, world)`` (not in the reference signature) renders only this rank's
+        contiguous ray range with ~1/world of the frame's in-bbox samples; the range is left in
+        ``self.last_ray_range`` (see apn_amd.shard for the tile all-gather)."""
         assert (t is None) ^ (rot_params is None)
         dev = self.canonical_feat.device
         L.require_cuda(self.canonical_feat, what="TemporalPoints.forward")
@@ -337,9 +342,12 @@ class TemporalPoints(torch.nn.Module):
                 bones = self.new_bones
         R = len(render_kwargs['rays_o'])
         try:
-            out = self._render(t_hat_pcd, recs, query_radius, render_kwargs, pose_embedding, calc_min_max)
+            out = self._render(t_hat_pcd, recs, query_radius, render_kwargs, pose_embedding, calc_min_max,
+                               shard=ray_shard)
         except NoPointsException:
             bg = render_kwargs['bg']
+            if ray_shard is not None:
+                R = self.last_ray_range[1] - self.last_ray_range[0]
             return {'rgb_marched': torch.ones(R, 3, device=dev) * bg,
                     'rgb_marched_direct': torch.ones(R, 3, device=dev) * bg,
                     'depth': torch.zeros(R, device=dev), 'weights': torch.ones(R, 3, device=dev) * bg,
@@ -353,7 +361,7 @@ class TemporalPoints(torch.nn.Module):
             ret['weights'] = wvis
         return ret
 
-    def _render(self, xyz, recs, query_radius, rk, pose_embedding, calc_min_max):
+    def _render(self, xyz, recs, query_radius, rk, pose_embedding, calc_min_max, shard=None):
         recA, recB, bbox_ord = recs
         dev = xyz.device
         lib = L.load()
@@ -384,6 +392,16 @@ class TemporalPoints(torch.nn.Module):
         offs = ws.get("offs", R + 1, torch.int32, dev)
         sws = ws.bytes("samp_ws", lib.apn_sample_pts_on_rays_workspace_bytes(R), dev)
         call("apn_inbbox_count", ptr(ro), ptr(rd), ptr(bbox6), near, far, stepdist, R, ptr(offs), ptr(sws), s)
+        if shard is not None:
+            # contiguous ray range holding ~1/world of the in-bbox samples
+            rank, world = shard
+            bounds = balanced_ray_split(offs, world)
+            r0, r1 = bounds[rank], bounds[rank + 1]
+            self.last_ray_range = (r0, r1)
+            self.last_ray_bounds = bounds
+            ro, rd, vd = ro[r0:r1], rd[r0:r1], vd[r0:r1]
+            offs = (offs[r0:r1 + 1] - offs[r0]).contiguous()
+            R = r1 - r0
         n_bbox = int(offs[R].item())
         self.last_stats = {"rays": R, "inbbox_samples": n_bbox}
         if n_bbox == 0:

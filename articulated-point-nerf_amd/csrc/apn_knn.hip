@@ -209,6 +209,74 @@ __device__ __forceinline__ void scan_ring_culled(const GridParams& g, const int*
   }
 }
 
+// Insert with duplicate check (a ball scan of a larger radius revisits the points of the
+// previous one; a revisited point has the same distance, so it is found in the list).
+template <int K>
+__device__ __forceinline__ void knn_insert_unique(float d, int id, float (&bd)[K], int (&bi)[K]) {
+  if (!knn_less(d, id, bd[K - 1], bi[K - 1])) return;
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (bi[k] == id) return;
+  bd[K - 1] = d; bi[K - 1] = id;
+#pragma unroll
+  for (int k = K - 1; k > 0; --k) {
+    if (knn_less(bd[k], bi[k], bd[k - 1], bi[k - 1])) {
+      float td = bd[k]; bd[k] = bd[k - 1]; bd[k - 1] = td;
+      int ti = bi[k]; bi[k] = bi[k - 1]; bi[k - 1] = ti;
+    }
+  }
+}
+
+template <int K>
+__device__ __forceinline__ void scan_range_u(const float4* __restrict__ sorted, int b, int e, float qx, float qy,
+                                             float qz, float dmax2, float (&bd)[K], int (&bi)[K]) {
+  int p = b;
+  for (; p + 4 <= e; p += 4) {
+    float4 P[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) P[u] = sorted[p + u];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float ddx = qx - P[u].x, ddy = qy - P[u].y, ddz = qz - P[u].z;
+      const float d = (ddx * ddx + ddy * ddy) + ddz * ddz;
+      if (d <= dmax2) knn_insert_unique<K>(d, __float_as_int(P[u].w), bd, bi);
+    }
+  }
+  for (; p < e; ++p) {
+    const float4 P = sorted[p];
+    const float ddx = qx - P.x, ddy = qy - P.y, ddz = qz - P.z;
+    const float d = (ddx * ddx + ddy * ddy) + ddz * ddz;
+    if (d <= dmax2) knn_insert_unique<K>(d, __float_as_int(P.w), bd, bi);
+  }
+}
+
+// Every point whose cell intersects the ball of squared radius R2 around q, shrunk on the fly to
+// the current K-th best: (z, y) rows outside the bound are skipped and each remaining row is
+// scanned over the x-chord of the ball (cells [x0, x1] are contiguous in the sorted array).
+// Bounds carry a 1e-4 relative slack, far above float rounding of the cell arithmetic.
+template <int K>
+__device__ __forceinline__ void scan_ball(const GridParams& g, const int* __restrict__ cell_start,
+                                          const float4* __restrict__ sorted, float qx, float qy, float qz, float R2,
+                                          float (&bd)[K], int (&bi)[K]) {
+  const float R = sqrtf(R2) * 1.0001f;
+  const int z0 = max((int)floorf((qz - R - g.oz) * g.inv_h), 0), z1 = min((int)floorf((qz + R - g.oz) * g.inv_h), g.dz - 1);
+  const int y0 = max((int)floorf((qy - R - g.oy) * g.inv_h), 0), y1 = min((int)floorf((qy + R - g.oy) * g.inv_h), g.dy - 1);
+  for (int z = z0; z <= z1; ++z) {
+    const float dz2 = slab_d2(qz, g.oz, g.h, z, z);
+    for (int y = y0; y <= y1; ++y) {
+      const float tau = fminf(bd[K - 1], R2) * 1.0001f;
+      const float dyz2 = dz2 + slab_d2(qy, g.oy, g.h, y, y);
+      if (dyz2 > tau) continue;
+      const float w = sqrtf(tau - dyz2) * 1.0001f;
+      const int x0 = max((int)floorf((qx - w - g.ox) * g.inv_h), 0);
+      const int x1 = min((int)floorf((qx + w - g.ox) * g.inv_h), g.dx - 1);
+      if (x0 > x1) continue;
+      const int row = (z * g.dy + y) * g.dx;
+      scan_range_u<K>(sorted, cell_start[row + x0], cell_start[row + x1 + 1], qx, qy, qz, g.r2, bd, bi);
+    }
+  }
+}
+
 // Pass 1: coarse rejection. Queries with >= 8 points in the 27 coarse cells around them are
 // compacted (in query order) per block into cand[blockIdx*256 ...]; blk_cnt[block] = count.
 __global__ __launch_bounds__(KNN_THREADS) void k_knn_classify(const float4* __restrict__ q_pos,
@@ -262,7 +330,7 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_search(
     const float4* __restrict__ q_pos, const int* __restrict__ q_ray, const int* __restrict__ cand,
     const int* __restrict__ n_cand_dev, const GridParams* __restrict__ gp, const int* __restrict__ cell_start,
     const float4* __restrict__ sorted, float4* __restrict__ t_pos, int* __restrict__ t_ray,
-    int* __restrict__ t_nbr, int* __restrict__ blk_cnt) {
+    int* __restrict__ t_nbr, int* __restrict__ blk_cnt, int mode) {
   __shared__ int wave_cnt[KNN_THREADS / 64];
   const int nc = *n_cand_dev;
   const int c = blockIdx.x * KNN_THREADS + threadIdx.x;
@@ -276,13 +344,26 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_search(
   if (c < nc) {
     qi = cand[c];
     q = q_pos[qi];
-    const int fx = (int)floorf((q.x - g.ox) * g.inv_h);
-    const int fy = (int)floorf((q.y - g.oy) * g.inv_h);
-    const int fz = (int)floorf((q.z - g.oz) * g.inv_h);
-    for (int k = 0; k <= g.kmax; ++k) {
-      scan_ring_culled<KNN_K, false>(g, cell_start, sorted, fx, fy, fz, k, q.x, q.y, q.z, g.r2, -1, bd, bi);
-      const float gk = (float)k * g.h * (1.f - 1e-4f);
-      if (bd[KNN_K - 1] < gk * gk) break;
+    if (mode == 0) {
+      // expanding balls R = 2h, 4h, ..., r: after a ball every point within R has been seen, so
+      // a K-th best strictly inside R is final
+      float R = 2.f * g.h;
+      for (;;) {
+        const float Rl = fminf(R, g.r);
+        const float R2 = Rl >= g.r ? g.r2 : Rl * Rl;
+        scan_ball<KNN_K>(g, cell_start, sorted, q.x, q.y, q.z, R2, bd, bi);
+        if (Rl >= g.r || bd[KNN_K - 1] < R2 * (1.f - 2e-4f)) break;
+        R *= 2.f;
+      }
+    } else {
+      const int fx = (int)floorf((q.x - g.ox) * g.inv_h);
+      const int fy = (int)floorf((q.y - g.oy) * g.inv_h);
+      const int fz = (int)floorf((q.z - g.oz) * g.inv_h);
+      for (int k = 0; k <= g.kmax; ++k) {
+        scan_ring_culled<KNN_K, false>(g, cell_start, sorted, fx, fy, fz, k, q.x, q.y, q.z, g.r2, -1, bd, bi);
+        const float gk = (float)k * g.h * (1.f - 1e-4f);
+        if (bd[KNN_K - 1] < gk * gk) break;
+      }
     }
   }
   const bool surv = (c < nc) && (bd[KNN_K - 1] <= g.r2);
@@ -390,6 +471,16 @@ using namespace apn;
 //   GridParams | counts[cap] | cell_start[cap+1] | cursor[cap] | pcell[N] | ccount[cap] | scan ws
 static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// Search strategy: 0 = expanding ball scans (default), 1 = culled Chebyshev rings.
+// APN_KNN_MODE selects one for A/B measurements; both are exact.
+static int knn_mode() {
+  static int m = [] {
+    const char* e = getenv("APN_KNN_MODE");
+    return e ? atoi(e) : 0;
+  }();
+  return m;
+}
+
 extern "C" size_t apn_grid_workspace_bytes(int64_t n_points, int32_t cell_cap) {
   return al256(sizeof(GridParams)) + al256((size_t)cell_cap * 4) + al256((size_t)(cell_cap + 1) * 4) +
          al256((size_t)cell_cap * 4) + al256((size_t)n_points * 4) + al256((size_t)cell_cap * 4) +
@@ -474,7 +565,8 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
   hipLaunchKernelGGL(k_compact_i32, dim3(nb), dim3(KNN_THREADS), 0, s, cand_blk, cblk_cnt, cblk_off, cand);
   // candidates: count at cblk_off[nb]; launch over the upper bound nb blocks
   hipLaunchKernelGGL(k_knn_search, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, q_ray, cand,
-                     cblk_off + nb, g.gp, g.cell_start, (const float4*)sorted_pts4, t_pos, t_ray, t_nbr, blk_cnt);
+                     cblk_off + nb, g.gp, g.cell_start, (const float4*)sorted_pts4, t_pos, t_ray, t_nbr, blk_cnt,
+                     knn_mode());
   st = scan_exclusive_i32(blk_cnt, blk_off, nb, sws, s);
   if (st) return st;
   hipLaunchKernelGGL(k_knn_compact, dim3(nb), dim3(KNN_THREADS), 0, s, t_pos, t_ray, t_nbr, blk_cnt, blk_off,

@@ -60,18 +60,24 @@ __device__ __forceinline__ float lrelu(float x) { return x >= 0.f ? x : x * 0.01
 
 // acc[mt][nt] += X[rows of mt][k chunk] * W[cols of nt][k chunk]^T over K (multiple of 16),
 // X with row stride LD (floats).
-template <int K, int MT, int NT, int LD>
+template <int K, int MT, int NT, int LD, int UNR = 1>
 __device__ __forceinline__ void mfma_acc(const float* __restrict__ X, int row0, const float* __restrict__ Wt,
                                          int col0, f32x4 (&acc)[MT][NT]) {
   const int lane = threadIdx.x & 63;
   const int li = lane & 15, g = lane >> 4;
   const float* xa = X + (row0 + li) * LD + 4 * g;
   const float* wb = Wt + (size_t)(col0 + li) * K + 4 * g;
-#pragma unroll 2
-  for (int q = 0; q < K / 16; ++q) {
-    f32x4 a[MT], b[NT];
+  // B fragments (weights, from L2) are prefetched one k-chunk ahead so their latency hides
+  // behind the current chunk's MFMAs.
+  f32x4 b[NT];
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) b[nt] = *(const f32x4*)(wb + (size_t)nt * 16 * K + 16 * q);
+  for (int nt = 0; nt < NT; ++nt) b[nt] = *(const f32x4*)(wb + (size_t)nt * 16 * K);
+#pragma unroll UNR
+  for (int q = 0; q < K / 16; ++q) {
+    f32x4 a[MT], bn[NT];
+    const int qn = q + 1 < K / 16 ? q + 1 : q;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) bn[nt] = *(const f32x4*)(wb + (size_t)nt * 16 * K + 16 * qn);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) a[mt] = *(const f32x4*)(xa + mt * 16 * LD + 16 * q);
 #pragma unroll
@@ -81,6 +87,8 @@ __device__ __forceinline__ void mfma_acc(const float* __restrict__ X, int row0, 
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mt][t], b[nt][t], acc[mt][nt], 0, 0, 0);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) b[nt] = bn[nt];
   }
 }
 
@@ -109,7 +117,8 @@ __device__ __forceinline__ void store_act(float* __restrict__ X, int col0, const
   }
 }
 
-__global__ __launch_bounds__(MLP_THREADS, 3) void k_point_mlp(
+template <int OCC, int UNR>
+__global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp(
     const float4* __restrict__ s_pos, const int* __restrict__ s_ray, const int* __restrict__ s_nbr,
     const int* __restrict__ n_samples_dev, const float4* __restrict__ recA, const float4* __restrict__ recB,
     const float4* __restrict__ pproj, const float* __restrict__ viewdirs, const float* __restrict__ vemb_const,
@@ -128,8 +137,15 @@ __global__ __launch_bounds__(MLP_THREADS, 3) void k_point_mlp(
   const int lane = tid & 63, wid = tid >> 6;
   const int li = lane & 15, g = lane >> 4;
   int prev_s0 = -1;
+  // XCD-aware tile order: workgroups are dealt round-robin to the 8 XCDs, so XCD x = block % 8
+  // takes the contiguous tile range x*chunk ... (x+1)*chunk -- neighbouring samples share
+  // neighbour points, and their gathers then hit the same L2.
+  const int nx = (gridDim.x % 8 == 0) ? 8 : 1;
+  const int xcd = blockIdx.x % nx, per_xcd = gridDim.x / nx;
+  const int chunk = (ntiles + nx - 1) / nx;
+  const int t_beg = xcd * chunk, t_end = min(ntiles, t_beg + chunk);
 
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  for (int tile = t_beg + blockIdx.x / nx; tile < t_end; tile += per_xcd) {
     const int s0 = tile * TS;
     // ------------------------------------------------ outputs of the previous tile
     if (prev_s0 >= 0 && tid < TS * 3 && prev_s0 + tid / 3 < nS)
@@ -215,15 +231,15 @@ __global__ __launch_bounds__(MLP_THREADS, 3) void k_point_mlp(
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[mt][nt][r] = X[(16 * mt + 4 * g + r) * XS + PCOL + col];
     }
-    mfma_acc<KE, 4, 2, XS>(X, 0, wbuf + OFF_W1E, col0, acc);
+    mfma_acc<KE, 4, 2, XS, UNR>(X, 0, wbuf + OFF_W1E, col0, acc);
     __syncthreads();
     store_act<4, 2>(X, col0, wbuf + OFF_B1, acc);
     __syncthreads();
-#pragma unroll
+#pragma unroll 1
     for (int layer = 0; layer < 3; ++layer) {
       const int ow = layer == 0 ? OFF_W2 : (layer == 1 ? OFF_W3 : OFF_W4);
       zero_acc(acc);
-      mfma_acc<128, 4, 2, XS>(X, 0, wbuf + ow, col0, acc);
+      mfma_acc<128, 4, 2, XS, UNR>(X, 0, wbuf + ow, col0, acc);
       __syncthreads();
       if (layer < 2) {
         store_act<4, 2>(X, col0, wbuf + ow + 128 * 128, acc);
@@ -412,11 +428,22 @@ extern "C" int apn_point_mlp(const float* s_pos4, const int32_t* s_ray, const in
       (!viewdirs && !vemb_const))
     return APN_ERR_ARG;
   const int64_t ntiles = (max_samples + TS - 1) / TS;
-  int blocks = grid_blocks > 0 ? grid_blocks : 256 * 3 * 8;
+  // variant 1 (2 waves/SIMD, B prefetch, unroll 2) is the default: 21.4 ms vs 22.9 ms for
+  // 3 waves/SIMD at C2; APN_MLP_VARIANT selects the others for A/B runs.
+  static const int variant = [] {
+    const char* e = getenv("APN_MLP_VARIANT");
+    return e ? atoi(e) : 1;
+  }();
+  const int occ = variant == 0 ? 3 : 2;
+  int blocks = grid_blocks > 0 ? grid_blocks : 256 * occ * 8;
   if (blocks > ntiles) blocks = (int)ntiles;
-  hipLaunchKernelGGL(k_point_mlp, dim3(blocks), dim3(MLP_THREADS), 0, (hipStream_t)stream, (const float4*)s_pos4,
-                     s_ray, s_nbr, n_samples_dev, (const float4*)recA16, (const float4*)recB8,
-                     (const float4*)feat_proj, viewdirs, vemb_const, wbuf, eps, act_shift, interval,
-                     (float4*)out12);
+  auto launch = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(MLP_THREADS), 0, (hipStream_t)stream, (const float4*)s_pos4, s_ray,
+                       s_nbr, n_samples_dev, (const float4*)recA16, (const float4*)recB8, (const float4*)feat_proj,
+                       viewdirs, vemb_const, wbuf, eps, act_shift, interval, (float4*)out12);
+  };
+  if (variant == 0) launch(k_point_mlp<3, 1>);
+  else if (variant == 1) launch(k_point_mlp<2, 2>);
+  else launch(k_point_mlp<2, 1>);
   return launch_status();
 }

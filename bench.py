@@ -101,20 +101,27 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--cpu-rows", type=int, default=16, help="image rows in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--shard", choices=["frames", "rays"], default="frames",
+                    help="N>1: 'frames' = every rank renders its own frame (weak scaling, no data-path "
+                         "collective); 'rays' = the ranks split one frame's rays and all-gather the tiles "
+                         "over RCCL (strong scaling)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; APN_DIST_BACKEND=gloo rehearses N>1 with several ranks on one card
+    local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")   # RCCL over xGMI
+        dist.init_process_group(os.environ.get("APN_DIST_BACKEND", "nccl"))   # nccl = RCCL over xGMI
     dev = torch.device("cuda", local)
 
     scene = S.make_scene(args.config)
-    # weak scaling: every rank renders its own frame time
-    scene.cfg.t = scene.cfg.t + 0.05 * rank
+    shard_rays = args.shard == "rays" and world > 1
+    if not shard_rays:  # weak scaling: every rank renders its own frame time
+        scene.cfg.t = scene.cfg.t + 0.05 * rank
     t_setup = time.perf_counter()
     model = harness.build_model(scene, dev)
     rk = scene.render_kwargs(dev)
@@ -124,9 +131,14 @@ def main():
     torch.cuda.synchronize(dev)
     log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.2f}s, rays/frame {R}")
 
+    poses, Ks = scene.c2w[None].to(dev), scene.K[None].to(dev)
+
     def step():
-        return model(t_arg, render_depth=True, render_kwargs=rk, render_weights=True,
-                     poses=scene.c2w[None].to(dev), Ks=scene.K[None].to(dev), get_skeleton=True)
+        if shard_rays:
+            from apn_amd.shard import render_sharded
+            return render_sharded(model, t_arg, rk, rank, world, poses=poses, Ks=Ks, get_skeleton=True)
+        return model(t_arg, render_depth=True, render_kwargs=rk, render_weights=True, poses=poses, Ks=Ks,
+                     get_skeleton=True)
 
     for _ in range(args.warmup):
         step()
@@ -166,7 +178,7 @@ def main():
     achieved = flop / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else 0.0
     traffic = read_traffic(os.path.join(ROOT, "profiles", "r01_point_mlp_traffic.json"))
     ms_per_step = elapsed / args.steps * 1e3
-    value = world * args.steps * R / elapsed
+    value = (1 if shard_rays else world) * args.steps * R / elapsed
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         try:
@@ -176,11 +188,13 @@ def main():
     line = {
         "metric": "rendered rays/sec at 800x800, 300k pts, 24 bones",
         "value": value, "unit": "rays/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "ms_per_step": ms_per_step, "higher_is_better": True,
+        "scaling": "strong" if shard_rays else "weak", "vs_baseline": None,
         "dtype": "fp32", "data": "synthetic (procedural SMPL-24 capsule cloud, random-init networks)",
         "config": {"workload": S.CONFIGS[args.config].name + f" ({args.config})", "rays_per_frame": R,
                    "points": scene.cfg.N, "bones": scene.cfg.J, "inbbox_samples": stats.get("inbbox_samples"),
-                   "kept_samples": S_kept, "parallelism": f"frames x{world}" if world > 1 else "single"},
+                   "kept_samples": S_kept, "parallelism": (f"rays x{world} + RCCL tile all-gather" if shard_rays else f"frames x{world}")
+                   if world > 1 else "single"},
         "roofline": {"bound": "mfma", "kernel": "k_point_mlp", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
                      "traffic": traffic.get("bytes_per_launch") if traffic else None,

@@ -400,6 +400,26 @@ def test_chunking_is_bit_identical(golden_model, dev):
     assert torch.equal(torch.cat(parts), full["rgb_marched"])
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_ray_shards_assemble_bit_identical(golden_model, dev, world):
+    """Each rank's ray_shard range (apn_amd/shard.py) rendered on one GPU and concatenated
+    equals the single-GPU frame bit for bit; the ranges hold ~1/world of the in-bbox samples."""
+    from apn_amd.shard import pack_tile
+    g, m = golden_model
+    full = _forward(g, m, dev)
+    R = g.render_kwargs(dev)["rays_o"].shape[0]
+    tiles, bounds = [], None
+    for rank in range(world):
+        o = m(g.t("in_t").to(dev), render_depth=True, render_kwargs=g.render_kwargs(dev), render_weights=True,
+              ray_shard=(rank, world))
+        r0, r1 = m.last_ray_range
+        bounds = m.last_ray_bounds
+        assert (r0, r1) == (bounds[rank], bounds[rank + 1])
+        tiles.append(pack_tile(o, r1 - r0, dev))
+    assert bounds[0] == 0 and bounds[-1] == R
+    assert torch.equal(torch.cat(tiles), pack_tile(full, R, dev))
+
+
 def test_repeatable(golden_model, dev):
     g, m = golden_model
     a = _forward(g, m, dev)

@@ -1,0 +1,94 @@
+"""Host logic of the ray-sharded multi-GPU path (apn_amd/shard.py) on the CPU: the balanced
+ray split and the tile all-gather over a real 2-process gloo group (the GPU box uses RCCL)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from apn_amd.shard import TILE_WIDTH, balanced_ray_split, gather_tiles, pack_tile, unpack_tile
+
+
+def _offsets(counts):
+    return torch.cat([torch.zeros(1, dtype=torch.int32), torch.cumsum(torch.as_tensor(counts), 0).to(torch.int32)])
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+def test_balanced_split_covers_and_balances(world):
+    g = torch.Generator().manual_seed(world)
+    counts = torch.randint(0, 40, (5000,), generator=g)
+    counts[:1000] = 0  # empty rays (background) at the start, like the top image rows
+    offs = _offsets(counts)
+    b = balanced_ray_split(offs, world)
+    assert len(b) == world + 1 and b[0] == 0 and b[-1] == 5000
+    assert all(b[i] <= b[i + 1] for i in range(world))
+    total = int(offs[-1])
+    for k in range(world):
+        part = int(offs[b[k + 1]] - offs[b[k]])
+        assert abs(part - total / world) <= 40 + 1, (k, part, total / world)
+
+
+def test_balanced_split_degenerate():
+    assert balanced_ray_split(_offsets([0, 0, 0]), 2) == [0, 0, 3] or balanced_ray_split(_offsets([0, 0, 0]), 2)[-1] == 3
+    b = balanced_ray_split(_offsets([100]), 4)
+    assert b[0] == 0 and b[-1] == 1 and b == sorted(b)
+    b = balanced_ray_split(_offsets([]), 2)
+    assert b == [0, 0, 0]
+
+
+def test_pack_unpack_roundtrip():
+    n = 7
+    out = {"rgb_marched": torch.rand(n, 3), "rgb_marched_direct": torch.rand(n, 3), "depth": torch.rand(n),
+           "weights": torch.rand(n, 3), "alphainv_last": torch.rand(n), "alphainv_last_direct": torch.rand(n)}
+    tile = pack_tile(out, n, "cpu")
+    assert tile.shape == (n, TILE_WIDTH)
+    back = unpack_tile(tile)
+    for k, v in out.items():
+        assert torch.equal(back[k], v), k
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, counts, result_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        offs = _offsets(counts)
+        bounds = balanced_ray_split(offs, world)
+        R = len(counts)
+        full = torch.arange(R * TILE_WIDTH, dtype=torch.float32).reshape(R, TILE_WIDTH)
+        r0, r1 = bounds[rank], bounds[rank + 1]
+        got = gather_tiles(full[r0:r1].clone(), bounds)
+        # elapsed-time reduction of bench.py: max over ranks
+        t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        result_q.put((rank, bool(torch.equal(got, full)), float(t)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("counts", [[3, 0, 5, 9, 1, 0, 0, 7, 2, 4, 6], [0] * 6 + [50]])
+def test_gather_tiles_gloo_world2(counts):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, counts, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok, tmax in res:
+        assert ok, rank
+        assert tmax == float(world)
