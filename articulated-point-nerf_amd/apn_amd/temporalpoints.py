@@ -12,6 +12,7 @@ are built once per call instead of once per chunk.
 from __future__ import annotations
 
 import colorsys
+import os
 import ctypes as C
 
 import numpy as np
@@ -24,7 +25,7 @@ from .pointwarper import PointWarper
 from .shard import balanced_ray_split
 from .tineuvox import poc_fre
 
-CELL_CAP = 1 << 20
+CELL_CAP = int(os.environ.get("APN_CELL_CAP", 1 << 20))
 
 
 class NoPointsException(Exception):

@@ -511,7 +511,11 @@ extern "C" int apn_grid_build(const float* xyz, int64_t n_points, const int32_t*
   APN_HIP_TRY(hipMemsetAsync(w.counts, 0, (size_t)cell_cap * 4, s));
   APN_HIP_TRY(hipMemsetAsync(w.cursor, 0, (size_t)cell_cap * 4, s));
   APN_HIP_TRY(hipMemsetAsync(w.ccount, 0, (size_t)cell_cap * 4, s));
-  hipLaunchKernelGGL(k_grid_params, dim3(1), dim3(64), 0, s, bbox_ord, query_radius, cell_cap, KNN_SUBDIV, w.gp);
+  static const int subdiv = [] {
+    const char* e = getenv("APN_KNN_SUBDIV");
+    return e ? atoi(e) : KNN_SUBDIV;
+  }();
+  hipLaunchKernelGGL(k_grid_params, dim3(1), dim3(64), 0, s, bbox_ord, query_radius, cell_cap, subdiv, w.gp);
   hipLaunchKernelGGL(k_grid_count, dim3(ceil_div(n_points, 256)), dim3(256), 0, s, xyz, n_points, w.gp, w.counts,
                      w.ccount, w.pcell);
   int st = scan_exclusive_i32(w.counts, w.cell_start, cell_cap, w.scan, s);

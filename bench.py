@@ -161,6 +161,24 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t)
+    if os.environ.get("APN_MLP_VARIANT") == "6":   # timed wave-local MLP: N / M / barrier split
+        import ctypes
+        from apn_amd import _lib
+        ph = (ctypes.c_uint64 * 6)()
+        _lib.call("apn_debug_mlp_phase_cycles", ph)
+        tot = max(ph[5], 1)
+        log("[mlp_w phases] " + ", ".join(f"{n} {100 * ph[i] / tot:.1f}%" for i, n in
+                                          enumerate(["N work", "M work", "barrier wait"]))
+            + f"; M cycles/tile {ph[1] / max(ph[4], 1):.0f}, N cycles/tile {ph[0] / max(ph[4], 1):.0f}")
+    if os.environ.get("APN_MLP_VARIANT") == "3":   # timed MLP variant: per-phase cycle split
+        import ctypes
+        from apn_amd import _lib
+        ph = (ctypes.c_uint64 * 6)()
+        _lib.call("apn_debug_mlp_phase_cycles", ph)
+        tot = sum(ph[:4]) or 1
+        log("[mlp phases] " + ", ".join(f"{n} {100 * ph[i] / tot:.1f}%" for i, n in
+                                        enumerate(["gather", "layer1", "layers2-4", "epilogue"]))
+            + f"; cycles/tile {tot / max(ph[4], 1):.0f}, in-loop share {tot / max(ph[5], 1):.3f}")
     ev = model.timing.get("mlp_events", [])
     mlp_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / max(len(ev), 1)
     S_kept = ev[-1][2] if ev else stats.get("kept_samples", 0)

@@ -144,6 +144,11 @@ int apn_composite(const float* smp12, const float* s_pos4, const int32_t* s_ray,
                   float* depth, float* weights_vis, float* alphainv_last,
                   float* alphainv_last_direct, int32_t* ray_ws, void* stream);
 
+/* Profiling aid (synchronous): per-phase cycle sums of the timed k_point_mlp variant
+ * (APN_MLP_VARIANT=3) {gather, layer 1, layers 2-4, epilogue, tiles, kernel cycles}, summed over
+ * workgroups since the last call; resets them. */
+int apn_debug_mlp_phase_cycles(uint64_t* out6);
+
 /* Utilities */
 size_t apn_scan_workspace_bytes(int64_t n);
 int apn_scan_exclusive_i32(const int32_t* in, int32_t* out, int64_t n, void* workspace, void* stream);
