@@ -60,7 +60,8 @@ constexpr int W_TOTAL = OFF_W1F + 128 * 128;
 constexpr int SW_B1 = 0, SW_B2 = 128, SW_B3 = 256, SW_B4 = 384, SW_WD = 512, SW_BD = 640, SW_BH = 644,
               SW_WV2 = 708, SW_BV2 = 900, SW_TOTAL = 904;
 
-__device__ __forceinline__ float lrelu(float x) { return x >= 0.f ? x : x * 0.01f; }
+// LeakyReLU(0.01): x >= 0 ? x : 0.01x == max(x, 0.01x) (the same rounded product; 2 VALU ops)
+__device__ __forceinline__ float lrelu(float x) { return fmaxf(x, x * 0.01f); }
 
 // acc[mt][nt] += X[rows of mt][k chunk] * W[cols of nt][k chunk]^T over K (multiple of 16),
 // X with row stride LD (floats).
@@ -107,14 +108,23 @@ __device__ __forceinline__ void mfma_acc_pf(const float* __restrict__ X, const f
   const float* xa = X + li * LD + 4 * g;
   const float* wb = Wt + (size_t)(col0 + li) * K + 4 * g;
   const float* wn = Wn + (size_t)(col0 + li) * KN + 4 * g;
-#pragma unroll UNR
+  // software pipeline: the A (LDS) and B (L2) fragments of chunk q+1 are issued before the
+  // MFMAs of chunk q; sched_barrier pins the issue point so the scheduler cannot sink the
+  // loads next to their use (which exposed the L2 latency once per chunk).
+  f32x4 a[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) a[mt] = *(const f32x4*)(xa + mt * 16 * LD);
+#pragma unroll 2
   for (int q = 0; q < K / 16; ++q) {
-    f32x4 a[MT], bn[NT];
+    f32x4 an[MT], bn[NT];
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
       bn[nt] = *(const f32x4*)(q + 1 < K / 16 ? wb + (size_t)nt * 16 * K + 16 * (q + 1) : wn + (size_t)nt * 16 * KN);
+    if (q + 1 < K / 16) {
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) a[mt] = *(const f32x4*)(xa + mt * 16 * LD + 16 * q);
+      for (int mt = 0; mt < MT; ++mt) an[mt] = *(const f32x4*)(xa + mt * 16 * LD + 16 * (q + 1));
+    }
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -122,8 +132,13 @@ __device__ __forceinline__ void mfma_acc_pf(const float* __restrict__ X, const f
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mt][t], b[nt][t], acc[mt][nt], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) b[nt] = bn[nt];
+    if (q + 1 < K / 16) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) a[mt] = an[mt];
+    }
   }
 }
 
@@ -497,355 +512,6 @@ __global__ __launch_bounds__(256) void k_feat_project(const float4* __restrict__
   }
 }
 
-// ============================================================================================
-// Wave-local ping-pong variant (default). Every wave owns whole rows: a wave tile is 2 samples x
-// 8 neighbours = 16 MLP rows and the wave computes all 128 output columns of every layer (one
-// 16-row M-tile x 8 N-tiles), so a tile never needs another wave -- no barriers inside the MLP.
-// A workgroup of 8 waves (2 per SIMD) runs two groups in anti-phase: while group 0 (waves 0-3,
-// one per SIMD) issues the feat_net MFMAs of its tiles, group 1 (waves 4-7) gathers and
-// finishes (heads, direct blend) its own, and vice versa; one s_barrier per phase keeps them
-// anti-aligned so each SIMD's matrix pipe always has a wave feeding it. Heads run on VALU
-// (2 samples per wave) with the folded head weights transposed in LDS.
-constexpr int W_TS = 2;          // samples per wave tile
-constexpr int W_ROWS = 16;       // MLP rows per wave tile
-constexpr int WXS = 136;         // X row stride (== 8 mod 64: conflict-free A-fragment reads)
-constexpr int W_WAVES = 8;
-constexpr int W_THREADS = 64 * W_WAVES;
-
-struct WaveLds {
-  float X[W_ROWS * WXS];         // layer input/activations of the wave's 16 rows
-  float to[W_ROWS];              // to_nn per row
-  float idw[W_ROWS];             // normalised IDW weight per row
-  float row[W_ROWS * 8];         // direct-blend terms per row: wdir, alpha_c, rgb_c(3), pcol(3)
-  float h[W_TS * KV];            // head input per sample: h (128), view embedding (27), zeros
-  float hid[W_TS * 64];          // head hidden layer (after ReLU)
-  float out[W_TS * 12];          // per-sample outputs
-  int nbr[W_ROWS];
-};
-
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// acc[0][nt] += X[16 rows][K] * W[16nt + (0..15)][K]^T for nt = 0..7 (all 128 columns); B
-// fragments double-buffered in registers.
-template <int K>
-__device__ __forceinline__ void mfma_rows16(const float* __restrict__ X, const float* __restrict__ Wt,
-                                            f32x4 (&acc)[8]) {
-  const int lane = threadIdx.x & 63;
-  const int li = lane & 15, g = lane >> 4;
-  const float* xa = X + li * WXS + 4 * g;
-  const float* wb = Wt + (size_t)li * K + 4 * g;
-  f32x4 b[8];
-#pragma unroll
-  for (int nt = 0; nt < 8; ++nt) b[nt] = *(const f32x4*)(wb + (size_t)nt * 16 * K);
-#pragma unroll 2
-  for (int q = 0; q < K / 16; ++q) {
-    f32x4 bn[8];
-    const int qn = q + 1 < K / 16 ? q + 1 : q;
-#pragma unroll
-    for (int nt = 0; nt < 8; ++nt) bn[nt] = *(const f32x4*)(wb + (size_t)nt * 16 * K + 16 * qn);
-    const f32x4 a = *(const f32x4*)(xa + 16 * q);
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int nt = 0; nt < 8; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], b[nt][t], acc[nt], 0, 0, 0);
-#pragma unroll
-    for (int nt = 0; nt < 8; ++nt) b[nt] = bn[nt];
-  }
-}
-
-// lrelu(acc + bias) -> X rows 4g + r, column 16nt + li
-__device__ __forceinline__ void store_rows16(float* __restrict__ X, const float* __restrict__ bias,
-                                             const f32x4 (&acc)[8]) {
-  const int lane = threadIdx.x & 63;
-  const int li = lane & 15, g = lane >> 4;
-#pragma unroll
-  for (int nt = 0; nt < 8; ++nt) {
-    const float bb = bias[16 * nt + li];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) X[(4 * g + r) * WXS + 16 * nt + li] = lrelu(acc[nt][r] + bb);
-  }
-}
-
-template <bool TIMED>
-__global__ __launch_bounds__(W_THREADS, 2) void k_point_mlp_w(
-    const float4* __restrict__ s_pos, const int* __restrict__ s_ray, const int* __restrict__ s_nbr,
-    const int* __restrict__ n_samples_dev, const float4* __restrict__ recA, const float4* __restrict__ recB,
-    const float* __restrict__ pproj, const float* __restrict__ viewdirs, const float* __restrict__ vemb_const,
-    const float* __restrict__ wbuf, float eps, float shift, float interval, float4* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) float sWHt[KV * 64];   // folded head weights, [input][output]
-  __shared__ float sW[SW_TOTAL];
-  __shared__ __attribute__((aligned(16))) WaveLds sL[W_WAVES];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int li = lane & 15, g = lane >> 4;
-
-  for (int i = tid; i < 64 * KV; i += W_THREADS) sWHt[(i % KV) * 64 + i / KV] = wbuf[OFF_WH + i];
-  for (int i = tid; i < 128; i += W_THREADS) {
-    sW[SW_B1 + i] = wbuf[OFF_B1 + i];
-    sW[SW_B2 + i] = wbuf[OFF_B2 + i];
-    sW[SW_B3 + i] = wbuf[OFF_B3 + i];
-    sW[SW_B4 + i] = wbuf[OFF_B4 + i];
-    sW[SW_WD + i] = wbuf[OFF_WD + i];
-  }
-  if (tid < 64) sW[SW_BH + tid] = wbuf[OFF_BH + tid];
-  if (tid < 192) sW[SW_WV2 + tid] = wbuf[OFF_WV2 + tid];
-  if (tid < 3) sW[SW_BV2 + tid] = wbuf[OFF_BV2 + tid];
-  if (tid == 0) sW[SW_BD] = wbuf[OFF_BD];
-  __syncthreads();
-
-  const int nS = *n_samples_dev;
-  const int ntiles = (nS + W_TS - 1) / W_TS;
-  // XCD-aware contiguous tile ranges (see k_point_mlp); wave slots within the XCD's range
-  const int nx = (gridDim.x % 8 == 0) ? 8 : 1;
-  const int xcd = blockIdx.x % nx, per_xcd = gridDim.x / nx;
-  const int chunk = (ntiles + nx - 1) / nx;
-  const int t_beg = xcd * chunk, t_end = min(ntiles, t_beg + chunk);
-  const int navail = max(t_end - t_beg, 0);
-  const int slots = per_xcd * W_WAVES;
-  const int slot0 = (blockIdx.x / nx) * W_WAVES, slot = slot0 + wid;
-  const int T = navail > slot0 ? (navail - slot0 + slots - 1) / slots : 0;    // block-uniform phase bound
-  const int myT = navail > slot ? (navail - slot + slots - 1) / slots : 0;
-  const int grp = wid >> 2;
-  WaveLds& L = sL[wid];
-
-  // gather coordinates: lane -> row r = (sample j, neighbour k), quarter p
-  const int r = lane >> 2, p = lane & 3, j = r >> 3, k = r & 7;
-  float pinit[8][4];   // P rows of this lane's C-layout rows (layer-1 accumulator init)
-
-  auto gather = [&](int i) {
-    const int tile = t_beg + slot + i * slots;
-    const int gs = tile * W_TS + j;
-    float* xr = L.X + r * WXS;
-    if (gs < nS) {
-      const int nb = s_nbr[(size_t)gs * 8 + k];
-      const float4 q = s_pos[gs];
-      const int ray = s_ray[gs];
-      const float4 a0 = recA[4 * (size_t)nb + 0];
-      const float4 a1 = recA[4 * (size_t)nb + 1];
-      const float4 a2 = recA[4 * (size_t)nb + 2];
-      const float4 a3 = recA[4 * (size_t)nb + 3];
-      const float dx = q.x - a0.x, dy = q.y - a0.y, dz = q.z - a0.z;
-      const float rc0 = (a1.x * dx + a1.y * dy) + a1.z * dz;
-      const float rc1 = (a1.w * dx + a2.x * dy) + a2.y * dz;
-      const float rc2 = (a2.z * dx + a2.w * dy) + a3.x * dz;
-      const float tn = (dx * dx + dy * dy) + dz * dz;
-      if (p == 0) {
-        L.to[r] = tn;
-        L.nbr[r] = nb;
-        xr[0] = rc0; xr[1] = rc1; xr[2] = rc2;
-        xr[KE - 1] = 0.f;
-      } else if (p == 1) {
-        const float4 b0 = recB[2 * (size_t)nb], b1 = recB[2 * (size_t)nb + 1];
-        float* rw = L.row + 8 * r;
-        rw[0] = expf(-(tn * tn) / a0.w);   // temporalpoints.py:461 (to_nn is already squared)
-        rw[1] = a3.y;
-        rw[2] = b0.x; rw[3] = b0.y; rw[4] = b0.z;
-        rw[5] = b1.x; rw[6] = b1.y; rw[7] = b1.z;
-      }
-#pragma unroll
-      for (int m = 0; m < 8; ++m) {   // 30 arguments rc[i] * 2^f (a = 10 i + f): sin col 3 + a, cos col 33 + a
-        const int a = p + 4 * m;
-        if (a < 30) {
-          const int ci = a / 10;
-          const float v = (ci == 0 ? rc0 : (ci == 1 ? rc1 : rc2)) * (float)(1 << (a - 10 * ci));
-          float sv, cv;
-          sincosf(v, &sv, &cv);
-          xr[3 + a] = sv;
-          xr[33 + a] = cv;
-        }
-      }
-      // view embedding element e of sample j: poc_fre(viewdirs, 2^0..2^3) = [v, sin (12), cos (12)]
-      const int e = 4 * k + p;
-      float v = 0.f;
-      if (e < 27) {
-        if (vemb_const) {
-          v = vemb_const[e];
-        } else {
-          const int ee = e < 3 ? 0 : (e < 15 ? e - 3 : e - 15);
-          const int ci = e < 3 ? e : ee >> 2;
-          const float vv = viewdirs[3 * ray + ci];
-          const float arg = vv * (float)(1 << (ee & 3));
-          v = e < 3 ? vv : (e < 15 ? sinf(arg) : cosf(arg));
-        }
-      }
-      L.h[j * KV + 128 + e] = v;
-    } else {
-      for (int c = p; c < KE; c += 4) xr[c] = 0.f;
-      L.h[j * KV + 128 + 4 * k + p] = 0.f;
-      if (p == 0) {
-        L.to[r] = 1.f;
-        L.nbr[r] = -1;
-      } else if (p == 1) {
-        for (int c = 0; c < 8; ++c) L.row[8 * r + c] = 0.f;
-      }
-    }
-    wave_sync();
-    if (lane < W_ROWS) {  // IDW weights (temporalpoints.py:473-475), normalised over the sample's 8 rows
-      const int jj = lane >> 3;
-      float w[8], sum = 0.f;
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
-        w[kk] = 1.f / (L.to[jj * 8 + kk] + eps);
-        sum += w[kk];
-      }
-      L.idw[lane] = w[lane & 7] / sum;
-    }
-    // layer-1 accumulator init: P[nbr(row)][col] for the C-layout rows 4g + rr, columns 16nt + li
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int nb = L.nbr[4 * g + rr];
-      const float* pr = pproj + (size_t)max(nb, 0) * FEAT + li;
-#pragma unroll
-      for (int nt = 0; nt < 8; ++nt) pinit[nt][rr] = nb >= 0 ? pr[16 * nt] : 0.f;
-    }
-  };
-
-  auto mlp = [&]() {  // feat_net (4 x Linear + LeakyReLU) on FP32 MFMA + IDW reduction -> L.h
-    f32x4 acc[8];
-#pragma unroll
-    for (int nt = 0; nt < 8; ++nt) acc[nt] = f32x4{pinit[nt][0], pinit[nt][1], pinit[nt][2], pinit[nt][3]};
-    mfma_rows16<KE>(L.X, wbuf + OFF_W1E, acc);
-    store_rows16(L.X, sW + SW_B1, acc);
-    wave_sync();
-#pragma unroll 1
-    for (int layer = 0; layer < 3; ++layer) {
-      const int ow = layer == 0 ? OFF_W2 : (layer == 1 ? OFF_W3 : OFF_W4);
-#pragma unroll
-      for (int nt = 0; nt < 8; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      mfma_rows16<128>(L.X, wbuf + ow, acc);
-      if (layer < 2) {
-        store_rows16(L.X, sW + SW_B2 + 128 * layer, acc);
-        wave_sync();
-      }
-    }
-    // h_s = sum_k w_k lrelu(out_k + b4): rows 4g + rr -> sample g >> 1, neighbour 4(g & 1) + rr;
-    // the neighbour order of the sum is sequential (k = 0..7), as in the reference
-    float iw[4];
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) iw[rr] = L.idw[4 * g + rr];
-#pragma unroll
-    for (int nt = 0; nt < 8; ++nt) {
-      const float bb = sW[SW_B4 + 16 * nt + li];
-      float pr[4], o[4];
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) pr[rr] = iw[rr] * lrelu(acc[nt][rr] + bb);
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) o[rr] = __shfl_xor(pr[rr], 16, 64);
-      float h = 0.f;
-      h = ((h + pr[0]) + pr[1]) + pr[2];
-      h = h + pr[3];
-      h = (((h + o[0]) + o[1]) + o[2]) + o[3];
-      if ((g & 1) == 0) L.h[(g >> 1) * KV + 16 * nt + li] = h;
-    }
-    wave_sync();
-  };
-
-  auto finish = [&](int i) {  // heads + direct blend + outputs of the wave's 2 samples
-    const int tile = t_beg + slot + i * slots;
-    const int s0 = tile * W_TS;
-    {  // densitynet: lane = (sample, 4-column part) -> raw2alpha (temporalpoints.py:496-499)
-      const int jj = lane >> 5, part = lane & 31;
-      const float* hr = L.h + jj * KV + 4 * part;
-      const float* wd = sW + SW_WD + 4 * part;
-      float a = ((hr[0] * wd[0] + hr[1] * wd[1]) + hr[2] * wd[2]) + hr[3] * wd[3];
-#pragma unroll
-      for (int o = 1; o < 32; o <<= 1) a += __shfl_xor(a, o, 64);
-      if (part == 0) {
-        const float ex = expf((a + sW[SW_BD]) + shift);
-        L.out[12 * jj + 3] = 1.f - powf(1.f + ex, -interval);
-      }
-    }
-    {  // folded rgb layer (155 -> 64) + ReLU: lane = output column, both samples
-      float h0 = sW[SW_BH + lane], h1 = h0;
-      const float* x0 = L.h;
-      const float* x1 = L.h + KV;
-#pragma unroll 8
-      for (int c = 0; c < KV; ++c) {
-        const float w = sWHt[c * 64 + lane];
-        h0 = fmaf(x0[c], w, h0);
-        h1 = fmaf(x1[c], w, h1);
-      }
-      L.hid[lane] = fmaxf(h0, 0.f);
-      L.hid[64 + lane] = fmaxf(h1, 0.f);
-    }
-    if (lane < 16) {  // direct blend + weight-vis colour (temporalpoints.py:459-470, 517-519)
-      const int jj = lane >> 3, qn = lane & 7;
-      const float* rw = L.row + 64 * jj;
-      float sumd = 0.f;
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) sumd += rw[8 * kk];
-      const float dn = sumd + 1e-12f;
-      float acc1 = 0.f;
-      if (qn == 0) {
-#pragma unroll
-        for (int kk = 0; kk < 8; ++kk) acc1 += (0.125f * rw[8 * kk]) * rw[8 * kk + 1];
-      } else if (qn < 4) {
-#pragma unroll
-        for (int kk = 0; kk < 8; ++kk) acc1 += (rw[8 * kk] / dn) * rw[8 * kk + 1 + qn];
-      } else if (qn < 7) {
-#pragma unroll
-        for (int kk = 0; kk < 8; ++kk) acc1 += L.idw[8 * jj + kk] * rw[8 * kk + 1 + qn];
-      }
-      const int slot_o = qn == 0 ? 7 : (qn < 4 ? 3 + qn : (qn < 7 ? 4 + qn : 11));
-      L.out[12 * jj + slot_o] = acc1;
-    }
-    wave_sync();
-    if (lane < 48) {  // views_linears.2 (64 -> 3) + sigmoid: lane = (sample, output, 8-column part)
-      const int jj = lane / 24, o = (lane % 24) >> 3, part = lane & 7;
-      const float* hr = L.hid + 64 * jj + 8 * part;
-      const float* w2 = sW + SW_WV2 + o * 64 + 8 * part;
-      float a = 0.f;
-#pragma unroll
-      for (int c = 0; c < 8; ++c) a += hr[c] * w2[c];
-      a += __shfl_xor(a, 1, 64);
-      a += __shfl_xor(a, 2, 64);
-      a += __shfl_xor(a, 4, 64);
-      if (part == 0) L.out[12 * jj + o] = 1.f / (1.f + expf(-(a + sW[SW_BV2 + o])));
-    }
-    wave_sync();
-    if (lane < 3 * W_TS && s0 + lane / 3 < nS) out[(size_t)s0 * 3 + lane] = *(const float4*)(L.out + 4 * lane);
-    wave_sync();
-  };
-
-  // phase schedule: group 0 runs lp = step, group 1 lp = step - 1; lp 0: gather(0);
-  // lp odd: mlp of tile (lp-1)/2; lp even > 0: finish((lp-2)/2) + gather(lp/2)
-  unsigned long long tn = 0, tm = 0, tb = 0, t0 = 0, t1 = 0;
-  if (TIMED) t0 = clock64();
-  for (int step = 0; step <= 2 * T + 1; ++step) {
-    const int lp = step - grp;
-    if (TIMED) t1 = clock64();
-    bool m = false;
-    if (lp >= 0) {
-      if (lp & 1) {
-        const int i = (lp - 1) >> 1;
-        if (i < myT) mlp();
-        m = true;
-      } else {
-        const int i = lp >> 1;
-        if (i >= 1 && i - 1 < myT) finish(i - 1);
-        if (i < myT) gather(i);
-      }
-    }
-    unsigned long long t2 = 0;
-    if (TIMED) {
-      t2 = clock64();
-      if (m) tm += t2 - t1; else tn += t2 - t1;
-    }
-    __builtin_amdgcn_s_barrier();
-    if (TIMED) tb += clock64() - t2;
-  }
-  if (TIMED && lane == 0) {  // per wave: {N-phase work, M-phase work, barrier wait, -, tiles, total}
-    atomicAdd(&g_mlp_phase[0], tn);
-    atomicAdd(&g_mlp_phase[1], tm);
-    atomicAdd(&g_mlp_phase[2], tb);
-    atomicAdd(&g_mlp_phase[4], (unsigned long long)myT);
-    atomicAdd(&g_mlp_phase[5], clock64() - t0);
-  }
-}
-
 }  // namespace apn
 
 using namespace apn;
@@ -898,21 +564,9 @@ extern "C" int apn_point_mlp(const float* s_pos4, const int32_t* s_ray, const in
                        s_nbr, n_samples_dev, (const float4*)recA16, (const float4*)recB8, (const float4*)feat_proj,
                        viewdirs, vemb_const, wbuf, eps, act_shift, interval, (float4*)out12);
   };
-  // APN_MLP_VARIANT: 0 = k_point_mlp (default), 3 = its phase-timed build, 5/6 = the wave-local
-  // ping-pong kernel (experimental; 6 = timed). All variants compute the same result.
+  // APN_MLP_VARIANT=3 selects the phase-timed build (profiling aid; same results).
   if (variant == 3) {
     launch(k_point_mlp<2, 2, true>);
-  } else if (variant == 5 || variant == 6) {
-    const int64_t wtiles = (max_samples + W_TS - 1) / W_TS;
-    int wblocks = grid_blocks > 0 ? grid_blocks : 256 * 8;   // one 8-wave workgroup per CU at a time
-    if ((int64_t)wblocks * W_WAVES > wtiles) wblocks = (int)((wtiles + W_WAVES - 1) / W_WAVES);
-    auto wl = [&](auto kern) {
-      hipLaunchKernelGGL(kern, dim3(wblocks), dim3(W_THREADS), 0, (hipStream_t)stream, (const float4*)s_pos4, s_ray,
-                         s_nbr, n_samples_dev, (const float4*)recA16, (const float4*)recB8, feat_proj, viewdirs,
-                         vemb_const, wbuf, eps, act_shift, interval, (float4*)out12);
-    };
-    if (variant == 6) wl(k_point_mlp_w<true>);
-    else wl(k_point_mlp_w<false>);
   } else {
     launch(k_point_mlp<2, 2>);
   }

@@ -161,15 +161,6 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t)
-    if os.environ.get("APN_MLP_VARIANT") == "6":   # timed wave-local MLP: N / M / barrier split
-        import ctypes
-        from apn_amd import _lib
-        ph = (ctypes.c_uint64 * 6)()
-        _lib.call("apn_debug_mlp_phase_cycles", ph)
-        tot = max(ph[5], 1)
-        log("[mlp_w phases] " + ", ".join(f"{n} {100 * ph[i] / tot:.1f}%" for i, n in
-                                          enumerate(["N work", "M work", "barrier wait"]))
-            + f"; M cycles/tile {ph[1] / max(ph[4], 1):.0f}, N cycles/tile {ph[0] / max(ph[4], 1):.0f}")
     if os.environ.get("APN_MLP_VARIANT") == "3":   # timed MLP variant: per-phase cycle split
         import ctypes
         from apn_amd import _lib
