@@ -38,9 +38,11 @@ SIGNATURES = {
     "apn_knn_radius": (C.c_int, [P, P, I64, P, P, I64, I32, P, F32, P, P, P, P, P, P]),
     "apn_nn1_distance": (C.c_int, [P, I64, F32, I32, P, P, P, P, P]),
     "apn_mlp_weight_layout": (C.c_int, [P]),
+    "apn_mlp_split_weights": (C.c_int, [P, P]),
     "apn_feat_project": (C.c_int, [P, I64, I32, P, P, P]),
     "apn_point_mlp": (C.c_int, [P, P, P, I64, P, P, P, P, I32, P, P, P, F32, F32, F32, I32, P, P]),
     "apn_composite": (C.c_int, [P, P, P, I64, P, I64, F32, F32, P, P, P, P, P, P, P, P]),
+    "apn_set_mlp_variant": (C.c_int, [I32]),
     "apn_debug_mlp_phase_cycles": (C.c_int, [P]),
     "apn_scan_workspace_bytes": (SZ, [I64]),
     "apn_scan_exclusive_i32": (C.c_int, [P, P, I64, P, P]),

@@ -106,7 +106,7 @@ def segment_coo_sum(src, index, n_out):
 
 _LAYOUT = None
 _LAYOUT_NAMES = ["W1E", "B1", "W2", "B2", "W3", "B3", "W4", "B4", "WD", "BD", "WH", "BH", "WV2", "BV2", "W1F",
-                 "TOTAL", "KE", "KV"]
+                 "TOTAL", "KE", "KV", "H16"]
 
 
 def mlp_layout():
@@ -132,6 +132,7 @@ def pack_mlp_weights(feat_net_layers, densitynet, rgbnet, pose_embedding=None, o
     l1, l2, l3, l4 = feat_net_layers
     dev = l1.weight.device
     buf = out if out is not None else torch.zeros(lay["TOTAL"], device=dev)
+    L.require_cuda(buf, what="pack_mlp_weights")
     KE, KV = lay["KE"], lay["KV"]
 
     def put(name, t):
@@ -167,6 +168,9 @@ def pack_mlp_weights(feat_net_layers, densitynet, rgbnet, pose_embedding=None, o
     put("BH", wv0[:, :nh] @ bf + v0.bias.detach().double())
     v2 = rgbnet.views_linears[2]
     put("WV2", v2.weight); put("BV2", v2.bias)
+    # fp16 hi/lo MFMA fragments of W1E (posenc columns reordered), W2-W4 and WH for the default
+    # (3-term split) apn_point_mlp kernel
+    call("apn_mlp_split_weights", ptr(buf), stream_ptr(dev))
     return buf
 
 

@@ -22,46 +22,18 @@
 // k-permutation: for a 16-wide k chunk q, lane group g = lane>>4 holds k = 16q + 4g + t in
 // element t of its float4, for both A (activations) and B (nn.Linear weight rows), so one
 // 16-byte load feeds 4 MFMAs.
-#include "apn_common.h"
+#include "apn_mlp_layout.h"
 
 namespace apn {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int TS = 8;             // samples per tile
-constexpr int TR = TS * 8;        // MLP rows per tile
 constexpr int XS = 200;           // LDS row stride (floats)
-constexpr int MLP_THREADS = 256;
-constexpr int FEAT = 128;
-constexpr int KE = 64;            // positional encoding 63, zero-padded
 constexpr int PCOL = 64;          // LDS column where the gathered P row starts
-constexpr int KV = 160;           // head input: h (128) + view embedding (27) + pad
-
-// Packed weight buffer layout (floats); apn_amd/ops.py:pack_mlp_weights reads it through
-// apn_mlp_weight_layout().
-constexpr int OFF_W1E = 0;                        // [128][64]  feat_net.0 columns 0..62
-constexpr int OFF_B1 = OFF_W1E + 128 * KE;        // [128]      (+ pose-embedding fold)
-constexpr int OFF_W2 = OFF_B1 + 128;              // [128][128]
-constexpr int OFF_B2 = OFF_W2 + 128 * 128;
-constexpr int OFF_W3 = OFF_B2 + 128;
-constexpr int OFF_B3 = OFF_W3 + 128 * 128;
-constexpr int OFF_W4 = OFF_B3 + 128;
-constexpr int OFF_B4 = OFF_W4 + 128 * 128;
-constexpr int OFF_WD = OFF_B4 + 128;              // [128]      densitynet
-constexpr int OFF_BD = OFF_WD + 128;              // [4]
-constexpr int OFF_WH = OFF_BD + 4;                // [64][160]  folded rgb head layer
-constexpr int OFF_BH = OFF_WH + 64 * KV;          // [64]
-constexpr int OFF_WV2 = OFF_BH + 64;              // [3][64]    views_linears.2
-constexpr int OFF_BV2 = OFF_WV2 + 3 * 64;         // [4]
-constexpr int OFF_W1F = OFF_BV2 + 4;              // [128][128] feat_net.0 columns 63..190 (for P)
-constexpr int W_TOTAL = OFF_W1F + 128 * 128;
 
 // Small weights staged in LDS once per workgroup (biases, densitynet, views_linears.2).
 constexpr int SW_B1 = 0, SW_B2 = 128, SW_B3 = 256, SW_B4 = 384, SW_WD = 512, SW_BD = 640, SW_BH = 644,
               SW_WV2 = 708, SW_BV2 = 900, SW_TOTAL = 904;
-
-// LeakyReLU(0.01): x >= 0 ? x : 0.01x == max(x, 0.01x) (the same rounded product; 2 VALU ops)
-__device__ __forceinline__ float lrelu(float x) { return fmaxf(x, x * 0.01f); }
 
 // acc[mt][nt] += X[rows of mt][k chunk] * W[cols of nt][k chunk]^T over K (multiple of 16),
 // X with row stride LD (floats).
@@ -518,7 +490,7 @@ using namespace apn;
 
 extern "C" int apn_mlp_weight_layout(int32_t* offsets) {
   const int32_t v[] = {OFF_W1E, OFF_B1, OFF_W2, OFF_B2, OFF_W3, OFF_B3, OFF_W4, OFF_B4, OFF_WD, OFF_BD,
-                       OFF_WH, OFF_BH, OFF_WV2, OFF_BV2, OFF_W1F, W_TOTAL, KE, KV};
+                       OFF_WH, OFF_BH, OFF_WV2, OFF_BV2, OFF_W1F, W_TOTAL, KE, KV, OFF_H16};
   for (int i = 0; i < (int)(sizeof(v) / sizeof(v[0])); ++i) offsets[i] = v[i];
   return (int)(sizeof(v) / sizeof(v[0]));
 }
@@ -535,6 +507,21 @@ extern "C" int apn_feat_project(const float* canonical_feat, int64_t n_points, i
   return launch_status();
 }
 
+// Kernel selection: initialised from APN_MLP_VARIANT, changed by apn_set_mlp_variant.
+static int& mlp_variant() {
+  static int v = [] {
+    const char* e = getenv("APN_MLP_VARIANT");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+extern "C" int apn_set_mlp_variant(int32_t variant) {
+  const int prev = mlp_variant();
+  if (variant >= 0 && variant <= 3) mlp_variant() = variant;
+  return prev;
+}
+
 // out12[n_samples][12] = {r,g,b,alpha, r_d,g_d,b_d,alpha_d, wr,wg,wb,0} per kept sample.
 extern "C" int apn_point_mlp(const float* s_pos4, const int32_t* s_ray, const int32_t* s_nbr, int64_t max_samples,
                              const int32_t* n_samples_dev, const float* recA16, const float* recB8,
@@ -547,11 +534,10 @@ extern "C" int apn_point_mlp(const float* s_pos4, const int32_t* s_ray, const in
       (!viewdirs && !vemb_const))
     return APN_ERR_ARG;
   const int64_t ntiles = (max_samples + TS - 1) / TS;
-  // 2 workgroups (8 waves) per CU; APN_MLP_VARIANT=3 selects the phase-timed build (profiling).
-  static const int variant = [] {
-    const char* e = getenv("APN_MLP_VARIANT");
-    return e ? atoi(e) : 0;
-  }();
+  // 2 workgroups (8 waves) per CU. APN_MLP_VARIANT: 0 (default) = 3-term fp16-split MFMA kernel
+  // (apn_mlp_h3.hip; wbuf prepared by apn_mlp_split_weights), 1 = FP32 MFMA kernel (this file),
+  // 2 / 3 = their phase-timed builds (profiling aid; same results).
+  const int variant = mlp_variant();
   static const int env_blocks = [] {
     const char* e = getenv("APN_MLP_BLOCKS");
     return e ? atoi(e) : 0;
@@ -564,17 +550,20 @@ extern "C" int apn_point_mlp(const float* s_pos4, const int32_t* s_ray, const in
                        s_nbr, n_samples_dev, (const float4*)recA16, (const float4*)recB8, (const float4*)feat_proj,
                        viewdirs, vemb_const, wbuf, eps, act_shift, interval, (float4*)out12);
   };
-  // APN_MLP_VARIANT=3 selects the phase-timed build (profiling aid; same results).
-  if (variant == 3) {
+  if (variant == 1) {
+    launch(k_point_mlp<2, 2>);
+  } else if (variant == 2) {
     launch(k_point_mlp<2, 2, true>);
   } else {
-    launch(k_point_mlp<2, 2>);
+    launch_point_mlp_h3(blocks, variant == 3, (hipStream_t)stream, (const float4*)s_pos4, s_ray, s_nbr,
+                        n_samples_dev, (const float4*)recA16, (const float4*)recB8, (const float4*)feat_proj,
+                        viewdirs, vemb_const, wbuf, eps, act_shift, interval, (float4*)out12);
   }
   return launch_status();
 }
 
-// Profiling aid: copy (and reset) the per-phase cycle sums of the timed k_point_mlp variant
-// (APN_MLP_VARIANT=3): {gather, layer 1, layers 2-4, epilogue, tiles, kernel} summed over
+// Profiling aid: copy (and reset) the per-phase cycle sums of the timed MLP variants
+// (APN_MLP_VARIANT=2, 3): {gather, layer 1, layers 2-4, epilogue, tiles, kernel} summed over
 // workgroups. Synchronous.
 extern "C" int apn_debug_mlp_phase_cycles(uint64_t* out6) {
   if (!out6) return APN_ERR_ARG;
@@ -582,5 +571,5 @@ extern "C" int apn_debug_mlp_phase_cycles(uint64_t* out6) {
   APN_HIP_TRY(hipMemcpyFromSymbol(out6, HIP_SYMBOL(g_mlp_phase), sizeof(uint64_t) * 6));
   static const unsigned long long zero[6] = {0, 0, 0, 0, 0, 0};
   APN_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_mlp_phase), zero, sizeof(zero)));
-  return APN_OK;
+  return debug_phase_cycles_h3(out6);
 }

@@ -1,0 +1,602 @@
+// Fused Point-NeRF neighbour MLP (temporalpoints.py:452-519) on fp16 MFMA with a 3-term split:
+// every fp32 operand x is carried as hi = fp16(x) (RNE) and lo = fp16(x - hi), and
+//
+//     a . b  ~=  hi(a) hi(b) + hi(a) lo(b) + lo(a) hi(b)        (fp32 accumulate)
+//
+// drops only lo(a) lo(b) (<= 2^-22 |a b|) and the fp16 rounding of the residual (<= 2^-22 |x|):
+// ~2e-7 relative per product, the size of fp32's own rounding. v_mfma_f32_16x16x32_f16 runs
+// 16x the FLOP rate of v_mfma_f32_16x16x4_f32, so the three terms cost 3/16 of the fp32 MFMA time.
+// Range: |activations|, |weights| < 65504 (fp16 max); the tests compare against the fp32 oracle.
+//
+// Same algebra as apn_mlp.hip (layer-1 projection P = canonical_feat W1f^T added to the
+// accumulator, rgbnet feature_linears folded into views_linears.0); differences in structure:
+//   * transposed product D^T[o][m] = W[o][k] X^T[k][m]: the weights are the MFMA A operand
+//     (fragments pre-arranged by apn_mlp_split_weights, one coalesced 1 KB load per wave), the
+//     activations the B operand, so a lane's accumulator holds 4 consecutive output features of
+//     one MLP row -- the epilogue writes them as one 8-byte hi + one 8-byte lo LDS store;
+//   * activations ping-pong between two LDS buffers (64 rows x [hi 128 | lo 128] halves, 16-B
+//     chunks XOR-swizzled by row: conflict-free ds_read_b128 operand reads), one barrier per layer;
+//   * the P rows are gathered straight into the layer-1 accumulators (global -> VGPR).
+//
+// Tile = 8 samples x 8 neighbours = 64 MLP rows per 256-thread workgroup (4 waves, wave w owns
+// output features 32w..32w+31 of every layer), 2 workgroups per CU.
+#include "apn_mlp_layout.h"
+
+namespace apn {
+namespace h3 {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+
+constexpr int XB = 512;            // bytes per activation row: hi 128 halves | lo 128 halves
+constexpr int XBUF = TR * XB;      // one activation buffer (32 KB)
+constexpr int HB = 800;            // bytes per head-input row: hi 160 | lo 160 | pad (800/4 = 8 mod 64)
+constexpr int HLO = 320;           // lo offset inside a head-input row
+
+constexpr int SW_B1 = 0, SW_B2 = 128, SW_B3 = 256, SW_B4 = 384, SW_WD = 512, SW_BD = 640, SW_BH = 644,
+              SW_WV2 = 708, SW_BV2 = 900, SW_TOTAL = 904;
+
+// sin and cos of x for the positional encoding, |x| < ~1e6 (arguments are rel_c * 2^f, f <= 9):
+// quadrant reduction k = rint(2x/pi), r = x - k pi/2 with pi/2 in two floats (fma, so k C1 is
+// exact), minimax polynomials on |r| <= pi/4 (Cephes sinf/cosf coefficients). Max error ~1e-7
+// absolute (fp32 sinf: ~7e-8), about a third of the VALU work of the library sincosf and no
+// large-argument branch (whose registers the library path keeps live).
+__device__ __forceinline__ void sincos_pe(float x, float& sn, float& cs) {
+  const float k = rintf(x * 0.636619772367581343f);
+  float r = fmaf(k, -0x1.921fb6p+0f, x);
+  r = fmaf(k, 0x1.777a5cp-25f, r);
+  const float z = r * r;
+  const float sp = fmaf(r * z, fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f), r);
+  const float cp = fmaf(z * z, fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f),
+                        fmaf(-0.5f, z, 1.f));
+  const int q = (int)k;
+  const float ss = (q & 1) ? cp : sp, cc = (q & 1) ? sp : cp;
+  sn = (q & 2) ? -ss : ss;
+  cs = ((q + 1) & 2) ? -cc : cc;
+}
+
+// Byte offset of logical 16-B chunk c (8 halves, 0..15) of the hi part of activation row m.
+__device__ __forceinline__ int act_off(int m, int c) { return m * XB + ((c ^ (m & 15)) << 4); }
+// Byte offset of fp32 chunk c (4 floats, 0..31) of row m of the layer-4 output.
+__device__ __forceinline__ int out32_off(int m, int c) { return m * XB + ((c ^ (m & 7)) << 4); }
+
+__device__ __forceinline__ void split4(const f32x4& v, h4& hi, h4& lo) {
+  hi = __builtin_convertvector(v, h4);
+  const f32x4 hb = __builtin_convertvector(hi, f32x4);
+  lo = __builtin_convertvector(v - hb, h4);
+}
+
+__device__ __forceinline__ f32x4 mfma3(const h8& ahi, const h8& alo, const h8& bhi, const h8& blo, f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, bhi, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, blo, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, bhi, acc, 0, 0, 0);
+  return acc;
+}
+
+// Weight fragments are read through a buffer descriptor: the per-lane offset (lane * 16 B) is
+// the only VGPR, the fragment offset a wave-uniform SGPR -- plain 64-bit pointers per fragment
+// would be hoisted out of the tile loop by the compiler (~80 live VGPR pairs).
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+// Fragment (o-tile ot, chunk q, part) of the matrix at half offset hbase with NQ chunks.
+__device__ __forceinline__ h8 frag(rsrc_t rs, int hbase, int nq, int ot, int q, int part) {
+  const int lane = threadIdx.x & 63;
+  const int soff = hbase * 2 + ((ot * nq + q) * 2 + part) * (FRAG_HALVES * 2);
+  return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, soff, 0));
+}
+
+// acc[mt][j] += W[o-tile 2w+j] X^T over NQ chunks of 32. `a` carries chunk 0 of this matrix's
+// fragments in and chunk 0 of the next matrix (Wn, NQN chunks, o-tiles otn0, otn0+1) out.
+template <int NQ, int NQN, int NTN>
+__device__ __forceinline__ void layer_mfma(const char* __restrict__ X, rsrc_t rs, int W, int ot0, int Wn, int otn0,
+                                           f32x4 (&acc)[4][2], h8 (&a)[2][2]) {
+  const int lane = threadIdx.x & 63;
+  const int li = lane & 15, g = lane >> 4;
+  h8 b[4][2];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    const char* p = X + act_off(16 * mt + li, g);
+    b[mt][0] = *(const h8*)p;
+    b[mt][1] = *(const h8*)(p + 256);
+  }
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    h8 an[2][2], bn[4][2];
+    if (q + 1 < NQ) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, W, NQ, ot0 + j, q + 1, pt);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const char* p = X + act_off(16 * mt + li, 4 * (q + 1) + g);
+        bn[mt][0] = *(const h8*)p;
+        bn[mt][1] = *(const h8*)(p + 256);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < NTN; ++j)
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, Wn, NQN, otn0 + j, 0, pt);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) acc[mt][j] = mfma3(a[j][0], a[j][1], b[mt][0], b[mt][1], acc[mt][j]);
+    __builtin_amdgcn_sched_barrier(0);
+    if (q + 1 < NQ) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        a[j][0] = an[j][0];
+        a[j][1] = an[j][1];
+      }
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        b[mt][0] = bn[mt][0];
+        b[mt][1] = bn[mt][1];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < NTN; ++j) {
+        a[j][0] = an[j][0];
+        a[j][1] = an[j][1];
+      }
+    }
+  }
+}
+
+// lrelu(acc + bias) -> hi/lo halves of the next layer's input rows (transposed C layout: lane
+// (li, g) of (mt, j) holds features 16(2w+j) + 4g + r of row 16 mt + li).
+__device__ __forceinline__ void store_act(char* __restrict__ X, int ot0, const float* __restrict__ bias,
+                                          const f32x4 (&acc)[4][2]) {
+  const int lane = threadIdx.x & 63;
+  const int li = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int o0 = 16 * (ot0 + j) + 4 * g;
+    const f32x4 bb = *(const f32x4*)(bias + o0);
+    const int c = o0 >> 3, sub = (g & 1) * 8;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      f32x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = lrelu(acc[mt][j][r] + bb[r]);
+      h4 hi, lo;
+      split4(v, hi, lo);
+      char* p = X + act_off(16 * mt + li, c) + sub;
+      *(h4*)p = hi;
+      *(h4*)(p + 256) = lo;
+    }
+  }
+}
+
+__device__ unsigned long long g_phase[6];
+
+template <bool TIMED>
+__global__ __launch_bounds__(MLP_THREADS, 2) void k_point_mlp_h3(
+    const float4* __restrict__ s_pos, const int* __restrict__ s_ray, const int* __restrict__ s_nbr,
+    const int* __restrict__ n_samples_dev, const float4* __restrict__ recA, const float4* __restrict__ recB,
+    const float4* __restrict__ pproj, const float* __restrict__ viewdirs, const float* __restrict__ vemb_const,
+    const float* __restrict__ wbuf, float eps, float shift, float interval, float4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) char Xs[2 * XBUF];
+  __shared__ float sTo[TR];
+  __shared__ float sIdw[TR];
+  __shared__ float sRow[TR * 8];     // direct blend per row: wdir, alpha_c, rgb_c(3), pcol(3)
+  __shared__ __attribute__((aligned(16))) float sOut[TS * 12];
+  __shared__ float sV[TS * 32];      // view embedding per sample (27 + zero pad)
+  __shared__ __attribute__((aligned(16))) float sW[SW_TOTAL];
+  __shared__ float sPart[4 * TS * 4];
+  char* const X0 = Xs;
+  char* const X1 = Xs + XBUF;
+
+  const int nS = *n_samples_dev;
+  const int ntiles = (nS + TS - 1) / TS;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(wbuf + OFF_H16), 0, H_TOTAL * 2, 0x00020000);
+  const int ot0 = 2 * wid;
+  for (int i = tid; i < 128; i += MLP_THREADS) {
+    sW[SW_B1 + i] = wbuf[OFF_B1 + i];
+    sW[SW_B2 + i] = wbuf[OFF_B2 + i];
+    sW[SW_B3 + i] = wbuf[OFF_B3 + i];
+    sW[SW_B4 + i] = wbuf[OFF_B4 + i];
+    sW[SW_WD + i] = wbuf[OFF_WD + i];
+  }
+  if (tid < 64) sW[SW_BH + tid] = wbuf[OFF_BH + tid];
+  if (tid < 192) sW[SW_WV2 + tid] = wbuf[OFF_WV2 + tid];
+  if (tid < 3) sW[SW_BV2 + tid] = wbuf[OFF_BV2 + tid];
+  if (tid == 0) sW[SW_BD] = wbuf[OFF_BD];
+  // XCD-aware tile order (as apn_mlp.hip): XCD x = block % 8 walks a contiguous tile range, so
+  // neighbouring samples (which share neighbour points) gather through the same L2.
+  const int nx = (gridDim.x % 8 == 0) ? 8 : 1;
+  const int xcd = blockIdx.x % nx, per_xcd = gridDim.x / nx;
+  const int chunk = (ntiles + nx - 1) / nx;
+  const int t_beg = xcd * chunk, t_end = min(ntiles, t_beg + chunk);
+
+  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, tk = 0, tk0 = 0;
+  if (TIMED) tk0 = clock64();
+#define APN_PHASE(i)                         \
+  if (TIMED) {                               \
+    const unsigned long long now = clock64(); \
+    ph[i] += now - tk;                       \
+    tk = now;                                \
+  }
+  // gather coordinates: row r = (sample s, neighbour k), quarter p of the row
+  const int gr = tid >> 2, gp = tid & 3, gsm = gr >> 3, gk = gr & 7;
+  // next-tile prefetch: this thread's gather row, and the 4 rows whose P this lane loads
+  int pf_nb = -1, pf_ray = 0, pf_pn[4];
+  float4 pf_q = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto fetch = [&](int tl) {
+    const int gs = tl * TS + gsm;
+    pf_nb = -1;
+    if (tl < t_end && gs < nS) {
+      pf_nb = s_nbr[(size_t)gs * 8 + gk];
+      pf_q = s_pos[gs];
+      pf_ray = s_ray[gs];
+    }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int m = 16 * mt + li;
+      pf_pn[mt] = (tl < t_end && tl * TS + (m >> 3) < nS) ? s_nbr[(size_t)tl * TR + m] : -1;
+    }
+  };
+  int tile = t_beg + blockIdx.x / nx;
+  fetch(tile);
+  h8 a[2][2];   // carried A-fragment prefetch (chunk 0 of the next weight matrix)
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int pt = 0; pt < 2; ++pt) a[j][pt] = frag(rs, H_W1E, 2, ot0 + j, 0, pt);
+  int prev_s0 = -1;
+  for (; tile < t_end; tile += per_xcd) {
+    const int s0 = tile * TS;
+    if (TIMED) { tk = clock64(); ph[4] += 1; }
+    // ------------------------------------------------ layer-1 accumulators = P[nbr] (global -> VGPR)
+    f32x4 acc[4][2];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int nb = pf_pn[mt];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const float4 v = nb >= 0 ? pproj[(size_t)nb * (FEAT / 4) + 4 * (ot0 + j) + g] : make_float4(0.f, 0.f, 0.f, 0.f);
+        acc[mt][j] = f32x4{v.x, v.y, v.z, v.w};
+      }
+    }
+    // ------------------------------------------------ gather + posenc + direct-blend terms
+    {
+      const int r = gr, p = gp, s = gsm, k = gk;
+      const int nb = pf_nb;
+      const float4 q = pf_q;
+      const int ray = pf_ray;
+      char* xr = X0 + r * XB;
+      const int c_sin = (2 * p) ^ (r & 15), c_cos = (2 * p + 1) ^ (r & 15);
+      if (nb >= 0) {
+        const float4 a0 = recA[4 * (size_t)nb + 0];
+        const float4 a1 = recA[4 * (size_t)nb + 1];
+        const float4 a2 = recA[4 * (size_t)nb + 2];
+        const float4 a3 = recA[4 * (size_t)nb + 3];
+        const float dx = q.x - a0.x, dy = q.y - a0.y, dz = q.z - a0.z;
+        const float rc0 = (a1.x * dx + a1.y * dy) + a1.z * dz;
+        const float rc1 = (a1.w * dx + a2.x * dy) + a2.y * dz;
+        const float rc2 = (a2.z * dx + a2.w * dy) + a3.x * dz;
+        const float tn = (dx * dx + dy * dy) + dz * dz;
+        if (p == 0) {
+          sTo[r] = tn;
+        } else if (p == 1) {
+          const float4 b0 = recB[2 * (size_t)nb], b1 = recB[2 * (size_t)nb + 1];
+          float* rw = sRow + 8 * r;
+          rw[0] = expf(-(tn * tn) / a0.w);   // temporalpoints.py:461 (to_nn is already squared)
+          rw[1] = a3.y;
+          rw[2] = b0.x; rw[3] = b0.y; rw[4] = b0.z;
+          rw[5] = b1.x; rw[6] = b1.y; rw[7] = b1.z;
+        }
+        // arguments a = p + 4j = 10 i + f: rel_c[i] * 2^f (column order: pe_col_to_ref)
+        f32x4 sv0, sv1, cv0, cv1;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int aa = p + 4 * j;
+          float sv, cv;
+          if (aa < 30) {
+            const int ci = aa / 10;
+            const float v = (ci == 0 ? rc0 : (ci == 1 ? rc1 : rc2)) * (float)(1 << (aa - 10 * ci));
+            sincos_pe(v, sv, cv);
+          } else {  // j == 7 of p = 2, 3
+            sv = p == 2 ? rc0 : rc2;
+            cv = p == 2 ? rc1 : 0.f;
+          }
+          if (j < 4) { sv0[j] = sv; cv0[j] = cv; } else { sv1[j - 4] = sv; cv1[j - 4] = cv; }
+        }
+        h4 hs0, ls0, hs1, ls1, hc0, lc0, hc1, lc1;
+        split4(sv0, hs0, ls0); split4(sv1, hs1, ls1);
+        split4(cv0, hc0, lc0); split4(cv1, hc1, lc1);
+        *(h8*)(xr + (c_sin << 4)) = __builtin_shufflevector(hs0, hs1, 0, 1, 2, 3, 4, 5, 6, 7);
+        *(h8*)(xr + (c_sin << 4) + 256) = __builtin_shufflevector(ls0, ls1, 0, 1, 2, 3, 4, 5, 6, 7);
+        *(h8*)(xr + (c_cos << 4)) = __builtin_shufflevector(hc0, hc1, 0, 1, 2, 3, 4, 5, 6, 7);
+        *(h8*)(xr + (c_cos << 4) + 256) = __builtin_shufflevector(lc0, lc1, 0, 1, 2, 3, 4, 5, 6, 7);
+        {  // view embedding element e of this sample: poc_fre(viewdirs, 2^0..2^3) = [v, sin (12), cos (12)]
+          const int e = 4 * k + p;
+          float v = 0.f;
+          if (e < 27) {
+            if (vemb_const) {
+              v = vemb_const[e];
+            } else {
+              const int ee = e < 3 ? 0 : (e < 15 ? e - 3 : e - 15);
+              const int ci = e < 3 ? e : ee >> 2;
+              const float vv = viewdirs[3 * ray + ci];
+              const float arg = vv * (float)(1 << (ee & 3));
+              v = e < 3 ? vv : (e < 15 ? sinf(arg) : cosf(arg));
+            }
+          }
+          sV[s * 32 + e] = v;
+        }
+      } else {
+        const h8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+        *(h8*)(xr + (c_sin << 4)) = z;
+        *(h8*)(xr + (c_sin << 4) + 256) = z;
+        *(h8*)(xr + (c_cos << 4)) = z;
+        *(h8*)(xr + (c_cos << 4) + 256) = z;
+        sV[s * 32 + 4 * k + p] = 0.f;
+        if (p == 0) {
+          sTo[r] = 1.f;
+        } else if (p == 1) {
+          for (int c = 0; c < 8; ++c) sRow[8 * r + c] = 0.f;
+        }
+      }
+    }
+    fetch(tile + per_xcd);
+    __syncthreads();
+    APN_PHASE(0)
+    // ------------------------------------------------ outputs of the previous tile
+    if (prev_s0 >= 0 && tid < TS * 3 && prev_s0 + tid / 3 < nS)
+      out[(size_t)prev_s0 * 3 + tid] = *(const float4*)(sOut + 4 * tid);
+    if (tid < TS) {  // IDW weights (temporalpoints.py:473-475)
+      float w[8], sum = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        w[k] = 1.f / (sTo[tid * 8 + k] + eps);
+        sum += w[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sIdw[tid * 8 + k] = w[k] / sum;
+    }
+    // ------------------------------------------------ feat_net: 4 x (Linear + LeakyReLU)
+    layer_mfma<2, 4, 2>(X0, rs, H_W1E, ot0, H_W2, ot0, acc, a);
+    store_act(X1, ot0, sW + SW_B1, acc);
+    __syncthreads();
+    APN_PHASE(1)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[mt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    layer_mfma<4, 4, 2>(X1, rs, H_W2, ot0, H_W3, ot0, acc, a);
+    store_act(X0, ot0, sW + SW_B2, acc);
+    __syncthreads();
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[mt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    layer_mfma<4, 4, 2>(X0, rs, H_W3, ot0, H_W4, ot0, acc, a);
+    store_act(X1, ot0, sW + SW_B3, acc);
+    __syncthreads();
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[mt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    layer_mfma<4, 5, 1>(X1, rs, H_W4, ot0, H_WH, wid, acc, a);
+    // layer-4 output lrelu(acc + b4) as fp32 rows (for the IDW sum)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int o0 = 16 * (ot0 + j) + 4 * g;
+      const f32x4 bb = *(const f32x4*)(sW + SW_B4 + o0);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        f32x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = lrelu(acc[mt][j][r] + bb[r]);
+        *(f32x4*)(X0 + out32_off(16 * mt + li, o0 >> 2)) = v;
+      }
+    }
+    __syncthreads();
+    APN_PHASE(2)
+    // ------------------------------------------------ IDW sum (temporalpoints.py:493-494), density head
+    {
+      const int s = tid >> 5, oq = tid & 31;
+      f32x4 h = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const f32x4 v = *(const f32x4*)(X0 + out32_off(8 * s + k, oq));
+        const float w = sIdw[8 * s + k];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h[r] = h[r] + w * v[r];
+      }
+      // densitynet Linear(128 -> 1) (tineuvox.py:158) over this thread's 4 features, then the half-wave
+      const f32x4 wd = *(const f32x4*)(sW + SW_WD + 4 * oq);
+      float d = ((h[0] * wd[0] + h[1] * wd[1]) + h[2] * wd[2]) + h[3] * wd[3];
+      d += __shfl_xor(d, 16, 64);
+      d += __shfl_xor(d, 8, 64);
+      d += __shfl_xor(d, 4, 64);
+      d += __shfl_xor(d, 2, 64);
+      d += __shfl_xor(d, 1, 64);
+      if (oq == 0) {  // Raw2Alpha (render_utils_kernel.cu:357-369)
+        const float e = expf((d + sW[SW_BD]) + shift);
+        sOut[12 * s + 3] = 1.f - powf(1.f + e, -interval);
+      }
+      // head input row s: [h (128) | view embedding (27) | 0] as hi/lo halves
+      char* hr = X1 + s * HB;
+      h4 hi, lo;
+      split4(h, hi, lo);
+      *(h4*)(hr + 8 * oq) = hi;
+      *(h4*)(hr + HLO + 8 * oq) = lo;
+      const float ve = sV[s * 32 + oq];
+      const _Float16 vh = (_Float16)ve;
+      *(_Float16*)(hr + 2 * (128 + oq)) = vh;
+      *(_Float16*)(hr + HLO + 2 * (128 + oq)) = (_Float16)(ve - (float)vh);
+    }
+    // direct blend + weight-vis colour (temporalpoints.py:459-470, 517-519): wave 1, lane =
+    // (sample, quantity); sums over the 8 neighbours in order
+    if (wid == 1) {
+      const int s = lane >> 3, qn = lane & 7;
+      const float* rw = sRow + 64 * s;
+      float sumd = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sumd += rw[8 * k];
+      const float dn = sumd + 1e-12f;
+      float acc1 = 0.f;
+      if (qn == 0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc1 += (0.125f * rw[8 * k]) * rw[8 * k + 1];
+      } else if (qn < 4) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc1 += (rw[8 * k] / dn) * rw[8 * k + 1 + qn];
+      } else if (qn < 7) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc1 += sIdw[8 * s + k] * rw[8 * k + 1 + qn];
+      }
+      // sOut[s] = {r, g, b, alpha, r_d, g_d, b_d, alpha_d, wr, wg, wb, 0}
+      const int slot = qn == 0 ? 7 : (qn < 4 ? 3 + qn : (qn < 7 ? 4 + qn : 11));
+      sOut[12 * s + slot] = acc1;
+    }
+    __syncthreads();
+    // ------------------------------------------------ rgb head: folded [h; v] -> 64, ReLU, -> 3, sigmoid
+    {
+      f32x4 ah = {0.f, 0.f, 0.f, 0.f};
+      const char* hr = X1 + li * HB;
+      const h8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int q = 0; q < KV / 32; ++q) {
+        h8 an[2][2];
+        if (q + 1 < KV / 32) {
+#pragma unroll
+          for (int pt = 0; pt < 2; ++pt) an[0][pt] = frag(rs, H_WH, KV / 32, wid, q + 1, pt);
+        } else {  // chunk 0 of the next tile's layer 1
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, H_W1E, 2, ot0 + j, 0, pt);
+        }
+        const h8 bh = li < TS ? *(const h8*)(hr + 16 * (4 * q + g)) : z;
+        const h8 bl = li < TS ? *(const h8*)(hr + HLO + 16 * (4 * q + g)) : z;
+        ah = mfma3(a[0][0], a[0][1], bh, bl, ah);
+        if (q + 1 < KV / 32) {
+          a[0][0] = an[0][0];
+          a[0][1] = an[0][1];
+        } else {
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            a[j][0] = an[j][0];
+            a[j][1] = an[j][1];
+          }
+        }
+      }
+      // lane (li = sample, g): head features o = 16 wid + 4 g + r
+      const int o0 = 16 * wid + 4 * g;
+      const f32x4 bb = *(const f32x4*)(sW + SW_BH + o0);
+      float pc[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = fmaxf(ah[r] + bb[r], 0.f);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) pc[c] += v * sW[SW_WV2 + 64 * c + o0 + r];
+      }
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        pc[c] += __shfl_xor(pc[c], 16, 64);
+        pc[c] += __shfl_xor(pc[c], 32, 64);
+      }
+      if (g == 0 && li < TS) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) sPart[(wid * TS + li) * 4 + c] = pc[c];
+      }
+    }
+    __syncthreads();
+    if (tid < TS * 3) {  // views_linears.2 bias + sigmoid (temporalpoints.py:513-515)
+      const int s = tid / 3, c = tid % 3;
+      const float v = ((sPart[(0 * TS + s) * 4 + c] + sPart[(1 * TS + s) * 4 + c]) + sPart[(2 * TS + s) * 4 + c]) +
+                      sPart[(3 * TS + s) * 4 + c];
+      sOut[12 * s + c] = 1.f / (1.f + expf(-(v + sW[SW_BV2 + c])));
+    }
+    APN_PHASE(3)
+    prev_s0 = s0;
+  }
+#undef APN_PHASE
+  if (TIMED && tid == 0) {
+    ph[5] = clock64() - tk0;
+    for (int i = 0; i < 6; ++i) atomicAdd(&g_phase[i], ph[i]);
+  }
+  __syncthreads();
+  if (prev_s0 >= 0 && tid < TS * 3 && prev_s0 + tid / 3 < nS)
+    out[(size_t)prev_s0 * 3 + tid] = *(const float4*)(sOut + 4 * tid);
+}
+
+// fp32 region of wbuf -> fp16 hi/lo fragments (layout: apn_mlp_layout.h). One thread per
+// (matrix, o-tile, chunk, lane).
+__global__ void k_split_weights(float* __restrict__ wbuf) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  // fragment-lanes per matrix: W1E 8x2x64, W2..W4 8x4x64, WH 4x5x64
+  constexpr int n1 = 8 * 2 * 64, n2 = 8 * 4 * 64, nh = 4 * 5 * 64;
+  int mat, i;
+  if (t < n1) { mat = 0; i = t; }
+  else if (t < n1 + 3 * n2) { mat = 1 + (t - n1) / n2; i = (t - n1) % n2; }
+  else if (t < n1 + 3 * n2 + nh) { mat = 4; i = t - n1 - 3 * n2; }
+  else return;
+  const int nq = mat == 0 ? 2 : (mat == 4 ? 5 : 4);
+  const int lane = i & 63, q = (i >> 6) % nq, ot = (i >> 6) / nq;
+  const int o = 16 * ot + (lane & 15), k0 = 32 * q + 8 * (lane >> 4);
+  const int hbase = mat == 0 ? H_W1E : (mat == 1 ? H_W2 : (mat == 2 ? H_W3 : (mat == 3 ? H_W4 : H_WH)));
+  _Float16* dst = (_Float16*)(wbuf + OFF_H16) + hbase + (size_t)((ot * nq + q) * 2) * FRAG_HALVES + lane * 8;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = k0 + j;
+    float w;
+    if (mat == 0) {
+      const int ref = pe_col_to_ref(k);
+      w = ref < 0 ? 0.f : wbuf[OFF_W1E + o * KE + ref];
+    } else if (mat == 4) {
+      w = wbuf[OFF_WH + o * KV + k];
+    } else {
+      const int off = mat == 1 ? OFF_W2 : (mat == 2 ? OFF_W3 : OFF_W4);
+      w = wbuf[off + o * 128 + k];
+    }
+    const _Float16 hi = (_Float16)w;
+    dst[j] = hi;
+    dst[FRAG_HALVES + j] = (_Float16)(w - (float)hi);
+  }
+}
+
+}  // namespace h3
+
+void launch_point_mlp_h3(int blocks, bool timed, hipStream_t stream, const float4* s_pos, const int* s_ray,
+                         const int* s_nbr, const int* n_samples_dev, const float4* recA, const float4* recB,
+                         const float4* pproj, const float* viewdirs, const float* vemb_const, const float* wbuf,
+                         float eps, float shift, float interval, float4* out) {
+  if (timed)
+    hipLaunchKernelGGL(h3::k_point_mlp_h3<true>, dim3(blocks), dim3(MLP_THREADS), 0, stream, s_pos, s_ray, s_nbr,
+                       n_samples_dev, recA, recB, pproj, viewdirs, vemb_const, wbuf, eps, shift, interval, out);
+  else
+    hipLaunchKernelGGL(h3::k_point_mlp_h3<false>, dim3(blocks), dim3(MLP_THREADS), 0, stream, s_pos, s_ray, s_nbr,
+                       n_samples_dev, recA, recB, pproj, viewdirs, vemb_const, wbuf, eps, shift, interval, out);
+}
+
+int debug_phase_cycles_h3(uint64_t* out6) {
+  uint64_t v[6];
+  APN_HIP_TRY(hipMemcpyFromSymbol(v, HIP_SYMBOL(h3::g_phase), sizeof(v)));
+  static const unsigned long long zero[6] = {0, 0, 0, 0, 0, 0};
+  APN_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(h3::g_phase), zero, sizeof(zero)));
+  for (int i = 0; i < 6; ++i) out6[i] += v[i];
+  return APN_OK;
+}
+
+}  // namespace apn
+
+using namespace apn;
+
+// fp32 packed weights -> the fp16 hi/lo fragment region read by the default apn_point_mlp kernel.
+extern "C" int apn_mlp_split_weights(float* wbuf, void* stream) {
+  if (!wbuf) return APN_ERR_ARG;
+  constexpr int n = 8 * 2 * 64 + 3 * 8 * 4 * 64 + 4 * 5 * 64;
+  hipLaunchKernelGGL(h3::k_split_weights, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, wbuf);
+  return launch_status();
+}

@@ -1,0 +1,74 @@
+// Tile shape and packed-weight layout shared by the neighbour-MLP kernels (apn_mlp.hip: FP32
+// MFMA; apn_mlp_h3.hip: 3-term fp16-split MFMA) and apn_amd/ops.py:pack_mlp_weights (through
+// apn_mlp_weight_layout()).
+#pragma once
+#include "apn_common.h"
+
+namespace apn {
+
+constexpr int TS = 8;             // samples per tile
+constexpr int TR = TS * 8;        // MLP rows per tile (sample, neighbour)
+constexpr int MLP_THREADS = 256;
+constexpr int FEAT = 128;
+constexpr int KE = 64;            // positional encoding 63, zero-padded
+constexpr int KV = 160;           // head input: h (128) + view embedding (27) + pad
+
+// Packed weight buffer layout (floats). fp32 region: nn.Linear [out][in] rows.
+constexpr int OFF_W1E = 0;                        // [128][64]  feat_net.0 columns 0..62
+constexpr int OFF_B1 = OFF_W1E + 128 * KE;        // [128]      (+ pose-embedding fold)
+constexpr int OFF_W2 = OFF_B1 + 128;              // [128][128]
+constexpr int OFF_B2 = OFF_W2 + 128 * 128;
+constexpr int OFF_W3 = OFF_B2 + 128;
+constexpr int OFF_B3 = OFF_W3 + 128 * 128;
+constexpr int OFF_W4 = OFF_B3 + 128;
+constexpr int OFF_B4 = OFF_W4 + 128 * 128;
+constexpr int OFF_WD = OFF_B4 + 128;              // [128]      densitynet
+constexpr int OFF_BD = OFF_WD + 128;              // [4]
+constexpr int OFF_WH = OFF_BD + 4;                // [64][160]  folded rgb head layer
+constexpr int OFF_BH = OFF_WH + 64 * KV;          // [64]
+constexpr int OFF_WV2 = OFF_BH + 64;              // [3][64]    views_linears.2
+constexpr int OFF_BV2 = OFF_WV2 + 3 * 64;         // [4]
+constexpr int OFF_W1F = OFF_BV2 + 4;              // [128][128] feat_net.0 columns 63..190 (for P)
+constexpr int W_F32_TOTAL = OFF_W1F + 128 * 128;
+
+// fp16 hi/lo region (written by apn_mlp_split_weights from the fp32 region): every matrix
+// W [O][K] in MFMA fragment order -- for o-tile ot (16 rows), k-chunk q (32 columns), part
+// (0 = hi = fp16(w), 1 = lo = fp16(w - hi)), lane l: 8 halves W[16 ot + (l & 15)][32 q + 8 (l >> 4) + j].
+// One 16-byte load per lane fetches a whole 1 KB fragment, coalesced.
+constexpr int OFF_H16 = (W_F32_TOTAL + 3) & ~3;   // float offset (16-B aligned)
+constexpr int FRAG_HALVES = 64 * 8;               // one fragment part
+constexpr int H_W1E = 0;                          // halves, relative to OFF_H16
+constexpr int H_W2 = H_W1E + 8 * 2 * 2 * FRAG_HALVES;
+constexpr int H_W3 = H_W2 + 8 * 4 * 2 * FRAG_HALVES;
+constexpr int H_W4 = H_W3 + 8 * 4 * 2 * FRAG_HALVES;
+constexpr int H_WH = H_W4 + 8 * 4 * 2 * FRAG_HALVES;
+constexpr int H_TOTAL = H_WH + 4 * 5 * 2 * FRAG_HALVES;
+constexpr int W_TOTAL = OFF_H16 + H_TOTAL / 2;
+
+// Column order of the positional encoding inside the fp16 kernel's layer-1 operand (64 columns):
+// gather thread p (4 per MLP row) owns columns 16p..16p+15 = sin(arg a_j), j = 0..7, then
+// cos(arg a_j), with a_j = p + 4 j the reference argument index a = 10 i + f (rel_c[i] * 2^f).
+// Slots whose a_j >= 30 carry rel_c: column 39 = rel_c[0], 47 = rel_c[1], 55 = rel_c[2], 63 = 0.
+// Returns the reference embedding index (poc_fre order: [x(3), sin(30), cos(30)]) or -1.
+__host__ __device__ constexpr int pe_col_to_ref(int c) {
+  const int p = c >> 4, j = c & 7, is_cos = (c >> 3) & 1;
+  const int a = p + 4 * j;
+  if (a < 30) return (is_cos ? 33 : 3) + a;
+  if (c == 39) return 0;
+  if (c == 47) return 1;
+  if (c == 55) return 2;
+  return -1;
+}
+
+// LeakyReLU(0.01): x >= 0 ? x : 0.01x == max(x, 0.01x) (the same rounded product; 2 VALU ops)
+__device__ __forceinline__ float lrelu(float x) { return fmaxf(x, x * 0.01f); }
+
+// Launcher of the fp16-split kernel (apn_mlp_h3.hip).
+void launch_point_mlp_h3(int blocks, bool timed, hipStream_t stream, const float4* s_pos, const int* s_ray,
+                         const int* s_nbr, const int* n_samples_dev, const float4* recA, const float4* recB,
+                         const float4* pproj, const float* viewdirs, const float* vemb_const, const float* wbuf,
+                         float eps, float shift, float interval, float4* out);
+// Adds (and resets) the phase-timed fp16-split kernel's cycle sums into out6.
+int debug_phase_cycles_h3(uint64_t* out6);
+
+}  // namespace apn

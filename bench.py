@@ -29,6 +29,10 @@ sys.path.insert(0, ROOT)
 from apn_amd import harness, synthetic as S  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
+FP16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 MFMA ~2.5 PF dense
+# the default MLP kernel computes each fp32 product as 3 fp16 MFMA terms (hi*hi + hi*lo + lo*hi,
+# fp32 accumulate), so fp32-accurate flops peak at a third of the fp16 dense rate
+SPLIT3_PEAK_TFLOPS = FP16_MFMA_PEAK_TFLOPS / 3
 HBM_PEAK_GBS = 8000.0
 
 
@@ -37,14 +41,21 @@ def flop_per_kept_sample(d_in=191, width=128):
     return 8 * 2 * (d_in * width + 3 * width * width) + 2 * (128 + 128 * 128 + 155 * 64 + 64 * 3)
 
 
-def mfma_executed_flop(n_samples):
-    """MFMA flops k_point_mlp issues: per 8-sample tile and wave, 16x16x4 f32 MFMAs for layer 1
-    (K=64), layers 2-4 (K=128) and the folded head (16 padded rows, K=160), 4 waves."""
+def mfma_executed_flop(n_samples, variant=0):
+    """MFMA flops the MLP kernel issues per launch, 4 waves per 8-sample tile.
+    variant 1 (FP32 MFMA): 16x16x4 f32 MFMAs for layer 1 (K=64), layers 2-4 (K=128) and the folded
+    head (16 padded rows, K=160). variant 0 (split): 16x16x32 f16 MFMAs, 3 per 32-wide k chunk
+    and 16x16 output block: layer 1 (2 chunks), layers 2-4 (4 chunks), 8 blocks per wave; head
+    (5 chunks, 1 block)."""
     tiles = (n_samples + 7) // 8
-    steps = lambda k: (k // 16) * 4          # 4 MFMA k-steps per 16-wide chunk
-    mfma_per_wave = steps(64) * 8 + 3 * steps(128) * 8 + steps(160) * 1   # 8 = 4 M-tiles x 2 N-tiles
-    assert mfma_per_wave == 936
-    return tiles * 4 * mfma_per_wave * (16 * 16 * 4 * 2)
+    if variant in (1, 2):
+        steps = lambda k: (k // 16) * 4          # 4 MFMA k-steps per 16-wide chunk
+        mfma_per_wave = steps(64) * 8 + 3 * steps(128) * 8 + steps(160) * 1   # 8 = 4 M-tiles x 2 N-tiles
+        assert mfma_per_wave == 936
+        return tiles * 4 * mfma_per_wave * (16 * 16 * 4 * 2)
+    mfma_per_wave = 3 * (2 * 8 + 3 * 4 * 8 + 5 * 1)
+    assert mfma_per_wave == 351
+    return tiles * 4 * mfma_per_wave * (16 * 16 * 32 * 2)
 
 
 def log(*a):
@@ -161,7 +172,7 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t)
-    if os.environ.get("APN_MLP_VARIANT") == "3":   # timed MLP variant: per-phase cycle split
+    if os.environ.get("APN_MLP_VARIANT") in ("2", "3"):   # timed MLP variants: per-phase cycle split
         import ctypes
         from apn_amd import _lib
         ph = (ctypes.c_uint64 * 6)()
@@ -180,11 +191,19 @@ def main():
             torch.distributed.destroy_process_group()
         return
 
+    variant = int(os.environ.get("APN_MLP_VARIANT", "0"))
     d_in = 191  # pose embedding folded into the bias for ZJU; F_alg still counts the reference D_in
     if model.pose_embedding_dim > 0:
         d_in = 191 + model.pose_embedding_dim
     flop = S_kept * flop_per_kept_sample(d_in)
     achieved = flop / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else 0.0
+    executed = mfma_executed_flop(S_kept, variant) / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else 0.0
+    if variant in (1, 2):
+        kernel, peak, mfma_peak = "k_point_mlp (fp32 MFMA)", FP32_MFMA_PEAK_TFLOPS, FP32_MFMA_PEAK_TFLOPS
+        peak_note = "peak = FP32 matrix peak"
+    else:
+        kernel, peak, mfma_peak = "k_point_mlp_h3 (3-term fp16-split MFMA)", SPLIT3_PEAK_TFLOPS, FP16_MFMA_PEAK_TFLOPS
+        peak_note = "peak = fp16 dense MFMA peak / 3 (three fp16 MFMA terms per fp32-accurate product)"
     traffic = read_traffic(os.path.join(ROOT, "profiles", "r01_point_mlp_traffic.json"))
     ms_per_step = elapsed / args.steps * 1e3
     value = (1 if shard_rays else world) * args.steps * R / elapsed
@@ -200,18 +219,22 @@ def main():
         "ms_per_step": ms_per_step, "higher_is_better": True,
         "scaling": "strong" if shard_rays else "weak", "vs_baseline": None,
         "dtype": "fp32", "data": "synthetic (procedural SMPL-24 capsule cloud, random-init networks)",
+        "mlp_arithmetic": ("fp32 as 3 fp16 MFMA terms (hi*hi+hi*lo+lo*hi), fp32 accumulate; parity vs the fp32 "
+                           "oracle <= 3e-7 on alpha/rgb" if variant in (0, 3) else "fp32 MFMA (v_mfma_f32_16x16x4_f32)"),
         "config": {"workload": S.CONFIGS[args.config].name + f" ({args.config})", "rays_per_frame": R,
                    "points": scene.cfg.N, "bones": scene.cfg.J, "inbbox_samples": stats.get("inbbox_samples"),
                    "kept_samples": S_kept, "parallelism": (f"rays x{world} + RCCL tile all-gather" if shard_rays else f"frames x{world}")
                    if world > 1 else "single"},
-        "roofline": {"bound": "mfma", "kernel": "k_point_mlp", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
+        "roofline": {"bound": "mfma", "kernel": kernel, "achieved": achieved, "peak": peak,
+                     "unit": "TFLOP/s", "frac": achieved / peak,
                      "traffic": traffic.get("bytes_per_launch") if traffic else None,
                      "flop_per_launch": flop, "avg_launch_ms": mlp_ms,
-                     "note": "achieved = reference F_alg (SURVEY.md 8(d)) / avg k_point_mlp time (HIP events); "
-                             "the kernel executes fewer MFMA flops (per-point layer-1 projection, folded rgb "
-                             "head, padded to 16-row tiles): see executed_tflops",
-                     "executed_tflops": mfma_executed_flop(S_kept) / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else 0.0},
+                     "note": "achieved = reference F_alg (SURVEY.md 8(d), fp32 flops) / avg MLP kernel time (HIP "
+                             "events on the launch stream); " + peak_note + "; the kernel issues fewer MFMA flops "
+                             "than F_alg (per-point layer-1 projection, folded rgb head, padded 16-row head "
+                             "tile): executed_tflops / mfma_util",
+                     "executed_tflops": executed,
+                     "mfma_util": executed / mfma_peak},
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)

@@ -114,11 +114,17 @@ int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t n_queries,
 int apn_nn1_distance(const float* xyz, int64_t n_points, float eps, int32_t cell_cap, float* nn_dist,
                      float* sorted_pts4, int32_t* bbox_ord, void* grid_workspace, void* stream);
 
-/* Packed MLP weight layout: writes 18 int32 offsets (W1E,B1,W2,B2,W3,B3,W4,B4,WD,BD,WH,BH,
- * WV2,BV2,W1F,TOTAL,KE,KV) and returns their count. W1E = feat_net.0 columns 0..62 (posenc),
- * W1F = feat_net.0 columns 63..190 (features), WH/BH = rgbnet feature_linears folded into
- * views_linears.0 (no activation between them), see apn_mlp.hip. */
+/* Packed MLP weight layout: writes 19 int32 offsets (W1E,B1,W2,B2,W3,B3,W4,B4,WD,BD,WH,BH,
+ * WV2,BV2,W1F,TOTAL,KE,KV,H16) and returns their count (float offsets; TOTAL = buffer length).
+ * W1E = feat_net.0 columns 0..62 (posenc), W1F = feat_net.0 columns 63..190 (features),
+ * WH/BH = rgbnet feature_linears folded into views_linears.0 (no activation between them),
+ * see apn_mlp.hip; H16 = start of the fp16 hi/lo fragment region (apn_mlp_layout.h). */
 int apn_mlp_weight_layout(int32_t* offsets);
+
+/* Fill the fp16 hi/lo fragment region of a packed weight buffer from its fp32 region
+ * (hi = fp16(w), lo = fp16(w - hi), MFMA fragment order). Call after every change of the fp32
+ * region and before apn_point_mlp with the default (split) kernel. */
+int apn_mlp_split_weights(float* wbuf, void* stream);
 
 /* Per-point layer-1 feature projection proj [N,128] = canonical_feat [N,128] x W1F^T
  * (temporalpoints.py:483-491 reassociated: W1 [emb; feat] = W1e emb + W1f feat). Computed once
@@ -129,12 +135,18 @@ int apn_feat_project(const float* canonical_feat, int64_t n_points, int32_t feat
 /* Fused neighbour MLP + heads + direct blend (temporalpoints.py:452-519) for the kept
  * samples; out12 [S,12] = {r,g,b,alpha, r_d,g_d,b_d,alpha_d, wr,wg,wb,0}. feat_proj is the
  * apn_feat_project output (feat_dim 128). vemb_const [27] (frozen_view_dir) or NULL to embed
- * viewdirs[ray]. */
+ * viewdirs[ray]. Default kernel: fp32 contraction as 3 fp16 MFMA terms (hi*hi + hi*lo + lo*hi,
+ * fp32 accumulate; wbuf prepared by apn_mlp_split_weights); variant 1 = the FP32-MFMA kernel. */
 int apn_point_mlp(const float* s_pos4, const int32_t* s_ray, const int32_t* s_nbr,
                   int64_t max_samples, const int32_t* n_samples_dev, const float* recA16,
                   const float* recB8, const float* feat_proj, int32_t feat_dim,
                   const float* viewdirs, const float* vemb_const, const float* wbuf, float eps,
                   float act_shift, float interval, int32_t grid_blocks, float* out12, void* stream);
+
+/* Select the apn_point_mlp kernel (process-wide; initial value from env APN_MLP_VARIANT, default 0):
+ * 0 = 3-term fp16-split MFMA, 1 = FP32 MFMA, 2 / 3 = phase-timed builds of 1 / 0 (profiling aid).
+ * Returns the previous selection; out-of-range values only query it. */
+int apn_set_mlp_variant(int32_t variant);
 
 /* Masks + Alphas2Weights + segment sums for both paths (temporalpoints.py:611-710).
  * ray_ws: 2*n_rays int32 scratch. */
@@ -145,7 +157,7 @@ int apn_composite(const float* smp12, const float* s_pos4, const int32_t* s_ray,
                   float* alphainv_last_direct, int32_t* ray_ws, void* stream);
 
 /* Profiling aid (synchronous): per-phase cycle sums of the timed k_point_mlp variant
- * (APN_MLP_VARIANT=3) {gather, layer 1, layers 2-4, epilogue, tiles, kernel cycles}, summed over
+ * (variants 2, 3) {gather, layer 1, layers 2-4, epilogue, tiles, kernel cycles}, summed over
  * workgroups since the last call; resets them. */
 int apn_debug_mlp_phase_cycles(uint64_t* out6);
 

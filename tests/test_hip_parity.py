@@ -178,10 +178,12 @@ def _records(orc, t_hat, colors):
     return recA, recB
 
 
+@pytest.mark.parametrize("variant", [0, 1], ids=["split3xfp16", "fp32"])
 @pytest.mark.parametrize("name", CASES)
-def test_mlp_stage_vs_oracle(dev, name):
+def test_mlp_stage_vs_oracle(dev, name, variant):
     """apn_point_mlp on the oracle's kept samples: alpha / rgb within 1e-5, the direct blend
-    and weight-vis colour within 1e-6 (same neighbour lists and records)."""
+    and weight-vis colour within 1e-6 (same neighbour lists and records), for both kernels
+    (3-term fp16-split MFMA, default; FP32 MFMA)."""
     from apn_amd import _lib as L
     from apn_amd.ops import pack_mlp_weights
     from model_io import model_from_golden
@@ -206,10 +208,16 @@ def test_mlp_stage_vs_oracle(dev, name):
     feat = feat_project(m.canonical_feat, wbuf)
     vd = g.t("in_viewdirs").to(dev)
     recA_d, recB_d = recA.to(dev), recB.to(dev)   # keep device copies alive across the async launch
-    L.call("apn_point_mlp", L.ptr(args[0]), L.ptr(args[1]), L.ptr(args[2]), S, L.ptr(ns), L.ptr(recA_d),
-           L.ptr(recB_d), L.ptr(feat), 128, L.ptr(vd), None, L.ptr(wbuf), 1e-6, float(orc.act_shift), 0.5, 0,
-           L.ptr(out12), L.stream_ptr(dev))
-    o = out12.cpu()
+    prev = L.load().apn_set_mlp_variant(variant)
+    try:
+        L.call("apn_point_mlp", L.ptr(args[0]), L.ptr(args[1]), L.ptr(args[2]), S, L.ptr(ns), L.ptr(recA_d),
+               L.ptr(recB_d), L.ptr(feat), 128, L.ptr(vd), None, L.ptr(wbuf), 1e-6, float(orc.act_shift), 0.5, 0,
+               L.ptr(out12), L.stream_ptr(dev))
+        o = out12.cpu()
+    finally:
+        L.load().apn_set_mlp_variant(prev)
+    print(f"{name} variant {variant}: max|d alpha| {(o[:, 3] - tr['alpha']).abs().max():.2e} "
+          f"max|d rgb| {(o[:, 0:3] - tr['rgbs']).abs().max():.2e}")
     assert (o[:, 3] - tr["alpha"]).abs().max() < 1e-5
     assert (o[:, 0:3] - tr["rgbs"]).abs().max() < 1e-5
     assert (o[:, 7] - tr["alpha_direct"]).abs().max() < 1e-6
