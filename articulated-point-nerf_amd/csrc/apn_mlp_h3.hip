@@ -194,7 +194,9 @@ __global__ __launch_bounds__(MLP_THREADS, 2) void k_point_mlp_h3(
   const int nS = *n_samples_dev;
   const int ntiles = (nS + TS - 1) / TS;
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wid = tid >> 6;
+  // wave index as a wave-uniform (SGPR) value: the fragment offsets derived from it must be
+  // scalar, or every buffer load becomes a readfirstlane waterfall loop
+  const int lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, g = lane >> 4;
   const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(wbuf + OFF_H16), 0, H_TOTAL * 2, 0x00020000);
   const int ot0 = 2 * wid;
