@@ -36,6 +36,8 @@ SIGNATURES = {
     "apn_grid_build": (C.c_int, [P, I64, P, F32, I32, P, P, P]),
     "apn_knn_workspace_bytes": (SZ, [I64]),
     "apn_knn_radius": (C.c_int, [P, P, I64, P, P, I64, I32, P, F32, P, P, P, P, P, P]),
+    "apn_set_knn_mode": (C.c_int, [I32]),
+    "apn_debug_knn_stats": (C.c_int, [P]),
     "apn_nn1_distance": (C.c_int, [P, I64, F32, I32, P, P, P, P, P]),
     "apn_mlp_weight_layout": (C.c_int, [P]),
     "apn_mlp_split_weights": (C.c_int, [P, P]),

@@ -329,7 +329,9 @@ class TemporalPoints(torch.nn.Module):
         t_embed = poc_fre(t, self.time_poc) if rot_params is None else None
         bone_Ts, global_t, joints_rel = self.forward_warp.pose(self.joints, t_embed, rot_params)
         colors = self._joint_colors(dev) if render_weights else None
+        self._mark("frame")
         t_hat_pcd, weights, recs = self._lbs(bone_Ts, global_t, records=True, colors=colors)
+        self._mark("lbs")
         self._last_weights = weights
         delta_joint = (self.joints - joints_rel).clone().detach()
         pose_embedding = (self.pose_embedding_net(poc_fre(delta_joint, self.pos_poc).view(1, -1))
@@ -362,6 +364,15 @@ class TemporalPoints(torch.nn.Module):
             ret['weights'] = wvis
         return ret
 
+    def _mark(self, name):
+        """HIP-event stage marker (only while self.timing is a dict): the time between consecutive
+        markers is charged to the stage named by the later one."""
+        if self.timing is None:
+            return
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        self.timing.setdefault("marks", []).append((name, e))
+
     def _render(self, xyz, recs, query_radius, rk, pose_embedding, calc_min_max, shard=None):
         recA, recB, bbox_ord = recs
         dev = xyz.device
@@ -385,10 +396,12 @@ class TemporalPoints(torch.nn.Module):
             call("apn_bbox_unpack", ptr(bbox_ord), qr, ptr(bbox6), s)
         else:
             bbox6 = torch.cat([self.xyz_min, self.xyz_max]).float().contiguous()
+        self._mark("bbox")
         # kNN grid over the warped cloud
         gws = ws.bytes("grid_ws", lib.apn_grid_workspace_bytes(N, CELL_CAP), dev)
         sorted4 = ws.get("sorted4", N * 4, torch.float32, dev)
         call("apn_grid_build", ptr(xyz), N, ptr(bbox_ord), qr, CELL_CAP, ptr(sorted4), ptr(gws), s)
+        self._mark("grid")
         # in-bbox samples
         offs = ws.get("offs", R + 1, torch.int32, dev)
         sws = ws.bytes("samp_ws", lib.apn_sample_pts_on_rays_workspace_bytes(R), dev)
@@ -411,6 +424,7 @@ class TemporalPoints(torch.nn.Module):
         q_ray = ws.get("q_ray", n_bbox, torch.int32, dev)
         call("apn_inbbox_fill", ptr(ro), ptr(rd), ptr(bbox6), near, far, stepdist, R, ptr(offs), ptr(q_pos),
              ptr(q_ray), s)
+        self._mark("sampling")
         # radius kNN + compaction of survivors
         s_pos = ws.get("s_pos", n_bbox * 4, torch.float32, dev)
         s_ray = ws.get("s_ray", n_bbox, torch.int32, dev)
@@ -419,6 +433,7 @@ class TemporalPoints(torch.nn.Module):
         kws = ws.bytes("knn_ws", lib.apn_knn_workspace_bytes(n_bbox), dev)
         call("apn_knn_radius", ptr(q_pos), ptr(q_ray), n_bbox, C.c_void_p(offs.data_ptr() + 4 * R), ptr(gws), N,
              CELL_CAP, ptr(sorted4), qr, ptr(s_pos), ptr(s_ray), ptr(s_nbr), ptr(nsurv), ptr(kws), s)
+        self._mark("knn")
         S = int(nsurv.item())
         self.last_stats["kept_samples"] = S
         if S == 0:
@@ -433,12 +448,14 @@ class TemporalPoints(torch.nn.Module):
         if self.timing is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
+            self.timing.setdefault("marks", []).append(("mlp_setup", e0))
         call("apn_point_mlp", ptr(s_pos), ptr(s_ray), ptr(s_nbr), S, ptr(nsurv), ptr(recA), ptr(recB), ptr(feat),
              128, ptr(vd), ptr(vemb), ptr(wbuf), self._eps, float(self.tineuvox.act_shift), interval, 0,
              ptr(out12), s)
         if self.timing is not None:
             e1.record()
             self.timing.setdefault("mlp_events", []).append((e0, e1, S))
+            self.timing["marks"].append(("mlp", e1))
         # compositing
         rgb = torch.empty(R, 3, device=dev); rgb_d = torch.empty(R, 3, device=dev)
         depth = torch.empty(R, device=dev); wvis = torch.empty(R, 3, device=dev)
@@ -446,4 +463,5 @@ class TemporalPoints(torch.nn.Module):
         rws = ws.get("ray_ws", 2 * R, torch.int32, dev)
         call("apn_composite", ptr(out12), ptr(s_pos), ptr(s_ray), S, ptr(nsurv), R, float(self.fast_color_thres), bg,
              ptr(rgb), ptr(rgb_d), ptr(depth), ptr(wvis), ptr(last), ptr(last_d), ptr(rws), s)
+        self._mark("composite")
         return rgb, rgb_d, depth, wvis, last, last_d

@@ -19,6 +19,8 @@
 //             seen, so the search stops exactly when the 8th best is closer than k*h(1-1e-4).
 #include "apn_common.h"
 
+#include <algorithm>
+
 namespace apn {
 
 struct GridParams {
@@ -277,6 +279,253 @@ __device__ __forceinline__ void scan_ball(const GridParams& g, const int* __rest
   }
 }
 
+// Signed offset sequence 0, -1, +1, -2, +2, ... (nearest-first order around a cell index).
+__device__ __forceinline__ int nf_offset(int i) { return (i & 1) ? -((i + 1) >> 1) : (i >> 1); }
+
+// scan_ball with the (z, y) rows visited nearest-first (offsets 0, -1, +1, ... around the query's
+// cell), so the running K-th best -- and with it the row culling bound -- shrinks as early as
+// possible. Same point set as scan_ball for the final result (culling is exact).
+template <int K>
+__device__ __forceinline__ void scan_ball_nf(const GridParams& g, const int* __restrict__ cell_start,
+                                             const float4* __restrict__ sorted, float qx, float qy, float qz,
+                                             float R2, float (&bd)[K], int (&bi)[K], int* ctr = nullptr) {
+  const float R = sqrtf(R2) * 1.0001f;
+  const int z0 = max((int)floorf((qz - R - g.oz) * g.inv_h), 0), z1 = min((int)floorf((qz + R - g.oz) * g.inv_h), g.dz - 1);
+  const int y0 = max((int)floorf((qy - R - g.oy) * g.inv_h), 0), y1 = min((int)floorf((qy + R - g.oy) * g.inv_h), g.dy - 1);
+  const int fz = min(max((int)floorf((qz - g.oz) * g.inv_h), z0), z1);
+  const int fy = min(max((int)floorf((qy - g.oy) * g.inv_h), y0), y1);
+  const int nz = 2 * max(fz - z0, z1 - fz) + 1, ny = 2 * max(fy - y0, y1 - fy) + 1;
+  for (int iz = 0; iz < nz; ++iz) {
+    const int z = fz + nf_offset(iz);
+    if (z < z0 || z > z1) continue;
+    const float dz2 = slab_d2(qz, g.oz, g.h, z, z);
+    if (dz2 > fminf(bd[K - 1], R2) * 1.0001f) continue;
+    for (int iy = 0; iy < ny; ++iy) {
+      const int y = fy + nf_offset(iy);
+      if (y < y0 || y > y1) continue;
+      const float tau = fminf(bd[K - 1], R2) * 1.0001f;
+      const float dyz2 = dz2 + slab_d2(qy, g.oy, g.h, y, y);
+      if (dyz2 > tau) continue;
+      const float w = sqrtf(tau - dyz2) * 1.0001f;
+      const int x0 = max((int)floorf((qx - w - g.ox) * g.inv_h), 0);
+      const int x1 = min((int)floorf((qx + w - g.ox) * g.inv_h), g.dx - 1);
+      if (x0 > x1) continue;
+      const int row = (z * g.dy + y) * g.dx;
+      const int b = cell_start[row + x0], e = cell_start[row + x1 + 1];
+      if (ctr) { ctr[0] += 1; ctr[1] += e - b; }
+      scan_range_u<K>(sorted, b, e, qx, qy, qz, g.r2, bd, bi);
+    }
+  }
+}
+
+// Upper bound on the number of points within sqrt(R2) of q: the points of every cell on the
+// ball's row chords (a superset of the ball). Loads only cell_start pairs (independent across
+// rows, no point reads); stops as soon as the bound reaches `need`.
+__device__ __forceinline__ int chord_count(const GridParams& g, const int* __restrict__ cell_start, float qx,
+                                           float qy, float qz, float R2, int need, int* ctr = nullptr) {
+  const float R = sqrtf(R2) * 1.0001f;
+  const int z0 = max((int)floorf((qz - R - g.oz) * g.inv_h), 0), z1 = min((int)floorf((qz + R - g.oz) * g.inv_h), g.dz - 1);
+  const int y0 = max((int)floorf((qy - R - g.oy) * g.inv_h), 0), y1 = min((int)floorf((qy + R - g.oy) * g.inv_h), g.dy - 1);
+  const int fz = min(max((int)floorf((qz - g.oz) * g.inv_h), z0), z1);
+  const int nz = 2 * max(fz - z0, z1 - fz) + 1;
+  const float tau = R2 * 1.0001f;
+  int c = 0;
+  for (int iz = 0; iz < nz && c < need; ++iz) {
+    const int z = fz + nf_offset(iz);
+    if (z < z0 || z > z1) continue;
+    const float dz2 = slab_d2(qz, g.oz, g.h, z, z);
+    if (dz2 > tau) continue;
+#pragma unroll 4
+    for (int y = y0; y <= y1; ++y) {
+      const float dyz2 = dz2 + slab_d2(qy, g.oy, g.h, y, y);
+      const float w = sqrtf(fmaxf(tau - dyz2, 0.f)) * 1.0001f;
+      const int x0 = max((int)floorf((qx - w - g.ox) * g.inv_h), 0);
+      const int x1 = min((int)floorf((qx + w - g.ox) * g.inv_h), g.dx - 1);
+      const int row = (z * g.dy + y) * g.dx;
+      if (dyz2 <= tau && x0 <= x1) {
+        c += cell_start[row + x1 + 1] - cell_start[row + x0];
+        if (ctr) ctr[0] += 1;
+      }
+    }
+  }
+  return c;
+}
+
+// ---- accessor-templated variants: CS(z, y, x) returns cell_start[(z*dy + y)*dx + x] (from LDS
+// when the tile kernel has staged that row, else from global memory).
+template <int K, class CS>
+__device__ __forceinline__ void scan_ball_cs(const GridParams& g, const CS& cs, const float4* __restrict__ sorted,
+                                             float qx, float qy, float qz, float R2, float (&bd)[K], int (&bi)[K]) {
+  const float R = sqrtf(R2) * 1.0001f;
+  const int z0 = max((int)floorf((qz - R - g.oz) * g.inv_h), 0), z1 = min((int)floorf((qz + R - g.oz) * g.inv_h), g.dz - 1);
+  const int y0 = max((int)floorf((qy - R - g.oy) * g.inv_h), 0), y1 = min((int)floorf((qy + R - g.oy) * g.inv_h), g.dy - 1);
+  const int fz = min(max((int)floorf((qz - g.oz) * g.inv_h), z0), z1);
+  const int fy = min(max((int)floorf((qy - g.oy) * g.inv_h), y0), y1);
+  const int nz = 2 * max(fz - z0, z1 - fz) + 1, ny = 2 * max(fy - y0, y1 - fy) + 1;
+  for (int iz = 0; iz < nz; ++iz) {
+    const int z = fz + nf_offset(iz);
+    if (z < z0 || z > z1) continue;
+    const float dz2 = slab_d2(qz, g.oz, g.h, z, z);
+    if (dz2 > fminf(bd[K - 1], R2) * 1.0001f) continue;
+    for (int iy = 0; iy < ny; ++iy) {
+      const int y = fy + nf_offset(iy);
+      if (y < y0 || y > y1) continue;
+      const float tau = fminf(bd[K - 1], R2) * 1.0001f;
+      const float dyz2 = dz2 + slab_d2(qy, g.oy, g.h, y, y);
+      if (dyz2 > tau) continue;
+      const float w = sqrtf(tau - dyz2) * 1.0001f;
+      const int x0 = max((int)floorf((qx - w - g.ox) * g.inv_h), 0);
+      const int x1 = min((int)floorf((qx + w - g.ox) * g.inv_h), g.dx - 1);
+      if (x0 > x1) continue;
+      scan_range_u<K>(sorted, cs(z, y, x0), cs(z, y, x1 + 1), qx, qy, qz, g.r2, bd, bi);
+    }
+  }
+}
+
+template <class CS>
+__device__ __forceinline__ int chord_count_cs(const GridParams& g, const CS& cs, float qx, float qy, float qz,
+                                              float R2, int need) {
+  const float R = sqrtf(R2) * 1.0001f;
+  const int z0 = max((int)floorf((qz - R - g.oz) * g.inv_h), 0), z1 = min((int)floorf((qz + R - g.oz) * g.inv_h), g.dz - 1);
+  const int y0 = max((int)floorf((qy - R - g.oy) * g.inv_h), 0), y1 = min((int)floorf((qy + R - g.oy) * g.inv_h), g.dy - 1);
+  const int fz = min(max((int)floorf((qz - g.oz) * g.inv_h), z0), z1);
+  const int nz = 2 * max(fz - z0, z1 - fz) + 1;
+  const float tau = R2 * 1.0001f;
+  int c = 0;
+  for (int iz = 0; iz < nz && c < need; ++iz) {
+    const int z = fz + nf_offset(iz);
+    if (z < z0 || z > z1) continue;
+    const float dz2 = slab_d2(qz, g.oz, g.h, z, z);
+    if (dz2 > tau) continue;
+    for (int y = y0; y <= y1; ++y) {
+      const float dyz2 = dz2 + slab_d2(qy, g.oy, g.h, y, y);
+      const float w = sqrtf(fmaxf(tau - dyz2, 0.f)) * 1.0001f;
+      const int x0 = max((int)floorf((qx - w - g.ox) * g.inv_h), 0);
+      const int x1 = min((int)floorf((qx + w - g.ox) * g.inv_h), g.dx - 1);
+      if (dyz2 <= tau && x0 <= x1) c += cs(z, y, x1 + 1) - cs(z, y, x0);
+    }
+  }
+  return c;
+}
+
+// ---- mode 5: tile-grouped search. Candidates are bucketed by tile (KT^3 fine cells); one
+// workgroup per tile stages the cell_start row segments of the tile's r-dilated region in LDS,
+// so the per-row bound lookups of every query in the tile are LDS reads, and the lanes of a
+// workgroup are spatial neighbours (similar search depth, little divergence).
+constexpr int KT = 4;
+constexpr int KT_LDS = 12288;   // ints of staged row bounds per workgroup (48 KB)
+
+__device__ __forceinline__ int tile_of(const GridParams& g, float4 q, int tdx, int tdy) {
+  const int fx = cell_coord(q.x, g.ox, g.inv_h, g.dx), fy = cell_coord(q.y, g.oy, g.inv_h, g.dy);
+  const int fz = cell_coord(q.z, g.oz, g.inv_h, g.dz);
+  return ((fz / KT) * tdy + fy / KT) * tdx + fx / KT;
+}
+
+__global__ __launch_bounds__(KNN_THREADS) void k_tile_count(const float4* __restrict__ q_pos,
+                                                           const int* __restrict__ cand,
+                                                           const int* __restrict__ n_cand_dev,
+                                                           const GridParams* __restrict__ gp, int* __restrict__ ctile,
+                                                           int* __restrict__ tile_cnt) {
+  const int c = blockIdx.x * KNN_THREADS + threadIdx.x;
+  if (c >= *n_cand_dev) return;
+  const GridParams g = *gp;
+  const int tdx = (g.dx + KT - 1) / KT, tdy = (g.dy + KT - 1) / KT;
+  const int t = tile_of(g, q_pos[cand[c]], tdx, tdy);
+  ctile[c] = t;
+  atomicAdd(tile_cnt + t, 1);
+}
+
+__global__ __launch_bounds__(KNN_THREADS) void k_tile_scatter(const int* __restrict__ n_cand_dev,
+                                                             const int* __restrict__ ctile,
+                                                             const int* __restrict__ tile_start,
+                                                             int* __restrict__ tile_cursor, int* __restrict__ order) {
+  const int c = blockIdx.x * KNN_THREADS + threadIdx.x;
+  if (c >= *n_cand_dev) return;
+  const int t = ctile[c];
+  order[tile_start[t] + atomicAdd(tile_cursor + t, 1)] = c;
+}
+
+// Non-empty tiles -> list (any order); n_list[0] = count.
+__global__ __launch_bounds__(KNN_THREADS) void k_tile_list(const int* __restrict__ tile_cnt, int n_tiles_max,
+                                                          int* __restrict__ list, int* __restrict__ n_list) {
+  const int t = blockIdx.x * KNN_THREADS + threadIdx.x;
+  const bool ne = t < n_tiles_max && tile_cnt[t] > 0;
+  const int lane = threadIdx.x & 63;
+  const unsigned long long bal = __ballot(ne);
+  if (!bal) return;
+  int base = 0;
+  if (lane == 0) base = atomicAdd(n_list, __popcll(bal));
+  base = __shfl(base, 0, 64);
+  if (ne) list[base + __popcll(bal & ((1ull << lane) - 1ull))] = t;
+}
+
+__global__ __launch_bounds__(KNN_THREADS) void k_knn_tiles(
+    const float4* __restrict__ q_pos, const int* __restrict__ cand, const GridParams* __restrict__ gp,
+    const int* __restrict__ cell_start, const float4* __restrict__ sorted, const int* __restrict__ tile_list,
+    const int* __restrict__ n_list_dev, const int* __restrict__ tile_start, const int* __restrict__ tile_cnt,
+    const int* __restrict__ order, int* __restrict__ flag, int* __restrict__ t_nbr) {
+  __shared__ int sCS[KT_LDS];
+  const GridParams g = *gp;
+  const int n_list = *n_list_dev;
+  const int tdx = (g.dx + KT - 1) / KT, tdy = (g.dy + KT - 1) / KT;
+  const int D = g.kmax + 1;
+  for (int li = blockIdx.x; li < n_list; li += gridDim.x) {
+    const int t = tile_list[li];
+    const int tx = t % tdx, ty = (t / tdx) % tdy, tz = t / (tdx * tdy);
+    // staged region: rows z in [rz0, rz0+nz), y in [ry0, ry0+ny), bound entries x in [rx0, rx0+nx1)
+    const int rz0 = max(tz * KT - D, 0), rz1 = min(tz * KT + KT - 1 + D, g.dz - 1);
+    const int ry0 = max(ty * KT - D, 0), ry1 = min(ty * KT + KT - 1 + D, g.dy - 1);
+    const int rx0 = max(tx * KT - D, 0), rx1 = min(tx * KT + KT + D, g.dx);
+    int nz = rz1 - rz0 + 1, ny = ry1 - ry0 + 1;
+    const int nx1 = rx1 - rx0 + 1;
+    if (nz * ny * nx1 > KT_LDS) nz = 0;   // does not fit: every lookup goes to global memory
+    const int tot = nz * ny * nx1;
+    for (int e = threadIdx.x; e < tot; e += KNN_THREADS) {
+      const int ix = e % nx1, r = e / nx1;
+      const int iy = r % ny, iz = r / ny;
+      sCS[e] = cell_start[((rz0 + iz) * g.dy + ry0 + iy) * g.dx + rx0 + ix];
+    }
+    __syncthreads();
+    auto cs = [&](int z, int y, int x) -> int {
+      const unsigned iz = z - rz0, iy = y - ry0, ix = x - rx0;
+      if (iz < (unsigned)nz && iy < (unsigned)ny && ix < (unsigned)nx1) return sCS[(iz * ny + iy) * nx1 + ix];
+      return cell_start[(z * g.dy + y) * g.dx + x];
+    };
+    const int n = tile_cnt[t], base = tile_start[t];
+    for (int i = threadIdx.x; i < n; i += KNN_THREADS) {
+      const int c = order[base + i];
+      const float4 q = q_pos[cand[c]];
+      float bd[KNN_K];
+      int bi[KNN_K];
+#pragma unroll
+      for (int k = 0; k < KNN_K; ++k) { bd[k] = INFINITY; bi[k] = 0x7fffffff; }
+      if (g.h > 0.25f * g.r) {
+        scan_ball_cs<KNN_K>(g, cs, sorted, q.x, q.y, q.z, g.r2, bd, bi);
+      } else {
+        // balls r/4, (chord-count rejection at r), r/2, r -- as mode 4
+        scan_ball_cs<KNN_K>(g, cs, sorted, q.x, q.y, q.z, 0.0625f * g.r2, bd, bi);
+        if (!(bd[KNN_K - 1] < 0.0625f * g.r2 * (1.f - 2e-4f))) {
+          if (chord_count_cs(g, cs, q.x, q.y, q.z, g.r2, KNN_K) < KNN_K) {
+            bd[KNN_K - 1] = INFINITY;
+          } else {
+            scan_ball_cs<KNN_K>(g, cs, sorted, q.x, q.y, q.z, 0.25f * g.r2, bd, bi);
+            if (!(bd[KNN_K - 1] < 0.25f * g.r2 * (1.f - 2e-4f)))
+              scan_ball_cs<KNN_K>(g, cs, sorted, q.x, q.y, q.z, g.r2, bd, bi);
+          }
+        }
+      }
+      const bool surv = bd[KNN_K - 1] <= g.r2;
+      flag[c] = surv;
+      if (surv) {
+        int4* nb = (int4*)(t_nbr + (int64_t)c * KNN_K);
+        nb[0] = make_int4(bi[0], bi[1], bi[2], bi[3]);
+        nb[1] = make_int4(bi[4], bi[5], bi[6], bi[7]);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // Pass 1: coarse rejection. Queries with >= 8 points in the 27 coarse cells around them are
 // compacted (in query order) per block into cand[blockIdx*256 ...]; blk_cnt[block] = count.
 __global__ __launch_bounds__(KNN_THREADS) void k_knn_classify(const float4* __restrict__ q_pos,
@@ -326,11 +575,20 @@ __global__ __launch_bounds__(KNN_THREADS) void k_compact_i32(const int* __restri
 
 // Pass 2: exact search for the compacted candidates. Survivors are compacted per block (order
 // preserved) into slots [blockIdx*256, ...) of t_*; blk_cnt[block] = survivors.
+// Profiling aid (mode 3 = mode 2 + counters): per query class {stop at 2h, rejected by the chord
+// count, stop at 4h, stop at r, rejected at r}: {queries, cycles, rows, points} summed.
+__device__ unsigned long long g_knn_stats[5 * 4];
+
+template <bool STATS>
 __global__ __launch_bounds__(KNN_THREADS) void k_knn_search(
     const float4* __restrict__ q_pos, const int* __restrict__ q_ray, const int* __restrict__ cand,
     const int* __restrict__ n_cand_dev, const GridParams* __restrict__ gp, const int* __restrict__ cell_start,
     const float4* __restrict__ sorted, float4* __restrict__ t_pos, int* __restrict__ t_ray,
     int* __restrict__ t_nbr, int* __restrict__ blk_cnt, int mode) {
+  int ctr[2] = {0, 0};
+  int* const cp = STATS ? ctr : nullptr;
+  int cls = 0;
+  const unsigned long long t0 = STATS ? clock64() : 0;
   __shared__ int wave_cnt[KNN_THREADS / 64];
   const int nc = *n_cand_dev;
   const int c = blockIdx.x * KNN_THREADS + threadIdx.x;
@@ -344,7 +602,29 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_search(
   if (c < nc) {
     qi = cand[c];
     q = q_pos[qi];
-    if (mode == 0) {
+    if (mode >= 2) {
+      // ball 2h (most samples inside the cloud stop here); then an exact rejection bound from the
+      // r-ball's chord counts (87% of the remaining non-survivors, no point reads); then balls
+      // 4h and r, rows nearest-first
+      scan_ball_nf<KNN_K>(g, cell_start, sorted, q.x, q.y, q.z, 4.f * g.h * g.h, bd, bi, cp);
+      if (!(bd[KNN_K - 1] < 4.f * g.h * g.h * (1.f - 2e-4f)) && 2.f * g.h < g.r) {
+        if (chord_count(g, cell_start, q.x, q.y, q.z, g.r2, KNN_K, cp) < KNN_K) {
+          bd[KNN_K - 1] = INFINITY;   // < 8 points within r: not a survivor
+          cls = 1;
+        } else {
+          float R = 4.f * g.h;
+          cls = 2;
+          for (;;) {
+            const float Rl = fminf(R, g.r);
+            const float R2 = Rl >= g.r ? g.r2 : Rl * Rl;
+            scan_ball_nf<KNN_K>(g, cell_start, sorted, q.x, q.y, q.z, R2, bd, bi, cp);
+            if (Rl >= g.r || bd[KNN_K - 1] < R2 * (1.f - 2e-4f)) break;
+            R *= 2.f;
+          }
+          if (!(bd[KNN_K - 1] < 16.f * g.h * g.h * (1.f - 2e-4f))) cls = bd[KNN_K - 1] <= g.r2 ? 3 : 4;
+        }
+      }
+    } else if (mode == 0) {
       // expanding balls R = 2h, 4h, ..., r: after a ball every point within R has been seen, so
       // a K-th best strictly inside R is final
       float R = 2.f * g.h;
@@ -367,6 +647,13 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_search(
     }
   }
   const bool surv = (c < nc) && (bd[KNN_K - 1] <= g.r2);
+  if (STATS && c < nc) {
+    const unsigned long long dt = clock64() - t0;
+    atomicAdd(&g_knn_stats[4 * cls + 0], 1ull);
+    atomicAdd(&g_knn_stats[4 * cls + 1], dt);
+    atomicAdd(&g_knn_stats[4 * cls + 2], (unsigned long long)ctr[0]);
+    atomicAdd(&g_knn_stats[4 * cls + 3], (unsigned long long)ctr[1]);
+  }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const unsigned long long bal = __ballot(surv);
   const int before = __popcll(bal & ((1ull << lane) - 1ull));
@@ -387,6 +674,312 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_search(
     nb[1] = make_int4(bi[4], bi[5], bi[6], bi[7]);
   }
   if (threadIdx.x == 0) blk_cnt[blockIdx.x] = tot;
+}
+
+// ---- mode 4: the search split into two passes so each wave runs a uniform loop structure
+// (one lane per query, lanes of a wave in the same phase; the single-pass kernel's lanes run
+// different phases side by side and the wave executes their union).
+// Pass A, every candidate: ball r/4; if 8 neighbours lie inside it the sample is a survivor;
+// else the r-ball chord count (exact upper bound) rejects it when < 8; the rest are appended to
+// the hard list. Results per candidate slot: flag[c] (survivor) and t_nbr[c].
+__global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_a(
+    const float4* __restrict__ q_pos, const int* __restrict__ cand, const int* __restrict__ n_cand_dev,
+    const GridParams* __restrict__ gp, const int* __restrict__ cell_start, const float4* __restrict__ sorted,
+    int* __restrict__ flag, int* __restrict__ t_nbr, int* __restrict__ hard, int* __restrict__ n_hard) {
+  const int nc = *n_cand_dev;
+  const int c = blockIdx.x * KNN_THREADS + threadIdx.x;
+  const GridParams g = *gp;
+  bool push = false;
+  if (c < nc) {
+    const float4 q = q_pos[cand[c]];
+    float bd[KNN_K];
+    int bi[KNN_K];
+#pragma unroll
+    for (int k = 0; k < KNN_K; ++k) { bd[k] = INFINITY; bi[k] = 0x7fffffff; }
+    bool done = true;
+    if (g.h > 0.25f * g.r) {  // coarse (cell-capped) grid: the whole search here
+      scan_ball_nf<KNN_K>(g, cell_start, sorted, q.x, q.y, q.z, g.r2, bd, bi);
+    } else {
+      const float R2 = 0.0625f * g.r2;   // ball r/4
+      scan_ball_nf<KNN_K>(g, cell_start, sorted, q.x, q.y, q.z, R2, bd, bi);
+      if (!(bd[KNN_K - 1] < R2 * (1.f - 2e-4f))) {
+        if (chord_count(g, cell_start, q.x, q.y, q.z, g.r2, KNN_K) < KNN_K)
+          bd[KNN_K - 1] = INFINITY;   // < 8 points within r
+        else
+          done = false;
+      }
+    }
+    if (done) {
+      const bool surv = bd[KNN_K - 1] <= g.r2;
+      flag[c] = surv;
+      if (surv) {
+        int4* nb = (int4*)(t_nbr + (int64_t)c * KNN_K);
+        nb[0] = make_int4(bi[0], bi[1], bi[2], bi[3]);
+        nb[1] = make_int4(bi[4], bi[5], bi[6], bi[7]);
+      }
+    } else {
+      push = true;
+    }
+  }
+  const int lane = threadIdx.x & 63;
+  const unsigned long long bal = __ballot(push);
+  if (bal) {
+    int base = 0;
+    if (lane == 0) base = atomicAdd(n_hard, __popcll(bal));
+    base = __shfl(base, 0, 64);
+    if (push) hard[base + __popcll(bal & ((1ull << lane) - 1ull))] = c;
+  }
+}
+
+// Pass B, the hard list: balls r/2, r with nearest-first rows and running culling.
+__global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_b(
+    const float4* __restrict__ q_pos, const int* __restrict__ cand, const int* __restrict__ hard,
+    const int* __restrict__ n_hard, const GridParams* __restrict__ gp, const int* __restrict__ cell_start,
+    const float4* __restrict__ sorted, int* __restrict__ flag, int* __restrict__ t_nbr) {
+  const int i = blockIdx.x * KNN_THREADS + threadIdx.x;
+  if (i >= *n_hard) return;
+  const GridParams g = *gp;
+  const int c = hard[i];
+  const float4 q = q_pos[cand[c]];
+  float bd[KNN_K];
+  int bi[KNN_K];
+#pragma unroll
+  for (int k = 0; k < KNN_K; ++k) { bd[k] = INFINITY; bi[k] = 0x7fffffff; }
+  // balls r/2, r
+  scan_ball_nf<KNN_K>(g, cell_start, sorted, q.x, q.y, q.z, 0.25f * g.r2, bd, bi);
+  if (!(bd[KNN_K - 1] < 0.25f * g.r2 * (1.f - 2e-4f)))
+    scan_ball_nf<KNN_K>(g, cell_start, sorted, q.x, q.y, q.z, g.r2, bd, bi);
+  const bool surv = bd[KNN_K - 1] <= g.r2;
+  flag[c] = surv;
+  if (surv) {
+    int4* nb = (int4*)(t_nbr + (int64_t)c * KNN_K);
+    nb[0] = make_int4(bi[0], bi[1], bi[2], bi[3]);
+    nb[1] = make_int4(bi[4], bi[5], bi[6], bi[7]);
+  }
+}
+
+// ---- mode 6: per-cell rejection bound. For every fine cell C holding a candidate, U(C) = number
+// of points in cells whose box lies within r of C's box -- an upper bound on the points within r of
+// ANY query in C (also of a query just outside the grid, clamped into C: its distance to a point
+// exceeds the box-box distance). Candidates with U(C) < 8 are rejected without a search; the
+// cell count is ~10x smaller than the candidate count, so the bound costs a tenth of a per-query
+// chord count.
+__global__ __launch_bounds__(KNN_THREADS) void k_mark_cells(const float4* __restrict__ q_pos,
+                                                           const int* __restrict__ cand,
+                                                           const int* __restrict__ n_cand_dev,
+                                                           const GridParams* __restrict__ gp, int* __restrict__ ccell,
+                                                           int* __restrict__ mark) {
+  const int c = blockIdx.x * KNN_THREADS + threadIdx.x;
+  if (c >= *n_cand_dev) return;
+  const GridParams g = *gp;
+  const float4 q = q_pos[cand[c]];
+  const int cell = (cell_coord(q.z, g.oz, g.inv_h, g.dz) * g.dy + cell_coord(q.y, g.oy, g.inv_h, g.dy)) * g.dx +
+                   cell_coord(q.x, g.ox, g.inv_h, g.dx);
+  ccell[c] = cell;
+  mark[cell] = 1;
+}
+
+__global__ __launch_bounds__(KNN_THREADS) void k_cell_bound(const GridParams* __restrict__ gp,
+                                                           const int* __restrict__ cell_start,
+                                                           const int* __restrict__ list, const int* __restrict__ n_list,
+                                                           int* __restrict__ ubound) {
+  const int i = blockIdx.x * KNN_THREADS + threadIdx.x;
+  if (i >= *n_list) return;
+  const GridParams g = *gp;
+  const int cell = list[i];
+  const int cx = cell % g.dx, cy = (cell / g.dx) % g.dy, cz = cell / (g.dx * g.dy);
+  const float lim = g.r2 * 1.0002f * g.inv_h * g.inv_h;   // (r/h)^2 with slack
+  const int K = (int)ceilf(sqrtf(lim)) + 1;
+  int u = 0;
+  for (int dz = -K; dz <= K; ++dz) {
+    const int z = cz + dz;
+    if (z < 0 || z >= g.dz) continue;
+    const float gz = (float)max(abs(dz) - 1, 0);
+    for (int dy = -K; dy <= K; ++dy) {
+      const int y = cy + dy;
+      const float gy = (float)max(abs(dy) - 1, 0);
+      const float rem = lim - gz * gz - gy * gy;
+      if (y < 0 || y >= g.dy || rem < 0.f) continue;
+      const int kx = (int)floorf(sqrtf(rem)) + 1;
+      const int row = (z * g.dy + y) * g.dx;
+      u += cell_start[row + min(cx + kx, g.dx - 1) + 1] - cell_start[row + max(cx - kx, 0)];
+    }
+  }
+  ubound[cell] = u;
+}
+
+// Pass A of mode 6: candidates whose cell bound is < 8 are rejected; the rest run the r/4 ball
+// and, unless it already holds the 8 nearest, go to the hard list (pass B).
+__global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_a6(
+    const float4* __restrict__ q_pos, const int* __restrict__ cand, const int* __restrict__ n_cand_dev,
+    const GridParams* __restrict__ gp, const int* __restrict__ cell_start, const float4* __restrict__ sorted,
+    const int* __restrict__ ccell, const int* __restrict__ ubound, int* __restrict__ flag, int* __restrict__ t_nbr,
+    int* __restrict__ hard, int* __restrict__ n_hard) {
+  const int nc = *n_cand_dev;
+  const int c = blockIdx.x * KNN_THREADS + threadIdx.x;
+  const GridParams g = *gp;
+  bool push = false;
+  if (c < nc) {
+    bool surv = false;
+    if (ubound[ccell[c]] >= KNN_K) {
+      const float4 q = q_pos[cand[c]];
+      float bd[KNN_K];
+      int bi[KNN_K];
+#pragma unroll
+      for (int k = 0; k < KNN_K; ++k) { bd[k] = INFINITY; bi[k] = 0x7fffffff; }
+      const float R2 = g.h > 0.25f * g.r ? g.r2 : 0.0625f * g.r2;
+      scan_ball_nf<KNN_K>(g, cell_start, sorted, q.x, q.y, q.z, R2, bd, bi);
+      if (R2 == g.r2 || bd[KNN_K - 1] < R2 * (1.f - 2e-4f)) {
+        surv = bd[KNN_K - 1] <= g.r2;
+        if (surv) {
+          int4* nb = (int4*)(t_nbr + (int64_t)c * KNN_K);
+          nb[0] = make_int4(bi[0], bi[1], bi[2], bi[3]);
+          nb[1] = make_int4(bi[4], bi[5], bi[6], bi[7]);
+        }
+      } else {
+        push = true;
+      }
+    }
+    if (!push) flag[c] = surv;
+  }
+  const int lane = threadIdx.x & 63;
+  const unsigned long long bal = __ballot(push);
+  if (bal) {
+    int base = 0;
+    if (lane == 0) base = atomicAdd(n_hard, __popcll(bal));
+    base = __shfl(base, 0, 64);
+    if (push) hard[base + __popcll(bal & ((1ull << lane) - 1ull))] = c;
+  }
+}
+
+// Ball scan as a per-lane state machine ("flat" loop): every iteration a lane either consumes
+// points of its current row range, or takes over the row range it loaded one step earlier and
+// examines the next row (nearest-first order, culled by the running K-th best) to load its
+// bounds. The wave therefore advances all lanes together whatever their row lengths (the nested
+// row/point loops of scan_ball_nf run the union of every lane's trip counts), and each row's
+// bounds load has a whole point-consuming phase to arrive. Same point set and result as
+// scan_ball_nf.
+template <int K>
+__device__ __forceinline__ void scan_ball_flat(const GridParams& g, const int* __restrict__ cell_start,
+                                               const float4* __restrict__ sorted, float qx, float qy, float qz,
+                                               float R2, float (&bd)[K], int (&bi)[K]) {
+  const float R = sqrtf(R2) * 1.0001f;
+  const int z0 = max((int)floorf((qz - R - g.oz) * g.inv_h), 0), z1 = min((int)floorf((qz + R - g.oz) * g.inv_h), g.dz - 1);
+  const int y0 = max((int)floorf((qy - R - g.oy) * g.inv_h), 0), y1 = min((int)floorf((qy + R - g.oy) * g.inv_h), g.dy - 1);
+  const int fz = min(max((int)floorf((qz - g.oz) * g.inv_h), z0), z1);
+  const int fy = min(max((int)floorf((qy - g.oy) * g.inv_h), y0), y1);
+  const int nz = 2 * max(fz - z0, z1 - fz) + 1, ny = 2 * max(fy - y0, y1 - fy) + 1;
+  const int nrows = (z1 < z0 || y1 < y0) ? 0 : nz * ny;
+  int cur = 0;                     // next row slot (iz * ny + iy) to examine
+  int b = 0, e = 0;                // range being consumed
+  int pb = 0, pe = 0;              // range loaded for the next row
+  bool pend = false;
+  for (;;) {
+    const bool has_pts = b < e;
+    if (!has_pts && !pend && cur >= nrows) break;
+    if (has_pts) {
+      const int p1 = b + 1 < e ? b + 1 : b;
+      const float4 P0 = sorted[b], P1 = sorted[p1];
+      const float d0x = qx - P0.x, d0y = qy - P0.y, d0z = qz - P0.z;
+      const float d0 = (d0x * d0x + d0y * d0y) + d0z * d0z;
+      const float d1x = qx - P1.x, d1y = qy - P1.y, d1z = qz - P1.z;
+      const float d1 = (d1x * d1x + d1y * d1y) + d1z * d1z;
+      if (d0 <= g.r2) knn_insert_unique<K>(d0, __float_as_int(P0.w), bd, bi);
+      if (p1 != b && d1 <= g.r2) knn_insert_unique<K>(d1, __float_as_int(P1.w), bd, bi);
+      b += 2;
+      if (b > e) b = e;
+    } else {
+      if (pend) { b = pb; e = pe; pend = false; }
+      // examine one row slot
+      if (cur < nrows) {
+        const int iz = cur / ny, iy = cur - iz * ny;
+        ++cur;
+        const int z = fz + nf_offset(iz), y = fy + nf_offset(iy);
+        if (z >= z0 && z <= z1 && y >= y0 && y <= y1) {
+          const float tau = fminf(bd[K - 1], R2) * 1.0001f;
+          const float dyz2 = slab_d2(qz, g.oz, g.h, z, z) + slab_d2(qy, g.oy, g.h, y, y);
+          if (dyz2 <= tau) {
+            const float w = sqrtf(tau - dyz2) * 1.0001f;
+            const int x0 = max((int)floorf((qx - w - g.ox) * g.inv_h), 0);
+            const int x1 = min((int)floorf((qx + w - g.ox) * g.inv_h), g.dx - 1);
+            if (x0 <= x1) {
+              const int row = (z * g.dy + y) * g.dx;
+              pb = cell_start[row + x0];
+              pe = cell_start[row + x1 + 1];
+              pend = true;
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+// Pass B with the flat ball scan (mode 7).
+__global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_b_flat(
+    const float4* __restrict__ q_pos, const int* __restrict__ cand, const int* __restrict__ hard,
+    const int* __restrict__ n_hard, const GridParams* __restrict__ gp, const int* __restrict__ cell_start,
+    const float4* __restrict__ sorted, int* __restrict__ flag, int* __restrict__ t_nbr) {
+  const int i = blockIdx.x * KNN_THREADS + threadIdx.x;
+  if (i >= *n_hard) return;
+  const GridParams g = *gp;
+  const int c = hard[i];
+  const float4 q = q_pos[cand[c]];
+  float bd[KNN_K];
+  int bi[KNN_K];
+#pragma unroll
+  for (int k = 0; k < KNN_K; ++k) { bd[k] = INFINITY; bi[k] = 0x7fffffff; }
+  scan_ball_flat<KNN_K>(g, cell_start, sorted, q.x, q.y, q.z, 0.25f * g.r2, bd, bi);
+  if (!(bd[KNN_K - 1] < 0.25f * g.r2 * (1.f - 2e-4f)))
+    scan_ball_flat<KNN_K>(g, cell_start, sorted, q.x, q.y, q.z, g.r2, bd, bi);
+  const bool surv = bd[KNN_K - 1] <= g.r2;
+  flag[c] = surv;
+  if (surv) {
+    int4* nb = (int4*)(t_nbr + (int64_t)c * KNN_K);
+    nb[0] = make_int4(bi[0], bi[1], bi[2], bi[3]);
+    nb[1] = make_int4(bi[4], bi[5], bi[6], bi[7]);
+  }
+}
+
+// Survivor counts per block of candidate slots (for the order-preserving compaction).
+__global__ __launch_bounds__(KNN_THREADS) void k_knn_flag_count(const int* __restrict__ flag,
+                                                                const int* __restrict__ n_cand_dev,
+                                                                int* __restrict__ blk_cnt) {
+  __shared__ int wave_cnt[KNN_THREADS / 64];
+  const int c = blockIdx.x * KNN_THREADS + threadIdx.x;
+  const bool f = c < *n_cand_dev && flag[c];
+  const unsigned long long bal = __ballot(f);
+  if ((threadIdx.x & 63) == 0) wave_cnt[threadIdx.x >> 6] = __popcll(bal);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int w = 0; w < KNN_THREADS / 64; ++w) t += wave_cnt[w];
+    blk_cnt[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(KNN_THREADS) void k_knn_flag_compact(
+    const float4* __restrict__ q_pos, const int* __restrict__ q_ray, const int* __restrict__ cand,
+    const int* __restrict__ n_cand_dev, const int* __restrict__ flag, const int* __restrict__ t_nbr,
+    const int* __restrict__ blk_off, float4* __restrict__ s_pos, int* __restrict__ s_ray, int* __restrict__ s_nbr) {
+  __shared__ int wave_cnt[KNN_THREADS / 64];
+  const int c = blockIdx.x * KNN_THREADS + threadIdx.x;
+  const bool f = c < *n_cand_dev && flag[c];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const unsigned long long bal = __ballot(f);
+  if (lane == 0) wave_cnt[wid] = __popcll(bal);
+  __syncthreads();
+  int base = blk_off[blockIdx.x];
+  for (int w = 0; w < wid; ++w) base += wave_cnt[w];
+  if (!f) return;
+  const int dst = base + __popcll(bal & ((1ull << lane) - 1ull));
+  const int qi = cand[c];
+  s_pos[dst] = q_pos[qi];
+  s_ray[dst] = q_ray[qi];
+  const int4* a = (const int4*)(t_nbr + (int64_t)c * KNN_K);
+  int4* b = (int4*)(s_nbr + (int64_t)dst * KNN_K);
+  b[0] = a[0];
+  b[1] = a[1];
 }
 
 __global__ __launch_bounds__(KNN_THREADS) void k_knn_compact(
@@ -467,28 +1060,48 @@ __global__ void k_bbox_init2(int* bbox_ord) {
 
 using namespace apn;
 
-// Workspace layout for apn_grid_build (bytes, each region 256-B aligned):
-//   GridParams | counts[cap] | cell_start[cap+1] | cursor[cap] | pcell[N] | ccount[cap] | scan ws
 static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// Search strategy: 0 = expanding ball scans (default), 1 = culled Chebyshev rings.
-// APN_KNN_MODE selects one for A/B measurements; both are exact.
-static int knn_mode() {
+// Search strategy (apn_set_knn_mode / APN_KNN_MODE; default 7, see include/apn_hip.h). All are
+// exact; the others stay for A/B measurements and as cross-checks in the tests.
+static int& knn_mode() {
   static int m = [] {
     const char* e = getenv("APN_KNN_MODE");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 7;
   }();
   return m;
 }
 
+extern "C" int apn_set_knn_mode(int32_t mode) {
+  const int prev = knn_mode();
+  if (mode >= 0 && mode <= 7) knn_mode() = mode;
+  return prev;
+}
+
+// Profiling aid (synchronous): copies and resets the mode-3 counters (20 uint64, see g_knn_stats).
+extern "C" int apn_debug_knn_stats(uint64_t* out20) {
+  if (!out20) return APN_ERR_ARG;
+  APN_HIP_TRY(hipDeviceSynchronize());
+  APN_HIP_TRY(hipMemcpyFromSymbol(out20, HIP_SYMBOL(g_knn_stats), sizeof(uint64_t) * 20));
+  static const unsigned long long zero[20] = {};
+  APN_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_knn_stats), zero, sizeof(zero)));
+  return APN_OK;
+}
+
+// Grid workspace (bytes, each region 256-B aligned):
+//   GridParams | counts[cap] | cell_start[cap+1] | cursor[cap] | pcell[N] | ccount[cap] | scan ws |
+//   tile_cnt[cap] | tile_start[cap+1] | tile_cursor[cap] | tile_list[cap] | n_tile_list[1]
+// (tiles of KT^3 cells never outnumber cells, so cap bounds the tile arrays).
 extern "C" size_t apn_grid_workspace_bytes(int64_t n_points, int32_t cell_cap) {
   return al256(sizeof(GridParams)) + al256((size_t)cell_cap * 4) + al256((size_t)(cell_cap + 1) * 4) +
          al256((size_t)cell_cap * 4) + al256((size_t)n_points * 4) + al256((size_t)cell_cap * 4) +
-         al256(scan_workspace_bytes(cell_cap));
+         al256(scan_workspace_bytes(cell_cap)) + al256((size_t)cell_cap * 4) * 3 +
+         al256((size_t)(cell_cap + 1) * 4) + al256(4);
 }
 
 struct GridWs {
   GridParams* gp; int* counts; int* cell_start; int* cursor; int* pcell; int* ccount; void* scan;
+  int* tile_cnt; int* tile_start; int* tile_cursor; int* tile_list; int* n_tile_list;
 };
 static GridWs grid_ws(void* ws, int64_t N, int cap) {
   char* p = (char*)ws;
@@ -499,7 +1112,12 @@ static GridWs grid_ws(void* ws, int64_t N, int cap) {
   w.cursor = (int*)p; p += al256((size_t)cap * 4);
   w.pcell = (int*)p; p += al256((size_t)N * 4);
   w.ccount = (int*)p; p += al256((size_t)cap * 4);
-  w.scan = p;
+  w.scan = p; p += al256(scan_workspace_bytes(cap));
+  w.tile_cnt = (int*)p; p += al256((size_t)cap * 4);
+  w.tile_start = (int*)p; p += al256((size_t)(cap + 1) * 4);
+  w.tile_cursor = (int*)p; p += al256((size_t)cap * 4);
+  w.tile_list = (int*)p; p += al256((size_t)cap * 4);
+  w.n_tile_list = (int*)p;
   return w;
 }
 
@@ -568,9 +1186,89 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
   if (st) return st;
   hipLaunchKernelGGL(k_compact_i32, dim3(nb), dim3(KNN_THREADS), 0, s, cand_blk, cblk_cnt, cblk_off, cand);
   // candidates: count at cblk_off[nb]; launch over the upper bound nb blocks
-  hipLaunchKernelGGL(k_knn_search, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, q_ray, cand,
-                     cblk_off + nb, g.gp, g.cell_start, (const float4*)sorted_pts4, t_pos, t_ray, t_nbr, blk_cnt,
-                     knn_mode());
+  if (knn_mode() == 6 || knn_mode() == 7) {
+    int* flag = t_ray;
+    int* hard = cand_blk;
+    int* n_hard = cblk_cnt + nb + 1;
+    int* ccell = (int*)t_pos;
+    int* mark = g.cursor;        // free after the grid build
+    int* ubound = g.counts;      // free after the grid build
+    APN_HIP_TRY(hipMemsetAsync(mark, 0, (size_t)cell_cap * 4, s));
+    APN_HIP_TRY(hipMemsetAsync(g.n_tile_list, 0, 4, s));
+    APN_HIP_TRY(hipMemsetAsync(n_hard, 0, 4, s));
+    hipLaunchKernelGGL(k_mark_cells, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, cblk_off + nb,
+                       g.gp, ccell, mark);
+    hipLaunchKernelGGL(k_tile_list, dim3(ceil_div(cell_cap, KNN_THREADS)), dim3(KNN_THREADS), 0, s, mark, cell_cap,
+                       g.tile_list, g.n_tile_list);
+    hipLaunchKernelGGL(k_cell_bound, dim3(ceil_div(std::min<int64_t>(cell_cap, slots), KNN_THREADS)),
+                       dim3(KNN_THREADS), 0, s, g.gp, g.cell_start, g.tile_list, g.n_tile_list, ubound);
+    hipLaunchKernelGGL(k_knn_pass_a6, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, cblk_off + nb,
+                       g.gp, g.cell_start, (const float4*)sorted_pts4, ccell, ubound, flag, t_nbr, hard, n_hard);
+    if (knn_mode() == 7)
+      hipLaunchKernelGGL(k_knn_pass_b_flat, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard,
+                         n_hard, g.gp, g.cell_start, (const float4*)sorted_pts4, flag, t_nbr);
+    else
+      hipLaunchKernelGGL(k_knn_pass_b, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard, n_hard,
+                         g.gp, g.cell_start, (const float4*)sorted_pts4, flag, t_nbr);
+    hipLaunchKernelGGL(k_knn_flag_count, dim3(nb), dim3(KNN_THREADS), 0, s, flag, cblk_off + nb, blk_cnt);
+    st = scan_exclusive_i32(blk_cnt, blk_off, nb, sws, s);
+    if (st) return st;
+    hipLaunchKernelGGL(k_knn_flag_compact, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, q_ray, cand,
+                       cblk_off + nb, flag, t_nbr, blk_off, (float4*)s_pos4, s_ray, s_nbr);
+    APN_HIP_TRY(hipMemcpyAsync(n_survivors_dev, blk_off + nb, 4, hipMemcpyDeviceToDevice, s));
+    return launch_status();
+  }
+  if (knn_mode() == 5) {
+    int* flag = t_ray;
+    int* order = cand_blk;
+    int* ctile = (int*)t_pos;
+    APN_HIP_TRY(hipMemsetAsync(g.tile_cnt, 0, (size_t)cell_cap * 4, s));
+    APN_HIP_TRY(hipMemsetAsync(g.tile_cursor, 0, (size_t)cell_cap * 4, s));
+    APN_HIP_TRY(hipMemsetAsync(g.n_tile_list, 0, 4, s));
+    hipLaunchKernelGGL(k_tile_count, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, cblk_off + nb,
+                       g.gp, ctile, g.tile_cnt);
+    st = scan_exclusive_i32(g.tile_cnt, g.tile_start, cell_cap, g.scan, s);
+    if (st) return st;
+    hipLaunchKernelGGL(k_tile_scatter, dim3(nb), dim3(KNN_THREADS), 0, s, cblk_off + nb, ctile, g.tile_start,
+                       g.tile_cursor, order);
+    hipLaunchKernelGGL(k_tile_list, dim3(ceil_div(cell_cap, KNN_THREADS)), dim3(KNN_THREADS), 0, s, g.tile_cnt,
+                       cell_cap, g.tile_list, g.n_tile_list);
+    hipLaunchKernelGGL(k_knn_tiles, dim3(256 * 3), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, g.gp,
+                       g.cell_start, (const float4*)sorted_pts4, g.tile_list, g.n_tile_list, g.tile_start,
+                       g.tile_cnt, order, flag, t_nbr);
+    hipLaunchKernelGGL(k_knn_flag_count, dim3(nb), dim3(KNN_THREADS), 0, s, flag, cblk_off + nb, blk_cnt);
+    st = scan_exclusive_i32(blk_cnt, blk_off, nb, sws, s);
+    if (st) return st;
+    hipLaunchKernelGGL(k_knn_flag_compact, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, q_ray, cand,
+                       cblk_off + nb, flag, t_nbr, blk_off, (float4*)s_pos4, s_ray, s_nbr);
+    APN_HIP_TRY(hipMemcpyAsync(n_survivors_dev, blk_off + nb, 4, hipMemcpyDeviceToDevice, s));
+    return launch_status();
+  }
+  if (knn_mode() == 4) {
+    int* flag = t_ray;              // per candidate slot
+    int* hard = cand_blk;           // free after the candidate compaction
+    int* n_hard = cblk_cnt + nb + 1;
+    APN_HIP_TRY(hipMemsetAsync(n_hard, 0, 4, s));
+    hipLaunchKernelGGL(k_knn_pass_a, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, cblk_off + nb,
+                       g.gp, g.cell_start, (const float4*)sorted_pts4, flag, t_nbr, hard, n_hard);
+    hipLaunchKernelGGL(k_knn_pass_b, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard, n_hard,
+                       g.gp, g.cell_start, (const float4*)sorted_pts4, flag, t_nbr);
+    hipLaunchKernelGGL(k_knn_flag_count, dim3(nb), dim3(KNN_THREADS), 0, s, flag, cblk_off + nb, blk_cnt);
+    st = scan_exclusive_i32(blk_cnt, blk_off, nb, sws, s);
+    if (st) return st;
+    hipLaunchKernelGGL(k_knn_flag_compact, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, q_ray, cand,
+                       cblk_off + nb, flag, t_nbr, blk_off, (float4*)s_pos4, s_ray, s_nbr);
+    APN_HIP_TRY(hipMemcpyAsync(n_survivors_dev, blk_off + nb, 4, hipMemcpyDeviceToDevice, s));
+    return launch_status();
+  }
+  if (knn_mode() == 3)
+    hipLaunchKernelGGL(k_knn_search<true>, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, q_ray, cand,
+                       cblk_off + nb, g.gp, g.cell_start, (const float4*)sorted_pts4, t_pos, t_ray, t_nbr, blk_cnt,
+                       3);
+  else
+    hipLaunchKernelGGL(k_knn_search<false>, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, q_ray, cand,
+                       cblk_off + nb, g.gp, g.cell_start, (const float4*)sorted_pts4, t_pos, t_ray, t_nbr, blk_cnt,
+                       knn_mode());
   st = scan_exclusive_i32(blk_cnt, blk_off, nb, sws, s);
   if (st) return st;
   hipLaunchKernelGGL(k_knn_compact, dim3(nb), dim3(KNN_THREADS), 0, s, t_pos, t_ray, t_nbr, blk_cnt, blk_off,

@@ -181,6 +181,23 @@ def main():
         log("[mlp phases] " + ", ".join(f"{n} {100 * ph[i] / tot:.1f}%" for i, n in
                                         enumerate(["gather", "layer1", "layers2-4", "epilogue"]))
             + f"; cycles/tile {tot / max(ph[4], 1):.0f}, in-loop share {tot / max(ph[5], 1):.3f}")
+    stage_ms = {}
+    marks = model.timing.get("marks", [])
+    for (_, a), (name, b) in zip(marks[:-1], marks[1:]):
+        if name != "frame":
+            stage_ms[name] = stage_ms.get(name, 0.0) + a.elapsed_time(b) / args.steps
+    log(f"[rank {rank}] stage ms/frame (HIP events): " + ", ".join(f"{k} {v:.3f}" for k, v in stage_ms.items()))
+    if os.environ.get("APN_KNN_MODE") == "3":   # kNN query-class counters
+        import ctypes
+        from apn_amd import _lib
+        st = (ctypes.c_uint64 * 20)()
+        _lib.call("apn_debug_knn_stats", st)
+        names = ["stop2h", "chord_reject", "stop4h", "stop_r", "reject_r"]
+        tot_cyc = sum(st[4 * i + 1] for i in range(5)) or 1
+        for i, nm in enumerate(names):
+            n = st[4 * i] or 1
+            log(f"[knn {nm}] queries/frame {st[4 * i] / args.steps:.0f} cycles share {100 * st[4 * i + 1] / tot_cyc:.1f}% "
+                f"cycles/query {st[4 * i + 1] / n:.0f} rows/query {st[4 * i + 2] / n:.1f} pts/query {st[4 * i + 3] / n:.1f}")
     ev = model.timing.get("mlp_events", [])
     mlp_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / max(len(ev), 1)
     S_kept = ev[-1][2] if ev else stats.get("kept_samples", 0)
@@ -235,6 +252,7 @@ def main():
                              "tile): executed_tflops / mfma_util",
                      "executed_tflops": executed,
                      "mfma_util": executed / mfma_peak},
+        "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)

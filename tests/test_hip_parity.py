@@ -120,17 +120,28 @@ def _golden_queries(g):
     return pts[~mo], rid[~mo], sid[~mo]
 
 
+@pytest.mark.parametrize("mode", [0, 1, 2, 4, 5, 6, 7])
+@pytest.mark.parametrize("cap", [1 << 20, 1 << 12])
 @pytest.mark.parametrize("name", CASES)
-def test_knn_stage_on_reference_cloud_bit_exact(dev, name):
+def test_knn_stage_on_reference_cloud_bit_exact(dev, name, cap, mode):
     """apn_grid_build + apn_knn_radius on the REFERENCE run's warped cloud and in-bbox samples
-    reproduce the reference's kNN survivors and neighbour indices exactly (golden trace)."""
+    reproduce the reference's kNN survivors and neighbour indices exactly (golden trace), for
+    every search strategy and for a fine (r/8) and a cell-cap-coarsened grid."""
+    from apn_amd import _lib as L
+    prev = L.load().apn_set_knn_mode(mode)
+    try:
+        _knn_on_reference_cloud(dev, name, cap)
+    finally:
+        L.load().apn_set_knn_mode(prev)
+
+
+def _knn_on_reference_cloud(dev, name, cap):
     from apn_amd import _lib as L
     g = Golden(name)
     t_hat = g.z["out_t_hat_pcd"].astype(F32)
     q, rid, sid = _golden_queries(g)
     N, nq = len(t_hat), len(q)
     bbox = np.concatenate([_ord(t_hat.min(0)), _ord(t_hat.max(0)), [0, 0]]).astype(np.int32)
-    cap = 1 << 20
     xyz = torch.from_numpy(t_hat).to(dev)
     bbox_t = torch.from_numpy(bbox).to(dev)
     sorted4 = torch.empty(N, 4, device=dev)
@@ -446,3 +457,28 @@ def test_no_points_fallback(dev):
     out = m(g.t("in_t").to(dev), render_depth=True, render_kwargs=rk, render_weights=True)
     assert out["alphainv_last"] is None
     assert torch.all(out["rgb_marched"] == g.cfg("bg")) and torch.all(out["depth"] == 0)
+
+
+@pytest.mark.parametrize("mode", [1, 2, 4, 5, 6, 7])
+def test_knn_modes_identical_full_scene(dev, mode):
+    """Full C2 frame (300k points, 640k rays, ~8M in-bbox samples): every kNN search strategy
+    gives bit-identical renders and survivor counts to the default one (size-independent
+    exactness property at the benchmark size)."""
+    from apn_amd import _lib as L, harness, synthetic as S
+    scene = S.make_scene("C2")
+    model = harness.build_model(scene, dev)
+    rk = scene.render_kwargs(dev)
+    t = torch.tensor([scene.cfg.t], device=dev)
+    outs = []
+    for md in (0, mode):   # mode 0 = the single-pass expanding-ball search
+        prev = L.load().apn_set_knn_mode(md)
+        try:
+            o = model(t, render_depth=True, render_kwargs=rk, render_weights=True)
+            torch.cuda.synchronize()
+        finally:
+            L.load().apn_set_knn_mode(prev)
+        outs.append(({k: v.clone() for k, v in o.items() if torch.is_tensor(v)}, dict(model.last_stats)))
+    (a, sa), (b, sb) = outs
+    assert sa == sb
+    for k in ("rgb_marched", "rgb_marched_direct", "depth", "weights"):
+        assert torch.equal(a[k], b[k]), k
