@@ -28,7 +28,8 @@ SIGNATURES = {
     "apn_raw2alpha": (C.c_int, [P, F32, F32, I64, P, P, P]),
     "apn_alpha2weight": (C.c_int, [P, P, I64, I64, P, P, P, P, P, P]),
     "apn_segment_sum": (C.c_int, [P, P, I64, I64, I64, P, P, P]),
-    "apn_lbs_skin": (C.c_int, [P, P, I64, I32, P, F32, P, P, P, P, P, P, P, F32, I32, P, P, P, P, P, P, P]),
+    "apn_lbs_workspace_bytes": (SZ, [I64]),
+    "apn_lbs_skin": (C.c_int, [P, P, I64, I32, P, F32, P, P, P, P, P, P, P, F32, I32, P, P, P, P, P, P, P, P]),
     "apn_bbox_unpack": (C.c_int, [P, F32, P, P]),
     "apn_inbbox_count": (C.c_int, [P, P, P, F32, F32, F32, I64, P, P, P]),
     "apn_inbbox_fill": (C.c_int, [P, P, P, F32, F32, F32, I64, P, P, P, P]),

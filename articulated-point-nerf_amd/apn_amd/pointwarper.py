@@ -178,10 +178,9 @@ def lbs_apply(pcd, weights, bone_Ts, global_t, get_frames=False):
     dev = pcd.device
     xyz = torch.empty(N, 3, device=dev)
     G = torch.empty(N, 4, 4, device=dev) if get_frames else None
-    bbox = torch.empty(8, dtype=torch.int32, device=dev)
     T34 = bone_Ts[:, :3, :].detach().float().reshape(J, 12).contiguous()
     gt = global_t.detach().float().reshape(3).contiguous()
     w = weights.detach().float().contiguous()
     call("apn_lbs_skin", ptr(pcd.contiguous()), ptr(w), N, J, None, 0.0, None, ptr(T34), ptr(gt), None, None, None,
-         None, 0.0, 1, ptr(xyz), None, ptr(G), None, None, ptr(bbox), stream_ptr(dev))
+         None, 0.0, 1, ptr(xyz), None, ptr(G), None, None, None, None, stream_ptr(dev))
     return xyz, G

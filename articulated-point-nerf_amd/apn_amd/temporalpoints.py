@@ -292,7 +292,8 @@ class TemporalPoints(torch.nn.Module):
              ptr(self.canonical_alpha.detach().contiguous()) if records else None,
              ptr(self.canonical_rgbs.detach().contiguous()) if records else None,
              ptr(self.direct_eps.detach().contiguous()) if records else None, mmd, 0, ptr(xyz), ptr(wout), None,
-             ptr(recA), ptr(recB), ptr(bbox), stream_ptr(dev))
+             ptr(recA), ptr(recB), ptr(bbox), ptr(ws.bytes("lbs_ws", L.load().apn_lbs_workspace_bytes(N), dev)),
+             stream_ptr(dev))
         return xyz, wout, (recA, recB, bbox)
 
     def _packed_weights(self, pose_embedding, dev):

@@ -24,7 +24,7 @@ __global__ __launch_bounds__(LBS_THREADS) void k_lbs_skin(
     const float* __restrict__ boneT12, const float* __restrict__ global_t, const float* __restrict__ colors,
     const float* __restrict__ alpha_c, const float* __restrict__ rgb_c, const float* __restrict__ direct_eps,
     float mmd, int weights_final, float* __restrict__ xyz_out, float* __restrict__ w_out,
-    float* __restrict__ G_out, float4* __restrict__ recA, float4* __restrict__ recB, int* __restrict__ bbox_ord) {
+    float* __restrict__ G_out, float4* __restrict__ recA, float4* __restrict__ recB, int* __restrict__ bbox_part) {
   extern __shared__ float lds[];
   const int Jp = J + 1;                          // odd row stride: conflict-free row reads
   float* sW = lds;                               // [LBS_THREADS][Jp]
@@ -141,50 +141,81 @@ __global__ __launch_bounds__(LBS_THREADS) void k_lbs_skin(
       Wo[e] = sW[r * Jp + c];
     }
   }
-  // bbox: wave reduce then one atomic per wave and axis
+  // bbox: wave reduce, then across the block's waves; one partial per block, reduced by
+  // k_bbox_reduce (all blocks hitting 6 global atomics serialised at one L2 channel and cost
+  // ~0.3 ms at 300k points)
+  if (bbox_part) {
+    __shared__ float sbb[LBS_THREADS / 64][6];
+    const int lane = tid & 63, wid = tid >> 6;
 #pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    float lo = bmin[a], hi = bmax[a];
+    for (int a = 0; a < 3; ++a) {
+      float lo = bmin[a], hi = bmax[a];
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      lo = fminf(lo, __shfl_xor(lo, o, 64));
-      hi = fmaxf(hi, __shfl_xor(hi, o, 64));
+      for (int o = 32; o > 0; o >>= 1) {
+        lo = fminf(lo, __shfl_xor(lo, o, 64));
+        hi = fmaxf(hi, __shfl_xor(hi, o, 64));
+      }
+      if (lane == 0) {
+        sbb[wid][a] = lo;
+        sbb[wid][3 + a] = hi;
+      }
     }
-    if ((tid & 63) == 0 && lo <= hi) {
-      atomicMin(bbox_ord + a, float_to_ordered(lo));
-      atomicMax(bbox_ord + 3 + a, float_to_ordered(hi));
+    __syncthreads();
+    if (tid < 6) {
+      float v = sbb[0][tid];
+      for (int w = 1; w < LBS_THREADS / 64; ++w) v = tid < 3 ? fminf(v, sbb[w][tid]) : fmaxf(v, sbb[w][tid]);
+      bbox_part[6 * blockIdx.x + tid] = float_to_ordered(v);
     }
   }
 }
 
-__global__ void k_bbox_init(int* bbox_ord) {
-  if (threadIdx.x < 3) bbox_ord[threadIdx.x] = 0x7f800000;            // +inf
-  else if (threadIdx.x < 6) bbox_ord[threadIdx.x] = (int)0x807fffff;  // ordered(-inf)
+// Per-block bbox partials -> bbox_ord[6] (one workgroup, deterministic).
+__global__ __launch_bounds__(256) void k_bbox_reduce(const int* __restrict__ part, int nblocks,
+                                                     int* __restrict__ bbox_ord) {
+  __shared__ int s[256][6];
+  const int tid = threadIdx.x;
+  int v[6] = {0x7f800000, 0x7f800000, 0x7f800000, (int)0x807fffff, (int)0x807fffff, (int)0x807fffff};
+  for (int b = tid; b < nblocks; b += 256)
+    for (int a = 0; a < 6; ++a) v[a] = a < 3 ? min(v[a], part[6 * b + a]) : max(v[a], part[6 * b + a]);
+  for (int a = 0; a < 6; ++a) s[tid][a] = v[a];
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (tid < st)
+      for (int a = 0; a < 6; ++a) s[tid][a] = a < 3 ? min(s[tid][a], s[tid + st][a]) : max(s[tid][a], s[tid + st][a]);
+    __syncthreads();
+  }
+  if (tid < 6) bbox_ord[tid] = s[0][tid];
 }
 
 }  // namespace apn
 
 using namespace apn;
 
+extern "C" size_t apn_lbs_workspace_bytes(int64_t n_points) {
+  return n_points > 0 ? (size_t)ceil_div(n_points, LBS_THREADS) * 6 * sizeof(int) : 0;
+}
+
 extern "C" int apn_lbs_skin(const float* canonical_pcd, const float* raw_weights, int64_t n_points, int32_t n_joints,
                             const float* theta_weight, float eps, const int32_t* merge_rules, const float* bone_T34,
                             const float* global_t, const float* joint_colors, const float* canonical_alpha,
                             const float* canonical_rgbs, const float* direct_eps, float mean_min_distance,
                             int32_t weights_final, float* xyz_out, float* weights_out, float* G_out, float* recA16,
-                            float* recB8, int32_t* bbox_ord, void* stream) {
+                            float* recB8, int32_t* bbox_ord, void* workspace, void* stream) {
   if (n_points <= 0 || n_joints <= 0 || n_joints > LBS_MAX_J) return APN_ERR_ARG;
-  if (!canonical_pcd || !raw_weights || (!weights_final && !theta_weight) || !bone_T34 || !global_t || !xyz_out ||
-      !bbox_ord)
+  if (!canonical_pcd || !raw_weights || (!weights_final && !theta_weight) || !bone_T34 || !global_t || !xyz_out)
     return APN_ERR_ARG;
+  if (bbox_ord && !workspace) return APN_ERR_ARG;
   if ((recA16 != nullptr) != (recB8 != nullptr)) return APN_ERR_ARG;
   if (recA16 && (!canonical_alpha || !canonical_rgbs || !direct_eps)) return APN_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int J = n_joints;
+  const int nblocks = ceil_div(n_points, LBS_THREADS);
+  int* part = bbox_ord ? (int*)workspace : nullptr;
   size_t lds = (size_t)(LBS_THREADS * (J + 1) + J * 12 + J * 3) * sizeof(float) + J * sizeof(int);
-  hipLaunchKernelGGL(k_bbox_init, dim3(1), dim3(64), 0, s, bbox_ord);
-  hipLaunchKernelGGL(k_lbs_skin, dim3(ceil_div(n_points, LBS_THREADS)), dim3(LBS_THREADS), lds, s, canonical_pcd,
-                     raw_weights, n_points, J, theta_weight, eps, merge_rules, bone_T34, global_t, joint_colors,
-                     canonical_alpha, canonical_rgbs, direct_eps, mean_min_distance, weights_final, xyz_out,
-                     weights_out, G_out, (float4*)recA16, (float4*)recB8, bbox_ord);
+  hipLaunchKernelGGL(k_lbs_skin, dim3(nblocks), dim3(LBS_THREADS), lds, s, canonical_pcd, raw_weights, n_points, J,
+                     theta_weight, eps, merge_rules, bone_T34, global_t, joint_colors, canonical_alpha, canonical_rgbs,
+                     direct_eps, mean_min_distance, weights_final, xyz_out, weights_out, G_out, (float4*)recA16,
+                     (float4*)recB8, part);
+  if (bbox_ord) hipLaunchKernelGGL(k_bbox_reduce, dim3(1), dim3(256), 0, s, part, nblocks, bbox_ord);
   return launch_status();
 }

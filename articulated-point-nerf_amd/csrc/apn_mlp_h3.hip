@@ -64,7 +64,19 @@ __device__ __forceinline__ int out32_off(int m, int c) { return m * XB + ((c ^ (
 __device__ __forceinline__ void split4(const f32x4& v, h4& hi, h4& lo) {
   hi = __builtin_convertvector(v, h4);
   const f32x4 hb = __builtin_convertvector(hi, f32x4);
-  lo = __builtin_convertvector(v - hb, h4);
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  const f32x2 d0 = f32x2{v[0], v[1]} - f32x2{hb[0], hb[1]};   // v_pk_add_f32 (neg)
+  const f32x2 d1 = f32x2{v[2], v[3]} - f32x2{hb[2], hb[3]};
+  lo = __builtin_convertvector(f32x4{d0[0], d0[1], d1[0], d1[1]}, h4);
+}
+
+// LeakyReLU(0.01) of 4 values: max(x, 0.01x) = med3(x, 0.01x, +inf) -- one v_med3_f32 per value
+// (fmaxf adds a NaN-canonicalising v_max per operand) and the products as two v_pk_mul_f32.
+__device__ __forceinline__ f32x4 lrelu4(const f32x4& v) {
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  const f32x2 s0 = f32x2{v[0], v[1]} * 0.01f, s1 = f32x2{v[2], v[3]} * 0.01f;
+  return f32x4{__builtin_amdgcn_fmed3f(v[0], s0[0], INFINITY), __builtin_amdgcn_fmed3f(v[1], s0[1], INFINITY),
+               __builtin_amdgcn_fmed3f(v[2], s1[0], INFINITY), __builtin_amdgcn_fmed3f(v[3], s1[1], INFINITY)};
 }
 
 __device__ __forceinline__ f32x4 mfma3(const h8& ahi, const h8& alo, const h8& bhi, const h8& blo, f32x4 acc) {
@@ -88,11 +100,51 @@ __device__ __forceinline__ h8 frag(rsrc_t rs, int hbase, int nq, int ot, int q, 
 
 // acc[mt][j] += W[o-tile 2w+j] X^T over NQ chunks of 32. `a` carries chunk 0 of this matrix's
 // fragments in and chunk 0 of the next matrix (Wn, NQN chunks, o-tiles otn0, otn0+1) out.
-template <int NQ, int NQN, int NTN>
+template <int NQ, int NQN, int NTN, bool BPF = true>
 __device__ __forceinline__ void layer_mfma(const char* __restrict__ X, rsrc_t rs, int W, int ot0, int Wn, int otn0,
                                            f32x4 (&acc)[4][2], h8 (&a)[2][2]) {
   const int lane = threadIdx.x & 63;
   const int li = lane & 15, g = lane >> 4;
+  if constexpr (!BPF) {
+    // no B double-buffering (fewer VGPRs): the chunk's activation fragments are read per M-tile
+    // right before its MFMAs
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      h8 an[2][2];
+      if (q + 1 < NQ) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, W, NQ, ot0 + j, q + 1, pt);
+      } else {
+#pragma unroll
+        for (int j = 0; j < NTN; ++j)
+#pragma unroll
+          for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, Wn, NQN, otn0 + j, 0, pt);
+      }
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const char* p = X + act_off(16 * mt + li, 4 * q + g);
+        const h8 bh = *(const h8*)p, bl = *(const h8*)(p + 256);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[mt][j] = mfma3(a[j][0], a[j][1], bh, bl, acc[mt][j]);
+      }
+      if (q + 1 < NQ) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          a[j][0] = an[j][0];
+          a[j][1] = an[j][1];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < NTN; ++j) {
+          a[j][0] = an[j][0];
+          a[j][1] = an[j][1];
+        }
+      }
+    }
+    return;
+  }
   h8 b[4][2];
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) {
@@ -147,8 +199,9 @@ __device__ __forceinline__ void layer_mfma(const char* __restrict__ X, rsrc_t rs
   }
 }
 
-// lrelu(acc + bias) -> hi/lo halves of the next layer's input rows (transposed C layout: lane
-// (li, g) of (mt, j) holds features 16(2w+j) + 4g + r of row 16 mt + li).
+// lrelu(acc [+ bias]) -> hi/lo halves of the next layer's input rows (transposed C layout: lane
+// (li, g) of (mt, j) holds features 16(2w+j) + 4g + r of row 16 mt + li). Layers 2-4 start their
+// accumulators from the bias (bias == nullptr here).
 __device__ __forceinline__ void store_act(char* __restrict__ X, int ot0, const float* __restrict__ bias,
                                           const f32x4 (&acc)[4][2]) {
   const int lane = threadIdx.x & 63;
@@ -156,13 +209,11 @@ __device__ __forceinline__ void store_act(char* __restrict__ X, int ot0, const f
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int o0 = 16 * (ot0 + j) + 4 * g;
-    const f32x4 bb = *(const f32x4*)(bias + o0);
+    const f32x4 bb = bias ? *(const f32x4*)(bias + o0) : f32x4{0.f, 0.f, 0.f, 0.f};
     const int c = o0 >> 3, sub = (g & 1) * 8;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
-      f32x4 v;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = lrelu(acc[mt][j][r] + bb[r]);
+      const f32x4 v = lrelu4(bias ? acc[mt][j] + bb : acc[mt][j]);
       h4 hi, lo;
       split4(v, hi, lo);
       char* p = X + act_off(16 * mt + li, c) + sub;
@@ -172,15 +223,32 @@ __device__ __forceinline__ void store_act(char* __restrict__ X, int ot0, const f
   }
 }
 
+// Accumulators of a layer start from its bias (broadcast over the M-tiles): the bias add of the
+// reference's x W^T + b costs no VALU (the first MFMA reads it as its C operand).
+__device__ __forceinline__ void init_bias(f32x4 (&acc)[4][2], int ot0, const float* __restrict__ bias) {
+  const int g = (threadIdx.x & 63) >> 4;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const f32x4 bb = *(const f32x4*)(bias + 16 * (ot0 + j) + 4 * g);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) acc[mt][j] = bb;
+  }
+}
+
 __device__ unsigned long long g_phase[6];
 
-template <bool TIMED>
-__global__ __launch_bounds__(MLP_THREADS, 2) void k_point_mlp_h3(
+// OCC = workgroups per CU: 2 = activations ping-pong between two LDS buffers (one barrier per
+// layer); 3 = one activation buffer + a separate head-input buffer (45 KB of LDS, an extra barrier
+// per layer, 12 waves per CU to hide the phases' latencies).
+template <bool TIMED, int OCC>
+__global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
     const float4* __restrict__ s_pos, const int* __restrict__ s_ray, const int* __restrict__ s_nbr,
     const int* __restrict__ n_samples_dev, const float4* __restrict__ recA, const float4* __restrict__ recB,
     const float4* __restrict__ pproj, const float* __restrict__ viewdirs, const float* __restrict__ vemb_const,
     const float* __restrict__ wbuf, float eps, float shift, float interval, float4* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) char Xs[2 * XBUF];
+  constexpr bool PP = OCC == 2;
+  __shared__ __attribute__((aligned(16))) char Xs[PP ? 2 * XBUF : XBUF];
+  __shared__ __attribute__((aligned(16))) char Hs[PP ? 16 : TS * HB];
   __shared__ float sTo[TR];
   __shared__ float sIdw[TR];
   __shared__ float sRow[TR * 8];     // direct blend per row: wdir, alpha_c, rgb_c(3), pcol(3)
@@ -189,7 +257,8 @@ __global__ __launch_bounds__(MLP_THREADS, 2) void k_point_mlp_h3(
   __shared__ __attribute__((aligned(16))) float sW[SW_TOTAL];
   __shared__ float sPart[4 * TS * 4];
   char* const X0 = Xs;
-  char* const X1 = Xs + XBUF;
+  char* const X1 = PP ? Xs + XBUF : Xs;
+  char* const HX = PP ? X1 : Hs;     // head input rows
 
   const int nS = *n_samples_dev;
   const int ntiles = (nS + TS - 1) / TS;
@@ -329,7 +398,9 @@ __global__ __launch_bounds__(MLP_THREADS, 2) void k_point_mlp_h3(
               const int ci = e < 3 ? e : ee >> 2;
               const float vv = viewdirs[3 * ray + ci];
               const float arg = vv * (float)(1 << (ee & 3));
-              v = e < 3 ? vv : (e < 15 ? sinf(arg) : cosf(arg));
+              float sn_, cs_;
+              sincos_pe(arg, sn_, cs_);
+              v = e < 3 ? vv : (e < 15 ? sn_ : cs_);
             }
           }
           sV[s * 32 + e] = v;
@@ -358,48 +429,38 @@ __global__ __launch_bounds__(MLP_THREADS, 2) void k_point_mlp_h3(
       float w[8], sum = 0.f;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        w[k] = 1.f / (sTo[tid * 8 + k] + eps);
+        w[k] = __builtin_amdgcn_rcpf(sTo[tid * 8 + k] + eps);   // v_rcp_f32 (1 ulp)
         sum += w[k];
       }
+      const float inv = __builtin_amdgcn_rcpf(sum);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) sIdw[tid * 8 + k] = w[k] / sum;
+      for (int k = 0; k < 8; ++k) sIdw[tid * 8 + k] = w[k] * inv;
     }
     // ------------------------------------------------ feat_net: 4 x (Linear + LeakyReLU)
-    layer_mfma<2, 4, 2>(X0, rs, H_W1E, ot0, H_W2, ot0, acc, a);
+    layer_mfma<2, 4, 2, PP>(X0, rs, H_W1E, ot0, H_W2, ot0, acc, a);
+    if (!PP) __syncthreads();
     store_act(X1, ot0, sW + SW_B1, acc);
     __syncthreads();
     APN_PHASE(1)
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[mt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    layer_mfma<4, 4, 2>(X1, rs, H_W2, ot0, H_W3, ot0, acc, a);
-    store_act(X0, ot0, sW + SW_B2, acc);
+    init_bias(acc, ot0, sW + SW_B2);
+    layer_mfma<4, 4, 2, PP>(X1, rs, H_W2, ot0, H_W3, ot0, acc, a);
+    if (!PP) __syncthreads();
+    store_act(X0, ot0, nullptr, acc);
     __syncthreads();
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[mt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    layer_mfma<4, 4, 2>(X0, rs, H_W3, ot0, H_W4, ot0, acc, a);
-    store_act(X1, ot0, sW + SW_B3, acc);
+    init_bias(acc, ot0, sW + SW_B3);
+    layer_mfma<4, 4, 2, PP>(X0, rs, H_W3, ot0, H_W4, ot0, acc, a);
+    if (!PP) __syncthreads();
+    store_act(X1, ot0, nullptr, acc);
     __syncthreads();
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[mt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    layer_mfma<4, 5, 1>(X1, rs, H_W4, ot0, H_WH, wid, acc, a);
-    // layer-4 output lrelu(acc + b4) as fp32 rows (for the IDW sum)
+    init_bias(acc, ot0, sW + SW_B4);
+    layer_mfma<4, 5, 1, PP>(X1, rs, H_W4, ot0, H_WH, wid, acc, a);
+    if (!PP) __syncthreads();
+    // layer-4 output lrelu(acc) (bias in the accumulator) as fp32 rows (for the IDW sum)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int o0 = 16 * (ot0 + j) + 4 * g;
-      const f32x4 bb = *(const f32x4*)(sW + SW_B4 + o0);
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        f32x4 v;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = lrelu(acc[mt][j][r] + bb[r]);
-        *(f32x4*)(X0 + out32_off(16 * mt + li, o0 >> 2)) = v;
-      }
+      for (int mt = 0; mt < 4; ++mt) *(f32x4*)(X0 + out32_off(16 * mt + li, o0 >> 2)) = lrelu4(acc[mt][j]);
     }
     __syncthreads();
     APN_PHASE(2)
@@ -427,7 +488,7 @@ __global__ __launch_bounds__(MLP_THREADS, 2) void k_point_mlp_h3(
         sOut[12 * s + 3] = 1.f - powf(1.f + e, -interval);
       }
       // head input row s: [h (128) | view embedding (27) | 0] as hi/lo halves
-      char* hr = X1 + s * HB;
+      char* hr = HX + s * HB;
       h4 hi, lo;
       split4(h, hi, lo);
       *(h4*)(hr + 8 * oq) = hi;
@@ -445,14 +506,14 @@ __global__ __launch_bounds__(MLP_THREADS, 2) void k_point_mlp_h3(
       float sumd = 0.f;
 #pragma unroll
       for (int k = 0; k < 8; ++k) sumd += rw[8 * k];
-      const float dn = sumd + 1e-12f;
+      const float idn = __builtin_amdgcn_rcpf(sumd + 1e-12f);
       float acc1 = 0.f;
       if (qn == 0) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) acc1 += (0.125f * rw[8 * k]) * rw[8 * k + 1];
       } else if (qn < 4) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc1 += (rw[8 * k] / dn) * rw[8 * k + 1 + qn];
+        for (int k = 0; k < 8; ++k) acc1 += (rw[8 * k] * idn) * rw[8 * k + 1 + qn];
       } else if (qn < 7) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) acc1 += sIdw[8 * s + k] * rw[8 * k + 1 + qn];
@@ -464,8 +525,9 @@ __global__ __launch_bounds__(MLP_THREADS, 2) void k_point_mlp_h3(
     __syncthreads();
     // ------------------------------------------------ rgb head: folded [h; v] -> 64, ReLU, -> 3, sigmoid
     {
-      f32x4 ah = {0.f, 0.f, 0.f, 0.f};
-      const char* hr = X1 + li * HB;
+      const int o0 = 16 * wid + 4 * g;
+      f32x4 ah = *(const f32x4*)(sW + SW_BH + o0);   // views_linears.0 (folded) bias
+      const char* hr = HX + li * HB;
       const h8 z = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
       for (int q = 0; q < KV / 32; ++q) {
@@ -494,12 +556,10 @@ __global__ __launch_bounds__(MLP_THREADS, 2) void k_point_mlp_h3(
         }
       }
       // lane (li = sample, g): head features o = 16 wid + 4 g + r
-      const int o0 = 16 * wid + 4 * g;
-      const f32x4 bb = *(const f32x4*)(sW + SW_BH + o0);
       float pc[3] = {0.f, 0.f, 0.f};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float v = fmaxf(ah[r] + bb[r], 0.f);
+        const float v = fmaxf(ah[r], 0.f);
 #pragma unroll
         for (int c = 0; c < 3; ++c) pc[c] += v * sW[SW_WV2 + 64 * c + o0 + r];
       }
@@ -574,12 +634,19 @@ void launch_point_mlp_h3(int blocks, bool timed, hipStream_t stream, const float
                          const int* s_nbr, const int* n_samples_dev, const float4* recA, const float4* recB,
                          const float4* pproj, const float* viewdirs, const float* vemb_const, const float* wbuf,
                          float eps, float shift, float interval, float4* out) {
-  if (timed)
-    hipLaunchKernelGGL(h3::k_point_mlp_h3<true>, dim3(blocks), dim3(MLP_THREADS), 0, stream, s_pos, s_ray, s_nbr,
-                       n_samples_dev, recA, recB, pproj, viewdirs, vemb_const, wbuf, eps, shift, interval, out);
-  else
-    hipLaunchKernelGGL(h3::k_point_mlp_h3<false>, dim3(blocks), dim3(MLP_THREADS), 0, stream, s_pos, s_ray, s_nbr,
-                       n_samples_dev, recA, recB, pproj, viewdirs, vemb_const, wbuf, eps, shift, interval, out);
+  static const int occ = [] {
+    const char* e = getenv("APN_MLP_OCC");
+    return e ? atoi(e) : 3;
+  }();
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(MLP_THREADS), 0, stream, s_pos, s_ray, s_nbr, n_samples_dev, recA,
+                       recB, pproj, viewdirs, vemb_const, wbuf, eps, shift, interval, out);
+  };
+  if (occ == 3) {
+    if (timed) go(h3::k_point_mlp_h3<true, 3>); else go(h3::k_point_mlp_h3<false, 3>);
+  } else {
+    if (timed) go(h3::k_point_mlp_h3<true, 2>); else go(h3::k_point_mlp_h3<false, 2>);
+  }
 }
 
 int debug_phase_cycles_h3(uint64_t* out6) {

@@ -69,13 +69,16 @@ int apn_segment_sum(const float* src, const int64_t* index, int64_t n_pts, int64
  *   bone_T34 [J,12]: rows 0..2 of each bone 4x4; merge_rules [J] int32 or NULL (identity);
  *   joint_colors [J,3] or NULL; weights_out [N,J] or NULL;
  *   recA16 [N,16] = {x,y,z, 2*(mmd*max(eps_n,0))^2+1e-12, Rinv(9), clip(alpha), 0,0};
- *   recB8 [N,8] = {clip(rgb), 0, sum_j col_j w_j, 0}; bbox_ord [6] ordered-int min/max. */
+ *   recB8 [N,8] = {clip(rgb), 0, sum_j col_j w_j, 0}; bbox_ord [6] ordered-int min/max of the
+ *   skinned cloud or NULL; workspace: apn_lbs_workspace_bytes(n_points) (needed with bbox_ord). */
+size_t apn_lbs_workspace_bytes(int64_t n_points);
 int apn_lbs_skin(const float* canonical_pcd, const float* raw_weights, int64_t n_points,
                  int32_t n_joints, const float* theta_weight, float eps, const int32_t* merge_rules,
                  const float* bone_T34, const float* global_t, const float* joint_colors,
                  const float* canonical_alpha, const float* canonical_rgbs, const float* direct_eps,
                  float mean_min_distance, int32_t weights_final, float* xyz_out, float* weights_out,
-                 float* G_out, float* recA16, float* recB8, int32_t* bbox_ord, void* stream);
+                 float* G_out, float* recA16, float* recB8, int32_t* bbox_ord, void* workspace,
+                 void* stream);
 /* weights_final = 1: raw_weights already are the per-point LBS weights (PointWarper.forward
  * input, pointwarper.py:213) -- softmax/merge skipped. G_out [N,16] (weighted_G_tw) or NULL. */
 

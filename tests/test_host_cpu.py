@@ -59,7 +59,8 @@ def test_invalid_arguments_rejected_without_gpu():
     assert lib.apn_point_mlp(*([None] * 3), 10, *([None] * 4), 64, *([None] * 3), 0.0, 0.0, 0.0, 0, None,
                              None) == 1  # feat_dim != 128
     assert lib.apn_lbs_skin(None, None, 0, 0, None, 0.0, None, None, None, None, None, None, None, 0.0, 0,
-                            None, None, None, None, None, None, None) == 1
+                            None, None, None, None, None, None, None, None) == 1
+    assert lib.apn_lbs_workspace_bytes(300_000) == 6 * 4 * ((300_000 + 255) // 256)
 
 
 def test_missing_library_fails_loudly(monkeypatch):
