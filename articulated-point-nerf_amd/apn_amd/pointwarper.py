@@ -132,9 +132,72 @@ class PointWarper(torch.nn.Module):
     def set_sibling_mask(self, sibling_mask):
         self.sibling_mask = sibling_mask.long()
 
+    def _tn_packed(self, dev):
+        """TransformNet weights packed for apn_skeleton_pose ([W0, b0, W1, b1, ..., W_last]),
+        cached on the parameters' versions."""
+        lins = [m for m in self.transform_net.net if isinstance(m, torch.nn.Linear)]
+        key = (str(dev),) + tuple((p.data_ptr(), p._version) for m in lins for p in m.parameters())
+        if getattr(self, "_tn_key", None) != key:
+            parts = []
+            for m in lins:
+                parts.append(m.weight.detach().float().reshape(-1))
+                if m.bias is not None:
+                    parts.append(m.bias.detach().float().reshape(-1))
+            self._tn_buf = torch.cat(parts).to(dev).contiguous()
+            self._tn_key = key
+        return self._tn_buf, lins[0].in_features, lins[0].out_features, len(lins)
+
+    def _tree_buffers(self, dev):
+        key = (str(dev), self.sibling_mask.data_ptr(), self.sibling_mask._version,
+               None if self.rot_mask is None else (self.rot_mask.data_ptr(), self.rot_mask._version))
+        if getattr(self, "_tree_key", None) != key:
+            self._tree = (self.parent_indices.to(dev, torch.int32).contiguous(),
+                          self.parent_joint_ex.to(dev, torch.int32).contiguous(),
+                          self.sibling_mask.to(dev, torch.int32).contiguous(),
+                          None if self.rot_mask is None else self.rot_mask.to(dev, torch.int32).contiguous())
+            self._tree_key = key
+        return self._tree
+
     def pose(self, joints, t=None, rot_params=None, global_t=None):
-        """Skeleton stage of forward (pointwarper.py:216-239): returns bone_Ts [J,4,4],
-        global_t [3] and joints_rel [J,3]. Sets prev_params / prev_thetas / prev_global_t."""
+        """Skeleton stage of forward (pointwarper.py:216-239) as one HIP launch
+        (apn_skeleton_pose): returns bone_Ts [J,4,4], global_t [3] and joints_rel [J,3]; the
+        bone rows [J,12] for apn_lbs_skin are kept in ``last_T34``. Sets prev_params /
+        prev_thetas / prev_global_t."""
+        assert (t is None) ^ (rot_params is None)
+        dev = joints.device
+        L.require_cuda(joints, what="PointWarper.pose")
+        J = joints.shape[0]
+        pi, pjx, sib, rmask = self._tree_buffers(dev)
+        jts = joints.detach().float().contiguous()
+        thetas = torch.empty(J, device=dev)
+        bone_Ts = torch.empty(J, 4, 4, device=dev)
+        T34 = torch.empty(J, 12, device=dev)
+        gt = torch.empty(3, device=dev)
+        joints_rel = torch.empty(J, 3, device=dev)
+        s = stream_ptr(dev)
+        if rot_params is None:
+            tn, t_dim, hidden, n_layers = self._tn_packed(dev)
+            te = t.detach().float().reshape(-1).contiguous()
+            params = torch.empty(J + 1, 4, device=dev)
+            call("apn_skeleton_pose", ptr(te), te.numel(), None, 4, J, ptr(tn), hidden, n_layers, ptr(jts), ptr(pi),
+                 pi.shape[1], ptr(pjx), ptr(sib), ptr(rmask), ptr(params), ptr(thetas), ptr(bone_Ts), ptr(T34),
+                 ptr(gt), ptr(joints_rel), s)
+            self.prev_params = params
+            self.prev_global_t = gt
+        else:
+            rp = rot_params.detach().float().contiguous()
+            call("apn_skeleton_pose", None, 0, ptr(rp), rp.shape[-1], J, None, 0, 0, ptr(jts), ptr(pi), pi.shape[1],
+                 ptr(pjx), ptr(sib), ptr(rmask), None, ptr(thetas), ptr(bone_Ts), ptr(T34), ptr(gt), ptr(joints_rel),
+                 s)
+            if global_t is not None:
+                gt = global_t
+        self.prev_thetas = thetas
+        self.last_T34 = T34
+        return bone_Ts, gt, joints_rel
+
+    def pose_torch(self, joints, t=None, rot_params=None, global_t=None):
+        """The skeleton stage as device torch ops (restatement of pointwarper.py:216-239 used to
+        cross-check apn_skeleton_pose in the tests)."""
         assert (t is None) ^ (rot_params is None)
         if rot_params is None:
             params = self.transform_net(t.unsqueeze(0))

@@ -227,7 +227,7 @@ class TemporalPoints(torch.nn.Module):
     def repose(self, rot_params):
         """temporalpoints.py:370-371 -> [xyz (N,3), joints_rel (J,3)] via the fused LBS kernel."""
         bone_Ts, global_t, joints_rel = self.forward_warp.pose(self.joints, rot_params=rot_params)
-        xyz, _, _ = self._lbs(bone_Ts, global_t, records=False)
+        xyz, _, _ = self._lbs(bone_Ts, global_t, records=False, T34=self.forward_warp.last_T34)
         return [xyz, joints_rel]
 
     def sample_ray(self, rays_o, rays_d, near, far, stepsize, xyz_min=None, xyz_max=None, **render_kwargs):
@@ -268,7 +268,7 @@ class TemporalPoints(torch.nn.Module):
         self.last_palette_perm = self._palette_cache[key][1]
         return self._palette_cache[key][0]
 
-    def _lbs(self, bone_Ts, global_t, records=True, colors=None):
+    def _lbs(self, bone_Ts, global_t, records=True, colors=None, T34=None):
         pcd = self.canonical_pcd.contiguous()
         L.require_cuda(pcd, self.weights, what="TemporalPoints")
         N, J = self.weights.shape
@@ -279,7 +279,8 @@ class TemporalPoints(torch.nn.Module):
         recA = ws.get("recA", N * 16, torch.float32, dev) if records else None
         recB = ws.get("recB", N * 8, torch.float32, dev) if records else None
         bbox = ws.get("bbox_ord", 8, torch.int32, dev)
-        T34 = bone_Ts[:, :3, :].detach().float().reshape(J, 12).contiguous()
+        if T34 is None:
+            T34 = bone_Ts[:, :3, :].detach().float().reshape(J, 12).contiguous()
         gt = global_t.detach().float().reshape(3).contiguous()
         rules = self._merge_rules()
         rules32 = rules.to(device=dev, dtype=torch.int32).contiguous() if rules is not None else None
@@ -331,7 +332,8 @@ class TemporalPoints(torch.nn.Module):
         bone_Ts, global_t, joints_rel = self.forward_warp.pose(self.joints, t_embed, rot_params)
         colors = self._joint_colors(dev) if render_weights else None
         self._mark("frame")
-        t_hat_pcd, weights, recs = self._lbs(bone_Ts, global_t, records=True, colors=colors)
+        t_hat_pcd, weights, recs = self._lbs(bone_Ts, global_t, records=True, colors=colors,
+                                             T34=self.forward_warp.last_T34)
         self._mark("lbs")
         self._last_weights = weights
         delta_joint = (self.joints - joints_rel).clone().detach()

@@ -294,6 +294,37 @@ def test_get_weights_and_pointwarper_vs_reference(golden_model, dev):
     assert (jr_r.cpu() - g.t("repose_joints_rel")).abs().max() < 1e-6
 
 
+@pytest.mark.parametrize("path", ["t", "rot4", "rot3"])
+def test_skeleton_pose_vs_torch_with_masks(golden_model, dev, path):
+    """apn_skeleton_pose (TransformNet -> Rodrigues -> masks -> recursive-halving chain) vs the
+    device-torch restatement, with a non-trivial sibling mask and rotation mask."""
+    g, m = golden_model
+    pw = m.forward_warp
+    J = m.joints.shape[0]
+    from apn_amd.tineuvox import poc_fre
+    gen = torch.Generator().manual_seed(1)
+    if path == "t":
+        kw = {"t": poc_fre(g.t("in_t").to(dev), m.time_poc)}
+    else:
+        kw = {"rot_params": (torch.randn(J, 4 if path == "rot4" else 3, generator=gen) * 0.3).to(dev)}
+    old_sib, old_rot = pw.sibling_mask, pw.rot_mask
+    try:
+        sib = torch.arange(J)
+        sib[J - 1] = J - 2
+        rm = torch.zeros(J, dtype=torch.bool)
+        rm[1] = True
+        pw.sibling_mask, pw.rot_mask = sib.to(dev), rm.to(dev)
+        a = pw.pose(m.joints.detach(), **kw)
+        th_a = pw.prev_thetas.clone()
+        b = pw.pose_torch(m.joints.detach(), **kw)
+        th_b = pw.prev_thetas
+    finally:
+        pw.sibling_mask, pw.rot_mask = old_sib, old_rot
+    for x, y in zip(a, b):
+        assert (x - y).abs().max() < 2e-6
+    assert (th_a - th_b).abs().max() < 1e-6
+
+
 def _forward(g, m, dev):
     return m(g.t("in_t").to(dev), render_depth=True, render_kwargs=g.render_kwargs(dev), render_weights=True,
              poses=g.t("in_c2w")[None].to(dev), Ks=g.t("in_K")[None].to(dev), get_skeleton=True)
