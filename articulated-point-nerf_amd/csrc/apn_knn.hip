@@ -758,100 +758,6 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_b(
   }
 }
 
-// ---- mode 6: per-cell rejection bound. For every fine cell C holding a candidate, U(C) = number
-// of points in cells whose box lies within r of C's box -- an upper bound on the points within r of
-// ANY query in C (also of a query just outside the grid, clamped into C: its distance to a point
-// exceeds the box-box distance). Candidates with U(C) < 8 are rejected without a search; the
-// cell count is ~10x smaller than the candidate count, so the bound costs a tenth of a per-query
-// chord count.
-__global__ __launch_bounds__(KNN_THREADS) void k_mark_cells(const float4* __restrict__ q_pos,
-                                                           const int* __restrict__ cand,
-                                                           const int* __restrict__ n_cand_dev,
-                                                           const GridParams* __restrict__ gp, int* __restrict__ ccell,
-                                                           int* __restrict__ mark) {
-  const int c = blockIdx.x * KNN_THREADS + threadIdx.x;
-  if (c >= *n_cand_dev) return;
-  const GridParams g = *gp;
-  const float4 q = q_pos[cand[c]];
-  const int cell = (cell_coord(q.z, g.oz, g.inv_h, g.dz) * g.dy + cell_coord(q.y, g.oy, g.inv_h, g.dy)) * g.dx +
-                   cell_coord(q.x, g.ox, g.inv_h, g.dx);
-  ccell[c] = cell;
-  mark[cell] = 1;
-}
-
-__global__ __launch_bounds__(KNN_THREADS) void k_cell_bound(const GridParams* __restrict__ gp,
-                                                           const int* __restrict__ cell_start,
-                                                           const int* __restrict__ list, const int* __restrict__ n_list,
-                                                           int* __restrict__ ubound) {
-  const int i = blockIdx.x * KNN_THREADS + threadIdx.x;
-  if (i >= *n_list) return;
-  const GridParams g = *gp;
-  const int cell = list[i];
-  const int cx = cell % g.dx, cy = (cell / g.dx) % g.dy, cz = cell / (g.dx * g.dy);
-  const float lim = g.r2 * 1.0002f * g.inv_h * g.inv_h;   // (r/h)^2 with slack
-  const int K = (int)ceilf(sqrtf(lim)) + 1;
-  int u = 0;
-  for (int dz = -K; dz <= K; ++dz) {
-    const int z = cz + dz;
-    if (z < 0 || z >= g.dz) continue;
-    const float gz = (float)max(abs(dz) - 1, 0);
-    for (int dy = -K; dy <= K; ++dy) {
-      const int y = cy + dy;
-      const float gy = (float)max(abs(dy) - 1, 0);
-      const float rem = lim - gz * gz - gy * gy;
-      if (y < 0 || y >= g.dy || rem < 0.f) continue;
-      const int kx = (int)floorf(sqrtf(rem)) + 1;
-      const int row = (z * g.dy + y) * g.dx;
-      u += cell_start[row + min(cx + kx, g.dx - 1) + 1] - cell_start[row + max(cx - kx, 0)];
-    }
-  }
-  ubound[cell] = u;
-}
-
-// Pass A of mode 6: candidates whose cell bound is < 8 are rejected; the rest run the r/4 ball
-// and, unless it already holds the 8 nearest, go to the hard list (pass B).
-__global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_a6(
-    const float4* __restrict__ q_pos, const int* __restrict__ cand, const int* __restrict__ n_cand_dev,
-    const GridParams* __restrict__ gp, const int* __restrict__ cell_start, const float4* __restrict__ sorted,
-    const int* __restrict__ ccell, const int* __restrict__ ubound, int* __restrict__ flag, int* __restrict__ t_nbr,
-    int* __restrict__ hard, int* __restrict__ n_hard) {
-  const int nc = *n_cand_dev;
-  const int c = blockIdx.x * KNN_THREADS + threadIdx.x;
-  const GridParams g = *gp;
-  bool push = false;
-  if (c < nc) {
-    bool surv = false;
-    if (ubound[ccell[c]] >= KNN_K) {
-      const float4 q = q_pos[cand[c]];
-      float bd[KNN_K];
-      int bi[KNN_K];
-#pragma unroll
-      for (int k = 0; k < KNN_K; ++k) { bd[k] = INFINITY; bi[k] = 0x7fffffff; }
-      const float R2 = g.h > 0.25f * g.r ? g.r2 : 0.0625f * g.r2;
-      scan_ball_nf<KNN_K>(g, cell_start, sorted, q.x, q.y, q.z, R2, bd, bi);
-      if (R2 == g.r2 || bd[KNN_K - 1] < R2 * (1.f - 2e-4f)) {
-        surv = bd[KNN_K - 1] <= g.r2;
-        if (surv) {
-          int4* nb = (int4*)(t_nbr + (int64_t)c * KNN_K);
-          nb[0] = make_int4(bi[0], bi[1], bi[2], bi[3]);
-          nb[1] = make_int4(bi[4], bi[5], bi[6], bi[7]);
-        }
-      } else {
-        push = true;
-      }
-    }
-    if (!push) flag[c] = surv;
-  }
-  const int lane = threadIdx.x & 63;
-  const unsigned long long bal = __ballot(push);
-  if (bal) {
-    int base = 0;
-    if (lane == 0) base = atomicAdd(n_hard, __popcll(bal));
-    base = __shfl(base, 0, 64);
-    if (push) hard[base + __popcll(bal & ((1ull << lane) - 1ull))] = c;
-  }
-}
-
 // Ball scan as a per-lane state machine ("flat" loop): every iteration a lane either consumes
 // points of its current row range, or takes over the row range it loaded one step earlier and
 // examines the next row (nearest-first order, culled by the running K-th best) to load its
@@ -912,6 +818,232 @@ __device__ __forceinline__ void scan_ball_flat(const GridParams& g, const int* _
         }
       }
     }
+  }
+}
+
+// ---- mode 6: per-cell rejection bound. For every fine cell C holding a candidate, U(C) = number
+// of points in cells whose box lies within r of C's box -- an upper bound on the points within r of
+// ANY query in C (also of a query just outside the grid, clamped into C: its distance to a point
+// exceeds the box-box distance). Candidates with U(C) < 8 are rejected without a search; the
+// cell count is ~10x smaller than the candidate count, so the bound costs a tenth of a per-query
+// chord count.
+__global__ __launch_bounds__(KNN_THREADS) void k_mark_cells(const float4* __restrict__ q_pos,
+                                                           const int* __restrict__ cand,
+                                                           const int* __restrict__ n_cand_dev,
+                                                           const GridParams* __restrict__ gp, int* __restrict__ ccell,
+                                                           int* __restrict__ mark) {
+  const int c = blockIdx.x * KNN_THREADS + threadIdx.x;
+  if (c >= *n_cand_dev) return;
+  const GridParams g = *gp;
+  const float4 q = q_pos[cand[c]];
+  const int cell = (cell_coord(q.z, g.oz, g.inv_h, g.dz) * g.dy + cell_coord(q.y, g.oy, g.inv_h, g.dy)) * g.dx +
+                   cell_coord(q.x, g.ox, g.inv_h, g.dx);
+  ccell[c] = cell;
+  mark[cell] = 1;
+}
+
+__global__ __launch_bounds__(KNN_THREADS) void k_cell_bound(const GridParams* __restrict__ gp,
+                                                           const int* __restrict__ cell_start,
+                                                           const int* __restrict__ list, const int* __restrict__ n_list,
+                                                           int* __restrict__ ubound) {
+  const int i = blockIdx.x * KNN_THREADS + threadIdx.x;
+  if (i >= *n_list) return;
+  const GridParams g = *gp;
+  const int cell = list[i];
+  const int cx = cell % g.dx, cy = (cell / g.dx) % g.dy, cz = cell / (g.dx * g.dy);
+  const float lim = g.r2 * 1.0002f * g.inv_h * g.inv_h;   // (r/h)^2 with slack
+  const int K = (int)ceilf(sqrtf(lim)) + 1;
+  int u = 0;
+  for (int dz = -K; dz <= K; ++dz) {
+    const int z = cz + dz;
+    if (z < 0 || z >= g.dz) continue;
+    const float gz = (float)max(abs(dz) - 1, 0);
+    for (int dy = -K; dy <= K; ++dy) {
+      const int y = cy + dy;
+      const float gy = (float)max(abs(dy) - 1, 0);
+      const float rem = lim - gz * gz - gy * gy;
+      if (y < 0 || y >= g.dy || rem < 0.f) continue;
+      const int kx = (int)floorf(sqrtf(rem)) + 1;
+      const int row = (z * g.dy + y) * g.dx;
+      u += cell_start[row + min(cx + kx, g.dx - 1) + 1] - cell_start[row + max(cx - kx, 0)];
+    }
+  }
+  ubound[cell] = u;
+}
+
+// Mode 8: the cell bound at three radii (r/4, r/2, r) in one pass -- u4[cell], u2[cell], u1[cell] --
+// so a query skips every ball level that cannot hold 8 points for any query of its cell.
+__global__ __launch_bounds__(KNN_THREADS) void k_cell_bound3(const GridParams* __restrict__ gp,
+                                                            const int* __restrict__ cell_start,
+                                                            const int* __restrict__ list,
+                                                            const int* __restrict__ n_list, int* __restrict__ u1,
+                                                            int* __restrict__ u2, int* __restrict__ u4) {
+  const int i = blockIdx.x * KNN_THREADS + threadIdx.x;
+  if (i >= *n_list) return;
+  const GridParams g = *gp;
+  const int cell = list[i];
+  const int cx = cell % g.dx, cy = (cell / g.dx) % g.dy, cz = cell / (g.dx * g.dy);
+  const float lim = g.r2 * 1.0002f * g.inv_h * g.inv_h;   // (r/h)^2 with slack
+  const int K = (int)ceilf(sqrtf(lim)) + 1;
+  int a1 = 0, a2 = 0, a4 = 0;
+  for (int dz = -K; dz <= K; ++dz) {
+    const int z = cz + dz;
+    if (z < 0 || z >= g.dz) continue;
+    const float gz = (float)max(abs(dz) - 1, 0);
+    for (int dy = -K; dy <= K; ++dy) {
+      const int y = cy + dy;
+      const float gy = (float)max(abs(dy) - 1, 0);
+      const float rem = lim - gz * gz - gy * gy;
+      if (y < 0 || y >= g.dy || rem < 0.f) continue;
+      const int row = (z * g.dy + y) * g.dx;
+      const int kx = (int)floorf(sqrtf(rem)) + 1;
+      a1 += cell_start[row + min(cx + kx, g.dx - 1) + 1] - cell_start[row + max(cx - kx, 0)];
+      const float rem2 = 0.25f * lim - gz * gz - gy * gy;
+      if (rem2 >= 0.f) {
+        const int k2 = (int)floorf(sqrtf(rem2)) + 1;
+        a2 += cell_start[row + min(cx + k2, g.dx - 1) + 1] - cell_start[row + max(cx - k2, 0)];
+        const float rem4 = 0.0625f * lim - gz * gz - gy * gy;
+        if (rem4 >= 0.f) {
+          const int k4 = (int)floorf(sqrtf(rem4)) + 1;
+          a4 += cell_start[row + min(cx + k4, g.dx - 1) + 1] - cell_start[row + max(cx - k4, 0)];
+        }
+      }
+    }
+  }
+  u1[cell] = a1;
+  u2[cell] = a2;
+  u4[cell] = a4;
+}
+
+// Pass A of mode 8: reject on u1 < 8; the r/4 ball (flat scan) only where u4 >= 8; the rest go to
+// the hard list tagged with their first useful level (r/2 if u2 >= 8, else r).
+__global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_a8(
+    const float4* __restrict__ q_pos, const int* __restrict__ cand, const int* __restrict__ n_cand_dev,
+    const GridParams* __restrict__ gp, const int* __restrict__ cell_start, const float4* __restrict__ sorted,
+    const int* __restrict__ ccell, const int* __restrict__ u1, const int* __restrict__ u2,
+    const int* __restrict__ u4, int* __restrict__ flag, int* __restrict__ t_nbr, int* __restrict__ hard,
+    int* __restrict__ n_hard, int* __restrict__ hard_r, int* __restrict__ n_hard_r) {
+  const int nc = *n_cand_dev;
+  const int c = blockIdx.x * KNN_THREADS + threadIdx.x;
+  const GridParams g = *gp;
+  bool push = false;
+  int tag = 0;
+  if (c < nc) {
+    bool surv = false;
+    const int cell = ccell[c];
+    if (u1[cell] >= KNN_K) {
+      const bool coarse = g.h > 0.25f * g.r;
+      if (coarse || u4[cell] >= KNN_K) {
+        const float4 q = q_pos[cand[c]];
+        float bd[KNN_K];
+        int bi[KNN_K];
+#pragma unroll
+        for (int k = 0; k < KNN_K; ++k) { bd[k] = INFINITY; bi[k] = 0x7fffffff; }
+        const float R2 = coarse ? g.r2 : 0.0625f * g.r2;
+        scan_ball_flat<KNN_K>(g, cell_start, sorted, q.x, q.y, q.z, R2, bd, bi);
+        if (R2 == g.r2 || bd[KNN_K - 1] < R2 * (1.f - 2e-4f)) {
+          surv = bd[KNN_K - 1] <= g.r2;
+          if (surv) {
+            int4* nb = (int4*)(t_nbr + (int64_t)c * KNN_K);
+            nb[0] = make_int4(bi[0], bi[1], bi[2], bi[3]);
+            nb[1] = make_int4(bi[4], bi[5], bi[6], bi[7]);
+          }
+        } else {
+          push = true;
+        }
+      } else {
+        push = true;
+      }
+      tag = u2[cell] >= KNN_K ? 0 : 1;
+    }
+    if (!push) flag[c] = surv;
+  }
+  // two hard lists by first level, so the waves of pass B run queries of similar depth
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int lst = 0; lst < 2; ++lst) {
+    const bool mine = push && tag == lst;
+    const unsigned long long bal = __ballot(mine);
+    if (bal) {
+      int base = 0;
+      if (lane == 0) base = atomicAdd(lst ? n_hard_r : n_hard, __popcll(bal));
+      base = __shfl(base, 0, 64);
+      if (mine) (lst ? hard_r : hard)[base + __popcll(bal & ((1ull << lane) - 1ull))] = 2 * c + tag;
+    }
+  }
+}
+
+// Pass B of mode 8: flat ball scans from the tagged first level (r/2 or r).
+__global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_b8(
+    const float4* __restrict__ q_pos, const int* __restrict__ cand, const int* __restrict__ hard,
+    const int* __restrict__ n_hard, const GridParams* __restrict__ gp, const int* __restrict__ cell_start,
+    const float4* __restrict__ sorted, int* __restrict__ flag, int* __restrict__ t_nbr) {
+  const int i = blockIdx.x * KNN_THREADS + threadIdx.x;
+  if (i >= *n_hard) return;
+  const GridParams g = *gp;
+  const int hc = hard[i];
+  const int c = hc >> 1;
+  const float4 q = q_pos[cand[c]];
+  float bd[KNN_K];
+  int bi[KNN_K];
+#pragma unroll
+  for (int k = 0; k < KNN_K; ++k) { bd[k] = INFINITY; bi[k] = 0x7fffffff; }
+  bool done = false;
+  if ((hc & 1) == 0) {
+    scan_ball_flat<KNN_K>(g, cell_start, sorted, q.x, q.y, q.z, 0.25f * g.r2, bd, bi);
+    done = bd[KNN_K - 1] < 0.25f * g.r2 * (1.f - 2e-4f);
+  }
+  if (!done) scan_ball_flat<KNN_K>(g, cell_start, sorted, q.x, q.y, q.z, g.r2, bd, bi);
+  const bool surv = bd[KNN_K - 1] <= g.r2;
+  flag[c] = surv;
+  if (surv) {
+    int4* nb = (int4*)(t_nbr + (int64_t)c * KNN_K);
+    nb[0] = make_int4(bi[0], bi[1], bi[2], bi[3]);
+    nb[1] = make_int4(bi[4], bi[5], bi[6], bi[7]);
+  }
+}
+
+// Pass A of mode 6: candidates whose cell bound is < 8 are rejected; the rest run the r/4 ball
+// and, unless it already holds the 8 nearest, go to the hard list (pass B).
+__global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_a6(
+    const float4* __restrict__ q_pos, const int* __restrict__ cand, const int* __restrict__ n_cand_dev,
+    const GridParams* __restrict__ gp, const int* __restrict__ cell_start, const float4* __restrict__ sorted,
+    const int* __restrict__ ccell, const int* __restrict__ ubound, int* __restrict__ flag, int* __restrict__ t_nbr,
+    int* __restrict__ hard, int* __restrict__ n_hard) {
+  const int nc = *n_cand_dev;
+  const int c = blockIdx.x * KNN_THREADS + threadIdx.x;
+  const GridParams g = *gp;
+  bool push = false;
+  if (c < nc) {
+    bool surv = false;
+    if (ubound[ccell[c]] >= KNN_K) {
+      const float4 q = q_pos[cand[c]];
+      float bd[KNN_K];
+      int bi[KNN_K];
+#pragma unroll
+      for (int k = 0; k < KNN_K; ++k) { bd[k] = INFINITY; bi[k] = 0x7fffffff; }
+      const float R2 = g.h > 0.25f * g.r ? g.r2 : 0.0625f * g.r2;
+      scan_ball_nf<KNN_K>(g, cell_start, sorted, q.x, q.y, q.z, R2, bd, bi);
+      if (R2 == g.r2 || bd[KNN_K - 1] < R2 * (1.f - 2e-4f)) {
+        surv = bd[KNN_K - 1] <= g.r2;
+        if (surv) {
+          int4* nb = (int4*)(t_nbr + (int64_t)c * KNN_K);
+          nb[0] = make_int4(bi[0], bi[1], bi[2], bi[3]);
+          nb[1] = make_int4(bi[4], bi[5], bi[6], bi[7]);
+        }
+      } else {
+        push = true;
+      }
+    }
+    if (!push) flag[c] = surv;
+  }
+  const int lane = threadIdx.x & 63;
+  const unsigned long long bal = __ballot(push);
+  if (bal) {
+    int base = 0;
+    if (lane == 0) base = atomicAdd(n_hard, __popcll(bal));
+    base = __shfl(base, 0, 64);
+    if (push) hard[base + __popcll(bal & ((1ull << lane) - 1ull))] = c;
   }
 }
 
@@ -1067,14 +1199,14 @@ static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 static int& knn_mode() {
   static int m = [] {
     const char* e = getenv("APN_KNN_MODE");
-    return e ? atoi(e) : 7;
+    return e ? atoi(e) : 8;
   }();
   return m;
 }
 
 extern "C" int apn_set_knn_mode(int32_t mode) {
   const int prev = knn_mode();
-  if (mode >= 0 && mode <= 7) knn_mode() = mode;
+  if (mode >= 0 && mode <= 8) knn_mode() = mode;
   return prev;
 }
 
@@ -1186,6 +1318,42 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
   if (st) return st;
   hipLaunchKernelGGL(k_compact_i32, dim3(nb), dim3(KNN_THREADS), 0, s, cand_blk, cblk_cnt, cblk_off, cand);
   // candidates: count at cblk_off[nb]; launch over the upper bound nb blocks
+  if (knn_mode() == 8) {
+    int* flag = t_ray;
+    int* hard = cand_blk;
+    int* n_hard = cblk_cnt + nb + 1;
+    int* ccell = (int*)t_pos;
+    int* mark = g.cursor;        // free after the grid build
+    int* u1 = g.counts;          // free after the grid build
+    int* u2 = g.tile_cnt;
+    int* u4 = g.tile_cursor;
+    APN_HIP_TRY(hipMemsetAsync(mark, 0, (size_t)cell_cap * 4, s));
+    APN_HIP_TRY(hipMemsetAsync(g.n_tile_list, 0, 4, s));
+    APN_HIP_TRY(hipMemsetAsync(n_hard, 0, 4, s));
+    hipLaunchKernelGGL(k_mark_cells, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, cblk_off + nb,
+                       g.gp, ccell, mark);
+    hipLaunchKernelGGL(k_tile_list, dim3(ceil_div(cell_cap, KNN_THREADS)), dim3(KNN_THREADS), 0, s, mark, cell_cap,
+                       g.tile_list, g.n_tile_list);
+    hipLaunchKernelGGL(k_cell_bound3, dim3(ceil_div(std::min<int64_t>(cell_cap, slots), KNN_THREADS)),
+                       dim3(KNN_THREADS), 0, s, g.gp, g.cell_start, g.tile_list, g.n_tile_list, u1, u2, u4);
+    int* hard_r = ccell + slots;          // second quarter of the t_pos region
+    int* n_hard_r = cblk_off + nb + 1;    // cblk_off has nb + 2 entries
+    APN_HIP_TRY(hipMemsetAsync(n_hard_r, 0, 4, s));
+    hipLaunchKernelGGL(k_knn_pass_a8, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, cblk_off + nb,
+                       g.gp, g.cell_start, (const float4*)sorted_pts4, ccell, u1, u2, u4, flag, t_nbr, hard, n_hard,
+                       hard_r, n_hard_r);
+    hipLaunchKernelGGL(k_knn_pass_b8, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard, n_hard,
+                       g.gp, g.cell_start, (const float4*)sorted_pts4, flag, t_nbr);
+    hipLaunchKernelGGL(k_knn_pass_b8, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard_r,
+                       n_hard_r, g.gp, g.cell_start, (const float4*)sorted_pts4, flag, t_nbr);
+    hipLaunchKernelGGL(k_knn_flag_count, dim3(nb), dim3(KNN_THREADS), 0, s, flag, cblk_off + nb, blk_cnt);
+    st = scan_exclusive_i32(blk_cnt, blk_off, nb, sws, s);
+    if (st) return st;
+    hipLaunchKernelGGL(k_knn_flag_compact, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, q_ray, cand,
+                       cblk_off + nb, flag, t_nbr, blk_off, (float4*)s_pos4, s_ray, s_nbr);
+    APN_HIP_TRY(hipMemcpyAsync(n_survivors_dev, blk_off + nb, 4, hipMemcpyDeviceToDevice, s));
+    return launch_status();
+  }
   if (knn_mode() == 6 || knn_mode() == 7) {
     int* flag = t_ray;
     int* hard = cand_blk;

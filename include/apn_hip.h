@@ -128,14 +128,16 @@ int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t n_queries,
                    void* stream);
 
 /* Select the apn_knn_radius search strategy (process-wide; initial value from env APN_KNN_MODE,
- * default 7): 0 = expanding balls 2h, 4h, r; 1 = culled Chebyshev rings; 2 = ball 2h, then an
+ * default 8): 0 = expanding balls 2h, 4h, r; 1 = culled Chebyshev rings; 2 = ball 2h, then an
  * r-ball chord-count rejection bound, then balls 4h, r with nearest-first rows; 3 = 2 with
  * per-class counters (profiling aid); 4 = the mode-2 search split into two passes (2h ball +
  * chord count for all candidates, balls r/2, r for the rest); 5 = the mode-4 search with the
  * candidates bucketed by 4^3-cell tiles, one workgroup per tile staging the region's cell bounds
  * in LDS; 6 = per-cell rejection bound (points within r of the query's cell box, computed once per
  * occupied cell) + ball r/4, then balls r/2, r for the rest; 7 = 6 with the r/2, r balls as a
- * per-lane state machine (rows and points consumed in lock-step across the wave). All are exact. Returns the previous selection;
+ * per-lane state machine (rows and points consumed in lock-step across the wave); 8 = 7 with the
+ * cell bound also at r/4 and r/2, so each query starts at its first level that can hold 8 points,
+ * and the r/4 ball as a state machine too. All are exact. Returns the previous selection;
  * out-of-range values only query it. */
 int apn_set_knn_mode(int32_t mode);
 
