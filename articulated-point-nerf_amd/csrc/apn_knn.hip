@@ -821,6 +821,81 @@ __device__ __forceinline__ void scan_ball_flat(const GridParams& g, const int* _
   }
 }
 
+// scan_ball_flat with incremental slot iteration: slabs advance in nearest-first order, and a
+// slab only enumerates the y offsets whose rows can intersect the ball under the current bound
+// (|dy| <= floor(sqrt(tau - dz^2)/h) + 1), so the square's corners and culled slabs cost no
+// iterations; no integer division per row.
+template <int K>
+__device__ __forceinline__ void scan_ball_flat2(const GridParams& g, const int* __restrict__ cell_start,
+                                                const float4* __restrict__ sorted, float qx, float qy, float qz,
+                                                float R2, float (&bd)[K], int (&bi)[K]) {
+  const float R = sqrtf(R2) * 1.0001f;
+  const int z0 = max((int)floorf((qz - R - g.oz) * g.inv_h), 0), z1 = min((int)floorf((qz + R - g.oz) * g.inv_h), g.dz - 1);
+  const int y0 = max((int)floorf((qy - R - g.oy) * g.inv_h), 0), y1 = min((int)floorf((qy + R - g.oy) * g.inv_h), g.dy - 1);
+  const int fz = min(max((int)floorf((qz - g.oz) * g.inv_h), z0), z1);
+  const int fy = min(max((int)floorf((qy - g.oy) * g.inv_h), y0), y1);
+  const int nz = (z1 < z0 || y1 < y0) ? 0 : 2 * max(fz - z0, z1 - fz) + 1;
+  const int ny = 2 * max(fy - y0, y1 - fy) + 1;
+  int iz = -1, iy = 0, nyz = 0;    // current slab (nf index), next y slot, y slots of the slab
+  int z = 0;
+  float dz2 = 0.f;
+  int b = 0, e = 0;                // range being consumed
+  int pb = 0, pe = 0;              // range loaded for the next row
+  bool pend = false;
+  for (;;) {
+    const bool has_pts = b < e;
+    const bool rows_left = iy < nyz || iz + 1 < nz;
+    if (!has_pts && !pend && !rows_left) break;
+    if (has_pts) {
+      const int p1 = b + 1 < e ? b + 1 : b;
+      const float4 P0 = sorted[b], P1 = sorted[p1];
+      const float d0x = qx - P0.x, d0y = qy - P0.y, d0z = qz - P0.z;
+      const float d0 = (d0x * d0x + d0y * d0y) + d0z * d0z;
+      const float d1x = qx - P1.x, d1y = qy - P1.y, d1z = qz - P1.z;
+      const float d1 = (d1x * d1x + d1y * d1y) + d1z * d1z;
+      if (d0 <= g.r2) knn_insert_unique<K>(d0, __float_as_int(P0.w), bd, bi);
+      if (p1 != b && d1 <= g.r2) knn_insert_unique<K>(d1, __float_as_int(P1.w), bd, bi);
+      b += 2;
+      if (b > e) b = e;
+    } else {
+      if (pend) { b = pb; e = pe; pend = false; }
+      const float tau = fminf(bd[K - 1], R2) * 1.0001f;
+      if (iy >= nyz) {               // next slab
+        ++iz;
+        iy = 0;
+        nyz = 0;
+        if (iz < nz) {
+          z = fz + nf_offset(iz);
+          if (z >= z0 && z <= z1) {
+            dz2 = slab_d2(qz, g.oz, g.h, z, z);
+            if (dz2 <= tau) {
+              const int my = (int)floorf(sqrtf(tau - dz2) * g.inv_h * 1.0001f) + 1;
+              nyz = min(2 * my + 1, ny);
+            }
+          }
+        }
+      } else {                       // one row of the slab
+        const int y = fy + nf_offset(iy);
+        ++iy;
+        if (y >= y0 && y <= y1) {
+          const float dyz2 = dz2 + slab_d2(qy, g.oy, g.h, y, y);
+          if (dyz2 <= tau) {
+            const float w = sqrtf(tau - dyz2) * 1.0001f;
+            const int x0 = max((int)floorf((qx - w - g.ox) * g.inv_h), 0);
+            const int x1 = min((int)floorf((qx + w - g.ox) * g.inv_h), g.dx - 1);
+            if (x0 <= x1) {
+              const int row = (z * g.dy + y) * g.dx;
+              pb = cell_start[row + x0];
+              pe = cell_start[row + x1 + 1];
+              pend = true;
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
 // ---- mode 6: per-cell rejection bound. For every fine cell C holding a candidate, U(C) = number
 // of points in cells whose box lies within r of C's box -- an upper bound on the points within r of
 // ANY query in C (also of a query just outside the grid, clamped into C: its distance to a point
@@ -940,7 +1015,7 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_a8(
 #pragma unroll
         for (int k = 0; k < KNN_K; ++k) { bd[k] = INFINITY; bi[k] = 0x7fffffff; }
         const float R2 = coarse ? g.r2 : 0.0625f * g.r2;
-        scan_ball_flat<KNN_K>(g, cell_start, sorted, q.x, q.y, q.z, R2, bd, bi);
+        scan_ball_flat2<KNN_K>(g, cell_start, sorted, q.x, q.y, q.z, R2, bd, bi);
         if (R2 == g.r2 || bd[KNN_K - 1] < R2 * (1.f - 2e-4f)) {
           surv = bd[KNN_K - 1] <= g.r2;
           if (surv) {
@@ -990,10 +1065,10 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_b8(
   for (int k = 0; k < KNN_K; ++k) { bd[k] = INFINITY; bi[k] = 0x7fffffff; }
   bool done = false;
   if ((hc & 1) == 0) {
-    scan_ball_flat<KNN_K>(g, cell_start, sorted, q.x, q.y, q.z, 0.25f * g.r2, bd, bi);
+    scan_ball_flat2<KNN_K>(g, cell_start, sorted, q.x, q.y, q.z, 0.25f * g.r2, bd, bi);
     done = bd[KNN_K - 1] < 0.25f * g.r2 * (1.f - 2e-4f);
   }
-  if (!done) scan_ball_flat<KNN_K>(g, cell_start, sorted, q.x, q.y, q.z, g.r2, bd, bi);
+  if (!done) scan_ball_flat2<KNN_K>(g, cell_start, sorted, q.x, q.y, q.z, g.r2, bd, bi);
   const bool surv = bd[KNN_K - 1] <= g.r2;
   flag[c] = surv;
   if (surv) {
