@@ -32,6 +32,32 @@ class NoPointsException(Exception):
     """temporalpoints.py:26-28."""
 
 
+class FrameStats(dict):
+    """Per-frame counts. 'kept_samples' (kNN survivors) stays on the device until asked for, so
+    rendering a frame needs no device->host sync after the kNN stage."""
+
+    def __init__(self, *args, nsurv=None, **kw):
+        super().__init__(*args, **kw)
+        self._nsurv = nsurv
+
+    def __missing__(self, key):
+        if key == "kept_samples" and self._nsurv is not None:
+            v = int(self._nsurv.item())
+            self[key] = v
+            return v
+        raise KeyError(key)
+
+    def get(self, key, default=None):
+        try:
+            return self[key]
+        except KeyError:
+            return default
+
+    def resolved(self):
+        self.get("kept_samples")
+        return dict(self)
+
+
 def hls_palette(n, h=0.01, l=0.6, s=0.65):
     """seaborn.color_palette('hls', n) (temporalpoints.py:692)."""
     hues = np.linspace(0, 1, n + 1)[:-1]
@@ -153,7 +179,7 @@ class TemporalPoints(torch.nn.Module):
         self._palette_cache = {}
         self.palette_perm_device = None   # None: the weights' device (reference behaviour)
         self.timing = None          # set to {} to record HIP-event timings of the MLP launch
-        self.last_stats = {}
+        self.last_stats = FrameStats()
 
     # view_poc / pos_poc alias the TiNeuVox buffers (temporalpoints.py:148-150); as properties
     # they follow .to(device) (the reference relies on a CUDA default tensor type instead).
@@ -420,7 +446,7 @@ class TemporalPoints(torch.nn.Module):
             offs = (offs[r0:r1 + 1] - offs[r0]).contiguous()
             R = r1 - r0
         n_bbox = int(offs[R].item())
-        self.last_stats = {"rays": R, "inbbox_samples": n_bbox}
+        self.last_stats = FrameStats({"rays": R, "inbbox_samples": n_bbox})
         if n_bbox == 0:
             raise NoPointsException("No points.")
         q_pos = ws.get("q_pos", n_bbox * 4, torch.float32, dev)
@@ -432,15 +458,17 @@ class TemporalPoints(torch.nn.Module):
         s_pos = ws.get("s_pos", n_bbox * 4, torch.float32, dev)
         s_ray = ws.get("s_ray", n_bbox, torch.int32, dev)
         s_nbr = ws.get("s_nbr", n_bbox * 8, torch.int32, dev)
-        nsurv = ws.get("nsurv", 1, torch.int32, dev)
+        nsurv = torch.empty(1, dtype=torch.int32, device=dev)   # per frame: FrameStats may read it later
         kws = ws.bytes("knn_ws", lib.apn_knn_workspace_bytes(n_bbox), dev)
         call("apn_knn_radius", ptr(q_pos), ptr(q_ray), n_bbox, C.c_void_p(offs.data_ptr() + 4 * R), ptr(gws), N,
              CELL_CAP, ptr(sorted4), qr, ptr(s_pos), ptr(s_ray), ptr(s_nbr), ptr(nsurv), ptr(kws), s)
         self._mark("knn")
-        S = int(nsurv.item())
-        self.last_stats["kept_samples"] = S
-        if S == 0:
-            raise NoPointsException("No points.")
+        # The survivor count stays on the device: the MLP and compositing kernels read it there and
+        # n_bbox bounds it, so no sync here. (If no sample survives, the kernels produce the
+        # reference's NoPointsException values -- bg colour, depth 0 -- with alphainv_last = 1
+        # tensors instead of None.)
+        S = n_bbox
+        self.last_stats._nsurv = nsurv
         # neighbour MLP + heads + direct blend
         wbuf, proj = self._packed_weights(pose_embedding, dev)
         out12 = ws.get("out12", S * 12, torch.float32, dev)
@@ -457,7 +485,7 @@ class TemporalPoints(torch.nn.Module):
              ptr(out12), s)
         if self.timing is not None:
             e1.record()
-            self.timing.setdefault("mlp_events", []).append((e0, e1, S))
+            self.timing.setdefault("mlp_events", []).append((e0, e1, nsurv))
             self.timing["marks"].append(("mlp", e1))
         # compositing
         rgb = torch.empty(R, 3, device=dev); rgb_d = torch.empty(R, 3, device=dev)

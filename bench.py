@@ -154,7 +154,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    stats = dict(model.last_stats)
+    stats = model.last_stats.resolved()
     log(f"[rank {rank}] scene: {stats}")
 
     model.timing = {}
@@ -200,7 +200,7 @@ def main():
                 f"cycles/query {st[4 * i + 1] / n:.0f} rows/query {st[4 * i + 2] / n:.1f} pts/query {st[4 * i + 3] / n:.1f}")
     ev = model.timing.get("mlp_events", [])
     mlp_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / max(len(ev), 1)
-    S_kept = ev[-1][2] if ev else stats.get("kept_samples", 0)
+    S_kept = int(ev[-1][2].item()) if ev else stats.get("kept_samples", 0)
     model.timing = None
 
     if rank != 0:

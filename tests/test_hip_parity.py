@@ -508,7 +508,7 @@ def test_knn_modes_identical_full_scene(dev, mode):
             torch.cuda.synchronize()
         finally:
             L.load().apn_set_knn_mode(prev)
-        outs.append(({k: v.clone() for k, v in o.items() if torch.is_tensor(v)}, dict(model.last_stats)))
+        outs.append(({k: v.clone() for k, v in o.items() if torch.is_tensor(v)}, model.last_stats.resolved()))
     (a, sa), (b, sb) = outs
     assert sa == sb
     for k in ("rgb_marched", "rgb_marched_direct", "depth", "weights"):
