@@ -86,7 +86,26 @@ __global__ void k_grid_count(const float* __restrict__ xyz, int64_t N, const Gri
   const int cell = (cz * g.dy + cy) * g.dx + cx;
   pcell[n] = cell;
   atomicAdd(counts + cell, 1);
-  atomicAdd(ccount + ((cz / g.cf) * g.cdy + cy / g.cf) * g.cdx + cx / g.cf, 1);
+  (void)ccount;
+}
+
+// Coarse-cell counts (the classify pass's 27-cell test) from the fine prefix: one thread per coarse
+// cell sums its cf x cf fine rows (cell_start differences) -- no per-point atomics on the ~10^3
+// coarse counters, which serialised at the L2.
+__global__ void k_coarse_counts(const GridParams* __restrict__ gp, const int* __restrict__ cell_start,
+                                int* __restrict__ ccount) {
+  const GridParams g = *gp;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= g.nc) return;
+  const int ccx = c % g.cdx, ccy = (c / g.cdx) % g.cdy, ccz = c / (g.cdx * g.cdy);
+  const int x0 = ccx * g.cf, x1 = min(x0 + g.cf, g.dx) - 1;
+  int n = 0;
+  for (int z = ccz * g.cf; z < min((ccz + 1) * g.cf, g.dz); ++z)
+    for (int y = ccy * g.cf; y < min((ccy + 1) * g.cf, g.dy); ++y) {
+      const int row = (z * g.dy + y) * g.dx;
+      n += cell_start[row + x1 + 1] - cell_start[row + x0];
+    }
+  ccount[c] = n;
 }
 
 __global__ void k_grid_scatter(const float* __restrict__ xyz, int64_t N, const int* __restrict__ pcell,
@@ -445,18 +464,30 @@ __global__ __launch_bounds__(KNN_THREADS) void k_tile_scatter(const int* __restr
   order[tile_start[t] + atomicAdd(tile_cursor + t, 1)] = c;
 }
 
-// Non-empty tiles -> list (any order); n_list[0] = count.
-__global__ __launch_bounds__(KNN_THREADS) void k_tile_list(const int* __restrict__ tile_cnt, int n_tiles_max,
-                                                          int* __restrict__ list, int* __restrict__ n_list) {
-  const int t = blockIdx.x * KNN_THREADS + threadIdx.x;
+// Non-zero entries -> list of their indices (any order); n_list[0] = count. One atomic per
+// 1024-entry block (per-wave atomics on the single counter serialised at the L2).
+constexpr int LIST_THREADS = 1024;
+__global__ __launch_bounds__(LIST_THREADS) void k_tile_list(const int* __restrict__ tile_cnt, int n_tiles_max,
+                                                           int* __restrict__ list, int* __restrict__ n_list) {
+  __shared__ int wcnt[LIST_THREADS / 64];
+  __shared__ int sbase;
+  const int t = blockIdx.x * LIST_THREADS + threadIdx.x;
   const bool ne = t < n_tiles_max && tile_cnt[t] > 0;
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const unsigned long long bal = __ballot(ne);
-  if (!bal) return;
-  int base = 0;
-  if (lane == 0) base = atomicAdd(n_list, __popcll(bal));
-  base = __shfl(base, 0, 64);
-  if (ne) list[base + __popcll(bal & ((1ull << lane) - 1ull))] = t;
+  if (lane == 0) wcnt[wid] = __popcll(bal);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int tot = 0;
+    for (int w = 0; w < LIST_THREADS / 64; ++w) {
+      const int c = wcnt[w];
+      wcnt[w] = tot;
+      tot += c;
+    }
+    sbase = tot ? atomicAdd(n_list, tot) : 0;
+  }
+  __syncthreads();
+  if (ne) list[sbase + wcnt[wid] + __popcll(bal & ((1ull << lane) - 1ull))] = t;
 }
 
 __global__ __launch_bounds__(KNN_THREADS) void k_knn_tiles(
@@ -1335,7 +1366,6 @@ extern "C" int apn_grid_build(const float* xyz, int64_t n_points, const int32_t*
   GridWs w = grid_ws(workspace, n_points, cell_cap);
   APN_HIP_TRY(hipMemsetAsync(w.counts, 0, (size_t)cell_cap * 4, s));
   APN_HIP_TRY(hipMemsetAsync(w.cursor, 0, (size_t)cell_cap * 4, s));
-  APN_HIP_TRY(hipMemsetAsync(w.ccount, 0, (size_t)cell_cap * 4, s));
   static const int subdiv = [] {
     const char* e = getenv("APN_KNN_SUBDIV");
     return e ? atoi(e) : KNN_SUBDIV;
@@ -1345,6 +1375,8 @@ extern "C" int apn_grid_build(const float* xyz, int64_t n_points, const int32_t*
                      w.ccount, w.pcell);
   int st = scan_exclusive_i32(w.counts, w.cell_start, cell_cap, w.scan, s);
   if (st) return st;
+  // coarse cells never outnumber fine cells (cap)
+  hipLaunchKernelGGL(k_coarse_counts, dim3(ceil_div(cell_cap, 256)), dim3(256), 0, s, w.gp, w.cell_start, w.ccount);
   hipLaunchKernelGGL(k_grid_scatter, dim3(ceil_div(n_points, 256)), dim3(256), 0, s, xyz, n_points, w.pcell,
                      w.cell_start, w.cursor, (float4*)sorted_pts4);
   return launch_status();
@@ -1407,7 +1439,7 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
     APN_HIP_TRY(hipMemsetAsync(n_hard, 0, 4, s));
     hipLaunchKernelGGL(k_mark_cells, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, cblk_off + nb,
                        g.gp, ccell, mark);
-    hipLaunchKernelGGL(k_tile_list, dim3(ceil_div(cell_cap, KNN_THREADS)), dim3(KNN_THREADS), 0, s, mark, cell_cap,
+    hipLaunchKernelGGL(k_tile_list, dim3(ceil_div(cell_cap, LIST_THREADS)), dim3(LIST_THREADS), 0, s, mark, cell_cap,
                        g.tile_list, g.n_tile_list);
     hipLaunchKernelGGL(k_cell_bound3, dim3(ceil_div(std::min<int64_t>(cell_cap, slots), KNN_THREADS)),
                        dim3(KNN_THREADS), 0, s, g.gp, g.cell_start, g.tile_list, g.n_tile_list, u1, u2, u4);
@@ -1441,7 +1473,7 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
     APN_HIP_TRY(hipMemsetAsync(n_hard, 0, 4, s));
     hipLaunchKernelGGL(k_mark_cells, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, cblk_off + nb,
                        g.gp, ccell, mark);
-    hipLaunchKernelGGL(k_tile_list, dim3(ceil_div(cell_cap, KNN_THREADS)), dim3(KNN_THREADS), 0, s, mark, cell_cap,
+    hipLaunchKernelGGL(k_tile_list, dim3(ceil_div(cell_cap, LIST_THREADS)), dim3(LIST_THREADS), 0, s, mark, cell_cap,
                        g.tile_list, g.n_tile_list);
     hipLaunchKernelGGL(k_cell_bound, dim3(ceil_div(std::min<int64_t>(cell_cap, slots), KNN_THREADS)),
                        dim3(KNN_THREADS), 0, s, g.gp, g.cell_start, g.tile_list, g.n_tile_list, ubound);
@@ -1474,7 +1506,7 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
     if (st) return st;
     hipLaunchKernelGGL(k_tile_scatter, dim3(nb), dim3(KNN_THREADS), 0, s, cblk_off + nb, ctile, g.tile_start,
                        g.tile_cursor, order);
-    hipLaunchKernelGGL(k_tile_list, dim3(ceil_div(cell_cap, KNN_THREADS)), dim3(KNN_THREADS), 0, s, g.tile_cnt,
+    hipLaunchKernelGGL(k_tile_list, dim3(ceil_div(cell_cap, LIST_THREADS)), dim3(LIST_THREADS), 0, s, g.tile_cnt,
                        cell_cap, g.tile_list, g.n_tile_list);
     hipLaunchKernelGGL(k_knn_tiles, dim3(256 * 3), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, g.gp,
                        g.cell_start, (const float4*)sorted_pts4, g.tile_list, g.n_tile_list, g.tile_start,

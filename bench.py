@@ -162,8 +162,11 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    host_s = 0.0
     for _ in range(args.steps):
+        h0 = time.perf_counter()
         step()
+        host_s += time.perf_counter() - h0
     torch.cuda.synchronize(dev)
     if world > 1:
         torch.distributed.barrier()
@@ -187,6 +190,7 @@ def main():
         if name != "frame":
             stage_ms[name] = stage_ms.get(name, 0.0) + a.elapsed_time(b) / args.steps
     log(f"[rank {rank}] stage ms/frame (HIP events): " + ", ".join(f"{k} {v:.3f}" for k, v in stage_ms.items()))
+    log(f"[rank {rank}] host time inside step() {1e3 * host_s / args.steps:.3f} ms/step (includes the n_bbox sync wait)")
     if os.environ.get("APN_KNN_MODE") == "3":   # kNN query-class counters
         import ctypes
         from apn_amd import _lib
