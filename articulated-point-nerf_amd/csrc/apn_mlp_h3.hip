@@ -237,6 +237,107 @@ __device__ __forceinline__ void init_bias(f32x4 (&acc)[4][2], int ot0, const flo
 
 __device__ unsigned long long g_phase[6];
 
+// Gather of one tile by the 256 V-threads (vt): row r = vt >> 2 (sample r >> 3, neighbour r & 7),
+// quarter p = vt & 3 of the row. Split in two: ws_gather_load issues the neighbour-record and
+// view-direction loads (a segment ahead), ws_gather writes the posenc hi/lo into PE (X layout,
+// chunks 0..7) and the row records into sTo/sRow/sV.
+struct GatherRegs {
+  float4 a0, a1, a2, a3, b0, b1;
+  float vv;
+};
+
+// Loads are unconditional (clamped indices; invalid rows read row 0 and are discarded later):
+// a load under a divergent branch makes the compiler drain vmcnt(0) at the join, which would
+// expose the latency of every load in flight.
+__device__ __forceinline__ void ws_gather_load(int vt, int nb, int ray, GatherRegs& G,
+                                               const float4* __restrict__ recA, const float4* __restrict__ recB,
+                                               const float* __restrict__ viewdirs,
+                                               const float* __restrict__ vemb_const) {
+  const int r = vt >> 2, p = vt & 3, k = r & 7;
+  const size_t n = (size_t)max(nb, 0);
+  G.a0 = recA[4 * n + 0];
+  G.a1 = recA[4 * n + 1];
+  G.a2 = recA[4 * n + 2];
+  G.a3 = recA[4 * n + 3];
+  G.b0 = recB[2 * n];
+  G.b1 = recB[2 * n + 1];
+  const int e = min(4 * k + p, 26);
+  const int ee = e < 3 ? 0 : (e < 15 ? e - 3 : e - 15);
+  G.vv = vemb_const ? 0.f : viewdirs[3 * (size_t)ray + (e < 3 ? e : ee >> 2)];
+}
+
+__device__ __forceinline__ void ws_gather(int vt, int nb, float4 q, const GatherRegs& G, char* __restrict__ PE,
+                                          float* __restrict__ sTo, float* __restrict__ sRow, float* __restrict__ sV,
+                                          const float* __restrict__ vemb_const) {
+  const int r = vt >> 2, p = vt & 3, s = r >> 3, k = r & 7;
+  char* xr = PE + r * XB;
+  const int c_sin = (2 * p) ^ (r & 15), c_cos = (2 * p + 1) ^ (r & 15);
+  if (nb >= 0) {
+    const float4 a0 = G.a0, a1 = G.a1, a2 = G.a2, a3 = G.a3;
+    const float dx = q.x - a0.x, dy = q.y - a0.y, dz = q.z - a0.z;
+    const float rc0 = (a1.x * dx + a1.y * dy) + a1.z * dz;
+    const float rc1 = (a1.w * dx + a2.x * dy) + a2.y * dz;
+    const float rc2 = (a2.z * dx + a2.w * dy) + a3.x * dz;
+    const float tn = (dx * dx + dy * dy) + dz * dz;
+    if (p == 0) {
+      sTo[r] = tn;
+    } else if (p == 1) {
+      float* rw = sRow + 8 * r;
+      rw[0] = expf(-(tn * tn) / a0.w);   // temporalpoints.py:461 (to_nn is already squared)
+      rw[1] = a3.y;
+      rw[2] = G.b0.x; rw[3] = G.b0.y; rw[4] = G.b0.z;
+      rw[5] = G.b1.x; rw[6] = G.b1.y; rw[7] = G.b1.z;
+    }
+    f32x4 sv0, sv1, cv0, cv1;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int aa = p + 4 * j;
+      float sv, cv;
+      if (aa < 30) {
+        const int ci = aa / 10;
+        const float v = (ci == 0 ? rc0 : (ci == 1 ? rc1 : rc2)) * (float)(1 << (aa - 10 * ci));
+        sincos_pe(v, sv, cv);
+      } else {
+        sv = p == 2 ? rc0 : rc2;
+        cv = p == 2 ? rc1 : 0.f;
+      }
+      if (j < 4) { sv0[j] = sv; cv0[j] = cv; } else { sv1[j - 4] = sv; cv1[j - 4] = cv; }
+    }
+    h4 hs0, ls0, hs1, ls1, hc0, lc0, hc1, lc1;
+    split4(sv0, hs0, ls0); split4(sv1, hs1, ls1);
+    split4(cv0, hc0, lc0); split4(cv1, hc1, lc1);
+    *(h8*)(xr + (c_sin << 4)) = __builtin_shufflevector(hs0, hs1, 0, 1, 2, 3, 4, 5, 6, 7);
+    *(h8*)(xr + (c_sin << 4) + 256) = __builtin_shufflevector(ls0, ls1, 0, 1, 2, 3, 4, 5, 6, 7);
+    *(h8*)(xr + (c_cos << 4)) = __builtin_shufflevector(hc0, hc1, 0, 1, 2, 3, 4, 5, 6, 7);
+    *(h8*)(xr + (c_cos << 4) + 256) = __builtin_shufflevector(lc0, lc1, 0, 1, 2, 3, 4, 5, 6, 7);
+    const int e = 4 * k + p;   // view embedding element e of this sample
+    float v = 0.f;
+    if (e < 27) {
+      if (vemb_const) {
+        v = vemb_const[e];
+      } else {
+        const int ee = e < 3 ? 0 : (e < 15 ? e - 3 : e - 15);
+        float sn_, cs_;
+        sincos_pe(G.vv * (float)(1 << (ee & 3)), sn_, cs_);
+        v = e < 3 ? G.vv : (e < 15 ? sn_ : cs_);
+      }
+    }
+    sV[s * 32 + e] = v;
+  } else {
+    const h8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+    *(h8*)(xr + (c_sin << 4)) = z;
+    *(h8*)(xr + (c_sin << 4) + 256) = z;
+    *(h8*)(xr + (c_cos << 4)) = z;
+    *(h8*)(xr + (c_cos << 4) + 256) = z;
+    sV[s * 32 + 4 * k + p] = 0.f;
+    if (p == 0) {
+      sTo[r] = 1.f;
+    } else if (p == 1) {
+      for (int c = 0; c < 8; ++c) sRow[8 * r + c] = 0.f;
+    }
+  }
+}
+
 // OCC = workgroups per CU: 2 = activations ping-pong between two LDS buffers (one barrier per
 // layer); 3 = one activation buffer + a separate head-input buffer (45 KB of LDS, an extra barrier
 // per layer, 12 waves per CU to hide the phases' latencies).
@@ -295,131 +396,57 @@ __global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
     ph[i] += now - tk;                       \
     tk = now;                                \
   }
-  // gather coordinates: row r = (sample s, neighbour k), quarter p of the row
-  const int gr = tid >> 2, gp = tid & 3, gsm = gr >> 3, gk = gr & 7;
-  // next-tile prefetch: this thread's gather row, and the 4 rows whose P this lane loads
-  int pf_nb = -1, pf_ray = 0, pf_pn[4];
+  // next-tile prefetch (unconditional clamped loads, validity apart -- see ws_gather_load):
+  // this thread's gather row (neighbour, sample position, ray) and the 4 rows whose P it loads
+  int pf_nb = 0, pf_ray = 0, pf_pn[4];
+  bool pf_ok = false, pf_pok[4];
   float4 pf_q = make_float4(0.f, 0.f, 0.f, 0.f);
   auto fetch = [&](int tl) {
-    const int gs = tl * TS + gsm;
-    pf_nb = -1;
-    if (tl < t_end && gs < nS) {
-      pf_nb = s_nbr[(size_t)gs * 8 + gk];
-      pf_q = s_pos[gs];
-      pf_ray = s_ray[gs];
-    }
+    const int tc = min(tl, t_end - 1);
+    const int gs = tc * TS + (tid >> 5);
+    const int gc = min(gs, nS - 1);
+    pf_ok = tl < t_end && gs < nS;
+    pf_nb = s_nbr[(size_t)gc * 8 + ((tid >> 2) & 7)];
+    pf_q = s_pos[gc];
+    pf_ray = s_ray[gc];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       const int m = 16 * mt + li;
-      pf_pn[mt] = (tl < t_end && tl * TS + (m >> 3) < nS) ? s_nbr[(size_t)tl * TR + m] : -1;
+      pf_pok[mt] = tl < t_end && tc * TS + (m >> 3) < nS;
+      pf_pn[mt] = s_nbr[min((size_t)tc * TR + m, (size_t)nS * 8 - 1)];
     }
   };
   int tile = t_beg + blockIdx.x / nx;
-  fetch(tile);
+  if (tile < t_end) fetch(tile);
   h8 a[2][2];   // carried A-fragment prefetch (chunk 0 of the next weight matrix)
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
     for (int pt = 0; pt < 2; ++pt) a[j][pt] = frag(rs, H_W1E, 2, ot0 + j, 0, pt);
   int prev_s0 = -1;
+  GatherRegs gregs;
   for (; tile < t_end; tile += per_xcd) {
     const int s0 = tile * TS;
     if (TIMED) { tk = clock64(); ph[4] += 1; }
-    // ------------------------------------------------ layer-1 accumulators = P[nbr] (global -> VGPR)
+    // ------------------------------------------------ loads: gather records first (consumed first),
+    // then the layer-1 accumulators = P[nbr] (global -> VGPR), then the next tile's indices
+    const int nb = pf_ok ? pf_nb : -1;
+    const float4 q = pf_q;
+    ws_gather_load(tid, nb, pf_ray, gregs, recA, recB, viewdirs, vemb_const);
     f32x4 acc[4][2];
+    bool pok[4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
-      const int nb = pf_pn[mt];
+      pok[mt] = pf_pok[mt];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const float4 v = nb >= 0 ? pproj[(size_t)nb * (FEAT / 4) + 4 * (ot0 + j) + g] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 v = pproj[(size_t)max(pf_pn[mt], 0) * (FEAT / 4) + 4 * (ot0 + j) + g];
         acc[mt][j] = f32x4{v.x, v.y, v.z, v.w};
       }
     }
-    // ------------------------------------------------ gather + posenc + direct-blend terms
-    {
-      const int r = gr, p = gp, s = gsm, k = gk;
-      const int nb = pf_nb;
-      const float4 q = pf_q;
-      const int ray = pf_ray;
-      char* xr = X0 + r * XB;
-      const int c_sin = (2 * p) ^ (r & 15), c_cos = (2 * p + 1) ^ (r & 15);
-      if (nb >= 0) {
-        const float4 a0 = recA[4 * (size_t)nb + 0];
-        const float4 a1 = recA[4 * (size_t)nb + 1];
-        const float4 a2 = recA[4 * (size_t)nb + 2];
-        const float4 a3 = recA[4 * (size_t)nb + 3];
-        const float dx = q.x - a0.x, dy = q.y - a0.y, dz = q.z - a0.z;
-        const float rc0 = (a1.x * dx + a1.y * dy) + a1.z * dz;
-        const float rc1 = (a1.w * dx + a2.x * dy) + a2.y * dz;
-        const float rc2 = (a2.z * dx + a2.w * dy) + a3.x * dz;
-        const float tn = (dx * dx + dy * dy) + dz * dz;
-        if (p == 0) {
-          sTo[r] = tn;
-        } else if (p == 1) {
-          const float4 b0 = recB[2 * (size_t)nb], b1 = recB[2 * (size_t)nb + 1];
-          float* rw = sRow + 8 * r;
-          rw[0] = expf(-(tn * tn) / a0.w);   // temporalpoints.py:461 (to_nn is already squared)
-          rw[1] = a3.y;
-          rw[2] = b0.x; rw[3] = b0.y; rw[4] = b0.z;
-          rw[5] = b1.x; rw[6] = b1.y; rw[7] = b1.z;
-        }
-        // arguments a = p + 4j = 10 i + f: rel_c[i] * 2^f (column order: pe_col_to_ref)
-        f32x4 sv0, sv1, cv0, cv1;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int aa = p + 4 * j;
-          float sv, cv;
-          if (aa < 30) {
-            const int ci = aa / 10;
-            const float v = (ci == 0 ? rc0 : (ci == 1 ? rc1 : rc2)) * (float)(1 << (aa - 10 * ci));
-            sincos_pe(v, sv, cv);
-          } else {  // j == 7 of p = 2, 3
-            sv = p == 2 ? rc0 : rc2;
-            cv = p == 2 ? rc1 : 0.f;
-          }
-          if (j < 4) { sv0[j] = sv; cv0[j] = cv; } else { sv1[j - 4] = sv; cv1[j - 4] = cv; }
-        }
-        h4 hs0, ls0, hs1, ls1, hc0, lc0, hc1, lc1;
-        split4(sv0, hs0, ls0); split4(sv1, hs1, ls1);
-        split4(cv0, hc0, lc0); split4(cv1, hc1, lc1);
-        *(h8*)(xr + (c_sin << 4)) = __builtin_shufflevector(hs0, hs1, 0, 1, 2, 3, 4, 5, 6, 7);
-        *(h8*)(xr + (c_sin << 4) + 256) = __builtin_shufflevector(ls0, ls1, 0, 1, 2, 3, 4, 5, 6, 7);
-        *(h8*)(xr + (c_cos << 4)) = __builtin_shufflevector(hc0, hc1, 0, 1, 2, 3, 4, 5, 6, 7);
-        *(h8*)(xr + (c_cos << 4) + 256) = __builtin_shufflevector(lc0, lc1, 0, 1, 2, 3, 4, 5, 6, 7);
-        {  // view embedding element e of this sample: poc_fre(viewdirs, 2^0..2^3) = [v, sin (12), cos (12)]
-          const int e = 4 * k + p;
-          float v = 0.f;
-          if (e < 27) {
-            if (vemb_const) {
-              v = vemb_const[e];
-            } else {
-              const int ee = e < 3 ? 0 : (e < 15 ? e - 3 : e - 15);
-              const int ci = e < 3 ? e : ee >> 2;
-              const float vv = viewdirs[3 * ray + ci];
-              const float arg = vv * (float)(1 << (ee & 3));
-              float sn_, cs_;
-              sincos_pe(arg, sn_, cs_);
-              v = e < 3 ? vv : (e < 15 ? sn_ : cs_);
-            }
-          }
-          sV[s * 32 + e] = v;
-        }
-      } else {
-        const h8 z = {0, 0, 0, 0, 0, 0, 0, 0};
-        *(h8*)(xr + (c_sin << 4)) = z;
-        *(h8*)(xr + (c_sin << 4) + 256) = z;
-        *(h8*)(xr + (c_cos << 4)) = z;
-        *(h8*)(xr + (c_cos << 4) + 256) = z;
-        sV[s * 32 + 4 * k + p] = 0.f;
-        if (p == 0) {
-          sTo[r] = 1.f;
-        } else if (p == 1) {
-          for (int c = 0; c < 8; ++c) sRow[8 * r + c] = 0.f;
-        }
-      }
-    }
     fetch(tile + per_xcd);
+    // ------------------------------------------------ gather + posenc + direct-blend terms
+    ws_gather(tid, nb, q, gregs, X0, sTo, sRow, sV, vemb_const);
     __syncthreads();
     APN_PHASE(0)
     // ------------------------------------------------ outputs of the previous tile
@@ -436,6 +463,11 @@ __global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
 #pragma unroll
       for (int k = 0; k < 8; ++k) sIdw[tid * 8 + k] = w[k] * inv;
     }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)   // rows past the last sample: P rows of point 0 were loaded
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        if (!pok[mt]) acc[mt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     // ------------------------------------------------ feat_net: 4 x (Linear + LeakyReLU)
     layer_mfma<2, 4, 2, PP>(X0, rs, H_W1E, ot0, H_W2, ot0, acc, a);
     if (!PP) __syncthreads();
