@@ -61,22 +61,27 @@ __device__ __forceinline__ int act_off(int m, int c) { return m * XB + ((c ^ (m 
 // Byte offset of fp32 chunk c (4 floats, 0..31) of row m of the layer-4 output.
 __device__ __forceinline__ int out32_off(int m, int c) { return m * XB + ((c ^ (m & 7)) << 4); }
 
+// hi = fp16(v) (RNE, v_cvt_pk_f16_f32); lo = fp16(v - hi) with one v_fma_mix{lo,hi}_f16 per value
+// (fma(hi as f16, -1, v as f32) rounded once to f16: v - hi is exact in fp32, so the bits equal
+// cvt(v - cvt(hi))) instead of a convert-back, a subtraction and a second convert.
+__device__ __forceinline__ uint32_t split_lo2(uint32_t hi2, float a, float b) {
+  uint32_t lo2;
+  asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %0, %1, -1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+      : "=&v"(lo2) : "v"(hi2), "v"(a), "v"(b));
+  return lo2;
+}
 __device__ __forceinline__ void split4(const f32x4& v, h4& hi, h4& lo) {
   hi = __builtin_convertvector(v, h4);
-  const f32x4 hb = __builtin_convertvector(hi, f32x4);
-  typedef float f32x2 __attribute__((ext_vector_type(2)));
-  const f32x2 d0 = f32x2{v[0], v[1]} - f32x2{hb[0], hb[1]};   // v_pk_add_f32 (neg)
-  const f32x2 d1 = f32x2{v[2], v[3]} - f32x2{hb[2], hb[3]};
-  lo = __builtin_convertvector(f32x4{d0[0], d0[1], d1[0], d1[1]}, h4);
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  const u32x2 hb = __builtin_bit_cast(u32x2, hi);
+  lo = __builtin_bit_cast(h4, (u32x2){split_lo2(hb[0], v[0], v[1]), split_lo2(hb[1], v[2], v[3])});
 }
-
-// LeakyReLU(0.01) of 4 values: max(x, 0.01x) = med3(x, 0.01x, +inf) -- one v_med3_f32 per value
-// (fmaxf adds a NaN-canonicalising v_max per operand) and the products as two v_pk_mul_f32.
+// LeakyReLU(0.01) as med3(x, 0.01x, +inf) with scalar multiplies (packed f32 VALU beside MFMAs
+// costs more than two plain ops, MI355X_MICROARCH.md constants table).
 __device__ __forceinline__ f32x4 lrelu4(const f32x4& v) {
-  typedef float f32x2 __attribute__((ext_vector_type(2)));
-  const f32x2 s0 = f32x2{v[0], v[1]} * 0.01f, s1 = f32x2{v[2], v[3]} * 0.01f;
-  return f32x4{__builtin_amdgcn_fmed3f(v[0], s0[0], INFINITY), __builtin_amdgcn_fmed3f(v[1], s0[1], INFINITY),
-               __builtin_amdgcn_fmed3f(v[2], s1[0], INFINITY), __builtin_amdgcn_fmed3f(v[3], s1[1], INFINITY)};
+  return f32x4{__builtin_amdgcn_fmed3f(v[0], v[0] * 0.01f, INFINITY), __builtin_amdgcn_fmed3f(v[1], v[1] * 0.01f, INFINITY),
+               __builtin_amdgcn_fmed3f(v[2], v[2] * 0.01f, INFINITY), __builtin_amdgcn_fmed3f(v[3], v[3] * 0.01f, INFINITY)};
 }
 
 __device__ __forceinline__ f32x4 mfma3(const h8& ahi, const h8& alo, const h8& bhi, const h8& blo, f32x4 acc) {
@@ -213,7 +218,8 @@ __device__ __forceinline__ void store_act(char* __restrict__ X, int ot0, const f
     const int c = o0 >> 3, sub = (g & 1) * 8;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
-      const f32x4 v = lrelu4(bias ? acc[mt][j] + bb : acc[mt][j]);
+      const f32x4 a = acc[mt][j];
+      const f32x4 v = lrelu4(bias ? f32x4{a[0] + bb[0], a[1] + bb[1], a[2] + bb[2], a[3] + bb[3]} : a);
       h4 hi, lo;
       split4(v, hi, lo);
       char* p = X + act_off(16 * mt + li, c) + sub;

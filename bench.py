@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -82,7 +83,7 @@ def cpu_baseline(model, scene, rows, threads):
     for k in ("rays_o", "rays_d", "viewdirs"):
         sub[k] = rk[k][sel].contiguous()
     t = torch.tensor([scene.cfg.t])
-    orc.forward(t, render_depth=True, render_kwargs=sub, render_weights=True, knn_tree=True)  # warm-up
+    ref = orc.forward(t, render_depth=True, render_kwargs=sub, render_weights=True, knn_tree=True)  # warm-up
     n_rep, t0 = 0, time.perf_counter()
     while n_rep < 2 or time.perf_counter() - t0 < 10.0:
         orc.forward(t, render_depth=True, render_kwargs=sub, render_weights=True, knn_tree=True)
@@ -93,7 +94,20 @@ def cpu_baseline(model, scene, rows, threads):
     nrays = rows * W
     return {"value": nrays / dt, "unit": "rays/s", "cores": threads, "kind": "port",
             "sample": f"{rows} evenly spaced rows x {W} = {nrays} rays of the same frame, {n_rep} timed repeats "
-                      f"(oracle: torch-CPU MLP, scipy cKDTree kNN), {dt:.2f} s/band"}
+                      f"(oracle: torch-CPU MLP, scipy cKDTree kNN), {dt:.2f} s/band"}, ref, sel
+
+
+def psnr_vs_oracle(gpu_out, ref, sel):
+    """PSNR of the GPU frame against the oracle's free-running render of the same rays (own LBS,
+    own bbox; see DESIGN.md §5 for why free-running renders are compared by PSNR)."""
+    res = {"rays": int(sel.numel())}
+    for key in ("rgb_marched", "rgb_marched_direct"):
+        a = gpu_out[key].detach().float().cpu()[sel]
+        b = ref[key].detach().float().cpu()
+        mse = float(((a - b) ** 2).mean())
+        res[key] = round(-10.0 * math.log10(max(mse, 1e-20)), 2)
+        res[key + "_frac_rays_within_1e-4"] = round(float(((a - b).abs().amax(-1) <= 1e-4).float().mean()), 5)
+    return res
 
 
 def read_traffic(path):
@@ -165,7 +179,7 @@ def main():
     host_s = 0.0
     for _ in range(args.steps):
         h0 = time.perf_counter()
-        step()
+        out = step()
         host_s += time.perf_counter() - h0
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -228,10 +242,11 @@ def main():
     traffic = read_traffic(os.path.join(ROOT, "profiles", "r01_point_mlp_traffic.json"))
     ms_per_step = elapsed / args.steps * 1e3
     value = (1 if shard_rays else world) * args.steps * R / elapsed
-    cpu = None
+    cpu = psnr = None
     if world == 1 and not args.no_cpu_baseline:
         try:
-            cpu = cpu_baseline(model, scene, args.cpu_rows, torch.get_num_threads())
+            cpu, ref, sel = cpu_baseline(model, scene, args.cpu_rows, torch.get_num_threads())
+            psnr = psnr_vs_oracle(out, ref, sel)
         except Exception as e:  # never lose the GPU line over the baseline leg
             log(f"cpu baseline failed: {e!r}")
     line = {
@@ -258,6 +273,7 @@ def main():
                      "mfma_util": executed / mfma_peak},
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
         "cpu_baseline": cpu,
+        "psnr_vs_oracle": psnr,
     }
     print(json.dumps(line), flush=True)
     if world > 1:
