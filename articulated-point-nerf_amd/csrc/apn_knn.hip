@@ -856,10 +856,10 @@ __device__ __forceinline__ void scan_ball_flat(const GridParams& g, const int* _
 // slab only enumerates the y offsets whose rows can intersect the ball under the current bound
 // (|dy| <= floor(sqrt(tau - dz^2)/h) + 1), so the square's corners and culled slabs cost no
 // iterations; no integer division per row.
-template <int K>
+template <int K, bool STATS = false>
 __device__ __forceinline__ void scan_ball_flat2(const GridParams& g, const int* __restrict__ cell_start,
                                                 const float4* __restrict__ sorted, float qx, float qy, float qz,
-                                                float R2, float (&bd)[K], int (&bi)[K]) {
+                                                float R2, float (&bd)[K], int (&bi)[K], unsigned* ctr = nullptr) {
   const float R = sqrtf(R2) * 1.0001f;
   const int z0 = max((int)floorf((qz - R - g.oz) * g.inv_h), 0), z1 = min((int)floorf((qz + R - g.oz) * g.inv_h), g.dz - 1);
   const int y0 = max((int)floorf((qy - R - g.oy) * g.inv_h), 0), y1 = min((int)floorf((qy + R - g.oy) * g.inv_h), g.dy - 1);
@@ -877,6 +877,7 @@ __device__ __forceinline__ void scan_ball_flat2(const GridParams& g, const int* 
     const bool has_pts = b < e;
     const bool rows_left = iy < nyz || iz + 1 < nz;
     if (!has_pts && !pend && !rows_left) break;
+    if (STATS) ctr[has_pts ? 1 : 0]++;
     if (has_pts) {
       const int p1 = b + 1 < e ? b + 1 : b;
       const float4 P0 = sorted[b], P1 = sorted[p1];
@@ -1080,12 +1081,14 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_a8(
 }
 
 // Pass B of mode 8: flat ball scans from the tagged first level (r/2 or r).
+template <bool STATS>
 __global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_b8(
     const float4* __restrict__ q_pos, const int* __restrict__ cand, const int* __restrict__ hard,
     const int* __restrict__ n_hard, const GridParams* __restrict__ gp, const int* __restrict__ cell_start,
     const float4* __restrict__ sorted, int* __restrict__ flag, int* __restrict__ t_nbr) {
   const int i = blockIdx.x * KNN_THREADS + threadIdx.x;
   if (i >= *n_hard) return;
+  unsigned c2[2] = {0, 0}, cr[2] = {0, 0};
   const GridParams g = *gp;
   const int hc = hard[i];
   const int c = hc >> 1;
@@ -1096,11 +1099,23 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_b8(
   for (int k = 0; k < KNN_K; ++k) { bd[k] = INFINITY; bi[k] = 0x7fffffff; }
   bool done = false;
   if ((hc & 1) == 0) {
-    scan_ball_flat2<KNN_K>(g, cell_start, sorted, q.x, q.y, q.z, 0.25f * g.r2, bd, bi);
+    scan_ball_flat2<KNN_K, STATS>(g, cell_start, sorted, q.x, q.y, q.z, 0.25f * g.r2, bd, bi, c2);
     done = bd[KNN_K - 1] < 0.25f * g.r2 * (1.f - 2e-4f);
   }
-  if (!done) scan_ball_flat2<KNN_K>(g, cell_start, sorted, q.x, q.y, q.z, g.r2, bd, bi);
+  if (!done) scan_ball_flat2<KNN_K, STATS>(g, cell_start, sorted, q.x, q.y, q.z, g.r2, bd, bi, cr);
   const bool surv = bd[KNN_K - 1] <= g.r2;
+  if (STATS) {   // per list: queries, done at r/2, survivors, r/2 row/pt iterations, r row/pt iterations,
+                 // rejected after the full r scan and their iterations
+    unsigned long long* st = g_knn_stats + 10 * (hc & 1);
+    atomicAdd(&st[0], 1ull);
+    if (done) atomicAdd(&st[1], 1ull);
+    if (surv) atomicAdd(&st[2], 1ull);
+    atomicAdd(&st[3], (unsigned long long)c2[0]);
+    atomicAdd(&st[4], (unsigned long long)c2[1]);
+    atomicAdd(&st[5], (unsigned long long)cr[0]);
+    atomicAdd(&st[6], (unsigned long long)cr[1]);
+    if (!done && !surv) { atomicAdd(&st[7], 1ull); atomicAdd(&st[8], (unsigned long long)(cr[0] + cr[1])); }
+  }
   flag[c] = surv;
   if (surv) {
     int4* nb = (int4*)(t_nbr + (int64_t)c * KNN_K);
@@ -1316,7 +1331,8 @@ extern "C" int apn_set_knn_mode(int32_t mode) {
   return prev;
 }
 
-// Profiling aid (synchronous): copies and resets the mode-3 counters (20 uint64, see g_knn_stats).
+// Profiling aid (synchronous): copies and resets the kNN counters (20 uint64, see g_knn_stats):
+// mode 3 query classes, or the mode-8 pass-B counters when APN_KNN_STATS is set.
 extern "C" int apn_debug_knn_stats(uint64_t* out20) {
   if (!out20) return APN_ERR_ARG;
   APN_HIP_TRY(hipDeviceSynchronize());
@@ -1449,9 +1465,11 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
     hipLaunchKernelGGL(k_knn_pass_a8, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, cblk_off + nb,
                        g.gp, g.cell_start, (const float4*)sorted_pts4, ccell, u1, u2, u4, flag, t_nbr, hard, n_hard,
                        hard_r, n_hard_r);
-    hipLaunchKernelGGL(k_knn_pass_b8, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard, n_hard,
+    static const bool stats = getenv("APN_KNN_STATS") != nullptr;   // profiling aid: apn_debug_knn_stats
+    auto pass_b = stats ? k_knn_pass_b8<true> : k_knn_pass_b8<false>;
+    hipLaunchKernelGGL(pass_b, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard, n_hard,
                        g.gp, g.cell_start, (const float4*)sorted_pts4, flag, t_nbr);
-    hipLaunchKernelGGL(k_knn_pass_b8, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard_r,
+    hipLaunchKernelGGL(pass_b, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard_r,
                        n_hard_r, g.gp, g.cell_start, (const float4*)sorted_pts4, flag, t_nbr);
     hipLaunchKernelGGL(k_knn_flag_count, dim3(nb), dim3(KNN_THREADS), 0, s, flag, cblk_off + nb, blk_cnt);
     st = scan_exclusive_i32(blk_cnt, blk_off, nb, sws, s);

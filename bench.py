@@ -216,6 +216,18 @@ def main():
             n = st[4 * i] or 1
             log(f"[knn {nm}] queries/frame {st[4 * i] / args.steps:.0f} cycles share {100 * st[4 * i + 1] / tot_cyc:.1f}% "
                 f"cycles/query {st[4 * i + 1] / n:.0f} rows/query {st[4 * i + 2] / n:.1f} pts/query {st[4 * i + 3] / n:.1f}")
+    if os.environ.get("APN_KNN_STATS"):   # mode-8 pass-B counters (per hard list)
+        import ctypes
+        from apn_amd import _lib
+        st = (ctypes.c_uint64 * 20)()
+        _lib.call("apn_debug_knn_stats", st)
+        n = args.steps + args.warmup
+        for lst, nm in enumerate(["from r/2", "from r"]):
+            v = st[10 * lst: 10 * lst + 9]
+            q = max(v[0], 1)
+            log(f"[knn pass B {nm}] queries/frame {v[0] / n:.0f}, done at r/2 {v[1] / q:.3f}, survive {v[2] / q:.3f}, "
+                f"r/2 scan rows+pts iters/query {v[3] / q:.1f}+{v[4] / q:.1f}, r scan {v[5] / q:.1f}+{v[6] / q:.1f}, "
+                f"rejected after full r scan {v[7] / q:.3f} ({v[8] / max(v[7], 1):.1f} iters each)")
     ev = model.timing.get("mlp_events", [])
     mlp_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / max(len(ev), 1)
     S_kept = int(ev[-1][2].item()) if ev else stats.get("kept_samples", 0)

@@ -142,7 +142,10 @@ int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t n_queries,
 int apn_set_knn_mode(int32_t mode);
 
 /* Profiling aid (synchronous): {queries, cycles, rows, points} for the mode-3 query classes
- * {stop at 2h, chord-count reject, stop at 4h, stop at r, reject at r}; resets them. */
+ * {stop at 2h, chord-count reject, stop at 4h, stop at r, reject at r}; with env APN_KNN_STATS
+ * set, mode 8 fills [10*l .. 10*l+8] per hard list l instead: {queries, done at r/2, survivors,
+ * r/2-scan row / point iterations, r-scan row / point iterations, rejected after the full r scan,
+ * their iterations}. Resets them. */
 int apn_debug_knn_stats(uint64_t* out20);
 
 /* mean_min_distance support (temporalpoints.py:104-111): per-point sqrt(d2_nn + eps) to the
