@@ -253,7 +253,9 @@ class TemporalPoints(torch.nn.Module):
     def repose(self, rot_params):
         """temporalpoints.py:370-371 -> [xyz (N,3), joints_rel (J,3)] via the fused LBS kernel."""
         bone_Ts, global_t, joints_rel = self.forward_warp.pose(self.joints, rot_params=rot_params)
+        self._mark("frame")
         xyz, _, _ = self._lbs(bone_Ts, global_t, records=False, T34=self.forward_warp.last_T34)
+        self._mark("lbs")
         return [xyz, joints_rel]
 
     def sample_ray(self, rays_o, rays_d, near, far, stepsize, xyz_min=None, xyz_max=None, **render_kwargs):

@@ -110,6 +110,77 @@ def psnr_vs_oracle(gpu_out, ref, sel):
     return res
 
 
+def lbs_sweep(args, rank, world, dev):
+    """C5: LBS-only repose throughput (BASELINE.json configs[4]; run.py:1364-1377 sweep). One step
+    = one pose of the sweep through TemporalPoints.repose (skeleton + fused LBS, 1M points, 48
+    bones); every rank sweeps its own poses (weak scaling). Roofline: k_lbs_skin against HBM with
+    B_alg = N*(24 + 4J) bytes per pose."""
+    scene = S.make_scene(args.config)
+    model = harness.build_model(scene, dev)
+    N, J = scene.cfg.N, scene.cfg.J
+    poses = S.repose_sweep(J).to(dev)
+    poses = poses.roll(rank, 0)
+    for i in range(args.warmup):
+        model.repose(poses[i % len(poses)])
+    model.timing = {}
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        model.repose(poses[i % len(poses)])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t)
+    marks = model.timing.get("marks", [])
+    lbs_ms = sum(a.elapsed_time(b) for (_, a), (nm, b) in zip(marks[:-1], marks[1:]) if nm == "lbs") / args.steps
+    model.timing = None
+    if rank != 0:
+        return
+    b_alg = N * (24 + 4 * J)
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        try:
+            from oracle.apn_oracle import OracleModel
+            torch.set_num_threads(torch.get_num_threads())
+            st = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+            orc = OracleModel(st, model.canonical_pcd.cpu(), model.bones, mean_min_distance_value=0.0)
+            pc = poses.cpu()
+            orc.repose(pc[0])
+            n_rep, c0 = 0, time.perf_counter()
+            while n_rep < 2 or (time.perf_counter() - c0 < 10.0 and n_rep < 8):
+                orc.repose(pc[n_rep % len(pc)])
+                n_rep += 1
+            dt = (time.perf_counter() - c0) / n_rep
+            cpu = {"value": N / dt, "unit": "points/s", "cores": torch.get_num_threads(), "kind": "port",
+                   "sample": f"{n_rep} poses of the same sweep, full 1M-point cloud (oracle: torch-CPU get_weights + "
+                             f"LBS), {dt:.2f} s/pose"}
+        except Exception as e:  # never lose the GPU line over the baseline leg
+            log(f"cpu baseline failed: {e!r}")
+    value = world * args.steps * N / elapsed
+    line = {
+        "metric": "LBS-only repose throughput, 1M pts, 48 bones (points/s)",
+        "value": value, "unit": "points/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "fp32", "data": "synthetic (procedural 48-joint capsule cloud, repose sweep)",
+        "config": {"workload": S.CONFIGS[args.config].name + f" ({args.config})", "points": N, "bones": J,
+                   "poses_per_s": world * args.steps / elapsed, "parallelism": f"poses x{world}" if world > 1 else "single"},
+        "roofline": {"bound": "hbm", "kernel": "k_lbs_skin", "achieved": b_alg / (lbs_ms * 1e-3) / 1e9 if lbs_ms > 0 else 0.0,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": b_alg / (lbs_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if lbs_ms > 0 else 0.0,
+                     "traffic": None, "bytes_per_launch": b_alg, "avg_launch_ms": lbs_ms,
+                     "note": "achieved = B_alg = N*(24+4J) bytes per pose (SURVEY.md 8(d) C5) / avg k_lbs_skin time "
+                             "(HIP events on the launch stream); the step also runs the skeleton kernel"},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+
+
 def read_traffic(path):
     try:
         with open(path) as f:
@@ -143,6 +214,11 @@ def main():
         dist.init_process_group(os.environ.get("APN_DIST_BACKEND", "nccl"))   # nccl = RCCL over xGMI
     dev = torch.device("cuda", local)
 
+    if args.config == "C5":
+        lbs_sweep(args, rank, world, dev)
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
     scene = S.make_scene(args.config)
     shard_rays = args.shard == "rays" and world > 1
     if not shard_rays:  # weak scaling: every rank renders its own frame time

@@ -121,3 +121,19 @@ def test_get_rays_matches_synthetic_rays():
     ro, rd, vd = get_rays_of_a_view(sc.cfg.H, sc.cfg.W, sc.K, sc.c2w, inverse_y=True)
     ro2, rd2, vd2 = sc.rays()
     assert torch.equal(rd.reshape(-1, 3), rd2) and torch.equal(vd.reshape(-1, 3), vd2)
+
+
+def test_bench_psnr_and_flop_accounting():
+    """bench.py host logic: PSNR of identical renders is capped (not inf), a known MSE maps to
+    its PSNR, and F_alg per kept sample is SURVEY.md 8(d)'s 1 230 848 / 1 361 920 flop."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    assert bench.flop_per_kept_sample(191) == 1_230_848
+    assert bench.flop_per_kept_sample(255) == 1_361_920
+    sel = torch.arange(4)
+    a = {"rgb_marched": torch.full((6, 3), 0.5), "rgb_marched_direct": torch.full((6, 3), 0.5)}
+    b = {"rgb_marched": torch.full((4, 3), 0.5), "rgb_marched_direct": torch.full((4, 3), 0.6)}
+    r = bench.psnr_vs_oracle(a, b, sel)
+    assert r["rgb_marched"] == 200.0 and r["rgb_marched_frac_rays_within_1e-4"] == 1.0
+    assert abs(r["rgb_marched_direct"] - 20.0) < 1e-3 and r["rgb_marched_direct_frac_rays_within_1e-4"] == 0.0
