@@ -13,10 +13,90 @@
 // HBM-bound: per point it reads 12 + 4J + 4 + 12 + 4 bytes and writes 12 + 4J + 96 bytes.
 #include "apn_common.h"
 
+#include <algorithm>
+
 namespace apn {
 
 constexpr int LBS_THREADS = 256;
 constexpr int LBS_MAX_J = 64;
+#ifndef QUAD_WAVES_PER_EU
+#define QUAD_WAVES_PER_EU 4
+#endif
+
+// Per-point tail shared by the LBS kernels: x' = G [x;1] + global_t, optional G (get_frames),
+// records (adjugate inverse of the blended 3x3, direct-render sigma, clipped colours); bbox seed.
+__device__ __forceinline__ void lbs_finish(int64_t n, const float (&G)[12], float sw, double pc0, double pc1, double pc2,
+                                           const float* __restrict__ pcd, const float* __restrict__ global_t, float mmd,
+                                           const float* __restrict__ direct_eps, const float* __restrict__ alpha_c,
+                                           const float* __restrict__ rgb_c, float* __restrict__ xyz_out,
+                                           float* __restrict__ G_out, float4* __restrict__ recA,
+                                           float4* __restrict__ recB, float (&bmin)[3], float (&bmax)[3]) {
+  if (G_out) {  // weighted_G_tw (pointwarper.py:243): rows 0..2 blended, row 3 = sum_j w_j [0,0,0,1]
+    float4* go = (float4*)(G_out + 16 * n);
+    go[0] = make_float4(G[0], G[1], G[2], G[3]);
+    go[1] = make_float4(G[4], G[5], G[6], G[7]);
+    go[2] = make_float4(G[8], G[9], G[10], G[11]);
+    go[3] = make_float4(0.f, 0.f, 0.f, sw);
+  }
+  const float px = pcd[3 * n], py = pcd[3 * n + 1], pz = pcd[3 * n + 2];
+  float x = ((G[0] * px + G[1] * py) + G[2] * pz) + G[3];
+  float y = ((G[4] * px + G[5] * py) + G[6] * pz) + G[7];
+  float z = ((G[8] * px + G[9] * py) + G[10] * pz) + G[11];
+  x = x + global_t[0]; y = y + global_t[1]; z = z + global_t[2];
+  xyz_out[3 * n] = x; xyz_out[3 * n + 1] = y; xyz_out[3 * n + 2] = z;
+  bmin[0] = bmax[0] = x; bmin[1] = bmax[1] = y; bmin[2] = bmax[2] = z;
+  if (recA) {
+    // inverse of the blended 3x3 (adjugate / det)
+    const float a00 = G[0], a01 = G[1], a02 = G[2], a10 = G[4], a11 = G[5], a12 = G[6];
+    const float a20 = G[8], a21 = G[9], a22 = G[10];
+    const float c00 = a11 * a22 - a12 * a21, c01 = a02 * a21 - a01 * a22, c02 = a01 * a12 - a02 * a11;
+    const float c10 = a12 * a20 - a10 * a22, c11 = a00 * a22 - a02 * a20, c12 = a02 * a10 - a00 * a12;
+    const float c20 = a10 * a21 - a11 * a20, c21 = a01 * a20 - a00 * a21, c22 = a00 * a11 - a01 * a10;
+    const float det = (a00 * c00 + a01 * c10) + a02 * c20;
+    const float id = 1.f / det;
+    const float sig = mmd * fmaxf(direct_eps[n], 0.f);
+    const float den = 2.f * (sig * sig) + 1e-12f;
+    const float ac = fminf(fmaxf(alpha_c[n], 0.f), 1.f);
+    recA[4 * n + 0] = make_float4(x, y, z, den);
+    recA[4 * n + 1] = make_float4(c00 * id, c01 * id, c02 * id, c10 * id);
+    recA[4 * n + 2] = make_float4(c11 * id, c12 * id, c20 * id, c21 * id);
+    recA[4 * n + 3] = make_float4(c22 * id, ac, 0.f, 0.f);
+    const float r = fminf(fmaxf(rgb_c[3 * n], 0.f), 1.f);
+    const float g = fminf(fmaxf(rgb_c[3 * n + 1], 0.f), 1.f);
+    const float b = fminf(fmaxf(rgb_c[3 * n + 2], 0.f), 1.f);
+    recB[2 * n + 0] = make_float4(r, g, b, 0.f);
+    recB[2 * n + 1] = make_float4((float)pc0, (float)pc1, (float)pc2, 0.f);
+  }  // recA
+}
+
+// bbox: wave reduce, then across the block's waves; one partial per block, reduced by
+// k_bbox_reduce (all blocks hitting 6 global atomics serialised at one L2 channel and cost
+// ~0.3 ms at 300k points)
+__device__ __forceinline__ void lbs_bbox_partial(const float (&bmin)[3], const float (&bmax)[3],
+                                                 int* __restrict__ bbox_part) {
+  const int tid = threadIdx.x;
+  __shared__ float sbb[LBS_THREADS / 64][6];
+  const int lane = tid & 63, wid = tid >> 6;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    float lo = bmin[a], hi = bmax[a];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      lo = fminf(lo, __shfl_xor(lo, o, 64));
+      hi = fmaxf(hi, __shfl_xor(hi, o, 64));
+    }
+    if (lane == 0) {
+      sbb[wid][a] = lo;
+      sbb[wid][3 + a] = hi;
+    }
+  }
+  __syncthreads();
+  if (tid < 6) {
+    float v = sbb[0][tid];
+    for (int w = 1; w < LBS_THREADS / 64; ++w) v = tid < 3 ? fminf(v, sbb[w][tid]) : fmaxf(v, sbb[w][tid]);
+    bbox_part[6 * blockIdx.x + tid] = float_to_ordered(v);
+  }
+}
 
 __global__ __launch_bounds__(LBS_THREADS) void k_lbs_skin(
     const float* __restrict__ pcd, const float* __restrict__ W, int64_t N, int J,
@@ -94,44 +174,11 @@ __global__ __launch_bounds__(LBS_THREADS) void k_lbs_skin(
       pc1 += (double)sC[3 * j + 1] * (double)w;
       pc2 += (double)sC[3 * j + 2] * (double)w;
     }
-    if (G_out) {  // weighted_G_tw (pointwarper.py:243): rows 0..2 blended, row 3 = sum_j w_j [0,0,0,1]
-      float sw = 0.f;
+    float sw = 0.f;
+    if (G_out)
       for (int j = 0; j < J; ++j) sw = sw + row[j];
-      float4* go = (float4*)(G_out + 16 * n);
-      go[0] = make_float4(G[0], G[1], G[2], G[3]);
-      go[1] = make_float4(G[4], G[5], G[6], G[7]);
-      go[2] = make_float4(G[8], G[9], G[10], G[11]);
-      go[3] = make_float4(0.f, 0.f, 0.f, sw);
-    }
-    const float px = pcd[3 * n], py = pcd[3 * n + 1], pz = pcd[3 * n + 2];
-    float x = ((G[0] * px + G[1] * py) + G[2] * pz) + G[3];
-    float y = ((G[4] * px + G[5] * py) + G[6] * pz) + G[7];
-    float z = ((G[8] * px + G[9] * py) + G[10] * pz) + G[11];
-    x = x + global_t[0]; y = y + global_t[1]; z = z + global_t[2];
-    xyz_out[3 * n] = x; xyz_out[3 * n + 1] = y; xyz_out[3 * n + 2] = z;
-    bmin[0] = bmax[0] = x; bmin[1] = bmax[1] = y; bmin[2] = bmax[2] = z;
-    if (recA) {
-    // inverse of the blended 3x3 (adjugate / det)
-    const float a00 = G[0], a01 = G[1], a02 = G[2], a10 = G[4], a11 = G[5], a12 = G[6];
-    const float a20 = G[8], a21 = G[9], a22 = G[10];
-    const float c00 = a11 * a22 - a12 * a21, c01 = a02 * a21 - a01 * a22, c02 = a01 * a12 - a02 * a11;
-    const float c10 = a12 * a20 - a10 * a22, c11 = a00 * a22 - a02 * a20, c12 = a02 * a10 - a00 * a12;
-    const float c20 = a10 * a21 - a11 * a20, c21 = a01 * a20 - a00 * a21, c22 = a00 * a11 - a01 * a10;
-    const float det = (a00 * c00 + a01 * c10) + a02 * c20;
-    const float id = 1.f / det;
-    const float sig = mmd * fmaxf(direct_eps[n], 0.f);
-    const float den = 2.f * (sig * sig) + 1e-12f;
-    const float ac = fminf(fmaxf(alpha_c[n], 0.f), 1.f);
-    recA[4 * n + 0] = make_float4(x, y, z, den);
-    recA[4 * n + 1] = make_float4(c00 * id, c01 * id, c02 * id, c10 * id);
-    recA[4 * n + 2] = make_float4(c11 * id, c12 * id, c20 * id, c21 * id);
-    recA[4 * n + 3] = make_float4(c22 * id, ac, 0.f, 0.f);
-    const float r = fminf(fmaxf(rgb_c[3 * n], 0.f), 1.f);
-    const float g = fminf(fmaxf(rgb_c[3 * n + 1], 0.f), 1.f);
-    const float b = fminf(fmaxf(rgb_c[3 * n + 2], 0.f), 1.f);
-    recB[2 * n + 0] = make_float4(r, g, b, 0.f);
-    recB[2 * n + 1] = make_float4((float)pc0, (float)pc1, (float)pc2, 0.f);
-    }  // recA
+    lbs_finish(n, G, sw, pc0, pc1, pc2, pcd, global_t, mmd, direct_eps, alpha_c, rgb_c, xyz_out, G_out, recA, recB,
+               bmin, bmax);
   }
   __syncthreads();
   if (w_out) {
@@ -141,32 +188,7 @@ __global__ __launch_bounds__(LBS_THREADS) void k_lbs_skin(
       Wo[e] = sW[r * Jp + c];
     }
   }
-  // bbox: wave reduce, then across the block's waves; one partial per block, reduced by
-  // k_bbox_reduce (all blocks hitting 6 global atomics serialised at one L2 channel and cost
-  // ~0.3 ms at 300k points)
-  if (bbox_part) {
-    __shared__ float sbb[LBS_THREADS / 64][6];
-    const int lane = tid & 63, wid = tid >> 6;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      float lo = bmin[a], hi = bmax[a];
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        lo = fminf(lo, __shfl_xor(lo, o, 64));
-        hi = fmaxf(hi, __shfl_xor(hi, o, 64));
-      }
-      if (lane == 0) {
-        sbb[wid][a] = lo;
-        sbb[wid][3 + a] = hi;
-      }
-    }
-    __syncthreads();
-    if (tid < 6) {
-      float v = sbb[0][tid];
-      for (int w = 1; w < LBS_THREADS / 64; ++w) v = tid < 3 ? fminf(v, sbb[w][tid]) : fmaxf(v, sbb[w][tid]);
-      bbox_part[6 * blockIdx.x + tid] = float_to_ordered(v);
-    }
-  }
+  if (bbox_part) lbs_bbox_partial(bmin, bmax, bbox_part);
 }
 
 // Per-block bbox partials -> bbox_ord[6] (one workgroup, deterministic).
@@ -192,7 +214,158 @@ __global__ __launch_bounds__(256) void k_bbox_reduce(const int* __restrict__ par
 using namespace apn;
 
 extern "C" size_t apn_lbs_workspace_bytes(int64_t n_points) {
-  return n_points > 0 ? (size_t)ceil_div(n_points, LBS_THREADS) * 6 * sizeof(int) : 0;
+  // one bbox partial per block; the quad kernel runs LBS_THREADS / 4 points per block
+  return n_points > 0 ? (size_t)ceil_div(n_points, LBS_THREADS / 4) * 6 * sizeof(int) : 0;
+}
+
+// Quad variant (identity merge rules, J % 4 == 0): four lanes share a point, each holding JL = J/4
+// consecutive weights in registers -- a point's 4J-byte row is read by its quad as one contiguous
+// run (16/8-B loads), there is no LDS weight tile (which capped the LDS kernel at 3 blocks per CU
+// at J = 48) and no staging barrier. Softmax max / sum and the blended G are combined across the
+// quad with xor shuffles ((q0 + q1) + (q2 + q3): sums regrouped by quarter, ~1 ulp from the
+// sequential order of k_lbs_skin); lane 0 of the quad runs the per-point tail.
+// xor-1 / xor-2 lane exchange inside a quad as DPP quad_perm moves (no LDS crossbar)
+template <int CTRL>
+__device__ __forceinline__ float quad_swap(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+template <int CTRL>
+__device__ __forceinline__ double quad_swap(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffff), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, true);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+constexpr int QX1 = 0xB1, QX2 = 0x4E;   // quad_perm [1,0,3,2] and [2,3,0,1]
+
+template <int JL>
+__device__ __forceinline__ void quad_load_row(const float* __restrict__ src, float (&row)[JL]) {
+  if constexpr (JL % 4 == 0) {
+#pragma unroll
+    for (int q = 0; q < JL / 4; ++q) {
+      const float4 v = ((const float4*)src)[q];
+      row[4 * q] = v.x; row[4 * q + 1] = v.y; row[4 * q + 2] = v.z; row[4 * q + 3] = v.w;
+    }
+  } else if constexpr (JL % 2 == 0) {
+#pragma unroll
+    for (int q = 0; q < JL / 2; ++q) {
+      const float2 v = ((const float2*)src)[q];
+      row[2 * q] = v.x; row[2 * q + 1] = v.y;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < JL; ++q) row[q] = src[q];
+  }
+}
+
+template <int JL, bool REC>
+__global__ __launch_bounds__(LBS_THREADS) __attribute__((amdgpu_waves_per_eu(QUAD_WAVES_PER_EU)))
+void k_lbs_skin_quad(
+    const float* __restrict__ pcd, const float* __restrict__ W, int64_t N, const float* __restrict__ theta_weight,
+    float eps, const float* __restrict__ boneT12, const float* __restrict__ global_t,
+    const float* __restrict__ colors, const float* __restrict__ alpha_c, const float* __restrict__ rgb_c,
+    const float* __restrict__ direct_eps, float mmd, int weights_final, float* __restrict__ xyz_out,
+    float* __restrict__ w_out, float* __restrict__ G_out, float4* __restrict__ recA, float4* __restrict__ recB,
+    int* __restrict__ bbox_part) {
+  constexpr int J = 4 * JL;
+  constexpr int PPB = LBS_THREADS / 4;   // points per block step
+  __shared__ __attribute__((aligned(16))) float sT[J * 12];
+  __shared__ float sC[J * 3];
+  const int tid = threadIdx.x, sub = tid & 3;
+  for (int e = tid; e < J * 12; e += LBS_THREADS) sT[e] = boneT12[e];
+  for (int e = tid; e < J * 3; e += LBS_THREADS) sC[e] = colors ? colors[e] : 0.f;
+  const float th = weights_final ? 1.f : fmaxf(eps, theta_weight[0]);
+  const int64_t stride = (int64_t)gridDim.x * PPB;
+  int64_t n = (int64_t)blockIdx.x * PPB + (tid >> 2);
+  // the next row is in flight while the current one is processed (grid-stride, one step ahead)
+  float nrow[JL];
+  quad_load_row<JL>(W + min(n, N - 1) * J + sub * JL, nrow);
+  __syncthreads();
+  float bmin[3] = {INFINITY, INFINITY, INFINITY}, bmax[3] = {-INFINITY, -INFINITY, -INFINITY};
+  const int64_t n_end = (N + PPB - 1) / PPB * PPB;   // every lane of a quad runs the same trips
+  for (; n < n_end; n += stride) {
+    const bool valid = n < N;
+    float row[JL];
+#pragma unroll
+    for (int j = 0; j < JL; ++j) row[j] = nrow[j];
+    quad_load_row<JL>(W + min(n + stride, N - 1) * J + sub * JL, nrow);
+    if (!weights_final) {   // softmax(W / th) over J (temporalpoints.py:403)
+      float m = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < JL; ++j) {
+        row[j] = row[j] / th;
+        m = fmaxf(m, row[j]);
+        if (j & 1) __builtin_amdgcn_sched_barrier(0);
+      }
+      m = fmaxf(m, quad_swap<QX1>(m));
+      m = fmaxf(m, quad_swap<QX2>(m));
+      float sum = 0.f;
+#pragma unroll
+      for (int j = 0; j < JL; ++j) {
+        row[j] = expf(row[j] - m);
+        sum += row[j];
+        if (j & 1) __builtin_amdgcn_sched_barrier(0);
+      }
+      sum += quad_swap<QX1>(sum);
+      sum += quad_swap<QX2>(sum);
+      const float inv = 1.f / sum;
+#pragma unroll
+      for (int j = 0; j < JL; ++j) row[j] = row[j] * inv;
+    }
+    float G[12];
+#pragma unroll
+    for (int e = 0; e < 12; ++e) G[e] = 0.f;
+#pragma unroll
+    for (int j = 0; j < JL; ++j) {
+      const float4* T4 = (const float4*)(sT + 12 * (sub * JL + j));
+      const float4 t0 = T4[0], t1 = T4[1], t2 = T4[2];
+      const float T[12] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w, t2.x, t2.y, t2.z, t2.w};
+#pragma unroll
+      for (int e = 0; e < 12; ++e) G[e] = G[e] + row[j] * T[e];
+      __builtin_amdgcn_sched_barrier(0);   // one joint's bone row live at a time
+    }
+#pragma unroll
+    for (int e = 0; e < 12; ++e) {
+      G[e] += quad_swap<QX1>(G[e]);
+      G[e] += quad_swap<QX2>(G[e]);
+    }
+    double pc0 = 0.0, pc1 = 0.0, pc2 = 0.0;
+    if (colors) {
+#pragma unroll
+      for (int j = 0; j < JL; ++j) {
+        const float* c = sC + 3 * (sub * JL + j);
+        pc0 += (double)c[0] * (double)row[j];
+        pc1 += (double)c[1] * (double)row[j];
+        pc2 += (double)c[2] * (double)row[j];
+      }
+      pc0 += quad_swap<QX1>(pc0); pc0 += quad_swap<QX2>(pc0);
+      pc1 += quad_swap<QX1>(pc1); pc1 += quad_swap<QX2>(pc1);
+      pc2 += quad_swap<QX1>(pc2); pc2 += quad_swap<QX2>(pc2);
+    }
+    float sw = 0.f;
+    if (G_out) {
+#pragma unroll
+      for (int j = 0; j < JL; ++j) sw = sw + row[j];
+      sw += quad_swap<QX1>(sw);
+      sw += quad_swap<QX2>(sw);
+    }
+    if (w_out && valid) {
+      float* dst = w_out + n * J + sub * JL;
+#pragma unroll
+      for (int j = 0; j < JL; ++j) dst[j] = row[j];
+    }
+    if (valid && sub == 0) {
+      float lo[3], hi[3];
+      lbs_finish(n, G, sw, pc0, pc1, pc2, pcd, global_t, mmd, direct_eps, alpha_c, rgb_c, xyz_out, G_out,
+                 REC ? recA : nullptr, REC ? recB : nullptr, lo, hi);
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        bmin[a] = fminf(bmin[a], lo[a]);
+        bmax[a] = fmaxf(bmax[a], hi[a]);
+      }
+    }
+  }
+  if (bbox_part) lbs_bbox_partial(bmin, bmax, bbox_part);
 }
 
 extern "C" int apn_lbs_skin(const float* canonical_pcd, const float* raw_weights, int64_t n_points, int32_t n_joints,
@@ -211,6 +384,43 @@ extern "C" int apn_lbs_skin(const float* canonical_pcd, const float* raw_weights
   const int J = n_joints;
   const int nblocks = ceil_div(n_points, LBS_THREADS);
   int* part = bbox_ord ? (int*)workspace : nullptr;
+  // quad kernel for identity merge rules and J % 4 == 0 (APN_LBS_LDS selects the LDS-tile kernel)
+  static const bool quad_ok = getenv("APN_LBS_LDS") == nullptr;
+  if (quad_ok && !merge_rules && J % 4 == 0 && ((uintptr_t)raw_weights % 16) == 0) {
+    // persistent grid (each block strides over point groups, one row ahead); <= 1 partial per block
+    static const int per_cu = [] {
+      const char* e = getenv("APN_LBS_BLOCKS_PER_CU");
+      return e ? atoi(e) : 4;
+    }();
+    const int qblocks = (int)std::min<int64_t>(ceil_div(n_points, LBS_THREADS / 4), 256 * per_cu);
+    auto quad = [&](auto kern_rec, auto kern_norec) {
+      auto kern = recA16 ? kern_rec : kern_norec;
+      hipLaunchKernelGGL(kern, dim3(qblocks), dim3(LBS_THREADS), 0, s, canonical_pcd, raw_weights, n_points,
+                         theta_weight, eps, bone_T34, global_t, joint_colors, canonical_alpha, canonical_rgbs,
+                         direct_eps, mean_min_distance, weights_final, xyz_out, weights_out, G_out, (float4*)recA16,
+                         (float4*)recB8, part);
+    };
+    switch (J / 4) {
+      case 1: quad(k_lbs_skin_quad<1, true>, k_lbs_skin_quad<1, false>); break;
+      case 2: quad(k_lbs_skin_quad<2, true>, k_lbs_skin_quad<2, false>); break;
+      case 3: quad(k_lbs_skin_quad<3, true>, k_lbs_skin_quad<3, false>); break;
+      case 4: quad(k_lbs_skin_quad<4, true>, k_lbs_skin_quad<4, false>); break;
+      case 5: quad(k_lbs_skin_quad<5, true>, k_lbs_skin_quad<5, false>); break;
+      case 6: quad(k_lbs_skin_quad<6, true>, k_lbs_skin_quad<6, false>); break;
+      case 7: quad(k_lbs_skin_quad<7, true>, k_lbs_skin_quad<7, false>); break;
+      case 8: quad(k_lbs_skin_quad<8, true>, k_lbs_skin_quad<8, false>); break;
+      case 9: quad(k_lbs_skin_quad<9, true>, k_lbs_skin_quad<9, false>); break;
+      case 10: quad(k_lbs_skin_quad<10, true>, k_lbs_skin_quad<10, false>); break;
+      case 11: quad(k_lbs_skin_quad<11, true>, k_lbs_skin_quad<11, false>); break;
+      case 12: quad(k_lbs_skin_quad<12, true>, k_lbs_skin_quad<12, false>); break;
+      case 13: quad(k_lbs_skin_quad<13, true>, k_lbs_skin_quad<13, false>); break;
+      case 14: quad(k_lbs_skin_quad<14, true>, k_lbs_skin_quad<14, false>); break;
+      case 15: quad(k_lbs_skin_quad<15, true>, k_lbs_skin_quad<15, false>); break;
+      default: quad(k_lbs_skin_quad<16, true>, k_lbs_skin_quad<16, false>); break;
+    }
+    if (bbox_ord) hipLaunchKernelGGL(k_bbox_reduce, dim3(1), dim3(256), 0, s, part, qblocks, bbox_ord);
+    return launch_status();
+  }
   size_t lds = (size_t)(LBS_THREADS * (J + 1) + J * 12 + J * 3) * sizeof(float) + J * sizeof(int);
   hipLaunchKernelGGL(k_lbs_skin, dim3(nblocks), dim3(LBS_THREADS), lds, s, canonical_pcd, raw_weights, n_points, J,
                      theta_weight, eps, merge_rules, bone_T34, global_t, joint_colors, canonical_alpha, canonical_rgbs,

@@ -60,7 +60,7 @@ def test_invalid_arguments_rejected_without_gpu():
                              None) == 1  # feat_dim != 128
     assert lib.apn_lbs_skin(None, None, 0, 0, None, 0.0, None, None, None, None, None, None, None, 0.0, 0,
                             None, None, None, None, None, None, None, None) == 1
-    assert lib.apn_lbs_workspace_bytes(300_000) == 6 * 4 * ((300_000 + 255) // 256)
+    assert lib.apn_lbs_workspace_bytes(300_000) == 6 * 4 * ((300_000 + 63) // 64)   # one partial per 64-point block
 
 
 def test_missing_library_fails_loudly(monkeypatch):
