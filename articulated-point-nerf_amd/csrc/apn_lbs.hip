@@ -218,12 +218,6 @@ extern "C" size_t apn_lbs_workspace_bytes(int64_t n_points) {
   return n_points > 0 ? (size_t)ceil_div(n_points, LBS_THREADS / 4) * 6 * sizeof(int) : 0;
 }
 
-// Quad variant (identity merge rules, J % 4 == 0): four lanes share a point, each holding JL = J/4
-// consecutive weights in registers -- a point's 4J-byte row is read by its quad as one contiguous
-// run (16/8-B loads), there is no LDS weight tile (which capped the LDS kernel at 3 blocks per CU
-// at J = 48) and no staging barrier. Softmax max / sum and the blended G are combined across the
-// quad with xor shuffles ((q0 + q1) + (q2 + q3): sums regrouped by quarter, ~1 ulp from the
-// sequential order of k_lbs_skin); lane 0 of the quad runs the per-point tail.
 // xor-1 / xor-2 lane exchange inside a quad as DPP quad_perm moves (no LDS crossbar)
 template <int CTRL>
 __device__ __forceinline__ float quad_swap(float v) {
@@ -258,7 +252,13 @@ __device__ __forceinline__ void quad_load_row(const float* __restrict__ src, flo
   }
 }
 
-template <int JL, bool REC>
+// Quad variant (record-free calls, identity merge rules, J % 4 == 0): four lanes share a point,
+// each holding JL = J/4 consecutive weights in registers -- a point's 4J-byte row is read by its
+// quad as one contiguous run (16/8-B loads), there is no LDS weight tile (which capped the LDS
+// kernel at 3 blocks per CU at J = 48) and no staging barrier. Softmax max / sum and the blended G
+// are combined across the quad with DPP moves ((q0 + q1) + (q2 + q3): sums regrouped by quarter,
+// ~1 ulp from the sequential order of k_lbs_skin); lane 0 of the quad runs the per-point tail.
+template <int JL>
 __global__ __launch_bounds__(LBS_THREADS) __attribute__((amdgpu_waves_per_eu(QUAD_WAVES_PER_EU)))
 void k_lbs_skin_quad(
     const float* __restrict__ pcd, const float* __restrict__ W, int64_t N, const float* __restrict__ theta_weight,
@@ -356,8 +356,8 @@ void k_lbs_skin_quad(
     }
     if (valid && sub == 0) {
       float lo[3], hi[3];
-      lbs_finish(n, G, sw, pc0, pc1, pc2, pcd, global_t, mmd, direct_eps, alpha_c, rgb_c, xyz_out, G_out,
-                 REC ? recA : nullptr, REC ? recB : nullptr, lo, hi);
+      lbs_finish(n, G, sw, pc0, pc1, pc2, pcd, global_t, mmd, direct_eps, alpha_c, rgb_c, xyz_out, G_out, nullptr,
+                 nullptr, lo, hi);
 #pragma unroll
       for (int a = 0; a < 3; ++a) {
         bmin[a] = fminf(bmin[a], lo[a]);
@@ -384,39 +384,41 @@ extern "C" int apn_lbs_skin(const float* canonical_pcd, const float* raw_weights
   const int J = n_joints;
   const int nblocks = ceil_div(n_points, LBS_THREADS);
   int* part = bbox_ord ? (int*)workspace : nullptr;
-  // quad kernel for identity merge rules and J % 4 == 0 (APN_LBS_LDS selects the LDS-tile kernel)
+  // quad kernel for the record-free calls (repose, LBS-only sweeps) with identity merge rules and
+  // J % 4 == 0 (APN_LBS_LDS selects the LDS-tile kernel). The render path keeps k_lbs_skin: its
+  // sequential sums reproduce the oracle's skinned cloud bit for bit, and the sampling bbox --
+  // hence every sample position -- follows that cloud (bbox sensitivity).
   static const bool quad_ok = getenv("APN_LBS_LDS") == nullptr;
-  if (quad_ok && !merge_rules && J % 4 == 0 && ((uintptr_t)raw_weights % 16) == 0) {
+  if (quad_ok && !recA16 && !merge_rules && J % 4 == 0 && ((uintptr_t)raw_weights % 16) == 0) {
     // persistent grid (each block strides over point groups, one row ahead); <= 1 partial per block
     static const int per_cu = [] {
       const char* e = getenv("APN_LBS_BLOCKS_PER_CU");
       return e ? atoi(e) : 4;
     }();
     const int qblocks = (int)std::min<int64_t>(ceil_div(n_points, LBS_THREADS / 4), 256 * per_cu);
-    auto quad = [&](auto kern_rec, auto kern_norec) {
-      auto kern = recA16 ? kern_rec : kern_norec;
+    auto quad = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3(qblocks), dim3(LBS_THREADS), 0, s, canonical_pcd, raw_weights, n_points,
                          theta_weight, eps, bone_T34, global_t, joint_colors, canonical_alpha, canonical_rgbs,
                          direct_eps, mean_min_distance, weights_final, xyz_out, weights_out, G_out, (float4*)recA16,
                          (float4*)recB8, part);
     };
     switch (J / 4) {
-      case 1: quad(k_lbs_skin_quad<1, true>, k_lbs_skin_quad<1, false>); break;
-      case 2: quad(k_lbs_skin_quad<2, true>, k_lbs_skin_quad<2, false>); break;
-      case 3: quad(k_lbs_skin_quad<3, true>, k_lbs_skin_quad<3, false>); break;
-      case 4: quad(k_lbs_skin_quad<4, true>, k_lbs_skin_quad<4, false>); break;
-      case 5: quad(k_lbs_skin_quad<5, true>, k_lbs_skin_quad<5, false>); break;
-      case 6: quad(k_lbs_skin_quad<6, true>, k_lbs_skin_quad<6, false>); break;
-      case 7: quad(k_lbs_skin_quad<7, true>, k_lbs_skin_quad<7, false>); break;
-      case 8: quad(k_lbs_skin_quad<8, true>, k_lbs_skin_quad<8, false>); break;
-      case 9: quad(k_lbs_skin_quad<9, true>, k_lbs_skin_quad<9, false>); break;
-      case 10: quad(k_lbs_skin_quad<10, true>, k_lbs_skin_quad<10, false>); break;
-      case 11: quad(k_lbs_skin_quad<11, true>, k_lbs_skin_quad<11, false>); break;
-      case 12: quad(k_lbs_skin_quad<12, true>, k_lbs_skin_quad<12, false>); break;
-      case 13: quad(k_lbs_skin_quad<13, true>, k_lbs_skin_quad<13, false>); break;
-      case 14: quad(k_lbs_skin_quad<14, true>, k_lbs_skin_quad<14, false>); break;
-      case 15: quad(k_lbs_skin_quad<15, true>, k_lbs_skin_quad<15, false>); break;
-      default: quad(k_lbs_skin_quad<16, true>, k_lbs_skin_quad<16, false>); break;
+      case 1: quad(k_lbs_skin_quad<1>); break;
+      case 2: quad(k_lbs_skin_quad<2>); break;
+      case 3: quad(k_lbs_skin_quad<3>); break;
+      case 4: quad(k_lbs_skin_quad<4>); break;
+      case 5: quad(k_lbs_skin_quad<5>); break;
+      case 6: quad(k_lbs_skin_quad<6>); break;
+      case 7: quad(k_lbs_skin_quad<7>); break;
+      case 8: quad(k_lbs_skin_quad<8>); break;
+      case 9: quad(k_lbs_skin_quad<9>); break;
+      case 10: quad(k_lbs_skin_quad<10>); break;
+      case 11: quad(k_lbs_skin_quad<11>); break;
+      case 12: quad(k_lbs_skin_quad<12>); break;
+      case 13: quad(k_lbs_skin_quad<13>); break;
+      case 14: quad(k_lbs_skin_quad<14>); break;
+      case 15: quad(k_lbs_skin_quad<15>); break;
+      default: quad(k_lbs_skin_quad<16>); break;
     }
     if (bbox_ord) hipLaunchKernelGGL(k_bbox_reduce, dim3(1), dim3(256), 0, s, part, qblocks, bbox_ord);
     return launch_status();
