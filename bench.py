@@ -173,7 +173,8 @@ def lbs_sweep(args, rank, world, dev):
         "roofline": {"bound": "hbm", "kernel": "k_lbs_skin", "achieved": b_alg / (lbs_ms * 1e-3) / 1e9 if lbs_ms > 0 else 0.0,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": b_alg / (lbs_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if lbs_ms > 0 else 0.0,
-                     "traffic": None, "bytes_per_launch": b_alg, "avg_launch_ms": lbs_ms,
+                     "traffic": (read_traffic(os.path.join(ROOT, "profiles", "r01_lbs_traffic_c5.json")) or {}).get(
+                         "bytes_per_launch"), "bytes_per_launch": b_alg, "avg_launch_ms": lbs_ms,
                      "note": "achieved = B_alg = N*(24+4J) bytes per pose (SURVEY.md 8(d) C5) / avg k_lbs_skin time "
                              "(HIP events on the launch stream); the step also runs the skeleton kernel"},
         "cpu_baseline": cpu,
