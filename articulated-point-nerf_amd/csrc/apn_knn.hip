@@ -881,12 +881,17 @@ __device__ __forceinline__ void scan_ball_flat2(const GridParams& g, const int* 
     if (has_pts) {
       const int p1 = b + 1 < e ? b + 1 : b;
       const float4 P0 = sorted[b], P1 = sorted[p1];
+      // the indices pass through an empty asm so they are loaded with the coordinates (one
+      // 16-B load per point) instead of by a separate load inside the insert branch, whose
+      // vmcnt(0) would also drain the row-bound loads in flight
+      int i0 = __float_as_int(P0.w), i1 = __float_as_int(P1.w);
+      asm("" : "+v"(i0), "+v"(i1));
       const float d0x = qx - P0.x, d0y = qy - P0.y, d0z = qz - P0.z;
       const float d0 = (d0x * d0x + d0y * d0y) + d0z * d0z;
       const float d1x = qx - P1.x, d1y = qy - P1.y, d1z = qz - P1.z;
       const float d1 = (d1x * d1x + d1y * d1y) + d1z * d1z;
-      if (d0 <= g.r2) knn_insert_unique<K>(d0, __float_as_int(P0.w), bd, bi);
-      if (p1 != b && d1 <= g.r2) knn_insert_unique<K>(d1, __float_as_int(P1.w), bd, bi);
+      if (d0 <= g.r2) knn_insert_unique<K>(d0, i0, bd, bi);
+      if (p1 != b && d1 <= g.r2) knn_insert_unique<K>(d1, i1, bd, bi);
       b += 2;
       if (b > e) b = e;
     } else {
