@@ -339,7 +339,7 @@ def main():
         except Exception as e:  # never lose the GPU line over the baseline leg
             log(f"cpu baseline failed: {e!r}")
     line = {
-        "metric": "rendered rays/sec at 800x800, 300k pts, 24 bones",
+        "metric": f"rendered rays/sec at {scene.cfg.W}x{scene.cfg.H}, {scene.cfg.N // 1000}k pts, {scene.cfg.J} bones",
         "value": value, "unit": "rays/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": ms_per_step, "higher_is_better": True,
         "scaling": "strong" if shard_rays else "weak", "vs_baseline": None,
