@@ -513,3 +513,26 @@ def test_knn_modes_identical_full_scene(dev, mode):
     assert sa == sb
     for k in ("rgb_marched", "rgb_marched_direct", "depth", "weights"):
         assert torch.equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("J", [8, 24, 32, 48])
+def test_repose_quad_lbs_vs_oracle(dev, J):
+    """LBS-only repose (the C5 path, k_lbs_skin_quad: four lanes per point, weights in registers)
+    at the BASELINE bone counts, including 48 (three 16-B loads per lane), vs the oracle's
+    get_weights + PointWarper on CPU. The quad regroups the softmax and blend sums by quarter, so
+    the bar is fp32 reassociation: 2e-6 on positions (|x| <= ~1.5), 1e-6 on joints."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "articulated-point-nerf_amd"))
+    from apn_amd import harness, synthetic as S
+    scene = S.make_scene(S.SceneConfig(f"repose J{J}", 20_000, J, 0, 0))
+    model = harness.build_model(scene, dev)
+    poses = S.repose_sweep(J, steps=3)
+    st = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    orc = O.OracleModel(st, model.canonical_pcd.cpu(), model.bones, mean_min_distance_value=0.0)
+    for k in (1, 2, 5):
+        xyz, jr = model.repose(poses[k].to(dev))
+        xo, jo = orc.repose(poses[k])
+        assert (xyz.cpu() - xo).abs().max() < 2e-6
+        assert (jr.cpu() - jo).abs().max() < 1e-6
