@@ -27,6 +27,8 @@ SIGNATURES = {
     "apn_sample_pts_on_rays_fill": (C.c_int, [P, P, P, P, F32, F32, F32, I64, P, P, P, P, P, P]),
     "apn_raw2alpha": (C.c_int, [P, F32, F32, I64, P, P, P]),
     "apn_alpha2weight": (C.c_int, [P, P, I64, I64, P, P, P, P, P, P]),
+    "apn_raw2alpha_backward": (C.c_int, [P, P, F32, I64, P, P]),
+    "apn_alpha2weight_backward": (C.c_int, [P, P, P, P, P, P, I64, I64, P, P, P, P]),
     "apn_segment_sum": (C.c_int, [P, P, I64, I64, I64, P, P, P]),
     "apn_lbs_workspace_bytes": (SZ, [I64]),
     "apn_lbs_skin": (C.c_int, [P, P, I64, I32, P, F32, P, P, P, P, P, P, P, F32, I32, P, P, P, P, P, P, P, P]),

@@ -88,6 +88,72 @@ def alpha2weight(alpha, ray_id, n_rays):
     return w, T, last, i_s, i_e
 
 
+def raw2alpha_backward(exp_d, grad_back, interval):
+    """render_utils.cpp:110-114 / render_utils_kernel.cu:395-428 -> grad w.r.t. density."""
+    L.require_cuda(exp_d, grad_back, what="raw2alpha_backward")
+    e = _f32c(exp_d); gb = _f32c(grad_back)
+    if gb.numel() != e.numel():
+        raise RuntimeError("raw2alpha_backward: exp and grad_back sizes differ")
+    g = torch.empty_like(e)
+    call("apn_raw2alpha_backward", ptr(e), ptr(gb), float(interval), e.numel(), ptr(g), stream_ptr(e.device))
+    return g
+
+
+def alpha2weight_backward(alpha, weight, T, alphainv_last, i_start, i_end, n_rays, grad_weights, grad_last):
+    """render_utils.cpp:125-141 / render_utils_kernel.cu:507-561 -> grad w.r.t. alpha."""
+    L.require_cuda(alpha, weight, T, alphainv_last, i_start, i_end, grad_weights, grad_last,
+                   what="alpha2weight_backward")
+    a = _f32c(alpha); w = _f32c(weight); t = _f32c(T); last = _f32c(alphainv_last)
+    gw = _f32c(grad_weights); gl = _f32c(grad_last)
+    i_s = i_start.to(torch.int64).contiguous(); i_e = i_end.to(torch.int64).contiguous()
+    n = a.numel(); R = int(n_rays)
+    if not (w.numel() == t.numel() == gw.numel() == n) or not (last.numel() == i_s.numel() == i_e.numel()
+                                                              == gl.numel() == R):
+        raise RuntimeError("alpha2weight_backward: inconsistent sizes")
+    g = torch.empty_like(a)
+    call("apn_alpha2weight_backward", ptr(a), ptr(w), ptr(t), ptr(last), ptr(i_s), ptr(i_e), n, R, ptr(gw), ptr(gl),
+         ptr(g), stream_ptr(a.device))
+    return g
+
+
+class Alphas2Weights(torch.autograd.Function):
+    """tineuvox.py:627-643 over the HIP ops: forward -> (weights, alphainv_last)."""
+
+    @staticmethod
+    def forward(ctx, alpha, ray_id, N):
+        weights, T, alphainv_last, i_start, i_end = alpha2weight(alpha, ray_id, N)
+        if alpha.requires_grad:
+            ctx.save_for_backward(alpha, weights, T, alphainv_last, i_start, i_end)
+            ctx.n_rays = N
+        return weights, alphainv_last
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, grad_weights, grad_last):
+        alpha, weights, T, alphainv_last, i_start, i_end = ctx.saved_tensors
+        grad = alpha2weight_backward(alpha, weights, T, alphainv_last, i_start, i_end, ctx.n_rays,
+                                     grad_weights, grad_last)
+        return grad, None, None
+
+
+class Raw2Alpha(torch.autograd.Function):
+    """tineuvox.py:646-670 over the HIP ops: alpha = 1 - (1 + exp(density + shift))^(-interval)."""
+
+    @staticmethod
+    def forward(ctx, density, shift, interval):
+        exp, alpha = raw2alpha(density, shift, interval)
+        if density.requires_grad:
+            ctx.save_for_backward(exp)
+            ctx.interval = interval
+        return alpha
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, grad_back):
+        exp = ctx.saved_tensors[0]
+        return raw2alpha_backward(exp, grad_back.contiguous(), ctx.interval), None, None
+
+
 def segment_coo_sum(src, index, n_out):
     """torch_scatter.segment_coo(src, index, out=zeros, reduce='sum') for sorted index."""
     L.require_cuda(src, index, what="segment_coo")

@@ -129,6 +129,43 @@ __global__ void k_alpha2weight(const float* __restrict__ alpha, int64_t n_rays, 
   last[r] = tc;
 }
 
+// render_utils_kernel.cu:395-406 (float instantiation). The clamp constant 1e10 is a double, so
+// min() returns double and the whole product runs in double, rounded once at the store:
+// ((min(e, 1e10) * powf(1 + e, -interval - 1)) * interval) * grad_back.
+__global__ void k_raw2alpha_backward(const float* __restrict__ exp_d, const float* __restrict__ grad_back,
+                                     float interval, int64_t n, float* __restrict__ grad) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float e = exp_d[i];
+  const double m = fmin((double)e, 1e10);
+  const float pw = powf(1.f + e, -interval - 1.f);
+  grad[i] = (float)(((m * (double)pw) * (double)interval) * (double)grad_back[i]);
+}
+
+// render_utils_kernel.cu:507-528: one ray per thread, walking its samples backwards. back_cum
+// accumulates in float; 1 - alpha is float, + 1e-10 (double) promotes the division and the
+// subtraction to double, rounded at the store. Samples outside [i_start, i_end) keep grad = 0.
+__global__ void k_alpha2weight_backward(const float* __restrict__ alpha, const float* __restrict__ weight,
+                                        const float* __restrict__ T, const float* __restrict__ last,
+                                        const int64_t* __restrict__ i_start, const int64_t* __restrict__ i_end,
+                                        int64_t n_rays, const float* __restrict__ grad_weights,
+                                        const float* __restrict__ grad_last, float* __restrict__ grad) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rays) return;
+  const int64_t s = i_start[r], e = i_end[r];
+  float back_cum = grad_last[r] * last[r];
+  for (int64_t i = e - 1; i >= s; --i) {
+    const float gw = grad_weights[i];
+    grad[i] = (float)((double)(gw * T[i]) - (double)back_cum / ((double)(1.f - alpha[i]) + 1e-10));
+    back_cum += gw * weight[i];
+  }
+}
+
+__global__ void k_zero_f32(float* __restrict__ p, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = 0.f;
+}
+
 __global__ void k_a2w_init(int64_t n, int64_t n_rays, float* __restrict__ weight, float* __restrict__ T,
                            float* __restrict__ last, int64_t* __restrict__ i_start, int64_t* __restrict__ i_end) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -256,6 +293,31 @@ extern "C" int apn_alpha2weight(const float* alpha, const int64_t* ray_id, int64
   hipLaunchKernelGGL(k_segment_bounds, dim3(ceil_div(n_pts, 256)), dim3(256), 0, s, ray_id, n_pts, i_start, i_end);
   hipLaunchKernelGGL(k_alpha2weight, dim3(ceil_div(n_rays, 256)), dim3(256), 0, s, alpha, n_rays, weight, T,
                      alphainv_last, i_start, i_end);
+  return launch_status();
+}
+
+extern "C" int apn_raw2alpha_backward(const float* exp_d, const float* grad_back, float interval, int64_t n_pts,
+                                      float* grad, void* stream) {
+  if (n_pts < 0 || (n_pts > 0 && (!exp_d || !grad_back || !grad))) return APN_ERR_ARG;
+  if (n_pts == 0) return APN_OK;
+  hipLaunchKernelGGL(k_raw2alpha_backward, dim3(ceil_div(n_pts, 256)), dim3(256), 0, (hipStream_t)stream, exp_d,
+                     grad_back, interval, n_pts, grad);
+  return launch_status();
+}
+
+extern "C" int apn_alpha2weight_backward(const float* alpha, const float* weight, const float* T,
+                                         const float* alphainv_last, const int64_t* i_start, const int64_t* i_end,
+                                         int64_t n_pts, int64_t n_rays, const float* grad_weights,
+                                         const float* grad_last, float* grad, void* stream) {
+  if (n_pts < 0 || n_rays < 0) return APN_ERR_ARG;
+  if (n_pts > 0 && (!alpha || !weight || !T || !grad_weights || !grad)) return APN_ERR_ARG;
+  if (n_rays > 0 && (!alphainv_last || !i_start || !i_end || !grad_last)) return APN_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  if (n_pts == 0) return APN_OK;
+  hipLaunchKernelGGL(k_zero_f32, dim3(ceil_div(n_pts, 256)), dim3(256), 0, s, grad, n_pts);
+  if (n_rays > 0)
+    hipLaunchKernelGGL(k_alpha2weight_backward, dim3(ceil_div(n_rays, 256)), dim3(256), 0, s, alpha, weight, T,
+                       alphainv_last, i_start, i_end, n_rays, grad_weights, grad_last, grad);
   return launch_status();
 }
 

@@ -54,6 +54,20 @@ int apn_alpha2weight(const float* alpha, const int64_t* ray_id, int64_t n_pts, i
                      float* weight, float* T, float* alphainv_last, int64_t* i_start, int64_t* i_end,
                      void* stream);
 
+/* raw2alpha_backward (render_utils.cpp:110-114, render_utils_kernel.cu:395-428), the backward of
+ * Raw2Alpha (tineuvox.py:646-670): grad = min(exp_d, 1e10) (1 + exp_d)^(-interval-1) interval
+ * grad_back, the product in double as in the reference's float instantiation. */
+int apn_raw2alpha_backward(const float* exp_d, const float* grad_back, float interval, int64_t n_pts,
+                           float* grad, void* stream);
+
+/* alpha2weight_backward (render_utils.cpp:125-141, render_utils_kernel.cu:507-561), the backward
+ * of Alphas2Weights (tineuvox.py:627-643); alpha/weight/T/alphainv_last/i_start/i_end are the
+ * apn_alpha2weight outputs. grad [n_pts] is zero outside each ray's [i_start, i_end). */
+int apn_alpha2weight_backward(const float* alpha, const float* weight, const float* T,
+                              const float* alphainv_last, const int64_t* i_start, const int64_t* i_end,
+                              int64_t n_pts, int64_t n_rays, const float* grad_weights,
+                              const float* grad_last, float* grad, void* stream);
+
 /* torch_scatter.segment_coo(src, index, out=zeros(n_out, C), reduce='sum')
  * (temporalpoints.py:653-677); index sorted; seg_workspace: 2*n_out int64. */
 int apn_segment_sum(const float* src, const int64_t* index, int64_t n_pts, int64_t channels,

@@ -141,6 +141,44 @@ def alpha2weight(alpha, ray_id, n_rays):
     return [weight, T, last, i_start, i_end]
 
 
+def raw2alpha_backward(exp_d, grad_back, interval):
+    """render_utils_kernel.cu:395-406 (float instantiation), the backward of Raw2Alpha
+    (tineuvox.py:662-670). min(exp_d, 1e10) has a double operand, so the product
+    ((min * powf(1 + e, -interval - 1)) * interval) * grad_back runs in double and rounds to float
+    once; the power itself is float."""
+    e = np.asarray(exp_d, F32); gb = np.asarray(grad_back, F32)
+    with np.errstate(over="ignore"):
+        pw = np.power((F32(1) + e).astype(F32), (F32(-F32(interval)) - F32(1)).astype(F32)).astype(F32)
+    m = np.minimum(e.astype(np.float64), 1e10)
+    return (((m * pw.astype(np.float64)) * np.float64(F32(interval))) * gb.astype(np.float64)).astype(F32)
+
+
+def alpha2weight_backward(alpha, weight, T, alphainv_last, i_start, i_end, n_rays, grad_weights, grad_last):
+    """render_utils_kernel.cu:507-528, the backward of Alphas2Weights (tineuvox.py:637-643).
+
+    Per ray, samples i_end-1 down to i_start: grad[i] = gw[i]*T[i] - back_cum/(1 - alpha[i] + 1e-10)
+    with gw*T and 1 - alpha in float, the division and subtraction in double (1e-10 is a double
+    literal), rounded at the store; back_cum (float) starts at grad_last*alphainv_last and adds
+    gw[i]*weight[i]. Samples outside [i_start, i_end) get 0. Vectorised over rays."""
+    a = np.asarray(alpha, F32); w = np.asarray(weight, F32); t = np.asarray(T, F32)
+    gw = np.asarray(grad_weights, F32)
+    last = np.asarray(alphainv_last, F32); gl = np.asarray(grad_last, F32)
+    s = np.asarray(i_start, np.int64); e = np.asarray(i_end, np.int64)
+    grad = np.zeros(len(a), F32)
+    back = (gl * last).astype(F32)
+    pos = e - 1
+    active = pos >= s
+    while active.any():
+        r = np.nonzero(active)[0]
+        idx = pos[r]
+        den = (F32(1) - a[idx]).astype(F32).astype(np.float64) + 1e-10
+        grad[idx] = ((gw[idx] * t[idx]).astype(F32).astype(np.float64) - back[r].astype(np.float64) / den).astype(F32)
+        back[r] = (back[r] + (gw[idx] * w[idx]).astype(F32)).astype(F32)
+        pos[r] = idx - 1
+        active = pos >= s
+    return grad
+
+
 def segment_sum(src, index, n):
     """torch_scatter.segment_coo(reduce='sum') over sorted ``index``: sequential in-order
     float32 accumulation into a zero output (temporalpoints.py:653-677)."""

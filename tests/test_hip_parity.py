@@ -95,6 +95,62 @@ def test_alpha2weight_early_exit_and_empty(dev):
         assert np.array_equal(x.cpu().numpy(), y)
 
 
+def test_raw2alpha_backward(dev):
+    """render_utils_kernel.cu:395-428 vs the oracle: the double product matches; the float
+    powf may differ by an ulp between HIP's ocml and the host libm (rtol 1e-6)."""
+    from apn_amd import render_utils as ru
+    rng = np.random.default_rng(5)
+    d = np.concatenate([rng.uniform(-30, 30, 20000), [40.0, 1e4]]).astype(F32)
+    gb = rng.normal(size=len(d)).astype(F32)
+    e_ref, _ = O.raw2alpha(d, -6.906755, 0.5)
+    ref = O.raw2alpha_backward(e_ref, gb, 0.5)
+    e, _ = ru.raw2alpha(torch.from_numpy(d).to(dev), -6.906755, 0.5)
+    got = ru.raw2alpha_backward(e, torch.from_numpy(gb).to(dev), 0.5).cpu().numpy()
+    assert np.array_equal(np.isfinite(got), np.isfinite(ref))
+    fin = np.isfinite(ref)
+    assert np.allclose(got[fin], ref[fin], rtol=1e-6, atol=1e-30)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_alpha2weight_backward_bit_exact(dev, name):
+    """render_utils_kernel.cu:507-561 on the reference's own compositing traces: float
+    back_cum, double division -- identical IEEE operations on both sides, so bit-exact."""
+    from apn_amd import render_utils as ru
+    g = Golden(name)
+    R = len(g.z["in_rays_o"])
+    rng = np.random.default_rng(7)
+    a, rid = g.z["trace_a2w_alpha"], g.z["trace_a2w_ray_id"]
+    w, T, last, i_s, i_e = O.alpha2weight(a, rid, R)
+    gw = rng.normal(size=len(a)).astype(F32)
+    gl = rng.normal(size=R).astype(F32)
+    ref = O.alpha2weight_backward(a, w, T, last, i_s, i_e, R, gw, gl)
+    t = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+    got = ru.alpha2weight_backward(t(a), t(w), t(T), t(last), t(i_s), t(i_e), R, t(gw), t(gl)).cpu().numpy()
+    assert np.array_equal(got, ref)
+
+
+def test_raw2alpha_alphas2weights_autograd(dev):
+    """Raw2Alpha -> Alphas2Weights (tineuvox.py:627-670) under torch autograd on the device:
+    the density gradient equals the oracle's backward chain."""
+    from apn_amd import render_utils as ru
+    rng = np.random.default_rng(9)
+    counts = rng.integers(0, 40, 300)
+    rid = np.concatenate([np.full(c, r) for r, c in enumerate(counts)]).astype(np.int64)
+    dens = rng.normal(2.0, 3.0, len(rid)).astype(F32)
+    gw = rng.normal(size=len(rid)).astype(F32)
+    gl = rng.normal(size=len(counts)).astype(F32)
+    d = torch.from_numpy(dens).to(dev).requires_grad_(True)
+    alpha = ru.Raw2Alpha.apply(d, -6.906755, 0.5)
+    w, last = ru.Alphas2Weights.apply(alpha, torch.from_numpy(rid).to(dev), len(counts))
+    ((w * torch.from_numpy(gw).to(dev)).sum() + (last * torch.from_numpy(gl).to(dev)).sum()).backward()
+    e_ref, a_ref = O.raw2alpha(dens, -6.906755, 0.5)
+    w_ref, T_ref, l_ref, s_ref, e_end = O.alpha2weight(a_ref, rid, len(counts))
+    ga = O.alpha2weight_backward(a_ref, w_ref, T_ref, l_ref, s_ref, e_end, len(counts), gw, gl)
+    gd = O.raw2alpha_backward(e_ref, ga, 0.5)
+    got = d.grad.cpu().numpy()
+    assert np.allclose(got, gd, rtol=1e-5, atol=1e-6)
+
+
 def test_segment_sum_bit_exact(dev):
     from apn_amd import render_utils as ru
     g = np.random.default_rng(3)

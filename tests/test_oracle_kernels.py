@@ -84,3 +84,58 @@ def test_knn_ties_broken_by_index():
     pts = np.array([[1, 0, 0], [-1, 0, 0], [0, 1, 0], [0, 0, 0.5]], F32)
     d2, idx = O.knn_kmin(np.zeros((1, 3), F32), pts, 3)
     assert list(idx[0]) == [3, 0, 1] and d2[0, 0] == F32(0.25)
+
+
+def test_raw2alpha_backward_is_the_derivative():
+    """raw2alpha_backward (render_utils_kernel.cu:395-406) against float64 autograd of the
+    forward alpha = 1 - (1 + exp(d + shift))^(-interval); the clamp min(exp, 1e10) only bites
+    past d + shift ~ 23 (where the true derivative is ~interval * e^(-interval*(d+shift)))."""
+    import torch
+    rng = np.random.default_rng(0)
+    shift, interval = -6.906755, 0.5
+    d = rng.uniform(-10, 15, 2000).astype(np.float32)
+    gb = rng.normal(size=2000).astype(np.float32)
+    e, _ = O.raw2alpha(d, shift, interval)
+    g = O.raw2alpha_backward(e, gb, interval)
+    dt = torch.tensor(d, dtype=torch.float64, requires_grad=True)
+    alpha = 1 - (1 + torch.exp(dt + np.float64(np.float32(shift)))) ** (-interval)
+    alpha.backward(torch.tensor(gb, dtype=torch.float64))
+    ref = dt.grad.numpy()
+    assert np.allclose(g, ref, rtol=2e-6, atol=1e-12)
+    # clamp: exp_d beyond 1e10 is replaced by 1e10 in the product
+    big = np.array([1e12], np.float32)
+    gc = O.raw2alpha_backward(big, np.ones(1, np.float32), interval)
+    expect = 1e10 * np.float64(np.power(np.float32(1) + big[0], np.float32(-interval - 1))) * interval
+    assert np.isclose(gc[0], expect, rtol=1e-6)
+
+
+def test_alpha2weight_backward_is_the_derivative():
+    """alpha2weight_backward (render_utils_kernel.cu:507-528) against float64 autograd of
+    sum(gw * w) + sum(gl * alphainv_last) for rays that never reach the T < 1e-3 break; a ray
+    that does break gets zero gradient past its i_end; empty rays give nothing."""
+    import torch
+    rng = np.random.default_rng(1)
+    counts = [5, 0, 9, 1, 7]
+    rid = np.concatenate([np.full(c, r) for r, c in enumerate(counts)]).astype(np.int64)
+    a = rng.uniform(0.0, 0.3, len(rid)).astype(np.float32)
+    R = len(counts)
+    w, T, last, i_s, i_e = O.alpha2weight(a, rid, R)
+    gw = rng.normal(size=len(a)).astype(np.float32)
+    gl = rng.normal(size=R).astype(np.float32)
+    g = O.alpha2weight_backward(a, w, T, last, i_s, i_e, R, gw, gl)
+    at = torch.tensor(a, dtype=torch.float64, requires_grad=True)
+    loss = 0
+    for r in range(R):
+        seg = at[rid == r]
+        if len(seg) == 0:
+            continue
+        trans = torch.cumprod(torch.cat([torch.ones(1, dtype=torch.float64), 1 - seg]), 0)
+        loss = loss + (torch.tensor(gw[rid == r], dtype=torch.float64) * seg * trans[:-1]).sum() + gl[r] * trans[-1]
+    loss.backward()
+    assert np.allclose(g, at.grad.numpy(), rtol=1e-5, atol=1e-6)
+    # early exit: a saturating ray stops at the sample that drops T below 1e-3
+    a2 = np.array([0.5, 0.999, 0.5, 0.5], np.float32)
+    rid2 = np.zeros(4, np.int64)
+    w2, T2, l2, s2, e2 = O.alpha2weight(a2, rid2, 1)
+    g2 = O.alpha2weight_backward(a2, w2, T2, l2, s2, e2, 1, np.ones(4, np.float32), np.ones(1, np.float32))
+    assert e2[0] == 2 and g2[2] == 0 and g2[3] == 0 and g2[0] != 0
