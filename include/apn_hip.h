@@ -74,6 +74,31 @@ int apn_segment_sum(const float* src, const int64_t* index, int64_t n_pts, int64
                     int64_t n_out, float* out, int64_t* seg_workspace, void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Optimizer-side kernels, in place on fp32 device buffers of n elements.
+ * ------------------------------------------------------------------------------------- */
+
+/* adam_upd (adam_upd.cpp:36-48, adam_upd_kernel.cu:8-23, 62-82); the bias-corrected step size
+ * lr sqrt(1 - b2^step) / (1 - b1^step) is evaluated on the host in float, as the reference does. */
+int apn_adam_upd(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                 int32_t step, float beta1, float beta2, float lr, float eps, void* stream);
+
+/* masked_adam_upd (adam_upd.cpp:50-62, adam_upd_kernel.cu:25-40): grad == 0 leaves the element. */
+int apn_masked_adam_upd(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                        int32_t step, float beta1, float beta2, float lr, float eps, void* stream);
+
+/* adam_upd_with_perlr (adam_upd.cpp:64-77, adam_upd_kernel.cu:42-58): step size scaled by perlr. */
+int apn_adam_upd_with_perlr(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                            const float* perlr, int64_t n, int32_t step, float beta1, float beta2,
+                            float lr, float eps, void* stream);
+
+/* total_variation_add_grad (total_variation.cpp:16-20, total_variation_kernel.cu:13-67) on a
+ * [1, C, sz_i, sz_j, sz_k] grid: grad += six clamped neighbour differences (weights / 6; the
+ * reference weights the i direction with wz, wx is unused); dense_mode = 0 skips grad == 0. */
+int apn_total_variation_add_grad(const float* param, float* grad, float wx, float wy, float wz,
+                                 int64_t sz_i, int64_t sz_j, int64_t sz_k, int64_t n,
+                                 int32_t dense_mode, void* stream);
+
+/* ---------------------------------------------------------------------------------------
  * Fused render pipeline stages (TemporalPoints.forward, temporalpoints.py:540-712).
  * ------------------------------------------------------------------------------------- */
 

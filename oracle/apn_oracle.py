@@ -179,6 +179,72 @@ def alpha2weight_backward(alpha, weight, T, alphainv_last, i_start, i_end, n_ray
     return grad
 
 
+def _powf():
+    """The C library's powf, which the reference's host code calls (std::pow(float, float));
+    numpy's float32 power can differ from it by an ulp."""
+    import ctypes
+    import ctypes.util
+    try:
+        libm = ctypes.CDLL(ctypes.util.find_library("m") or "libm.so.6")
+        f = libm.powf
+        f.restype = ctypes.c_float
+        f.argtypes = [ctypes.c_float, ctypes.c_float]
+        return lambda x, y: F32(f(float(x), float(y)))
+    except (OSError, AttributeError):   # pragma: no cover
+        return lambda x, y: F32(np.power(F32(x), F32(y)))
+
+
+def adam_step_size(step, beta1, beta2, lr):
+    """adam_upd_kernel.cu:70 (host, float): lr * sqrt(1 - b2^step) / (1 - b1^step) with the C
+    library's powf."""
+    powf = _powf()
+    b1, b2, lr = F32(beta1), F32(beta2), F32(lr)
+    return F32(lr * np.sqrt(F32(1) - powf(b2, F32(step))) / (F32(1) - powf(b1, F32(step))))
+
+
+def adam_upd(param, grad, exp_avg, exp_avg_sq, step, beta1, beta2, lr, eps, masked=False, perlr=None):
+    """adam_upd_kernel.cu:8-58 in float without contraction (in place on the given arrays):
+    m = b1 m + (1-b1) g; v = b2 v + ((1-b2) g) g; p -= (ss [* perlr]) m / (sqrt(v) + eps);
+    masked: elements with g == 0 are left untouched."""
+    p, g, m, v = param, np.asarray(grad, F32), exp_avg, exp_avg_sq
+    b1, b2, e = F32(beta1), F32(beta2), F32(eps)
+    ss = adam_step_size(step, beta1, beta2, lr)
+    sel = (g != 0) if masked else np.ones(g.shape, bool)
+    m_new = (b1 * m + (F32(1) - b1) * g).astype(F32)
+    v_new = (b2 * v + ((F32(1) - b2) * g).astype(F32) * g).astype(F32)
+    scale = (ss * np.asarray(perlr, F32)).astype(F32) if perlr is not None else ss
+    p_new = (p - ((scale * m_new).astype(F32) / (np.sqrt(v_new) + e).astype(F32)).astype(F32)).astype(F32)
+    m[sel] = m_new[sel]; v[sel] = v_new[sel]; p[sel] = p_new[sel]
+
+
+def total_variation_add_grad(param, grad, wx, wy, wz, dense_mode):
+    """total_variation_kernel.cu:13-67 on a [1, C, I, J, K] float grid, in place on ``grad``:
+    six clamped differences in source order, weights / 6, the I direction weighted by wz."""
+    P = np.asarray(param, F32)
+    C, I, J, K = P.shape[1:]
+    wy6, wz6 = F32(F32(wy) / F32(6)), F32(F32(wz) / F32(6))
+    p = P.reshape(C, I, J, K)
+    gr = grad.reshape(C, I, J, K)
+    cl = lambda x: np.clip(x, F32(-1), F32(1)).astype(F32)
+    z = np.zeros_like(p)
+
+    def nb(axis, sh):   # clamp(p - neighbour) where the neighbour along ``axis`` (-sh side) exists
+        d = np.zeros_like(p)
+        src = [slice(None)] * 4; dst = [slice(None)] * 4
+        if sh > 0:
+            dst[axis] = slice(1, None); src[axis] = slice(0, -1)
+        else:
+            dst[axis] = slice(0, -1); src[axis] = slice(1, None)
+        d[tuple(dst)] = cl(p[tuple(dst)] - p[tuple(src)])
+        return d
+    acc = z.copy()
+    terms = [(3, 1, wz6), (3, -1, wz6), (2, 1, wy6), (2, -1, wy6), (1, 1, wz6), (1, -1, wz6)]
+    for axis, sh, w in terms:
+        acc = (acc + (w * nb(axis, sh)).astype(F32)).astype(F32)
+    sel = np.ones_like(gr, bool) if dense_mode else (gr != 0)
+    gr[sel] = (gr[sel] + acc[sel]).astype(F32)
+
+
 def segment_sum(src, index, n):
     """torch_scatter.segment_coo(reduce='sum') over sorted ``index``: sequential in-order
     float32 accumulation into a zero output (temporalpoints.py:653-677)."""

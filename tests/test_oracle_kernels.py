@@ -139,3 +139,60 @@ def test_alpha2weight_backward_is_the_derivative():
     w2, T2, l2, s2, e2 = O.alpha2weight(a2, rid2, 1)
     g2 = O.alpha2weight_backward(a2, w2, T2, l2, s2, e2, 1, np.ones(4, np.float32), np.ones(1, np.float32))
     assert e2[0] == 2 and g2[2] == 0 and g2[3] == 0 and g2[0] != 0
+
+
+def test_adam_oracle_first_step_and_float64():
+    """adam_upd (adam_upd_kernel.cu:8-82): from zero state the first step moves every
+    coordinate by ~lr * sign(g); five steps track a float64 evaluation of the same recurrence."""
+    rng = np.random.default_rng(2)
+    n = 1000
+    p = rng.normal(size=n).astype(np.float32); p0 = p.copy()
+    m = np.zeros(n, np.float32); v = np.zeros(n, np.float32)
+    g = rng.normal(size=n).astype(np.float32)
+    O.adam_upd(p, g, m, v, 1, 0.9, 0.99, 1e-3, 1e-8)
+    assert np.allclose(p0 - p, 1e-3 * np.sign(g), rtol=1e-4, atol=1e-6)   # p - 1e-3 rounds at ulp(p) <= 2.4e-7
+    p64, m64, v64 = p0.astype(np.float64), np.zeros(n), np.zeros(n)
+    p = p0.copy(); m[:] = 0; v[:] = 0
+    for step in range(1, 6):
+        g = rng.normal(size=n).astype(np.float32)
+        O.adam_upd(p, g, m, v, step, 0.9, 0.99, 1e-3, 1e-8)
+        m64 = 0.9 * m64 + 0.1 * g; v64 = 0.99 * v64 + 0.01 * g.astype(np.float64) ** 2
+        ss = 1e-3 * np.sqrt(1 - 0.99 ** step) / (1 - 0.9 ** step)
+        p64 = p64 - ss * m64 / (np.sqrt(v64) + 1e-8)
+    assert np.allclose(p, p64, rtol=1e-5, atol=1e-6)
+    # masked: zero gradients leave parameter and moments untouched
+    p = p0.copy(); m = np.ones(n, np.float32); v = np.ones(n, np.float32)
+    g = np.zeros(n, np.float32); g[::3] = 1.0
+    O.adam_upd(p, g, m, v, 1, 0.9, 0.99, 1e-3, 1e-8, masked=True)
+    keep = g == 0
+    assert np.array_equal(p[keep], p0[keep]) and np.all(m[keep] == 1) and np.all(p[~keep] != p0[~keep])
+
+
+def test_total_variation_oracle_direct():
+    """total_variation_add_grad (total_variation_kernel.cu:13-35) against a per-element loop of
+    the kernel's expression (float64 accumulate is exact here: the terms are small multiples)."""
+    rng = np.random.default_rng(4)
+    P = rng.normal(size=(1, 2, 3, 4, 5)).astype(np.float32)
+    G = rng.normal(size=P.shape).astype(np.float32)
+    G.reshape(-1)[::4] = 0
+    for dense in (True, False):
+        got = G.copy()
+        O.total_variation_add_grad(P, got, 1.0, 2.0, 3.0, dense)
+        ref = G.copy().reshape(-1)
+        p = P.reshape(-1)
+        C, I, J, K = P.shape[1:]
+        wy, wz = np.float32(2.0) / np.float32(6), np.float32(3.0) / np.float32(6)
+        cl = lambda x: min(max(x, -1.0), 1.0)
+        for idx in range(p.size):
+            if not dense and ref[idx] == 0:
+                continue
+            k = idx % K; j = idx // K % J; i = idx // K // J % I
+            acc = 0.0
+            acc += 0 if k == 0 else wz * cl(p[idx] - p[idx - 1])
+            acc += 0 if k == K - 1 else wz * cl(p[idx] - p[idx + 1])
+            acc += 0 if j == 0 else wy * cl(p[idx] - p[idx - K])
+            acc += 0 if j == J - 1 else wy * cl(p[idx] - p[idx + K])
+            acc += 0 if i == 0 else wz * cl(p[idx] - p[idx - K * J])
+            acc += 0 if i == I - 1 else wz * cl(p[idx] - p[idx + K * J])
+            ref[idx] += acc
+        assert np.allclose(got.reshape(-1), ref, rtol=1e-6, atol=1e-6)
