@@ -43,6 +43,7 @@ SIGNATURES = {
     "apn_set_knn_mode": (C.c_int, [I32]),
     "apn_debug_knn_stats": (C.c_int, [P]),
     "apn_nn1_distance": (C.c_int, [P, I64, F32, I32, P, P, P, P, P]),
+    "apn_knn_points": (C.c_int, [P, I64, P, I64, I32, I32, P, P, P, P, P, P]),
     "apn_mlp_weight_layout": (C.c_int, [P]),
     "apn_mlp_split_weights": (C.c_int, [P, P]),
     "apn_feat_project": (C.c_int, [P, I64, I32, P, P, P]),

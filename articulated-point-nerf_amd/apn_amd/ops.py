@@ -116,6 +116,26 @@ def alpha2weight_backward(alpha, weight, T, alphainv_last, i_start, i_end, n_ray
     return g
 
 
+def knn_points(q, pts, k, cell_cap=1 << 20):
+    """K nearest points of ``pts`` for every row of ``q`` (unbounded; the pykeops argKmin of
+    temporalpoints.py:104-111, 737-748) -> (d2 [M,k] float32 ascending, idx [M,k] int64)."""
+    L.require_cuda(q, pts, what="knn_points")
+    qq = _f32c(q).reshape(-1, 3); pp = _f32c(pts).reshape(-1, 3)
+    M, N = qq.shape[0], pp.shape[0]
+    if not 1 <= int(k) <= min(16, N):
+        raise RuntimeError(f"knn_points: k must be in [1, min(16, n_points)], got {k}")
+    dev = pp.device
+    lib = L.load()
+    sorted4 = torch.empty(N, 4, device=dev)
+    bbox = torch.empty(8, dtype=torch.int32, device=dev)
+    gws = torch.empty(int(lib.apn_grid_workspace_bytes(N, cell_cap)), dtype=torch.uint8, device=dev)
+    idx = torch.empty(M, int(k), dtype=torch.int64, device=dev)
+    d2 = torch.empty(M, int(k), device=dev)
+    call("apn_knn_points", ptr(qq), M, ptr(pp), N, int(k), int(cell_cap), ptr(sorted4), ptr(bbox), ptr(gws),
+         ptr(idx), ptr(d2), stream_ptr(dev))
+    return d2, idx
+
+
 class Alphas2Weights(torch.autograd.Function):
     """tineuvox.py:627-643 over the HIP ops: forward -> (weights, alphainv_last)."""
 

@@ -229,6 +229,73 @@ class TemporalPoints(torch.nn.Module):
             self._mmd_f = float(self._mmd)
         return self._mmd
 
+    # ------------------------------------------------------------------ training losses
+    # (temporalpoints.py:714-800): torch expressions around neighbour indices from the HIP
+    # kNN (apn_knn_points) in place of pykeops' argKmin, so autograd flows as in the reference.
+    def _canonical_knn(self):
+        """nn_i [N, neighbours] (self first) and nn_distance (temporalpoints.py:104-110)."""
+        if getattr(self, "_nn_cache", None) is None or self._nn_cache[0].device != self.canonical_pcd.device:
+            from .ops import knn_points
+            pcd = self.canonical_pcd.detach().contiguous()
+            _, nn_i = knn_points(pcd, pcd, self.neighbours)
+            nn_distance = torch.sqrt(((pcd[:, None, :] - pcd[nn_i, :]) ** 2).sum(-1) + self.eps.to(pcd.device))
+            self._nn_cache = (nn_i, nn_distance)
+        return self._nn_cache
+
+    @property
+    def nn_i(self):
+        return self._canonical_knn()[0]
+
+    @property
+    def nn_distance(self):
+        return self._canonical_knn()[1]
+
+    def get_neighbour_weight_tv_loss(self):
+        diff = self._last_weights[:, None, :] - self._last_weights[self.nn_i, :]
+        return torch.abs(diff).mean()
+
+    def get_weight_sparsity_loss(self):
+        eps = self.eps.to(self._last_weights.device)
+        return -(self._last_weights * torch.log(self._last_weights + eps)
+                 + (1 - self._last_weights) * torch.log(1 - self._last_weights + eps)).mean()
+
+    def get_arap_loss(self, warped_pcd, c=0.03):
+        eps = self.eps.to(warped_pcd.device)
+        warped_nn_distance = torch.sqrt((warped_pcd[:, None, :] - warped_pcd[self.nn_i, :]).pow(2).sum(-1) + eps)
+        return (self.nn_distance - warped_nn_distance).abs().sum()
+
+    def get_joint_arap_loss(self):
+        joint_distance = (self.joints[self.bone_arap_mask][0::2, :] - self.joints[self.bone_arap_mask][1::2, :])
+        return ((self.og_joint_distance.to(joint_distance.device) - joint_distance) ** 2).sum()
+
+    def get_joint_chamfer_loss(self):
+        _, c2 = self.get_chamfer_loss(self.skeleton_pcd.to(self.joints.device), self.joints, c=None, get_raw=True)
+        return c2.sum()
+
+    def _rho(self, x, c):
+        return (2 * (x / c) ** 2) / ((x / c) ** 2 + 4)
+
+    def get_chamfer_loss(self, pcd1, pcd2, N=None, M=None, c=0.03, get_raw=False):
+        from .ops import knn_points
+        if N is not None:
+            pcd1 = pcd1[torch.randint(0, pcd1.shape[0], (N,)).long().to(pcd1.device)]
+        if M is not None:
+            pcd2 = pcd2[torch.randint(0, pcd2.shape[0], (M,)).long().to(pcd2.device)]
+        _, nn_i1 = knn_points(pcd1.detach(), pcd2.detach(), 1)   # D_ij.argKmin(dim=1, K=1)
+        _, nn_i2 = knn_points(pcd2.detach(), pcd1.detach(), 1)   # D_ij.argKmin(dim=0, K=1)
+        nn_distance1 = ((pcd1[:, None, :] - pcd2[nn_i1, :]) ** 2).sum(-1)
+        nn_distance2 = ((pcd2[:, None, :] - pcd1[nn_i2, :]) ** 2).sum(-1)
+        if get_raw:
+            return nn_distance1, nn_distance2
+        if c is None:
+            return nn_distance1.mean() + nn_distance2.mean()
+        return self._rho(nn_distance1, c).mean() + self._rho(nn_distance2, c).mean()
+
+    def get_transformation_regularisation_loss(self, d=0.0873):
+        t = self.forward_warp.prev_global_t.abs()
+        thetas = self.forward_warp.prev_thetas.abs()
+        return (torch.abs(t).sum() + thetas.sum()) / len(thetas + 1)
+
     # ------------------------------------------------------------------ reference API
     def _merge_rules(self):
         J = self.weights.shape[1]

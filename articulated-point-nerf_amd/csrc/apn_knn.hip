@@ -1291,6 +1291,49 @@ __global__ void k_nn1(const float* __restrict__ xyz, int64_t N, const GridParams
   nn_dist[n] = sqrtf(best + eps);
 }
 
+// Unbounded K nearest neighbours of arbitrary queries in a point set (the pykeops
+// `D_ij.argKmin(dim=1, K)` of temporalpoints.py:104-111, 737-748): cubes of Chebyshev radius
+// 1, 2, 4, ... fine cells around the query's (clamped) cell; after cube k every point closer than
+// k*h has been seen (also for a query outside the grid), so the search stops once the K-th best
+// is closer than k*h. Queries still open after 64 rings fall back to a scan of every point.
+// Ties by point index; distances (dx^2 + dy^2) + dz^2 as the reference's recomputation.
+template <int K>
+__global__ void k_knn_points(const float* __restrict__ q, int64_t M, const GridParams* __restrict__ gp,
+                             const int* __restrict__ cell_start, const float4* __restrict__ sorted,
+                             const float* __restrict__ pts, int64_t N, int k_out, int64_t* __restrict__ idx_out,
+                             float* __restrict__ d2_out) {
+  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  const GridParams g = *gp;
+  const float qx = q[3 * m], qy = q[3 * m + 1], qz = q[3 * m + 2];
+  const int fx = cell_coord(qx, g.ox, g.inv_h, g.dx), fy = cell_coord(qy, g.oy, g.inv_h, g.dy);
+  const int fz = cell_coord(qz, g.oz, g.inv_h, g.dz);
+  float bd[K];
+  int bi[K];
+  const int dmax = max(g.dx, max(g.dy, g.dz));
+  bool done = false;
+  for (int k = 1; k <= 64; k *= 2) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) { bd[j] = INFINITY; bi[j] = 0x7fffffff; }
+    scan_cube<K, false>(g, cell_start, sorted, fx, fy, fz, k, qx, qy, qz, INFINITY, -1, bd, bi);
+    const float gk = (float)k * g.h * (1.f - 1e-4f);
+    if (bd[K - 1] < gk * gk || k >= dmax) { done = true; break; }   // k >= dmax: the cube is the grid
+  }
+  if (!done) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) { bd[j] = INFINITY; bi[j] = 0x7fffffff; }
+    for (int64_t n = 0; n < N; ++n) {
+      const float dx = qx - pts[3 * n], dy = qy - pts[3 * n + 1], dz = qz - pts[3 * n + 2];
+      const float d = (dx * dx + dy * dy) + dz * dz;
+      knn_insert<K>(d, (int)n, bd, bi);
+    }
+  }
+  for (int j = 0; j < k_out; ++j) {
+    idx_out[m * k_out + j] = bi[j];
+    d2_out[m * k_out + j] = bd[j];
+  }
+}
+
 __global__ void k_bbox_from_points(const float* __restrict__ xyz, int64_t N, int* __restrict__ bbox_ord) {
   const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -1587,5 +1630,28 @@ extern "C" int apn_nn1_distance(const float* xyz, int64_t n_points, float eps, i
   GridWs g = grid_ws(grid_workspace, n_points, cell_cap);
   hipLaunchKernelGGL(k_nn1, dim3(ceil_div(n_points, 256)), dim3(256), 0, s, xyz, n_points, g.gp, g.cell_start,
                      (const float4*)sorted_pts4, eps, nn_dist);
+  return launch_status();
+}
+
+extern "C" int apn_knn_points(const float* q, int64_t n_queries, const float* pts, int64_t n_points, int32_t k,
+                              int32_t cell_cap, float* sorted_pts4, int32_t* bbox_ord, void* grid_workspace,
+                              int64_t* idx_out, float* d2_out, void* stream) {
+  if (n_queries < 0 || n_points <= 0 || k < 1 || k > 16 || k > n_points || !pts || !sorted_pts4 || !bbox_ord ||
+      !grid_workspace || (n_queries > 0 && (!q || !idx_out || !d2_out)))
+    return APN_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_bbox_init2, dim3(1), dim3(64), 0, s, bbox_ord);
+  hipLaunchKernelGGL(k_bbox_from_points, dim3(ceil_div(n_points, 256)), dim3(256), 0, s, pts, n_points, bbox_ord);
+  int st = apn_grid_build(pts, n_points, bbox_ord, 0.01f, cell_cap, sorted_pts4, grid_workspace, stream);
+  if (st) return st;
+  if (n_queries == 0) return launch_status();
+  GridWs g = grid_ws(grid_workspace, n_points, cell_cap);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(ceil_div(n_queries, 128)), dim3(128), 0, s, q, n_queries, g.gp, g.cell_start,
+                       (const float4*)sorted_pts4, pts, n_points, k, idx_out, d2_out);
+  };
+  if (k == 1) go(k_knn_points<1>);
+  else if (k <= 8) go(k_knn_points<8>);
+  else go(k_knn_points<16>);
   return launch_status();
 }

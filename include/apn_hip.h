@@ -192,6 +192,16 @@ int apn_debug_knn_stats(uint64_t* out20);
 int apn_nn1_distance(const float* xyz, int64_t n_points, float eps, int32_t cell_cap, float* nn_dist,
                      float* sorted_pts4, int32_t* bbox_ord, void* grid_workspace, void* stream);
 
+/* Unbounded K nearest neighbours (K <= 16) of queries q [n_queries,3] in pts [n_points,3] -- the
+ * pykeops `LazyTensor` argKmin of the training losses (temporalpoints.py:104-111, 737-748, 777-780)
+ * and of nn_i / nn_distance: grid over pts (scratch sorted_pts4 [n_points,4], bbox_ord [8],
+ * grid_workspace of apn_grid_workspace_bytes(n_points, cell_cap)), ring search with an exact stop
+ * rule, full scan for queries still open after 64 rings. idx_out / d2_out [n_queries,k], ascending
+ * squared distance, ties by index (pykeops leaves their order unspecified). */
+int apn_knn_points(const float* q, int64_t n_queries, const float* pts, int64_t n_points, int32_t k,
+                   int32_t cell_cap, float* sorted_pts4, int32_t* bbox_ord, void* grid_workspace,
+                   int64_t* idx_out, float* d2_out, void* stream);
+
 /* Packed MLP weight layout: writes 19 int32 offsets (W1E,B1,W2,B2,W3,B3,W4,B4,WD,BD,WH,BH,
  * WV2,BV2,W1F,TOTAL,KE,KV,H16) and returns their count (float offsets; TOTAL = buffer length).
  * W1E = feat_net.0 columns 0..62 (posenc), W1F = feat_net.0 columns 63..190 (features),

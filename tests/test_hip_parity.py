@@ -663,3 +663,58 @@ def test_masked_adam_optimizer(dev):
         O.adam_upd(pl, gl, *st["l"], step, 0.9, 0.99, 5e-3, 1e-8, masked=True)
     assert np.array_equal(grid.detach().cpu().numpy(), pg)
     assert np.array_equal(lin.detach().cpu().numpy(), pl)
+
+
+@pytest.mark.parametrize("k", [1, 8, 16])
+def test_knn_points_bit_exact(dev, k):
+    """apn_knn_points (unbounded argKmin of the training losses) vs brute force: indices and
+    squared distances bit-exact (ties by index), with queries inside, on and far outside the
+    point cloud, and a self-query (self first, distance 0)."""
+    from apn_amd.ops import knn_points
+    rng = np.random.default_rng(21)
+    pts = rng.normal(size=(20000, 3)).astype(F32) * F32(0.3)
+    q = np.concatenate([rng.normal(size=(3000, 3)).astype(F32) * F32(0.4),
+                        rng.uniform(-5, 5, (200, 3)).astype(F32), pts[:100]])
+    d2, idx = knn_points(torch.from_numpy(q).to(dev), torch.from_numpy(pts).to(dev), k)
+    d_ref, i_ref = O.knn_kmin(q, pts, k, use_tree=False)
+    assert np.array_equal(idx.cpu().numpy(), i_ref)
+    assert np.array_equal(d2.cpu().numpy(), d_ref)
+    assert np.all(idx.cpu().numpy()[-100:, 0] == np.arange(100))
+
+
+def test_training_losses_vs_cpu(golden_model, dev):
+    """temporalpoints.py:714-800 losses on the golden model: the HIP-kNN versions equal the same
+    torch expressions on the CPU with brute-force neighbours; gradients flow to the warp."""
+    g, m = golden_model
+    out = _forward(g, m, dev)
+    warped = out["t_hat_pcd"].detach().clone().requires_grad_(True)
+    pcd = m.canonical_pcd.detach().cpu()
+    _, nn_ref = O.knn_kmin(pcd.numpy(), pcd.numpy(), m.neighbours, use_tree=False)
+    assert np.array_equal(m.nn_i.cpu().numpy(), nn_ref)
+    nn_ref = torch.from_numpy(nn_ref)
+    eps = m.eps.float()
+    nd_ref = torch.sqrt(((pcd[:, None, :] - pcd[nn_ref, :]) ** 2).sum(-1) + eps)
+    assert torch.allclose(m.nn_distance.cpu(), nd_ref, rtol=0, atol=1e-7)
+    arap = m.get_arap_loss(warped)
+    w_cpu = warped.detach().cpu()
+    wd = torch.sqrt((w_cpu[:, None, :] - w_cpu[nn_ref, :]).pow(2).sum(-1) + eps)
+    assert abs(float(arap.detach()) - float((nd_ref - wd).abs().sum())) <= 1e-4 * max(1.0, abs(float(arap.detach())))
+    arap.backward()
+    assert warped.grad is not None and torch.isfinite(warped.grad).all()
+    lw = m._last_weights.detach().cpu()
+    tv_ref = torch.abs(lw[:, None, :] - lw[nn_ref, :]).mean()
+    assert abs(float(m.get_neighbour_weight_tv_loss()) - float(tv_ref)) < 1e-6
+    jt = m.joints.detach().cpu()
+    # a skeleton cloud along the bones (the golden models were built without one)
+    sk = torch.cat([jt[p][None] + torch.linspace(0, 1, 7)[:, None] * (jt[c] - jt[p])[None]
+                    for p, c in m.bones], 0).float()
+    m.skeleton_pcd = sk
+    _, i1 = O.knn_kmin(sk.numpy(), jt.numpy(), 1, use_tree=False)
+    _, i2 = O.knn_kmin(jt.numpy(), sk.numpy(), 1, use_tree=False)
+    c1 = ((sk[:, None, :] - jt[torch.from_numpy(i1), :]) ** 2).sum(-1)
+    c2 = ((jt[:, None, :] - sk[torch.from_numpy(i2), :]) ** 2).sum(-1)
+    ch = m.get_chamfer_loss(sk.to(dev), m.joints, c=0.03)
+    ch_ref = m._rho(c1, 0.03).mean() + m._rho(c2, 0.03).mean()
+    assert abs(float(ch) - float(ch_ref)) < 1e-6
+    assert abs(float(m.get_joint_chamfer_loss()) - float(c2.sum())) < 1e-6
+    assert float(m.get_joint_arap_loss()) >= 0 and torch.isfinite(m.get_weight_sparsity_loss())
