@@ -291,6 +291,28 @@ class TemporalPoints(torch.nn.Module):
             return nn_distance1.mean() + nn_distance2.mean()
         return self._rho(nn_distance1, c).mean() + self._rho(nn_distance2, c).mean()
 
+    def get_batch_chamfer_loss(self, pcd1, pcd2, N=None, M=None):
+        """temporalpoints.py:765-795 (run.py:690 uses it on 2D projections): per batch element
+        argKmin(K=1) both ways; 2D points are padded with a zero coordinate, which leaves every
+        squared distance unchanged."""
+        from .ops import knn_points
+        assert len(pcd1) == len(pcd2)
+        if N is not None:
+            pcd1 = pcd1[:, torch.randint(0, pcd1.shape[1], (N,), device=pcd1.device).long()]
+        if M is not None:
+            pcd2 = pcd2[:, torch.randint(0, pcd2.shape[1], (M,), device=pcd1.device).long()]
+
+        def pad3(x):
+            x = x.detach().float()
+            return torch.cat([x, x.new_zeros(x.shape[:-1] + (3 - x.shape[-1],))], -1) if x.shape[-1] < 3 else x
+        nn_i1 = torch.stack([knn_points(pad3(a), pad3(b), 1)[1] for a, b in zip(pcd1, pcd2)])   # (B, N, 1)
+        nn_i2 = torch.stack([knn_points(pad3(b), pad3(a), 1)[1] for a, b in zip(pcd1, pcd2)])   # (B, M, 1)
+        idx = nn_i1.unsqueeze(-1).expand(-1, -1, -1, pcd2.shape[-1])
+        nn_distance1 = (pcd1[:, :, None, :] - torch.gather(pcd2[:, :, None, :], 1, idx)).pow(2)
+        idx = nn_i2.unsqueeze(-1).expand(-1, -1, -1, pcd1.shape[-1])
+        nn_distance2 = (pcd2[:, :, None, :] - torch.gather(pcd1[:, :, None, :], 1, idx)).pow(2)
+        return nn_distance1.sum(-1).mean() + nn_distance2.sum(-1).mean()
+
     def get_transformation_regularisation_loss(self, d=0.0873):
         t = self.forward_warp.prev_global_t.abs()
         thetas = self.forward_warp.prev_thetas.abs()

@@ -718,3 +718,20 @@ def test_training_losses_vs_cpu(golden_model, dev):
     assert abs(float(ch) - float(ch_ref)) < 1e-6
     assert abs(float(m.get_joint_chamfer_loss()) - float(c2.sum())) < 1e-6
     assert float(m.get_joint_arap_loss()) >= 0 and torch.isfinite(m.get_weight_sparsity_loss())
+
+
+def test_batch_chamfer_loss_2d(golden_model, dev):
+    """get_batch_chamfer_loss (temporalpoints.py:765-795) on 2D point sets (as run.py:690 calls
+    it) vs the same expression with brute-force neighbours on the CPU."""
+    g, m = golden_model
+    rng = np.random.default_rng(23)
+    a = rng.normal(size=(2, 300, 2)).astype(F32); b = rng.normal(size=(2, 200, 2)).astype(F32)
+    loss = m.get_batch_chamfer_loss(torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev))
+    ref = 0.0
+    for x, y in ((a, b), (b, a)):
+        tot = []
+        for bi in range(2):
+            d2, _ = O.knn_kmin(np.pad(x[bi], ((0, 0), (0, 1))), np.pad(y[bi], ((0, 0), (0, 1))), 1, use_tree=False)
+            tot.append(d2[:, 0].astype(np.float64))
+        ref += np.concatenate(tot).mean()
+    assert abs(float(loss) - ref) < 1e-5
