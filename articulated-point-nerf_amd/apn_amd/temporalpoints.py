@@ -433,16 +433,31 @@ class TemporalPoints(torch.nn.Module):
             self._pack_key = key
         return buf, self._ws.bufs["feat_proj"]
 
-    @torch.no_grad()
     def forward(self, t, render_depth=False, render_kwargs=None, query_radius=0.01, render_weights=False,
                 rot_params=None, render_pcd_direct=False, poses=None, Ks=None, cam_per_ray=None, calc_min_max=True,
                 get_skeleton=False, ray_shard=None):
         """temporalpoints.py:540-712.
 
+        With autograd enabled (the reference's train_pcd step, run.py:574-716) this is the
+        differentiable path ``_forward_train``; under ``torch.no_grad()`` (the reference's render
+        loops, run.py:80, 241) it is the fused HIP pipeline.
+
         ``ray_shard=(rank, world)`` (not in the reference signature) renders only this rank's
         contiguous ray range with ~1/world of the frame's in-bbox samples; the range is left in
         ``self.last_ray_range`` (see apn_amd.shard for the tile all-gather)."""
         assert (t is None) ^ (rot_params is None)
+        if torch.is_grad_enabled():
+            if ray_shard is not None:
+                raise NotImplementedError("ray_shard is a render-path option (use torch.no_grad())")
+            from .train import forward_train
+            return forward_train(self, t, render_depth, render_kwargs, query_radius, render_weights, rot_params,
+                                 poses, Ks, calc_min_max, get_skeleton)
+        with torch.no_grad():
+            return self._forward_render(t, render_depth, render_kwargs, query_radius, render_weights, rot_params,
+                                        poses, Ks, calc_min_max, get_skeleton, ray_shard)
+
+    def _forward_render(self, t, render_depth, render_kwargs, query_radius, render_weights, rot_params, poses, Ks,
+                        calc_min_max, get_skeleton, ray_shard):
         dev = self.canonical_feat.device
         L.require_cuda(self.canonical_feat, what="TemporalPoints.forward")
         t_embed = poc_fre(t, self.time_poc) if rot_params is None else None

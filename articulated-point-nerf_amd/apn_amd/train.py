@@ -1,0 +1,212 @@
+"""Differentiable forward of TemporalPoints -- the reference's train_pcd step.
+
+run.py:574-716 calls ``model(time_sel, False, render_kwargs, ...)`` with autograd on, takes
+``rgb_marched`` into an MSE loss plus the regularisers and steps the optimizer.
+``TemporalPoints.forward`` routes here whenever ``torch.is_grad_enabled()``; under
+``torch.no_grad()`` it stays on the fused render pipeline.
+
+What runs where:
+  * ray sampling in the cloud's bbox, the uniform grid and the radius-bounded exact 8-NN
+    (the pykeops ``Kmin_argKmin`` + radius filter, temporalpoints.py:423-447) -- HIP kernels
+    through the C-ABI (``apn_grid_build``, ``apn_inbbox_count/fill``, ``apn_knn_radius``); they
+    produce integer indices only, so nothing there needs a gradient;
+  * ``Raw2Alpha`` / ``Alphas2Weights`` (tineuvox.py:627-670) -- the HIP forward and backward
+    kernels (``apn_raw2alpha{,_backward}``, ``apn_alpha2weight{,_backward}``);
+  * everything differentiable in between -- get_weights, the skeleton chain, LBS blend, the 3x3
+    inverse, the IDW weights, the gathers, feat_net / densitynet / rgbnet, the direct blend and
+    the ray sums -- as the reference's own torch expressions, so autograd gives the reference's
+    gradients (the GEMMs go to hipBLASLt).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib as L
+from ._lib import call, ptr, stream_ptr
+from .ops import Alphas2Weights, Raw2Alpha
+from .tineuvox import poc_fre
+
+__all__ = ["forward_train", "lbs_blend", "radius_knn", "ordered_bbox"]
+
+
+def ordered_bbox(xyz: torch.Tensor) -> torch.Tensor:
+    """Cloud min/max as the order-preserving int32 encoding the grid kernels read
+    (``float_to_ordered`` in csrc/apn_common.h), 8 slots like the LBS kernel's bbox_ord."""
+    mm = torch.cat([xyz.min(dim=0)[0], xyz.max(dim=0)[0]]).float().contiguous()
+    i = mm.view(torch.int32)
+    out = torch.zeros(8, dtype=torch.int32, device=xyz.device)
+    out[:6] = torch.where(i >= 0, i, i ^ 0x7fffffff)
+    return out
+
+
+def lbs_blend(pcd, weights, bone_Ts, global_t):
+    """pointwarper.py:241-266 as differentiable torch: G_n = sum_j W_nj T_j, x' = G_n [x;1] + t."""
+    J = bone_Ts.shape[0]
+    G = (weights @ bone_Ts.reshape(J, 16)).reshape(-1, 4, 4)
+    xyz = torch.bmm(G[:, :3, :3], pcd.unsqueeze(-1)).squeeze(-1) + G[:, :3, 3] + global_t
+    return xyz, G
+
+
+def radius_knn(model, xyz, bbox6, rk, query_radius):
+    """Sampling in bbox6 + radius-bounded exact 8-NN on the HIP path (temporalpoints.py:423-447).
+    Returns (ray_pts [S,3], ray_id [S] i64, step_id [S] i64, s_i [S,8] i64, n_inbbox); S may be 0."""
+    from .temporalpoints import CELL_CAP
+    dev = xyz.device
+    lib = L.load()
+    s = stream_ptr(dev)
+    N = xyz.shape[0]
+    xyz = xyz.detach().float().contiguous()
+    ro = rk['rays_o'].detach().float().contiguous()
+    rd = rk['rays_d'].detach().float().contiguous()
+    L.require_cuda(ro, rd, what="render_kwargs")
+    R = ro.shape[0]
+    qr = float(query_radius)
+    stepdist = float(rk['stepsize']) * float(model.voxel_size)
+    near, far = float(rk['near']), float(rk['far'])
+    bbox_ord = ordered_bbox(xyz)
+    gws = torch.empty(int(lib.apn_grid_workspace_bytes(N, CELL_CAP)), dtype=torch.uint8, device=dev)
+    sorted4 = torch.empty(N, 4, device=dev)
+    call("apn_grid_build", ptr(xyz), N, ptr(bbox_ord), qr, CELL_CAP, ptr(sorted4), ptr(gws), s)
+    offs = torch.empty(R + 1, dtype=torch.int32, device=dev)
+    sws = torch.empty(int(lib.apn_sample_pts_on_rays_workspace_bytes(R)), dtype=torch.uint8, device=dev)
+    call("apn_inbbox_count", ptr(ro), ptr(rd), ptr(bbox6), near, far, stepdist, R, ptr(offs), ptr(sws), s)
+    n_bbox = int(offs[R].item())
+    empty = (xyz.new_zeros(0, 3), torch.zeros(0, dtype=torch.int64, device=dev),
+             torch.zeros(0, dtype=torch.int64, device=dev), torch.zeros(0, 8, dtype=torch.int64, device=dev), n_bbox)
+    if n_bbox == 0:
+        return empty
+    q_pos = torch.empty(n_bbox, 4, device=dev)
+    q_ray = torch.empty(n_bbox, dtype=torch.int32, device=dev)
+    call("apn_inbbox_fill", ptr(ro), ptr(rd), ptr(bbox6), near, far, stepdist, R, ptr(offs), ptr(q_pos),
+         ptr(q_ray), s)
+    s_pos = torch.empty(n_bbox, 4, device=dev)
+    s_ray = torch.empty(n_bbox, dtype=torch.int32, device=dev)
+    s_nbr = torch.empty(n_bbox, 8, dtype=torch.int32, device=dev)
+    nsurv = torch.empty(1, dtype=torch.int32, device=dev)
+    kws = torch.empty(int(lib.apn_knn_workspace_bytes(n_bbox)), dtype=torch.uint8, device=dev)
+    call("apn_knn_radius", ptr(q_pos), ptr(q_ray), n_bbox, C.c_void_p(offs.data_ptr() + 4 * R), ptr(gws), N,
+         CELL_CAP, ptr(sorted4), qr, ptr(s_pos), ptr(s_ray), ptr(s_nbr), ptr(nsurv), ptr(kws), s)
+    S = int(nsurv.item())
+    if S == 0:
+        return empty
+    pos = s_pos[:S]
+    return (pos[:, :3].contiguous(), s_ray[:S].long(), pos[:, 3].contiguous().view(torch.int32).long(),
+            s_nbr[:S].long(), n_bbox)
+
+
+def _ray_sum(src, ray_id, R):
+    """torch_scatter.segment_coo(..., reduce='sum') into zeros (differentiable index_add)."""
+    out = src.new_zeros((R,) + tuple(src.shape[1:]))
+    return out.index_add(0, ray_id, src)
+
+
+def forward_train(model, t, render_depth=False, render_kwargs=None, query_radius=0.01, render_weights=False,
+                  rot_params=None, poses=None, Ks=None, calc_min_max=True, get_skeleton=False):
+    """temporalpoints.py:540-712 (+ aggregate_pts 416-521) with autograd; same return dict."""
+    from .temporalpoints import NoPointsException, project_point_to_image_plane
+    rk = render_kwargs
+    dev = model.canonical_feat.device
+    L.require_cuda(model.canonical_feat, what="TemporalPoints.forward")
+    K = model.neighbours
+    # skeleton + LBS (temporalpoints.py:547-569; pointwarper.py:213-279)
+    t_embed = poc_fre(t, model.time_poc) if rot_params is None else None
+    weights = model.get_weights()
+    model._last_weights = weights
+    fw = model.forward_warp
+    bone_Ts, global_t, joints_rel = fw.pose_torch(model.joints, t_embed, rot_params)
+    t_hat_pcd, G = lbs_blend(fw.canonical_pcd, weights, bone_Ts, global_t)
+    Rinv = torch.linalg.inv(G[:, :3, :3])       # == torch.inverse(G)[:, :3, :3] for affine G (569, 478)
+    delta_joint = (model.joints - joints_rel).clone().detach()
+    pose_embedding = (model.pose_embedding_net(poc_fre(delta_joint, model.pos_poc).view(1, -1))
+                      if model.pose_embedding_dim > 0 else None)
+    joints = bones = None
+    if get_skeleton:
+        joints = project_point_to_image_plane(joints_rel + global_t, poses.to(dev), Ks.to(dev, torch.float32))
+        bones = model.bones
+        if model.joints_to_keep is not None:
+            joints = joints[:, model.joints_to_keep]
+            bones = model.new_bones
+    R = len(rk['rays_o'])
+    bg = rk['bg']
+    # sampling bbox (423-427) and kNN (433-447)
+    qr = float(query_radius)
+    if calc_min_max:
+        xd = t_hat_pcd.detach()
+        bbox6 = torch.cat([xd.min(dim=0)[0] - qr, xd.max(dim=0)[0] + qr]).float().contiguous()
+    else:
+        bbox6 = torch.cat([model.xyz_min, model.xyz_max]).float().contiguous()
+    ray_pts, ray_id, step_id, s_i, n_bbox = radius_knn(model, t_hat_pcd, bbox6, rk, qr)
+    model.last_stats = {"rays": R, "inbbox_samples": n_bbox, "survivors": len(s_i)}
+    model.last_train_knn = (ray_id, s_i)
+    if len(s_i) == 0:       # NoPointsException fallback (598-609)
+        return {'rgb_marched': torch.ones(R, 3, device=dev) * bg,
+                'rgb_marched_direct': torch.ones(R, 3, device=dev) * bg,
+                'depth': torch.zeros(R, device=dev), 'weights': torch.ones(R, 3, device=dev) * bg,
+                't_hat_pcd': t_hat_pcd, 'alphainv_last': None, 'grid': None, 'joints': joints, 'bones': bones}
+    rel_p = ray_pts[:, None, :] - t_hat_pcd[s_i, :]
+    to_nn = (rel_p ** 2).sum(-1)
+    # direct render blend (459-470, forced on at 592)
+    sig = model.mean_min_distance * torch.clamp(model.direct_eps, min=0.)
+    w_direct = torch.exp(-(to_nn ** 2) / (2 * (sig[s_i]) ** 2 + 1e-12))
+    w_direct_density = ((1. / K) * w_direct).unsqueeze(-1)
+    w_direct = (w_direct / (w_direct.sum(dim=-1) + 1e-12)[:, None]).unsqueeze(-1)
+    rgbs_direct = (w_direct * model.canonical_rgbs.clip(0, 1)[s_i, :]).sum(dim=1)
+    alpha_direct = (w_direct_density * model.canonical_alpha.clip(0, 1)[s_i].unsqueeze(-1)).sum(dim=1).squeeze(-1)
+    # point-NeRF aggregation (472-494)
+    w = 1 / (to_nn + model.eps.to(dev))
+    w = (w / w.sum(dim=-1)[:, None]).unsqueeze(-1)
+    rel_c = torch.bmm(Rinv[s_i].reshape(-1, 3, 3), rel_p.reshape(-1, 3, 1)).squeeze(-1)
+    feat_in = [poc_fre(rel_c, model.pos_poc), model.canonical_feat[s_i].reshape(-1, model.canonical_feat.shape[-1])]
+    if pose_embedding is not None:
+        feat_in.append(pose_embedding.expand(len(rel_c), -1))
+    out = model.feat_net(torch.cat(feat_in, dim=-1))
+    h = (out.reshape(len(s_i), K, -1) * w).sum(dim=1)
+    # heads (496-515)
+    density = model.densitynet(h).squeeze(-1)
+    interval = float(rk['stepsize']) * float(model.tineuvox.voxel_size_ratio)
+    alpha = Raw2Alpha.apply(density.contiguous(), float(model.tineuvox.act_shift), interval)
+    if model.no_view_dir:
+        raise NotImplementedError("no_view_dir=True breaks the reference forward (viewdirs_emb_reshape undefined)")
+    if model.frozen_view_dir is not None:
+        views = model.viewdirs_emb.expand(len(ray_id), -1)
+    else:
+        views = poc_fre(rk['viewdirs'], model.view_poc)[ray_id]
+    rgbs = torch.sigmoid(model.rgbnet(h, views))
+    lbsw = (weights[s_i, :] * w).sum(dim=1) if render_weights else None
+    ray_id_d = ray_id
+    thr = model.fast_color_thres
+    # pre-masks (611-627)
+    if thr > 0:
+        m = torch.where(alpha > thr)[0]
+        ray_id, step_id, alpha, rgbs = ray_id[m], step_id[m], alpha[m], rgbs[m]
+        lbsw = lbsw[m] if lbsw is not None else None
+        md = torch.where(alpha_direct > thr)[0]
+        ray_id_d, alpha_direct, rgbs_direct = ray_id_d[md], alpha_direct[md], rgbs_direct[md]
+
+    def a2w(a, rid):
+        if a.numel() == 0:
+            return a, torch.ones(R, device=dev)
+        return Alphas2Weights.apply(a.contiguous(), rid.contiguous(), R)
+    weights_r, alphainv_last = a2w(alpha, ray_id)
+    weights_d, alphainv_last_d = a2w(alpha_direct, ray_id_d)
+    # post-masks (633-651)
+    if thr > 0:
+        m = torch.where(weights_r > thr)[0]
+        weights_r, ray_id, step_id, rgbs = weights_r[m], ray_id[m], step_id[m], rgbs[m]
+        lbsw = lbsw[m] if lbsw is not None else None
+        md = torch.where(weights_d > thr)[0]
+        weights_d, ray_id_d, rgbs_direct = weights_d[md], ray_id_d[md], rgbs_direct[md]
+    # ray sums (653-677)
+    rgb_marched = _ray_sum(weights_r.unsqueeze(-1) * rgbs, ray_id, R) + alphainv_last.unsqueeze(-1) * bg
+    rgb_marched_d = _ray_sum(weights_d.unsqueeze(-1) * rgbs_direct, ray_id_d, R) + alphainv_last_d.unsqueeze(-1) * bg
+    ret = {'t_hat_pcd': t_hat_pcd, 'rgb_marched': rgb_marched, 'alphainv_last': alphainv_last,
+           'alphainv_last_direct': alphainv_last_d, 'grid': None, 'rgb_marched_direct': rgb_marched_d,
+           'joints': joints, 'bones': bones}
+    if render_depth:
+        ret['depth'] = _ray_sum(weights_r * step_id, ray_id, R)
+    if render_weights:      # 690-710
+        col = lbsw @ model._joint_colors(dev)
+        ret['weights'] = _ray_sum(weights_r.unsqueeze(-1) * col, ray_id, R) + alphainv_last.unsqueeze(-1) * bg
+    return ret

@@ -203,6 +203,7 @@ def main():
                          "collective); 'rays' = the ranks split one frame's rays and all-gather the tiles "
                          "over RCCL (strong scaling)")
     args = ap.parse_args()
+    torch.set_grad_enabled(False)   # a render benchmark: the reference renders under no_grad (run.py:80, 241)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

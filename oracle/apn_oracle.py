@@ -404,7 +404,7 @@ def transform_net(t_embed: torch.Tensor, tn: dict, J: int) -> torch.Tensor:
     return out.reshape(J + 1, 4)
 
 
-def pointwarper_forward(st: dict, weights, joints, t_embed=None, rot_params=None):
+def pointwarper_forward(st: dict, weights, joints, t_embed=None, rot_params=None, blend="sum"):
     """pointwarper.py:213-279 with get_frames=True, get_skeleton=True, avg_procrustes=False.
 
     Returns (xyz (N,3), joints_rel (J,3), G (N,4,4), joints_warped (J,3)).
@@ -420,7 +420,10 @@ def pointwarper_forward(st: dict, weights, joints, t_embed=None, rot_params=None
     R_t = R_t[st["sibling_mask"]]
     R_t[st["rot_mask"]] = torch.eye(3)
     bone_Ts = bone_transforms(R_t, joints, st["parent_indices"], st["parent_joint_ex"])
-    G = (bone_Ts * weights[:, :, None, None]).sum(dim=1)
+    if blend == "sum":
+        G = (bone_Ts * weights[:, :, None, None]).sum(dim=1)
+    else:   # another summation order, to measure the gradient's own float32 noise floor (tests)
+        G = (weights @ bone_Ts.reshape(J, 16)).reshape(-1, 4, 4)
     xyz = st["canonical_pcd"]
     xyzh = torch.cat([xyz, torch.ones((len(xyz), 1))], -1)
     xyz = torch.bmm(G, xyzh.unsqueeze(-1)).squeeze(-1)[:, :3]
@@ -690,3 +693,133 @@ class OracleModel:
             wm = segment_sum((w[:, None] * col).astype(F32), ray_id, N)
             ret["weights"] = torch.from_numpy((wm + (last[:, None] * F32(bg)).astype(F32)).astype(F32))
         return ret
+
+
+# ----------------------------------------------------------------------------------------
+# Training-mode forward -- run.py:574-716 renders with autograd on.
+# The render_utils kernels enter autograd through their restated forward/backward pairs
+# (tineuvox.py:627-670), everything else is the reference's torch expressions.
+# ----------------------------------------------------------------------------------------
+
+class _Raw2AlphaFn(torch.autograd.Function):
+    """tineuvox.py:646-670 over raw2alpha / raw2alpha_backward above."""
+
+    @staticmethod
+    def forward(ctx, density, shift, interval):
+        e, a = raw2alpha(density.detach().numpy(), shift, interval)
+        ctx.save_for_backward(torch.from_numpy(np.ascontiguousarray(e)))
+        ctx.interval = interval
+        return torch.from_numpy(np.ascontiguousarray(a))
+
+    @staticmethod
+    def backward(ctx, g):
+        e, = ctx.saved_tensors
+        return torch.from_numpy(raw2alpha_backward(e.numpy(), g.contiguous().numpy(), ctx.interval)), None, None
+
+
+class _Alphas2WeightsFn(torch.autograd.Function):
+    """tineuvox.py:627-643 over alpha2weight / alpha2weight_backward above."""
+
+    @staticmethod
+    def forward(ctx, alpha, ray_id, n_rays):
+        w, T, last, i_s, i_e = alpha2weight(alpha.detach().numpy(), ray_id.numpy(), n_rays)
+        ctx.saved = (alpha.detach().numpy(), w, T, last, i_s, i_e)
+        ctx.n_rays = n_rays
+        return torch.from_numpy(w), torch.from_numpy(last)
+
+    @staticmethod
+    def backward(ctx, gw, gl):
+        a, w, T, last, i_s, i_e = ctx.saved
+        g = alpha2weight_backward(a, w, T, last, i_s, i_e, ctx.n_rays, gw.contiguous().numpy(),
+                                  gl.contiguous().numpy())
+        return torch.from_numpy(g), None, None
+
+
+def oracle_trainable(om: "OracleModel") -> dict:
+    """Make the OracleModel's parameters autograd leaves; returns them under the reference's
+    state-dict names."""
+    params = {"weights": om.W, "theta_weight": om.theta_weight, "canonical_feat": om.feat,
+              "canonical_alpha": om.alpha_c, "canonical_rgbs": om.rgb_c, "direct_eps": om.direct_eps,
+              "joints": om.joints}
+    for k, v in om.nets.items():
+        params[k] = v
+    for k, v in om.pw["transform_net"].items():
+        params["forward_warp.transform_net." + k] = v
+    for v in params.values():
+        v.requires_grad_(True)
+    return params
+
+
+def oracle_forward_train(om: "OracleModel", t, render_kwargs, query_radius=0.01, xyz_min=None, xyz_max=None,
+                         knn_tree=None, blend="sum", jitter=0.0, jitter_seed=0):
+    """temporalpoints.py:540-712 + aggregate_pts (416-521) with autograd on (render_pcd_direct
+    forced, no depth / weights outputs). ``xyz_min/xyz_max`` fix the sampling bbox (else the
+    cloud's, 423-427). Returns rgb_marched, rgb_marched_direct, t_hat_pcd, last_weights."""
+    rk = {k: (v.detach().cpu() if torch.is_tensor(v) else v) for k, v in render_kwargs.items()}
+    R = len(rk["rays_o"]); K = om.K; bg = rk["bg"]
+    t_embed = poc_fre(torch.as_tensor(t).reshape(1).float(), om.time_poc)
+    weights = om.get_weights()
+    t_hat, joints_rel, G, _, _, _ = pointwarper_forward(om.pw, weights, om.joints, t_embed, None, blend=blend)
+    Rinv = torch.inverse(G)
+    gen = torch.Generator().manual_seed(jitter_seed)
+
+    def jit(x):
+        # relative ulp-scale perturbation of the float32 quantities another device computes with
+        # another summation order (warped cloud, 3x3 inverses, joint offsets): tests use it to
+        # measure the gradient's own float32 noise floor
+        if not jitter:
+            return x
+        sgn = torch.randint(0, 3, x.shape, generator=gen).float() - 1.0
+        return x + x.detach() * (jitter * sgn)
+    t_hat = jit(t_hat)
+    Rinv = jit(Rinv)
+    pose_embedding = None
+    if om.pose_embedding_dim > 0:
+        delta = jit((om.joints - joints_rel).clone().detach())
+        pose_embedding = pose_embedding_net(poc_fre(delta, om.pos_poc).view(1, -1), om.nets)
+    if xyz_min is None:
+        xyz_min = torch.min(t_hat.detach(), dim=0)[0] - query_radius
+        xyz_max = torch.max(t_hat.detach(), dim=0)[0] + query_radius
+    pts, ray_id, step_id, _ = om.sample_ray(rk["rays_o"], rk["rays_d"], rk["near"], rk["far"], rk["stepsize"],
+                                            torch.as_tensor(xyz_min).cpu().float(),
+                                            torch.as_tensor(xyz_max).cpu().float())
+    d2, s_i = knn_kmin(pts, t_hat.detach().numpy(), K, use_tree=knn_tree)
+    keep = np.nonzero(d2[:, -1] <= F32(query_radius))[0]
+    s_i = torch.from_numpy(s_i[keep]); ray_id = torch.from_numpy(ray_id[keep]); ray_pts = torch.from_numpy(pts[keep])
+    om.trace = dict(s_i=s_i, ray_id=ray_id, n_inbbox=len(pts), t_hat_pcd=t_hat.detach())
+    rel_p = ray_pts[:, None, :] - t_hat[s_i, :]
+    to_nn = (rel_p ** 2).sum(-1)
+    sig = om.mmd * torch.max(om.direct_eps, torch.tensor(0.))
+    w_direct = torch.exp(-(to_nn ** 2) / (2 * (sig[s_i]) ** 2 + 1e-12))
+    w_dd = (torch.tensor(1. / K) * w_direct).unsqueeze(-1)
+    w_direct = (w_direct / (w_direct.sum(dim=-1) + 1e-12)[:, None]).unsqueeze(-1)
+    rgbs_d = (w_direct * om.rgb_c.clip(0, 1)[s_i, :]).sum(dim=1)
+    alpha_d = (w_dd * om.alpha_c.clip(0, 1)[s_i].unsqueeze(-1)).sum(dim=1).squeeze(-1)
+    w = 1 / (to_nn + om.eps)
+    w = (w / w.sum(dim=-1)[:, None]).unsqueeze(-1)
+    rel_c = torch.bmm(Rinv[s_i][..., :3, :3].reshape(-1, 3, 3), rel_p.reshape(-1, 3).unsqueeze(-1)).squeeze(-1)
+    x = [poc_fre(rel_c, om.pos_poc), om.feat[s_i].reshape(-1, om.feat.shape[-1])]
+    if pose_embedding is not None:
+        x.append(pose_embedding.expand(len(x[0]), -1))
+    h = (feat_net(torch.cat(x, -1), om.nets).reshape(len(s_i), K, -1) * w).sum(dim=1)
+    density = _lin(h, om.nets, "densitynet").squeeze(-1)
+    alpha = _Raw2AlphaFn.apply(density.contiguous(), om.act_shift, rk["stepsize"] * om.voxel_size_ratio)
+    views = poc_fre(rk["viewdirs"], om.view_poc)[ray_id]
+    rgbs = torch.sigmoid(rgbnet(h, views, om.nets))
+    thr = om.fast_color_thres
+    ray_id_d = ray_id
+    if thr > 0:
+        m = torch.where(alpha > thr)[0]
+        ray_id, alpha, rgbs = ray_id[m], alpha[m], rgbs[m]
+        md = torch.where(alpha_d > thr)[0]
+        ray_id_d, alpha_d, rgbs_d = ray_id_d[md], alpha_d[md], rgbs_d[md]
+    wr, last = _Alphas2WeightsFn.apply(alpha.contiguous(), ray_id, R)
+    wd, last_d = _Alphas2WeightsFn.apply(alpha_d.contiguous(), ray_id_d, R)
+    if thr > 0:
+        m = torch.where(wr > thr)[0]
+        wr, ray_id, rgbs = wr[m], ray_id[m], rgbs[m]
+        md = torch.where(wd > thr)[0]
+        wd, ray_id_d, rgbs_d = wd[md], ray_id_d[md], rgbs_d[md]
+    rgb = torch.zeros(R, 3).index_add(0, ray_id, wr.unsqueeze(-1) * rgbs) + last.unsqueeze(-1) * bg
+    rgb_d = torch.zeros(R, 3).index_add(0, ray_id_d, wd.unsqueeze(-1) * rgbs_d) + last_d.unsqueeze(-1) * bg
+    return {"rgb_marched": rgb, "rgb_marched_direct": rgb_d, "t_hat_pcd": t_hat, "last_weights": weights}

@@ -10,3 +10,5 @@ for p in (ROOT, os.path.join(ROOT, "articulated-point-nerf_amd"), os.path.dirnam
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI)")
     config.addinivalue_line("markers", "slow: longer CPU test")
+    config.addinivalue_line("markers", "autograd: runs with autograd on (TemporalPoints.forward then takes "
+                            "the differentiable training path)")

@@ -115,3 +115,24 @@ def test_bbox_sensitivity_of_reference_sampling():
     assert survivors(tp, lo, hi) == survivors(t, lo, hi)
     lo2 = (tp.min(0) - np.float32(0.01)).astype(np.float32); hi2 = (tp.max(0) + np.float32(0.01)).astype(np.float32)
     assert survivors(tp, lo2, hi2)[1] != survivors(t, lo, hi)[1]
+
+
+def test_oracle_train_forward_matches_render_and_golden(golden):
+    """The oracle's autograd twin (train_pcd path) renders the same image as the
+    no-grad oracle, matches the reference's golden render, and its gradients are finite and reach
+    every parameter group of the path."""
+    m = golden.oracle(mean_min_distance_value=golden.t("in_mean_min_distance"))
+    ref = m.forward(golden.t("in_t"), render_kwargs=golden.render_kwargs(), knn_tree=False)
+    params = O.oracle_trainable(m)
+    out = O.oracle_forward_train(m, golden.t("in_t"), golden.render_kwargs(), knn_tree=False)
+    assert (out["rgb_marched"].detach() - ref["rgb_marched"]).abs().max() < 1e-6
+    assert (out["rgb_marched_direct"].detach() - ref["rgb_marched_direct"]).abs().max() < 1e-6
+    err = (out["rgb_marched"].detach() - golden.t("out_rgb_marched")).abs().max(-1)[0]
+    assert float((err > 1e-4).float().mean()) <= 5e-3
+    loss = (out["rgb_marched"] - 0.5).pow(2).mean() + (out["rgb_marched_direct"] - 0.5).pow(2).mean()
+    loss.backward()
+    for k in ("weights", "theta_weight", "joints", "canonical_feat", "canonical_alpha", "canonical_rgbs",
+              "direct_eps", "feat_net.0.weight", "densitynet.weight", "rgbnet.views_linears.2.weight",
+              "forward_warp.transform_net.net.0.weight"):
+        gk = params[k].grad
+        assert gk is not None and torch.isfinite(gk).all() and float(gk.abs().max()) > 0, k
