@@ -28,7 +28,7 @@ from ._lib import call, ptr, stream_ptr
 from .ops import Alphas2Weights, Raw2Alpha
 from .tineuvox import poc_fre
 
-__all__ = ["forward_train", "lbs_blend", "radius_knn", "ordered_bbox"]
+__all__ = ["forward_train", "lbs_blend", "inv3x3", "radius_knn", "ordered_bbox"]
 
 
 def ordered_bbox(xyz: torch.Tensor) -> torch.Tensor:
@@ -42,11 +42,28 @@ def ordered_bbox(xyz: torch.Tensor) -> torch.Tensor:
 
 
 def lbs_blend(pcd, weights, bone_Ts, global_t):
-    """pointwarper.py:241-266 as differentiable torch: G_n = sum_j W_nj T_j, x' = G_n [x;1] + t."""
+    """pointwarper.py:241-266 as differentiable torch: G_n = sum_j W_nj T_j, x' = G_n [x;1] + t.
+    Only the 3x4 rows are formed (the bottom row is exactly [0,0,0,1]); the per-point 3x3 products
+    are broadcast multiply-adds (batched 3x3 bmm / linalg.inv go to tiny-GEMM / LU library kernels
+    that cost ~10x more here)."""
     J = bone_Ts.shape[0]
-    G = (weights @ bone_Ts.reshape(J, 16)).reshape(-1, 4, 4)
-    xyz = torch.bmm(G[:, :3, :3], pcd.unsqueeze(-1)).squeeze(-1) + G[:, :3, 3] + global_t
+    G = (weights @ bone_Ts[:, :3, :].reshape(J, 12)).reshape(-1, 3, 4)
+    xyz = (G[:, :, :3] * pcd[:, None, :]).sum(-1) + G[:, :, 3] + global_t
     return xyz, G
+
+
+def inv3x3(A):
+    """Adjugate inverse of [N,3,3] (differentiable elementwise ops); == torch.inverse(G)[:, :3, :3]
+    for the affine G of temporalpoints.py:569 up to float32 rounding."""
+    a, b, c = A[:, 0, 0], A[:, 0, 1], A[:, 0, 2]
+    d, e, f = A[:, 1, 0], A[:, 1, 1], A[:, 1, 2]
+    g, h, i = A[:, 2, 0], A[:, 2, 1], A[:, 2, 2]
+    c00, c01, c02 = e * i - f * h, f * g - d * i, d * h - e * g
+    det = a * c00 + b * c01 + c * c02
+    adj = torch.stack([c00, c * h - b * i, b * f - c * e,
+                       c01, a * i - c * g, c * d - a * f,
+                       c02, b * g - a * h, a * e - b * d], dim=-1)
+    return (adj / det[:, None]).reshape(-1, 3, 3)
 
 
 def radius_knn(model, xyz, bbox6, rk, query_radius):
@@ -117,7 +134,7 @@ def forward_train(model, t, render_depth=False, render_kwargs=None, query_radius
     fw = model.forward_warp
     bone_Ts, global_t, joints_rel = fw.pose_torch(model.joints, t_embed, rot_params)
     t_hat_pcd, G = lbs_blend(fw.canonical_pcd, weights, bone_Ts, global_t)
-    Rinv = torch.linalg.inv(G[:, :3, :3])       # == torch.inverse(G)[:, :3, :3] for affine G (569, 478)
+    Rinv = inv3x3(G[:, :, :3])       # torch.inverse(G)[:, :3, :3] for affine G (569, 478)
     delta_joint = (model.joints - joints_rel).clone().detach()
     pose_embedding = (model.pose_embedding_net(poc_fre(delta_joint, model.pos_poc).view(1, -1))
                       if model.pose_embedding_dim > 0 else None)
@@ -157,7 +174,7 @@ def forward_train(model, t, render_depth=False, render_kwargs=None, query_radius
     # point-NeRF aggregation (472-494)
     w = 1 / (to_nn + model.eps.to(dev))
     w = (w / w.sum(dim=-1)[:, None]).unsqueeze(-1)
-    rel_c = torch.bmm(Rinv[s_i].reshape(-1, 3, 3), rel_p.reshape(-1, 3, 1)).squeeze(-1)
+    rel_c = (Rinv[s_i] * rel_p[:, :, None, :]).sum(-1).reshape(-1, 3)
     feat_in = [poc_fre(rel_c, model.pos_poc), model.canonical_feat[s_i].reshape(-1, model.canonical_feat.shape[-1])]
     if pose_embedding is not None:
         feat_in.append(pose_embedding.expand(len(rel_c), -1))

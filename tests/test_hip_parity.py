@@ -915,35 +915,44 @@ def _train_grad_check(g, m, dev):
 
 @pytest.mark.autograd
 def test_train_step_with_optimizer_reduces_loss(dev):
-    """A few train_pcd iterations (forward with autograd, MSE + ARAP + TV + sparsity losses,
-    backward, Adam step) on the C1 scene fitting the fused render of a perturbed pose: the
-    photometric loss decreases."""
+    """train_pcd iterations (run.py:574-716) on the C1 scene: forward with autograd, the default
+    loss weights (render 200, ARAP 5e-3, TV 10, sparsity 0.2, transformation reg 0.1), backward,
+    MaskedAdam (HIP kernels) over the reference's lrate_* groups (configs/nerf/default.py:86-92),
+    on a fixed batch of 2048 rays fitting the fused render of another time step: the optimised
+    total loss decreases."""
     import os
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                     "articulated-point-nerf_amd"))
     from apn_amd import harness, synthetic as S
+    from apn_amd.optim import MaskedAdam
     scene = S.make_scene("C1")
     model = harness.build_model(scene, dev)
     rk = scene.render_kwargs(dev)
     with torch.no_grad():
         target = model(torch.tensor([0.6], device=dev), render_kwargs=rk)["rgb_marched"].clone()
-    opt = torch.optim.Adam([p for p in model.parameters() if p.requires_grad], lr=1e-3)
+    lrates = dict(gammas=1e-3, weights=1e-4, theta_weight=1e-4, forward_warp=1e-4, joints=1e-5, feat_net=1e-3)
+    groups = []
+    for k, lr in lrates.items():
+        p = getattr(model, k)
+        groups.append({"params": list(p.parameters()) if isinstance(p, torch.nn.Module) else [p], "lr": lr,
+                       "skip_zero_grad": False})
+    opt = MaskedAdam(groups)
     gen = torch.Generator().manual_seed(0)
+    sel = torch.randint(0, len(rk["rays_o"]), (2048,), generator=gen).to(dev)
+    sub = dict(rk)
+    for k in ("rays_o", "rays_d", "viewdirs"):
+        sub[k] = rk[k][sel]
     losses = []
     t = torch.tensor([scene.cfg.t], device=dev)
-    for it in range(12):
-        sel = torch.randint(0, len(rk["rays_o"]), (2048,), generator=gen).to(dev)
-        sub = dict(rk)
-        for k in ("rays_o", "rays_d", "viewdirs"):
-            sub[k] = rk[k][sel]
+    for it in range(20):
         opt.zero_grad(set_to_none=True)
         out = model(t, False, sub, render_pcd_direct=False)
         mse = torch.nn.functional.mse_loss(out["rgb_marched"], target[sel])
-        loss = mse + 1e-3 * model.get_arap_loss(out["t_hat_pcd"]) + 1e-2 * model.get_neighbour_weight_tv_loss() \
-            + 1e-4 * model.get_weight_sparsity_loss()
+        loss = 2e2 * mse + 5e-3 * model.get_arap_loss(out["t_hat_pcd"]) + 1e1 * model.get_neighbour_weight_tv_loss() \
+            + 2e-1 * model.get_weight_sparsity_loss() + 1e-1 * model.get_transformation_regularisation_loss()
         loss.backward()
         opt.step()
-        losses.append(float(mse))
+        losses.append(float(loss.detach()))
     assert np.isfinite(losses).all()
-    assert np.mean(losses[-3:]) < np.mean(losses[:3]), losses
+    assert np.mean(losses[-3:]) < 0.9 * np.mean(losses[:3]), losses
