@@ -55,6 +55,9 @@ SIGNATURES = {
     "apn_masked_adam_upd": (C.c_int, [P, P, P, P, I64, I32, F32, F32, F32, F32, P]),
     "apn_adam_upd_with_perlr": (C.c_int, [P, P, P, P, P, I64, I32, F32, F32, F32, F32, P]),
     "apn_total_variation_add_grad": (C.c_int, [P, P, F32, F32, F32, I64, I64, I64, I64, I32, P]),
+    "apn_lbs_train_workspace_bytes": (SZ, [I64, I32]),
+    "apn_lbs_train_fwd": (C.c_int, [P, P, I64, I32, P, F32, P, P, P, P, P, P, P]),
+    "apn_lbs_train_bwd": (C.c_int, [P, P, I64, I32, P, F32, P, P, P, P, P, P, P, P, P, P, P, P]),
     "apn_scan_workspace_bytes": (SZ, [I64]),
     "apn_scan_exclusive_i32": (C.c_int, [P, P, I64, P, P]),
     "apn_version": (C.c_char_p, []),

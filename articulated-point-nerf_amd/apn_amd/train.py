@@ -28,7 +28,7 @@ from ._lib import call, ptr, stream_ptr
 from .ops import Alphas2Weights, Raw2Alpha
 from .tineuvox import poc_fre
 
-__all__ = ["forward_train", "lbs_blend", "inv3x3", "radius_knn", "ordered_bbox"]
+__all__ = ["forward_train", "LBSTrain", "lbs_train", "lbs_blend", "inv3x3", "radius_knn", "ordered_bbox"]
 
 
 def ordered_bbox(xyz: torch.Tensor) -> torch.Tensor:
@@ -64,6 +64,60 @@ def inv3x3(A):
                        c01, a * i - c * g, c * d - a * f,
                        c02, b * g - a * h, a * e - b * d], dim=-1)
     return (adj / det[:, None]).reshape(-1, 3, 3)
+
+
+class LBSTrain(torch.autograd.Function):
+    """get_weights + LBS blend/apply + the 3x3 inverse as one HIP forward and one HIP backward
+    (apn_lbs_train_fwd / _bwd): (W [N,J], theta [1], T34 [J,12], global_t [3]) ->
+    (xyz [N,3], Rinv [N,3,3], sm [N,J]); canonical points and eps are constants."""
+
+    @staticmethod
+    def forward(ctx, W, theta, T34, global_t, pcd, eps):
+        N, J = W.shape
+        dev = W.device
+        Wc, th, T, gt = (x.detach().float().contiguous() for x in (W, theta, T34, global_t))
+        sm = torch.empty(N, J, device=dev)
+        G12 = torch.empty(N, 12, device=dev)
+        xyz = torch.empty(N, 3, device=dev)
+        Rinv = torch.empty(N, 3, 3, device=dev)
+        call("apn_lbs_train_fwd", ptr(pcd), ptr(Wc), N, J, ptr(th), float(eps), ptr(T), ptr(gt), ptr(sm), ptr(G12),
+             ptr(xyz), ptr(Rinv), stream_ptr(dev))
+        ctx.save_for_backward(Wc, th, T, sm, Rinv, pcd)
+        ctx.eps = float(eps)
+        return xyz, Rinv, sm
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, d_xyz, d_Rinv, d_sm):
+        Wc, th, T, sm, Rinv, pcd = ctx.saved_tensors
+        N, J = Wc.shape
+        dev = Wc.device
+        c = lambda x: None if x is None else x.float().contiguous()
+        d_xyz, d_Rinv, d_sm = c(d_xyz), c(d_Rinv), c(d_sm)
+        dW = torch.empty(N, J, device=dev)
+        dT = torch.empty(J, 12, device=dev)
+        dgt = torch.empty(3, device=dev)
+        dth = torch.empty(1, device=dev)
+        ws = torch.empty(int(L.load().apn_lbs_train_workspace_bytes(N, J)), dtype=torch.uint8, device=dev)
+        call("apn_lbs_train_bwd", ptr(pcd), ptr(Wc), N, J, ptr(th), ctx.eps, ptr(T), ptr(sm), ptr(Rinv), ptr(d_xyz),
+             ptr(d_Rinv), ptr(d_sm), ptr(dW), ptr(dT), ptr(dgt), ptr(dth), ptr(ws), stream_ptr(dev))
+        return dW, dth, dT, dgt, None, None
+
+
+def lbs_train(model, bone_Ts, global_t):
+    """(t_hat_pcd, Rinv, weights) of the training forward: the fused HIP Function for identity
+    merge rules and J <= 64, else the torch composition (get_weights + lbs_blend + inv3x3)."""
+    J = bone_Ts.shape[0]
+    if model._merge_rules() is None and J <= 64:
+        pcd = model.forward_warp.canonical_pcd.detach().float().contiguous()
+        th = model.theta_weight.reshape(1)
+        gt = global_t.reshape(3)
+        xyz, Rinv, weights = LBSTrain.apply(model.weights, th, bone_Ts[:, :3, :].reshape(J, 12), gt, pcd,
+                                            model._eps)
+        return xyz, Rinv, weights
+    weights = model.get_weights()
+    xyz, G = lbs_blend(model.forward_warp.canonical_pcd, weights, bone_Ts, global_t)
+    return xyz, inv3x3(G[:, :, :3]), weights
 
 
 def radius_knn(model, xyz, bbox6, rk, query_radius):
@@ -129,12 +183,11 @@ def forward_train(model, t, render_depth=False, render_kwargs=None, query_radius
     K = model.neighbours
     # skeleton + LBS (temporalpoints.py:547-569; pointwarper.py:213-279)
     t_embed = poc_fre(t, model.time_poc) if rot_params is None else None
-    weights = model.get_weights()
-    model._last_weights = weights
     fw = model.forward_warp
     bone_Ts, global_t, joints_rel = fw.pose_torch(model.joints, t_embed, rot_params)
-    t_hat_pcd, G = lbs_blend(fw.canonical_pcd, weights, bone_Ts, global_t)
-    Rinv = inv3x3(G[:, :, :3])       # torch.inverse(G)[:, :3, :3] for affine G (569, 478)
+    # get_weights + blend/apply + torch.inverse(G)[:, :3, :3] (569, 478)
+    t_hat_pcd, Rinv, weights = lbs_train(model, bone_Ts, global_t)
+    model._last_weights = weights
     delta_joint = (model.joints - joints_rel).clone().detach()
     pose_embedding = (model.pose_embedding_net(poc_fre(delta_joint, model.pos_poc).view(1, -1))
                       if model.pose_embedding_dim > 0 else None)

@@ -98,6 +98,25 @@ int apn_total_variation_add_grad(const float* param, float* grad, float wx, floa
                                  int64_t sz_i, int64_t sz_j, int64_t sz_k, int64_t n,
                                  int32_t dense_mode, void* stream);
 
+/* Differentiable LBS of the training path (replaces the autograd composition of
+ * TemporalPoints.get_weights temporalpoints.py:401-414, PointWarper.forward's blend/apply
+ * pointwarper.py:241-266 and torch.inverse(G)[:3,:3] temporalpoints.py:569). Identity merge rules,
+ * 1 <= n_joints <= 64. T34 [J,12] = bone_Ts[:, :3, :]; theta = theta_weight (device, 1 float).
+ * fwd: sm_out [N,J] softmax(W/max(eps,theta)), G12_out [N,12] blended 3x4 rows, xyz_out [N,3],
+ * Rinv_out [N,9] (adjugate inverse of G[:, :3]).
+ * bwd: d_xyz [N,3], d_Rinv [N,9], d_sm [N,J] (each may be NULL = zero) -> dW [N,J], dT34 [J,12],
+ * d_global_t [3], d_theta [1] (overwritten; block partials reduced in a fixed order in workspace of
+ * apn_lbs_train_workspace_bytes). */
+size_t apn_lbs_train_workspace_bytes(int64_t n_points, int32_t n_joints);
+int apn_lbs_train_fwd(const float* pcd, const float* W, int64_t n_points, int32_t n_joints,
+                      const float* theta, float eps, const float* T34, const float* global_t,
+                      float* sm_out, float* G12_out, float* xyz_out, float* Rinv_out, void* stream);
+int apn_lbs_train_bwd(const float* pcd, const float* W, int64_t n_points, int32_t n_joints,
+                      const float* theta, float eps, const float* T34, const float* sm,
+                      const float* Rinv, const float* d_xyz, const float* d_Rinv, const float* d_sm,
+                      float* dW, float* dT34, float* d_global_t, float* d_theta, void* workspace,
+                      void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * Fused render pipeline stages (TemporalPoints.forward, temporalpoints.py:540-712).
  * ------------------------------------------------------------------------------------- */

@@ -751,10 +751,11 @@ def oracle_trainable(om: "OracleModel") -> dict:
 
 
 def oracle_forward_train(om: "OracleModel", t, render_kwargs, query_radius=0.01, xyz_min=None, xyz_max=None,
-                         knn_tree=None, blend="sum", jitter=0.0, jitter_seed=0):
+                         knn_tree=None, blend="sum", jitter=0.0, jitter_seed=0, t_hat_snap=None):
     """temporalpoints.py:540-712 + aggregate_pts (416-521) with autograd on (render_pcd_direct
     forced, no depth / weights outputs). ``xyz_min/xyz_max`` fix the sampling bbox (else the
-    cloud's, 423-427). Returns rgb_marched, rgb_marched_direct, t_hat_pcd, last_weights."""
+    cloud's, 423-427). ``t_hat_snap``: see below. Returns rgb_marched, rgb_marched_direct,
+    t_hat_pcd, last_weights."""
     rk = {k: (v.detach().cpu() if torch.is_tensor(v) else v) for k, v in render_kwargs.items()}
     R = len(rk["rays_o"]); K = om.K; bg = rk["bg"]
     t_embed = poc_fre(torch.as_tensor(t).reshape(1).float(), om.time_poc)
@@ -771,6 +772,10 @@ def oracle_forward_train(om: "OracleModel", t, render_kwargs, query_radius=0.01,
             return x
         sgn = torch.randint(0, 3, x.shape, generator=gen).float() - 1.0
         return x + x.detach() * (jitter * sgn)
+    if t_hat_snap is not None:
+        # take another device's warped cloud as the value (straight-through: the gradient still
+        # flows through this oracle's own LBS), so a 1-ulp difference cannot flip a kNN decision
+        t_hat = t_hat + (torch.as_tensor(t_hat_snap).detach().cpu().float() - t_hat).detach()
     t_hat = jit(t_hat)
     Rinv = jit(Rinv)
     pose_embedding = None
