@@ -58,6 +58,11 @@ SIGNATURES = {
     "apn_lbs_train_workspace_bytes": (SZ, [I64, I32]),
     "apn_lbs_train_fwd": (C.c_int, [P, P, I64, I32, P, F32, P, P, P, P, P, P, P]),
     "apn_lbs_train_bwd": (C.c_int, [P, P, I64, I32, P, F32, P, P, P, P, P, P, P, P, P, P, P, P]),
+    "apn_nbr_loss_workspace_bytes": (SZ, []),
+    "apn_nbr_tv_loss": (C.c_int, [P, I64, I32, P, I32, P, P, P]),
+    "apn_nbr_tv_loss_backward": (C.c_int, [P, I64, I32, P, I32, P, P, P, P, P]),
+    "apn_arap_loss": (C.c_int, [P, I64, P, I32, P, F32, P, P, P]),
+    "apn_arap_loss_backward": (C.c_int, [P, I64, P, I32, P, F32, P, P, P, P, P]),
     "apn_scan_workspace_bytes": (SZ, [I64]),
     "apn_scan_exclusive_i32": (C.c_int, [P, P, I64, P, P]),
     "apn_version": (C.c_char_p, []),

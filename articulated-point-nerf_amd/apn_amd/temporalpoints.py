@@ -239,7 +239,8 @@ class TemporalPoints(torch.nn.Module):
             pcd = self.canonical_pcd.detach().contiguous()
             _, nn_i = knn_points(pcd, pcd, self.neighbours)
             nn_distance = torch.sqrt(((pcd[:, None, :] - pcd[nn_i, :]) ** 2).sum(-1) + self.eps.to(pcd.device))
-            self._nn_cache = (nn_i, nn_distance)
+            from .train import reverse_csr
+            self._nn_cache = (nn_i, nn_distance) + reverse_csr(nn_i)
         return self._nn_cache
 
     @property
@@ -251,8 +252,11 @@ class TemporalPoints(torch.nn.Module):
         return self._canonical_knn()[1]
 
     def get_neighbour_weight_tv_loss(self):
-        diff = self._last_weights[:, None, :] - self._last_weights[self.nn_i, :]
-        return torch.abs(diff).mean()
+        """temporalpoints.py:714-716 as the fused HIP NbrTVLoss (no [N,K,J] gather, no scatter-add
+        backward)."""
+        from .train import NbrTVLoss
+        nn_i, _, rev_ptr, rev_edge = self._canonical_knn()
+        return NbrTVLoss.apply(self._last_weights, nn_i, rev_ptr, rev_edge)
 
     def get_weight_sparsity_loss(self):
         eps = self.eps.to(self._last_weights.device)
@@ -260,9 +264,10 @@ class TemporalPoints(torch.nn.Module):
                  + (1 - self._last_weights) * torch.log(1 - self._last_weights + eps)).mean()
 
     def get_arap_loss(self, warped_pcd, c=0.03):
-        eps = self.eps.to(warped_pcd.device)
-        warped_nn_distance = torch.sqrt((warped_pcd[:, None, :] - warped_pcd[self.nn_i, :]).pow(2).sum(-1) + eps)
-        return (self.nn_distance - warped_nn_distance).abs().sum()
+        """temporalpoints.py:723-725 as the fused HIP ArapLoss (gather-only backward)."""
+        from .train import ArapLoss
+        nn_i, nn_distance, rev_ptr, rev_edge = self._canonical_knn()
+        return ArapLoss.apply(warped_pcd, nn_i, nn_distance, float(self.eps), rev_ptr, rev_edge)
 
     def get_joint_arap_loss(self):
         joint_distance = (self.joints[self.bone_arap_mask][0::2, :] - self.joints[self.bone_arap_mask][1::2, :])

@@ -28,7 +28,8 @@ from ._lib import call, ptr, stream_ptr
 from .ops import Alphas2Weights, Raw2Alpha
 from .tineuvox import poc_fre
 
-__all__ = ["forward_train", "LBSTrain", "lbs_train", "lbs_blend", "inv3x3", "radius_knn", "ordered_bbox"]
+__all__ = ["forward_train", "LBSTrain", "lbs_train", "lbs_blend", "inv3x3", "radius_knn", "ordered_bbox",
+           "reverse_csr", "NbrTVLoss", "ArapLoss"]
 
 
 def ordered_bbox(xyz: torch.Tensor) -> torch.Tensor:
@@ -102,6 +103,79 @@ class LBSTrain(torch.autograd.Function):
         call("apn_lbs_train_bwd", ptr(pcd), ptr(Wc), N, J, ptr(th), ctx.eps, ptr(T), ptr(sm), ptr(Rinv), ptr(d_xyz),
              ptr(d_Rinv), ptr(d_sm), ptr(dW), ptr(dT), ptr(dgt), ptr(dth), ptr(ws), stream_ptr(dev))
         return dW, dth, dT, dgt, None, None
+
+
+def reverse_csr(nn_i: torch.Tensor):
+    """Reverse adjacency of the kNN graph nn_i [N,K] (int64): rev_ptr [N+1], rev_edge [N*K] = edge
+    ids i*K+k grouped by their target nn_i[i,k], ascending within a target (stable sort) -- the
+    in-edges the HIP loss backward gathers instead of an atomic scatter-add."""
+    N = nn_i.shape[0]
+    flat = nn_i.reshape(-1)
+    rev_edge = torch.argsort(flat, stable=True).contiguous()
+    rev_ptr = torch.zeros(N + 1, dtype=torch.int64, device=nn_i.device)
+    rev_ptr[1:] = torch.cumsum(torch.bincount(flat, minlength=N), 0)
+    return rev_ptr, rev_edge
+
+
+class NbrTVLoss(torch.autograd.Function):
+    """get_neighbour_weight_tv_loss (temporalpoints.py:714-716): mean |w_i - w_nn(i,k)| over
+    [N,K,J] as one fused HIP edge reduction (apn_nbr_tv_loss); backward apn_nbr_tv_loss_backward
+    (out-edges + reverse-CSR in-edges, no scatter). nn_i / rev_ptr / rev_edge are constants."""
+
+    @staticmethod
+    def forward(ctx, w, nn_i, rev_ptr, rev_edge):
+        L.require_cuda(w, nn_i, what="NbrTVLoss")
+        wc = w.detach().float().contiguous()
+        N, J = wc.shape
+        K = nn_i.shape[1]
+        dev = wc.device
+        loss = torch.empty((), device=dev)
+        ws = torch.empty(int(L.load().apn_nbr_loss_workspace_bytes()), dtype=torch.uint8, device=dev)
+        call("apn_nbr_tv_loss", ptr(wc), N, J, ptr(nn_i), K, ptr(loss), ptr(ws), stream_ptr(dev))
+        ctx.save_for_backward(wc, nn_i, rev_ptr, rev_edge)
+        return loss
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, d_loss):
+        wc, nn_i, rev_ptr, rev_edge = ctx.saved_tensors
+        N, J = wc.shape
+        dw = torch.empty_like(wc)
+        dl = d_loss.float().contiguous()
+        call("apn_nbr_tv_loss_backward", ptr(wc), N, J, ptr(nn_i), nn_i.shape[1], ptr(rev_ptr), ptr(rev_edge),
+             ptr(dl), ptr(dw), stream_ptr(wc.device))
+        return dw, None, None, None
+
+
+class ArapLoss(torch.autograd.Function):
+    """get_arap_loss (temporalpoints.py:723-725): sum_ik |d0_ik - sqrt(|x_i - x_nn(i,k)|^2 + eps)| as
+    one fused HIP edge reduction (apn_arap_loss); backward apn_arap_loss_backward (gathers only).
+    nn_i, the canonical distances d0 [N,K] and the reverse CSR are constants."""
+
+    @staticmethod
+    def forward(ctx, x, nn_i, d0, eps, rev_ptr, rev_edge):
+        L.require_cuda(x, nn_i, d0, what="ArapLoss")
+        xc = x.detach().float().contiguous()
+        N = xc.shape[0]
+        K = nn_i.shape[1]
+        dev = xc.device
+        d0c = d0.detach().float().contiguous()
+        loss = torch.empty((), device=dev)
+        ws = torch.empty(int(L.load().apn_nbr_loss_workspace_bytes()), dtype=torch.uint8, device=dev)
+        call("apn_arap_loss", ptr(xc), N, ptr(nn_i), K, ptr(d0c), float(eps), ptr(loss), ptr(ws), stream_ptr(dev))
+        ctx.save_for_backward(xc, nn_i, d0c, rev_ptr, rev_edge)
+        ctx.eps = float(eps)
+        return loss
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, d_loss):
+        xc, nn_i, d0c, rev_ptr, rev_edge = ctx.saved_tensors
+        dx = torch.empty_like(xc)
+        dl = d_loss.float().contiguous()
+        call("apn_arap_loss_backward", ptr(xc), xc.shape[0], ptr(nn_i), nn_i.shape[1], ptr(d0c), ctx.eps,
+             ptr(rev_ptr), ptr(rev_edge), ptr(dl), ptr(dx), stream_ptr(xc.device))
+        return dx, None, None, None, None, None
 
 
 def lbs_train(model, bone_Ts, global_t):

@@ -117,6 +117,26 @@ int apn_lbs_train_bwd(const float* pcd, const float* W, int64_t n_points, int32_
                       float* dW, float* dT34, float* d_global_t, float* d_theta, void* workspace,
                       void* stream);
 
+/* Neighbour-graph losses of the training step over the static canonical kNN graph nn_i [N,K]
+ * (int64, self first; temporalpoints.py:104-110). Replace the gather + autograd scatter-add of
+ * get_neighbour_weight_tv_loss (temporalpoints.py:714-716: mean |w_i - w_nn| over [N,K,J]) and
+ * get_arap_loss (temporalpoints.py:723-725: sum |d0_ik - sqrt(|x_i - x_nn|^2 + eps)|).
+ * Forward: loss_out[0] (device), block partials in `workspace` (apn_nbr_loss_workspace_bytes)
+ * reduced in a fixed order. Backward: d_loss is the device scalar dL/dloss; rev_ptr [N+1] /
+ * rev_edge [N*K] is the reverse CSR of the graph (edge ids i*K+k grouped by target, ascending);
+ * dw [N,J] / dx [N,3] are overwritten (gathers only, no atomics). */
+size_t apn_nbr_loss_workspace_bytes(void);
+int apn_nbr_tv_loss(const float* w, int64_t n_points, int32_t n_channels, const int64_t* nn_i, int32_t k,
+                    float* loss_out, void* workspace, void* stream);
+int apn_nbr_tv_loss_backward(const float* w, int64_t n_points, int32_t n_channels, const int64_t* nn_i,
+                             int32_t k, const int64_t* rev_ptr, const int64_t* rev_edge, const float* d_loss,
+                             float* dw, void* stream);
+int apn_arap_loss(const float* x, int64_t n_points, const int64_t* nn_i, int32_t k, const float* nn_dist0,
+                  float eps, float* loss_out, void* workspace, void* stream);
+int apn_arap_loss_backward(const float* x, int64_t n_points, const int64_t* nn_i, int32_t k,
+                           const float* nn_dist0, float eps, const int64_t* rev_ptr, const int64_t* rev_edge,
+                           const float* d_loss, float* dx, void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * Fused render pipeline stages (TemporalPoints.forward, temporalpoints.py:540-712).
  * ------------------------------------------------------------------------------------- */
