@@ -122,3 +122,27 @@ def test_temporalpoints_losses_route_to_hip():
     assert "ArapLoss" in type(arap.grad_fn).__name__
     assert abs(float(arap) - float(_arap_ref(x.detach().double(), nn_i, nn_d.double(), float(m.eps)))) < 1e-4
     assert "apn_amd" in sys.modules
+
+
+@pytest.mark.gpu
+@pytest.mark.autograd
+@pytest.mark.parametrize("M,K", [(1, 155), (300, 128), (4096 * 2 + 5, 155), (212736 + 7, 128)])
+def test_splitk_linear_vs_float64(M, K):
+    """SplitKLinear (training feat_net layers): output and all three gradients within fp32
+    rounding of the float64 autograd of torch.nn.functional.linear."""
+    from apn_amd.train import SplitKLinear
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(M)
+    x = torch.randn(M, K, generator=g)
+    w = torch.randn(128, K, generator=g) / K ** 0.5
+    b = torch.randn(128, generator=g)
+    dy = torch.randn(M, 128, generator=g)
+    ps64 = [t.double().to(dev).requires_grad_(True) for t in (x, w, b)]
+    torch.nn.functional.linear(*ps64).backward(dy.double().to(dev))
+    ps = [t.to(dev).requires_grad_(True) for t in (x, w, b)]
+    y = SplitKLinear.apply(*ps)
+    y.backward(dy.to(dev))
+    y64 = torch.nn.functional.linear(*[t.detach() for t in ps64])
+    for a, r, name in [(y, y64, "y")] + [(p.grad, q.grad, n) for p, q, n in zip(ps, ps64, "xwb")]:
+        err = float((a.double() - r).abs().max() / r.abs().max().clamp_min(1e-30))
+        assert err < 2e-6, (name, err)
