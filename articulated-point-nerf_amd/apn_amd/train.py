@@ -33,10 +33,18 @@ __all__ = ["forward_train", "LBSTrain", "lbs_train", "lbs_blend", "inv3x3", "rad
            "SplitKLinear", "feat_net_forward"]
 
 
+def cloud_min_max(xyz: torch.Tensor):
+    """(min [3], max [3]) of an [N,3] cloud, reduced along contiguous rows of its transpose (the
+    strided dim-0 reductions took ~0.15 ms each at 300k points); min/max are exact, so the values
+    equal xyz.min(0)/xyz.max(0)."""
+    xt = xyz.t().contiguous()
+    return xt.amin(dim=1), xt.amax(dim=1)
+
+
 def ordered_bbox(xyz: torch.Tensor) -> torch.Tensor:
     """Cloud min/max as the order-preserving int32 encoding the grid kernels read
     (``float_to_ordered`` in csrc/apn_common.h), 8 slots like the LBS kernel's bbox_ord."""
-    mm = torch.cat([xyz.min(dim=0)[0], xyz.max(dim=0)[0]]).float().contiguous()
+    mm = torch.cat(cloud_min_max(xyz)).float().contiguous()
     i = mm.view(torch.int32)
     out = torch.zeros(8, dtype=torch.int32, device=xyz.device)
     out[:6] = torch.where(i >= 0, i, i ^ 0x7fffffff)
@@ -335,7 +343,8 @@ def forward_train(model, t, render_depth=False, render_kwargs=None, query_radius
     qr = float(query_radius)
     if calc_min_max:
         xd = t_hat_pcd.detach()
-        bbox6 = torch.cat([xd.min(dim=0)[0] - qr, xd.max(dim=0)[0] + qr]).float().contiguous()
+        lo, hi = cloud_min_max(xd)
+        bbox6 = torch.cat([lo - qr, hi + qr]).float().contiguous()
     else:
         bbox6 = torch.cat([model.xyz_min, model.xyz_max]).float().contiguous()
     ray_pts, ray_id, step_id, s_i, n_bbox = radius_knn(model, t_hat_pcd, bbox6, rk, qr)

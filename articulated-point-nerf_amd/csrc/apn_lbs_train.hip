@@ -154,14 +154,21 @@ __global__ __launch_bounds__(LT_THREADS) void k_lbs_train_bwd(
   }
 }
 
+// one block per reduced value (12 J + 4 of them): the block's threads stride over the per-block
+// partials, then a fixed shuffle tree + a fixed combine of the wave sums (deterministic)
 __global__ __launch_bounds__(256) void k_lbs_train_reduce(const float* __restrict__ part, int nblocks, int J,
                                                           float* __restrict__ dT34, float* __restrict__ dgt,
                                                           float* __restrict__ dtheta) {
+  __shared__ float sw[4];
   const int nv = 12 * J + 4;
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= nv) return;
+  const int i = blockIdx.x;
   float v = 0.f;
-  for (int b = 0; b < nblocks; ++b) v += part[(int64_t)b * nv + i];
+  for (int b = threadIdx.x; b < nblocks; b += 256) v += part[(int64_t)b * nv + i];
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) sw[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  v = (sw[0] + sw[1]) + (sw[2] + sw[3]);
   if (i < 12 * J) dT34[i] = v;
   else if (i < 12 * J + 3) dgt[i - 12 * J] = v;
   else dtheta[0] = v;
@@ -197,7 +204,7 @@ extern "C" int apn_lbs_train_bwd(const float* pcd, const float* W, int64_t n, in
   float* part = (float*)workspace;
   hipLaunchKernelGGL(k_lbs_train_bwd, dim3(nb), dim3(LT_THREADS), 0, (hipStream_t)stream, pcd, W, n, (int)J, theta,
                      eps, T34, sm, Rinv, d_xyz, d_Rinv, d_sm, dW, part);
-  hipLaunchKernelGGL(k_lbs_train_reduce, dim3(ceil_div(12 * J + 4, 256)), dim3(256), 0, (hipStream_t)stream, part,
+  hipLaunchKernelGGL(k_lbs_train_reduce, dim3(12 * J + 4), dim3(256), 0, (hipStream_t)stream, part,
                      nb, (int)J, dT34, d_global_t, d_theta);
   return launch_status();
 }

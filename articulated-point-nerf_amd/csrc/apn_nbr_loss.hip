@@ -32,16 +32,22 @@ __device__ __forceinline__ float block_sum(float v) {
   return s;
 }
 
+// Indices are 32-bit (the C entry points require n * max(J, K) < 2^31): a 64-bit division per
+// element is a long software sequence on CDNA. KT = compile-time neighbour count (8, the
+// TemporalPoints default) or 0 = runtime Kr.
 // one thread per (point, channel): sum_k |w_i[j] - w_nn[j]|
+template <int KT>
 __global__ void __launch_bounds__(kLossThreads) k_tv_partial(const float* __restrict__ w, const int64_t* __restrict__ nn,
-                                                             int64_t n, int J, int K, float* __restrict__ partials) {
+                                                             int n, int J, int Kr, float* __restrict__ partials) {
+  const int K = KT ? KT : Kr;
   float acc = 0.f;
-  const int64_t total = n * J;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t i = t / J;
-    const int j = (int)(t - i * J);
+  const unsigned total = (unsigned)n * (unsigned)J;
+  for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const unsigned i = t / (unsigned)J;
+    const unsigned j = t - i * (unsigned)J;
     const float wi = w[t];
-    for (int k = 0; k < K; ++k) acc += fabsf(wi - w[nn[i * K + k] * J + j]);
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc += fabsf(wi - w[(unsigned)nn[i * K + k] * J + j]);
   }
   const float s = block_sum(acc);
   if (threadIdx.x == 0) partials[blockIdx.x] = s;
@@ -58,14 +64,16 @@ __device__ __forceinline__ float edge_dist(const float* __restrict__ x, int64_t 
   return sqrtf(u + eps);
 }
 
+template <int KT>
 __global__ void __launch_bounds__(kLossThreads) k_arap_partial(const float* __restrict__ x, const int64_t* __restrict__ nn,
-                                                               const float* __restrict__ d0, int64_t n, int K, float eps,
+                                                               const float* __restrict__ d0, int n, int Kr, float eps,
                                                                float* __restrict__ partials) {
+  const int K = KT ? KT : Kr;
   float acc = 0.f;
-  const int64_t total = n * K;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+  const unsigned total = (unsigned)n * (unsigned)K;
+  for (unsigned e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
     float dx, dy, dz;
-    const float s = edge_dist(x, e / K, nn[e], eps, dx, dy, dz);
+    const float s = edge_dist(x, e / (unsigned)K, nn[e], eps, dx, dy, dz);
     acc += fabsf(d0[e] - s);
   }
   const float s = block_sum(acc);
@@ -82,19 +90,23 @@ __global__ void __launch_bounds__(kLossThreads) k_reduce_partials(const float* _
 }
 
 // d w[i,j] = dL/count * (sum_k sgn(w_i - w_nn(i,k)) - sum_{e in rev(i)} sgn(w_src(e) - w_i))
+template <int KT>
 __global__ void __launch_bounds__(kLossThreads) k_tv_bwd(const float* __restrict__ w, const int64_t* __restrict__ nn,
                                                          const int64_t* __restrict__ rev_ptr,
-                                                         const int64_t* __restrict__ rev_edge, int64_t n, int J, int K,
+                                                         const int64_t* __restrict__ rev_edge, int n, int J, int Kr,
                                                          const float* __restrict__ d_loss, float inv_count,
                                                          float* __restrict__ dw) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n * J) return;
-  const int64_t i = t / J;
-  const int j = (int)(t - i * J);
+  const int K = KT ? KT : Kr;
+  const unsigned t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (unsigned)n * (unsigned)J) return;
+  const unsigned i = t / (unsigned)J;
+  const unsigned j = t - i * (unsigned)J;
   const float wi = w[t];
   float s = 0.f;
-  for (int k = 0; k < K; ++k) s += sgnf(wi - w[nn[i * K + k] * J + j]);
-  for (int64_t e = rev_ptr[i], e1 = rev_ptr[i + 1]; e < e1; ++e) s -= sgnf(w[(rev_edge[e] / K) * J + j] - wi);
+#pragma unroll
+  for (int k = 0; k < K; ++k) s += sgnf(wi - w[(unsigned)nn[i * K + k] * J + j]);
+  for (unsigned e = (unsigned)rev_ptr[i], e1 = (unsigned)rev_ptr[i + 1]; e < e1; ++e)
+    s -= sgnf(w[((unsigned)rev_edge[e] / (unsigned)K) * J + j] - wi);
   dw[t] = (d_loss[0] * inv_count) * s;
 }
 
@@ -102,27 +114,30 @@ __global__ void __launch_bounds__(kLossThreads) k_tv_bwd(const float* __restrict
 // c = (-sgn(d0 - s) dL) / (2 s)   (abs, sqrt and pow(2) backward in torch's order)
 __device__ __forceinline__ float arap_coef(float d0, float s, float g) { return (-sgnf(d0 - s) * g) / (2.f * s); }
 
+template <int KT>
 __global__ void __launch_bounds__(kLossThreads) k_arap_bwd(const float* __restrict__ x, const int64_t* __restrict__ nn,
                                                            const float* __restrict__ d0,
                                                            const int64_t* __restrict__ rev_ptr,
-                                                           const int64_t* __restrict__ rev_edge, int64_t n, int K,
+                                                           const int64_t* __restrict__ rev_edge, int n, int Kr,
                                                            float eps, const float* __restrict__ d_loss,
                                                            float* __restrict__ dx_out) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int K = KT ? KT : Kr;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const float g = d_loss[0];
   float gx = 0.f, gy = 0.f, gz = 0.f;
+#pragma unroll
   for (int k = 0; k < K; ++k) {
-    const int64_t e = i * K + k;
+    const int e = i * K + k;
     float dx, dy, dz;
     const float s = edge_dist(x, i, nn[e], eps, dx, dy, dz);
     const float c = arap_coef(d0[e], s, g);
     gx += c * (2.f * dx); gy += c * (2.f * dy); gz += c * (2.f * dz);
   }
-  for (int64_t r = rev_ptr[i], r1 = rev_ptr[i + 1]; r < r1; ++r) {
-    const int64_t e = rev_edge[r];
+  for (unsigned r = (unsigned)rev_ptr[i], r1 = (unsigned)rev_ptr[i + 1]; r < r1; ++r) {
+    const unsigned e = (unsigned)rev_edge[r];
     float dx, dy, dz;
-    const float s = edge_dist(x, e / K, i, eps, dx, dy, dz);
+    const float s = edge_dist(x, e / (unsigned)K, i, eps, dx, dy, dz);
     const float c = arap_coef(d0[e], s, g);
     gx -= c * (2.f * dx); gy -= c * (2.f * dy); gz -= c * (2.f * dz);
   }
@@ -135,6 +150,15 @@ using namespace apn;
 
 extern "C" size_t apn_nbr_loss_workspace_bytes(void) { return (size_t)kLossBlocks * sizeof(float); }
 
+// 32-bit element / edge indexing in the kernels
+static inline bool fits32(int64_t n, int64_t a, int64_t b) { return n * (a > b ? a : b) < ((int64_t)1 << 31); }
+
+#define APN_LAUNCH_K(kern, K, grid, ...)                                                                   \
+  do {                                                                                                     \
+    if ((K) == 8) hipLaunchKernelGGL(kern<8>, grid, dim3(kLossThreads), 0, (hipStream_t)stream, __VA_ARGS__); \
+    else hipLaunchKernelGGL(kern<0>, grid, dim3(kLossThreads), 0, (hipStream_t)stream, __VA_ARGS__);          \
+  } while (0)
+
 static inline int partial_blocks(int64_t work) {
   const int b = ceil_div(work, kLossThreads);
   return b < 1 ? 1 : (b > kLossBlocks ? kLossBlocks : b);
@@ -143,9 +167,9 @@ static inline int partial_blocks(int64_t work) {
 extern "C" int apn_nbr_tv_loss(const float* w, int64_t n_points, int32_t n_channels, const int64_t* nn_i,
                                int32_t k, float* loss_out, void* workspace, void* stream) {
   if (n_points <= 0 || n_channels <= 0 || k <= 0 || !w || !nn_i || !loss_out || !workspace) return APN_ERR_ARG;
+  if (!fits32(n_points, n_channels, k)) return APN_ERR_ARG;
   const int nb = partial_blocks(n_points * n_channels);
-  hipLaunchKernelGGL(k_tv_partial, dim3(nb), dim3(kLossThreads), 0, (hipStream_t)stream, w, nn_i, n_points,
-                     (int)n_channels, (int)k, (float*)workspace);
+  APN_LAUNCH_K(k_tv_partial, k, dim3(nb), w, nn_i, (int)n_points, (int)n_channels, (int)k, (float*)workspace);
   const float inv = (float)(1.0 / ((double)n_points * (double)k * (double)n_channels));
   hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kLossThreads), 0, (hipStream_t)stream,
                      (const float*)workspace, nb, inv, true, loss_out);
@@ -157,19 +181,19 @@ extern "C" int apn_nbr_tv_loss_backward(const float* w, int64_t n_points, int32_
                                         const float* d_loss, float* dw, void* stream) {
   if (n_points <= 0 || n_channels <= 0 || k <= 0 || !w || !nn_i || !rev_ptr || !rev_edge || !d_loss || !dw)
     return APN_ERR_ARG;
+  if (!fits32(n_points, n_channels, k)) return APN_ERR_ARG;
   const float inv = (float)(1.0 / ((double)n_points * (double)k * (double)n_channels));
-  hipLaunchKernelGGL(k_tv_bwd, dim3(ceil_div(n_points * n_channels, kLossThreads)), dim3(kLossThreads), 0,
-                     (hipStream_t)stream, w, nn_i, rev_ptr, rev_edge, n_points, (int)n_channels, (int)k, d_loss, inv,
-                     dw);
+  APN_LAUNCH_K(k_tv_bwd, k, dim3(ceil_div(n_points * n_channels, kLossThreads)), w, nn_i, rev_ptr, rev_edge,
+               (int)n_points, (int)n_channels, (int)k, d_loss, inv, dw);
   return launch_status();
 }
 
 extern "C" int apn_arap_loss(const float* x, int64_t n_points, const int64_t* nn_i, int32_t k, const float* nn_dist0,
                              float eps, float* loss_out, void* workspace, void* stream) {
   if (n_points <= 0 || k <= 0 || !x || !nn_i || !nn_dist0 || !loss_out || !workspace) return APN_ERR_ARG;
+  if (!fits32(n_points, 3, k)) return APN_ERR_ARG;
   const int nb = partial_blocks(n_points * k);
-  hipLaunchKernelGGL(k_arap_partial, dim3(nb), dim3(kLossThreads), 0, (hipStream_t)stream, x, nn_i, nn_dist0,
-                     n_points, (int)k, eps, (float*)workspace);
+  APN_LAUNCH_K(k_arap_partial, k, dim3(nb), x, nn_i, nn_dist0, (int)n_points, (int)k, eps, (float*)workspace);
   hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kLossThreads), 0, (hipStream_t)stream,
                      (const float*)workspace, nb, 1.f, false, loss_out);
   return launch_status();
@@ -180,7 +204,8 @@ extern "C" int apn_arap_loss_backward(const float* x, int64_t n_points, const in
                                       const int64_t* rev_edge, const float* d_loss, float* dx, void* stream) {
   if (n_points <= 0 || k <= 0 || !x || !nn_i || !nn_dist0 || !rev_ptr || !rev_edge || !d_loss || !dx)
     return APN_ERR_ARG;
-  hipLaunchKernelGGL(k_arap_bwd, dim3(ceil_div(n_points, kLossThreads)), dim3(kLossThreads), 0, (hipStream_t)stream,
-                     x, nn_i, nn_dist0, rev_ptr, rev_edge, n_points, (int)k, eps, d_loss, dx);
+  if (!fits32(n_points, 3, k)) return APN_ERR_ARG;
+  APN_LAUNCH_K(k_arap_bwd, k, dim3(ceil_div(n_points, kLossThreads)), x, nn_i, nn_dist0, rev_ptr, rev_edge,
+               (int)n_points, (int)k, eps, d_loss, dx);
   return launch_status();
 }

@@ -124,7 +124,8 @@ int apn_lbs_train_bwd(const float* pcd, const float* W, int64_t n_points, int32_
  * Forward: loss_out[0] (device), block partials in `workspace` (apn_nbr_loss_workspace_bytes)
  * reduced in a fixed order. Backward: d_loss is the device scalar dL/dloss; rev_ptr [N+1] /
  * rev_edge [N*K] is the reverse CSR of the graph (edge ids i*K+k grouped by target, ascending);
- * dw [N,J] / dx [N,3] are overwritten (gathers only, no atomics). */
+ * dw [N,J] / dx [N,3] are overwritten (gathers only, no atomics). Requires n_points * max(n_channels
+ * or 3, k) < 2^31 (32-bit indexing in the kernels). */
 size_t apn_nbr_loss_workspace_bytes(void);
 int apn_nbr_tv_loss(const float* w, int64_t n_points, int32_t n_channels, const int64_t* nn_i, int32_t k,
                     float* loss_out, void* workspace, void* stream);
