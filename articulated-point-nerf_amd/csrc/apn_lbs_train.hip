@@ -11,13 +11,16 @@
 //   dsm_tot_j = dsm_j + <dG, T_j>;  dz_j = sm_j (dsm_tot_j - sum_k sm_k dsm_tot_k)
 //   dW_j = dz_j / th;  dtheta += -sum_j dz_j W_j / th^2 (only while theta > eps)
 //   dT_j += sm_j dG;  dglobal_t += dx
-// The J x 12 + 4 parameter reductions are wave-reduced with DPP/shuffles, summed per block in a
-// fixed order and then over blocks by one reduction kernel: deterministic, no atomics.
+// dT = sm^T dG is a [J x N] . [N x 12] product with a long N: each backward block stages its
+// points' sm rows and dG rows in LDS and computes its [J x 12] partial there (thread per output,
+// fixed point order); dglobal_t / dtheta are wave-reduced. The per-block partials are summed by
+// one block per value in a fixed order: deterministic, no atomics.
 #include "apn_common.h"
 
 namespace apn {
 
 constexpr int LT_THREADS = 256;
+constexpr int LB_THREADS = 128;   // backward: points per block (LDS tile 3 (J+1) + 13 floats per point)
 constexpr int LT_MAXJ = 64;
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -71,16 +74,32 @@ __global__ __launch_bounds__(LT_THREADS) void k_lbs_train_fwd(const float* __res
 }
 
 // part layout per block: [J*12] dT, [3] dglobal_t, [1] dtheta
-__global__ __launch_bounds__(LT_THREADS) void k_lbs_train_bwd(
+__global__ __launch_bounds__(LB_THREADS) void k_lbs_train_bwd(
     const float* __restrict__ pcd, const float* __restrict__ W, int64_t n, int J, const float* __restrict__ theta,
     float eps, const float* __restrict__ T34, const float* __restrict__ sm, const float* __restrict__ Rinv,
     const float* __restrict__ dxyz, const float* __restrict__ dRinv, const float* __restrict__ dsm,
     float* __restrict__ dW, float* __restrict__ part) {
   __shared__ float sT[LT_MAXJ * 12];
-  __shared__ float sRed[LT_THREADS / 64][LT_MAXJ * 12 + 4];
-  for (int i = threadIdx.x; i < J * 12; i += LT_THREADS) sT[i] = T34[i];
+  __shared__ float sRed[LB_THREADS / 64][4];
+  extern __shared__ float dyn[];
+  const int sstride = J + 1;                 // odd strides: conflict-free per-row access
+  float* sS = dyn;                            // [LB_THREADS][J + 1]  sm rows of the block's points
+  float* sD = sS + LB_THREADS * sstride;      // [LB_THREADS][J + 1]  dsm rows, then the dW rows
+  float* sW = sD + LB_THREADS * sstride;      // [LB_THREADS][J + 1]  W rows
+  float* sG = sW + LB_THREADS * sstride;      // [LB_THREADS][13]     dG rows
+  for (int i = threadIdx.x; i < J * 12; i += LB_THREADS) sT[i] = T34[i];
+  // the block's rows of sm / dsm / W are contiguous: coalesced loads into the LDS tiles
+  const int64_t p0 = (int64_t)blockIdx.x * LB_THREADS;
+  const int rows = (int)(n - p0 < LB_THREADS ? n - p0 : LB_THREADS);
+  const int cnt = rows * J;
+  for (int i = threadIdx.x; i < cnt; i += LB_THREADS) {
+    const int r = i / J, c = i - r * J;
+    sS[r * sstride + c] = sm[p0 * J + i];
+    sD[r * sstride + c] = dsm ? dsm[p0 * J + i] : 0.f;
+    sW[r * sstride + c] = W[p0 * J + i];
+  }
   __syncthreads();
-  const int64_t p = (int64_t)blockIdx.x * LT_THREADS + threadIdx.x;
+  const int64_t p = p0 + threadIdx.x;
   const bool live = p < n;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const float th_raw = theta[0];
@@ -112,45 +131,55 @@ __global__ __launch_bounds__(LT_THREADS) void k_lbs_train_bwd(
 #pragma unroll
     for (int k = 0; k < 12; ++k) dG[k] = 0.f;
   }
-  const float* smr = sm + q * J;
-  const float* dsr = dsm ? dsm + q * J : nullptr;
+#pragma unroll
+  for (int k = 0; k < 12; ++k) sG[threadIdx.x * 13 + k] = dG[k];
+  float* smr = sS + threadIdx.x * sstride;
+  float* dsr = sD + threadIdx.x * sstride;
+  const float* wr = sW + threadIdx.x * sstride;
   // pass 1: sum_k sm_k dsm_tot_k
   float ssd = 0.f;
   for (int j = 0; j < J; ++j) {
-    float t = dsr ? dsr[j] : 0.f;
+    float t = live ? dsr[j] : 0.f;
 #pragma unroll
     for (int k = 0; k < 12; ++k) t += dG[k] * sT[12 * j + k];
-    ssd += smr[j] * t;
+    ssd += (live ? smr[j] : 0.f) * t;
   }
-  // pass 2: dW, dtheta, and the dT wave sums
+  // pass 2: dW (into the dsm row, stored coalesced below), dtheta; dead rows of the sm tile
+  // are zeroed for the dT partial
   float dth = 0.f;
-  const float* wr = W + q * J;
   for (int j = 0; j < J; ++j) {
-    float t = dsr ? dsr[j] : 0.f;
+    float t = live ? dsr[j] : 0.f;
 #pragma unroll
     for (int k = 0; k < 12; ++k) t += dG[k] * sT[12 * j + k];
     const float s_j = live ? smr[j] : 0.f;
     const float dz = s_j * (t - ssd);
-    if (live) dW[q * J + j] = dz / th;
-    dth -= dz * wr[j];
-#pragma unroll
-    for (int k = 0; k < 12; ++k) {
-      const float v = wave_sum(s_j * dG[k]);
-      if (lane == 0) sRed[wid][12 * j + k] = v;
-    }
+    dsr[j] = dz / th;
+    dth -= dz * (live ? wr[j] : 0.f);
+    smr[j] = s_j;
   }
   dth = th_raw > eps ? dth / (th * th) : 0.f;
   const float e0 = wave_sum(dx[0]), e1 = wave_sum(dx[1]), e2 = wave_sum(dx[2]), e3 = wave_sum(live ? dth : 0.f);
-  if (lane == 0) {
-    sRed[wid][12 * J] = e0; sRed[wid][12 * J + 1] = e1; sRed[wid][12 * J + 2] = e2; sRed[wid][12 * J + 3] = e3;
-  }
+  if (lane == 0) { sRed[wid][0] = e0; sRed[wid][1] = e1; sRed[wid][2] = e2; sRed[wid][3] = e3; }
   __syncthreads();
+  for (int i = threadIdx.x; i < cnt; i += LB_THREADS) {
+    const int r = i / J, c = i - r * J;
+    dW[p0 * J + i] = sD[r * sstride + c];
+  }
   const int nv = 12 * J + 4;
-  for (int i = threadIdx.x; i < nv; i += LT_THREADS) {
+  float* out = part + (int64_t)blockIdx.x * nv;
+  // dT partial: thread per (j, k), the block's points in order
+  for (int o = threadIdx.x; o < 12 * J; o += LB_THREADS) {
+    const int j = o / 12, k = o - 12 * j;
+    float acc = 0.f;
+#pragma unroll 8
+    for (int r = 0; r < LB_THREADS; ++r) acc += sS[r * sstride + j] * sG[r * 13 + k];
+    out[o] = acc;
+  }
+  if (threadIdx.x < 4) {
     float v = 0.f;
 #pragma unroll
-    for (int w = 0; w < LT_THREADS / 64; ++w) v += sRed[w][i];
-    part[(int64_t)blockIdx.x * nv + i] = v;
+    for (int w = 0; w < LB_THREADS / 64; ++w) v += sRed[w][threadIdx.x];
+    out[12 * J + threadIdx.x] = v;
   }
 }
 
@@ -179,7 +208,7 @@ __global__ __launch_bounds__(256) void k_lbs_train_reduce(const float* __restric
 using namespace apn;
 
 extern "C" size_t apn_lbs_train_workspace_bytes(int64_t n_points, int32_t n_joints) {
-  return (size_t)ceil_div(n_points > 0 ? n_points : 1, LT_THREADS) * (12 * (size_t)n_joints + 4) * sizeof(float);
+  return (size_t)ceil_div(n_points > 0 ? n_points : 1, LB_THREADS) * (12 * (size_t)n_joints + 4) * sizeof(float);
 }
 
 extern "C" int apn_lbs_train_fwd(const float* pcd, const float* W, int64_t n, int32_t J, const float* theta,
@@ -200,9 +229,10 @@ extern "C" int apn_lbs_train_bwd(const float* pcd, const float* W, int64_t n, in
   if (n < 1 || J < 1 || J > LT_MAXJ) return APN_ERR_ARG;
   if (!pcd || !W || !theta || !T34 || !sm || !Rinv || !dW || !dT34 || !d_global_t || !d_theta || !workspace)
     return APN_ERR_ARG;
-  const int nb = ceil_div(n, LT_THREADS);
+  const int nb = ceil_div(n, LB_THREADS);
   float* part = (float*)workspace;
-  hipLaunchKernelGGL(k_lbs_train_bwd, dim3(nb), dim3(LT_THREADS), 0, (hipStream_t)stream, pcd, W, n, (int)J, theta,
+  const size_t lds = (size_t)LB_THREADS * (3 * (J + 1) + 13) * sizeof(float);
+  hipLaunchKernelGGL(k_lbs_train_bwd, dim3(nb), dim3(LB_THREADS), lds, (hipStream_t)stream, pcd, W, n, (int)J, theta,
                      eps, T34, sm, Rinv, d_xyz, d_Rinv, d_sm, dW, part);
   hipLaunchKernelGGL(k_lbs_train_reduce, dim3(12 * J + 4), dim3(256), 0, (hipStream_t)stream, part,
                      nb, (int)J, dT34, d_global_t, d_theta);
