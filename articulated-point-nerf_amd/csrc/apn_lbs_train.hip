@@ -37,27 +37,43 @@ __global__ __launch_bounds__(LT_THREADS) void k_lbs_train_fwd(const float* __res
                                                               float* __restrict__ G12, float* __restrict__ xyz,
                                                               float* __restrict__ Rinv) {
   __shared__ float sT[LT_MAXJ * 12];
+  extern __shared__ float tile[];   // [LT_THREADS][J + 1]: the block's W rows, then its sm rows
+  const int sstride = J + 1;
   for (int i = threadIdx.x; i < J * 12; i += LT_THREADS) sT[i] = T34[i];
+  const int64_t p0 = (int64_t)blockIdx.x * LT_THREADS;
+  const int rows = (int)(n - p0 < LT_THREADS ? n - p0 : LT_THREADS);
+  const int cnt = rows * J;
+  for (int i = threadIdx.x; i < cnt; i += LT_THREADS) {   // coalesced: the rows are contiguous
+    const int r = i / J;
+    tile[r * sstride + (i - r * J)] = W[p0 * J + i];
+  }
   __syncthreads();
-  const int64_t p = (int64_t)blockIdx.x * LT_THREADS + threadIdx.x;
-  if (p >= n) return;
+  const int64_t p = p0 + threadIdx.x;
+  const bool live = p < n;
   const float th = fmaxf(eps, theta[0]);
-  const float* w = W + p * J;
-  float mx = -INFINITY;
-  for (int j = 0; j < J; ++j) mx = fmaxf(mx, w[j] / th);
-  float s = 0.f;
-  for (int j = 0; j < J; ++j) s += expf(w[j] / th - mx);
-  const float inv_s = 1.f / s;
+  float* w = tile + threadIdx.x * sstride;
   float g[12];
 #pragma unroll
   for (int k = 0; k < 12; ++k) g[k] = 0.f;
-  float* smr = sm + p * J;
-  for (int j = 0; j < J; ++j) {
-    const float v = expf(w[j] / th - mx) * inv_s;
-    smr[j] = v;
+  if (live) {
+    float mx = -INFINITY;
+    for (int j = 0; j < J; ++j) mx = fmaxf(mx, w[j] / th);
+    float s = 0.f;
+    for (int j = 0; j < J; ++j) s += expf(w[j] / th - mx);
+    const float inv_s = 1.f / s;
+    for (int j = 0; j < J; ++j) {
+      const float v = expf(w[j] / th - mx) * inv_s;
+      w[j] = v;
 #pragma unroll
-    for (int k = 0; k < 12; ++k) g[k] += v * sT[12 * j + k];
+      for (int k = 0; k < 12; ++k) g[k] += v * sT[12 * j + k];
+    }
   }
+  __syncthreads();
+  for (int i = threadIdx.x; i < cnt; i += LT_THREADS) {
+    const int r = i / J;
+    sm[p0 * J + i] = tile[r * sstride + (i - r * J)];
+  }
+  if (!live) return;
   const float px = pcd[3 * p], py = pcd[3 * p + 1], pz = pcd[3 * p + 2];
 #pragma unroll
   for (int r = 0; r < 3; ++r)
@@ -217,7 +233,8 @@ extern "C" int apn_lbs_train_fwd(const float* pcd, const float* W, int64_t n, in
   if (n < 0 || J < 1 || J > LT_MAXJ) return APN_ERR_ARG;
   if (n == 0) return APN_OK;
   if (!pcd || !W || !theta || !T34 || !global_t || !sm_out || !G12_out || !xyz_out || !Rinv_out) return APN_ERR_ARG;
-  hipLaunchKernelGGL(k_lbs_train_fwd, dim3(ceil_div(n, LT_THREADS)), dim3(LT_THREADS), 0, (hipStream_t)stream, pcd,
+  hipLaunchKernelGGL(k_lbs_train_fwd, dim3(ceil_div(n, LT_THREADS)), dim3(LT_THREADS),
+                     (size_t)LT_THREADS * (J + 1) * sizeof(float), (hipStream_t)stream, pcd,
                      W, n, (int)J, theta, eps, T34, global_t, sm_out, G12_out, xyz_out, Rinv_out);
   return launch_status();
 }
