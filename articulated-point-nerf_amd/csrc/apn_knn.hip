@@ -1633,6 +1633,50 @@ extern "C" int apn_nn1_distance(const float* xyz, int64_t n_points, float eps, i
   return launch_status();
 }
 
+// Small sets (the chamfer losses: a few thousand points on each side, often 2D pixel sets with
+// a zero z): every query scans every point through 256-point LDS tiles -- no bbox / grid build
+// launches, no ring search over a degenerate grid. Same distance expression and tie rule
+// (knn_insert) as k_knn_points, so the result is the same brute-force answer.
+constexpr int KNN_BRUTE_Q = 64;      // queries per block (more blocks for small M)
+constexpr int KNN_BRUTE_TILE = 256;  // points per LDS tile
+template <int K>
+__global__ __launch_bounds__(KNN_BRUTE_Q) void k_knn_brute(const float* __restrict__ q, int64_t M,
+                                                           const float* __restrict__ pts, int64_t N, int k_out,
+                                                           int64_t* __restrict__ idx_out,
+                                                           float* __restrict__ d2_out) {
+  __shared__ float4 tile[KNN_BRUTE_TILE];
+  const int64_t m = (int64_t)blockIdx.x * KNN_BRUTE_Q + threadIdx.x;
+  const bool live = m < M;
+  const float qx = live ? q[3 * m] : 0.f, qy = live ? q[3 * m + 1] : 0.f, qz = live ? q[3 * m + 2] : 0.f;
+  float bd[K];
+  int bi[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) { bd[j] = INFINITY; bi[j] = 0x7fffffff; }
+  for (int64_t base = 0; base < N; base += KNN_BRUTE_TILE) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < KNN_BRUTE_TILE; i += KNN_BRUTE_Q) {
+      const int64_t n = base + i;
+      tile[i] = n < N ? make_float4(pts[3 * n], pts[3 * n + 1], pts[3 * n + 2], 0.f) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    __syncthreads();
+    const int cnt = (int)(N - base < KNN_BRUTE_TILE ? N - base : KNN_BRUTE_TILE);
+    for (int i = 0; i < cnt; ++i) {
+      const float4 P = tile[i];
+      const float dx = qx - P.x, dy = qy - P.y, dz = qz - P.z;
+      const float d = (dx * dx + dy * dy) + dz * dz;
+      knn_insert<K>(d, (int)(base + i), bd, bi);
+    }
+  }
+  if (!live) return;
+  for (int j = 0; j < k_out; ++j) {
+    idx_out[m * k_out + j] = bi[j];
+    d2_out[m * k_out + j] = bd[j];
+  }
+}
+
+// brute force when the whole pair count is small (and the grid would cost more than the scan)
+static inline bool knn_points_brute(int64_t M, int64_t N) { return N <= 16384 && M * N <= ((int64_t)1 << 27); }
+
 extern "C" int apn_knn_points(const float* q, int64_t n_queries, const float* pts, int64_t n_points, int32_t k,
                               int32_t cell_cap, float* sorted_pts4, int32_t* bbox_ord, void* grid_workspace,
                               int64_t* idx_out, float* d2_out, void* stream) {
@@ -1640,6 +1684,16 @@ extern "C" int apn_knn_points(const float* q, int64_t n_queries, const float* pt
       !grid_workspace || (n_queries > 0 && (!q || !idx_out || !d2_out)))
     return APN_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
+  if (n_queries > 0 && knn_points_brute(n_queries, n_points)) {
+    auto brute = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(ceil_div(n_queries, KNN_BRUTE_Q)), dim3(KNN_BRUTE_Q), 0, s, q, n_queries, pts,
+                         n_points, k, idx_out, d2_out);
+    };
+    if (k == 1) brute(k_knn_brute<1>);
+    else if (k <= 8) brute(k_knn_brute<8>);
+    else brute(k_knn_brute<16>);
+    return launch_status();
+  }
   hipLaunchKernelGGL(k_bbox_init2, dim3(1), dim3(64), 0, s, bbox_ord);
   hipLaunchKernelGGL(k_bbox_from_points, dim3(ceil_div(n_points, 256)), dim3(256), 0, s, pts, n_points, bbox_ord);
   int st = apn_grid_build(pts, n_points, bbox_ord, 0.01f, cell_cap, sorted_pts4, grid_workspace, stream);

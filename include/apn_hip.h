@@ -236,7 +236,9 @@ int apn_nn1_distance(const float* xyz, int64_t n_points, float eps, int32_t cell
  * pykeops `LazyTensor` argKmin of the training losses (temporalpoints.py:104-111, 737-748, 777-780)
  * and of nn_i / nn_distance: grid over pts (scratch sorted_pts4 [n_points,4], bbox_ord [8],
  * grid_workspace of apn_grid_workspace_bytes(n_points, cell_cap)), ring search with an exact stop
- * rule, full scan for queries still open after 64 rings. idx_out / d2_out [n_queries,k], ascending
+ * rule, full scan for queries still open after 64 rings. Small sets (n_points <= 16384 and
+ * n_queries * n_points <= 2^27: the chamfer losses) skip the grid and scan all points through LDS
+ * tiles (the scratch buffers are then untouched). idx_out / d2_out [n_queries,k], ascending
  * squared distance, ties by index (pykeops leaves their order unspecified). */
 int apn_knn_points(const float* q, int64_t n_queries, const float* pts, int64_t n_points, int32_t k,
                    int32_t cell_cap, float* sorted_pts4, int32_t* bbox_ord, void* grid_workspace,

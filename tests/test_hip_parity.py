@@ -695,6 +695,25 @@ def test_knn_points_bit_exact(dev, k):
     assert np.all(idx.cpu().numpy()[-100:, 0] == np.arange(100))
 
 
+@pytest.mark.parametrize("k", [1, 8, 16])
+def test_knn_points_small_sets_bit_exact(dev, k):
+    """The small-set path of apn_knn_points (LDS-tiled scan, no grid): the 2D chamfer case --
+    pixel coordinates padded with z = 0, duplicates for index ties, a ragged last tile -- and a
+    3D set, vs brute force: indices and squared distances bit-exact."""
+    from apn_amd.ops import knn_points
+    rng = np.random.default_rng(7)
+    pix = rng.uniform(0, 800, (3001, 2)).astype(F32)
+    pix[1000:1005] = pix[5]   # exact duplicates: ties by index (a group of 6 fits the oracle's K+6 candidates)
+    pts2 = np.concatenate([pix, np.zeros((len(pix), 1), F32)], 1)
+    q2 = np.concatenate([rng.uniform(-50, 850, (2999, 2)).astype(F32), np.zeros((2999, 1), F32)], 1)
+    pts3 = rng.normal(size=(777, 3)).astype(F32)
+    for q, pts in ((q2, pts2), (pts2, q2), (pts3[:100], pts3)):
+        d2, idx = knn_points(torch.from_numpy(q).to(dev), torch.from_numpy(pts).to(dev), k)
+        d_ref, i_ref = O.knn_kmin(q, pts, k, use_tree=False)
+        assert np.array_equal(idx.cpu().numpy(), i_ref)
+        assert np.array_equal(d2.cpu().numpy(), d_ref)
+
+
 @pytest.mark.autograd
 def test_training_losses_vs_cpu(golden_model, dev):
     """temporalpoints.py:714-800 losses on the golden model: the HIP-kNN versions equal the same
