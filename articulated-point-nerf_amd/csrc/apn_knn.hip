@@ -1634,18 +1634,23 @@ extern "C" int apn_nn1_distance(const float* xyz, int64_t n_points, float eps, i
 }
 
 // Small sets (the chamfer losses: a few thousand points on each side, often 2D pixel sets with
-// a zero z): every query scans every point through 256-point LDS tiles -- no bbox / grid build
+// a zero z): every query scans every point through 512-point LDS tiles, split over 8 waves
+// (lane = query, wave = point slice) and merged in LDS -- no bbox / grid build
 // launches, no ring search over a degenerate grid. Same distance expression and tie rule
 // (knn_insert) as k_knn_points, so the result is the same brute-force answer.
-constexpr int KNN_BRUTE_Q = 64;      // queries per block (more blocks for small M)
-constexpr int KNN_BRUTE_TILE = 256;  // points per LDS tile
+constexpr int KNN_BRUTE_Q = 64;      // queries per block (one per lane of a wave)
+constexpr int KNN_BRUTE_S = 8;       // waves per block: each scans every 8th point of a tile
+constexpr int KNN_BRUTE_TILE = 512;  // points per LDS tile
 template <int K>
-__global__ __launch_bounds__(KNN_BRUTE_Q) void k_knn_brute(const float* __restrict__ q, int64_t M,
-                                                           const float* __restrict__ pts, int64_t N, int k_out,
-                                                           int64_t* __restrict__ idx_out,
-                                                           float* __restrict__ d2_out) {
+__global__ __launch_bounds__(KNN_BRUTE_Q * KNN_BRUTE_S) void k_knn_brute(const float* __restrict__ q, int64_t M,
+                                                                         const float* __restrict__ pts, int64_t N,
+                                                                         int k_out, int64_t* __restrict__ idx_out,
+                                                                         float* __restrict__ d2_out) {
   __shared__ float4 tile[KNN_BRUTE_TILE];
-  const int64_t m = (int64_t)blockIdx.x * KNN_BRUTE_Q + threadIdx.x;
+  __shared__ float md[KNN_BRUTE_S - 1][K][KNN_BRUTE_Q];
+  __shared__ int mi[KNN_BRUTE_S - 1][K][KNN_BRUTE_Q];
+  const int lane = threadIdx.x & 63, slice = threadIdx.x >> 6;
+  const int64_t m = (int64_t)blockIdx.x * KNN_BRUTE_Q + lane;
   const bool live = m < M;
   const float qx = live ? q[3 * m] : 0.f, qy = live ? q[3 * m + 1] : 0.f, qz = live ? q[3 * m + 2] : 0.f;
   float bd[K];
@@ -1654,20 +1659,30 @@ __global__ __launch_bounds__(KNN_BRUTE_Q) void k_knn_brute(const float* __restri
   for (int j = 0; j < K; ++j) { bd[j] = INFINITY; bi[j] = 0x7fffffff; }
   for (int64_t base = 0; base < N; base += KNN_BRUTE_TILE) {
     __syncthreads();
-    for (int i = threadIdx.x; i < KNN_BRUTE_TILE; i += KNN_BRUTE_Q) {
+    for (int i = threadIdx.x; i < KNN_BRUTE_TILE; i += KNN_BRUTE_Q * KNN_BRUTE_S) {
       const int64_t n = base + i;
       tile[i] = n < N ? make_float4(pts[3 * n], pts[3 * n + 1], pts[3 * n + 2], 0.f) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     __syncthreads();
     const int cnt = (int)(N - base < KNN_BRUTE_TILE ? N - base : KNN_BRUTE_TILE);
-    for (int i = 0; i < cnt; ++i) {
+    for (int i = slice; i < cnt; i += KNN_BRUTE_S) {
       const float4 P = tile[i];
       const float dx = qx - P.x, dy = qy - P.y, dz = qz - P.z;
       const float d = (dx * dx + dy * dy) + dz * dz;
       knn_insert<K>(d, (int)(base + i), bd, bi);
     }
   }
-  if (!live) return;
+  // merge: each slice holds the exact top K of its points; (d, index) order makes the merged
+  // list the global top K whatever the slice assignment
+  if (slice > 0) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) { md[slice - 1][j][lane] = bd[j]; mi[slice - 1][j][lane] = bi[j]; }
+  }
+  __syncthreads();
+  if (slice > 0 || !live) return;
+  for (int s2 = 0; s2 < KNN_BRUTE_S - 1; ++s2)
+#pragma unroll
+    for (int j = 0; j < K; ++j) knn_insert<K>(md[s2][j][lane], mi[s2][j][lane], bd, bi);
   for (int j = 0; j < k_out; ++j) {
     idx_out[m * k_out + j] = bi[j];
     d2_out[m * k_out + j] = bd[j];
@@ -1686,7 +1701,8 @@ extern "C" int apn_knn_points(const float* q, int64_t n_queries, const float* pt
   hipStream_t s = (hipStream_t)stream;
   if (n_queries > 0 && knn_points_brute(n_queries, n_points)) {
     auto brute = [&](auto kern) {
-      hipLaunchKernelGGL(kern, dim3(ceil_div(n_queries, KNN_BRUTE_Q)), dim3(KNN_BRUTE_Q), 0, s, q, n_queries, pts,
+      hipLaunchKernelGGL(kern, dim3(ceil_div(n_queries, KNN_BRUTE_Q)), dim3(KNN_BRUTE_Q * KNN_BRUTE_S), 0, s, q,
+                         n_queries, pts,
                          n_points, k, idx_out, d2_out);
     };
     if (k == 1) brute(k_knn_brute<1>);
