@@ -33,6 +33,8 @@ struct GridParams {
 
 constexpr int KNN_K = 8;
 constexpr int KNN_THREADS = 256;
+// launch bound (in-bbox samples) up to which pass B runs 4 lanes per hard query
+constexpr int64_t KNN_SPLIT_MAX_QUERIES = (int64_t)1 << 20;
 constexpr int KNN_SUBDIV = 8;   // fine cell side = r / KNN_SUBDIV (before the cell cap)
 
 __device__ __forceinline__ int floor_div(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
@@ -856,10 +858,16 @@ __device__ __forceinline__ void scan_ball_flat(const GridParams& g, const int* _
 // slab only enumerates the y offsets whose rows can intersect the ball under the current bound
 // (|dy| <= floor(sqrt(tau - dz^2)/h) + 1), so the square's corners and culled slabs cost no
 // iterations; no integer division per row.
-template <int K, bool STATS = false>
+// S > 1: the caller is one of S lanes sharing the query; in every slab this lane walks only the
+// nearest-first y slots iy = slice, slice + S, ... (the slot -> row map depends on the query
+// alone, so the lanes partition each slab's rows whatever bound sizes the slab). Pruning with
+// the lane-local K-th distance stays exact: K points of this lane already beat every point of a
+// pruned row.
+template <int K, bool STATS = false, int S = 1>
 __device__ __forceinline__ void scan_ball_flat2(const GridParams& g, const int* __restrict__ cell_start,
                                                 const float4* __restrict__ sorted, float qx, float qy, float qz,
-                                                float R2, float (&bd)[K], int (&bi)[K], unsigned* ctr = nullptr) {
+                                                float R2, float (&bd)[K], int (&bi)[K], unsigned* ctr = nullptr,
+                                                int slice = 0) {
   const float R = sqrtf(R2) * 1.0001f;
   const int z0 = max((int)floorf((qz - R - g.oz) * g.inv_h), 0), z1 = min((int)floorf((qz + R - g.oz) * g.inv_h), g.dz - 1);
   const int y0 = max((int)floorf((qy - R - g.oy) * g.inv_h), 0), y1 = min((int)floorf((qy + R - g.oy) * g.inv_h), g.dy - 1);
@@ -899,7 +907,7 @@ __device__ __forceinline__ void scan_ball_flat2(const GridParams& g, const int* 
       const float tau = fminf(bd[K - 1], R2) * 1.0001f;
       if (iy >= nyz) {               // next slab
         ++iz;
-        iy = 0;
+        iy = S == 1 ? 0 : slice;
         nyz = 0;
         if (iz < nz) {
           z = fz + nf_offset(iz);
@@ -913,7 +921,7 @@ __device__ __forceinline__ void scan_ball_flat2(const GridParams& g, const int* 
         }
       } else {                       // one row of the slab
         const int y = fy + nf_offset(iy);
-        ++iy;
+        iy += S;
         if (y >= y0 && y <= y1) {
           const float dyz2 = dz2 + slab_d2(qy, g.oy, g.h, y, y);
           if (dyz2 <= tau) {
@@ -1121,6 +1129,66 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_b8(
     atomicAdd(&st[6], (unsigned long long)cr[1]);
     if (!done && !surv) { atomicAdd(&st[7], 1ull); atomicAdd(&st[8], (unsigned long long)(cr[0] + cr[1])); }
   }
+  flag[c] = surv;
+  if (surv) {
+    int4* nb = (int4*)(t_nbr + (int64_t)c * KNN_K);
+    nb[0] = make_int4(bi[0], bi[1], bi[2], bi[3]);
+    nb[1] = make_int4(bi[4], bi[5], bi[6], bi[7]);
+  }
+}
+
+// top-K lists of the S lanes of a query group merged in every lane (snapshot, then unique
+// inserts in a fixed lane order): all lanes end with the same sorted list
+template <int S>
+__device__ __forceinline__ void group_merge(float (&bd)[KNN_K], int (&bi)[KNN_K]) {
+  float sd[KNN_K];
+  int si[KNN_K];
+#pragma unroll
+  for (int k = 0; k < KNN_K; ++k) { sd[k] = bd[k]; si[k] = bi[k]; }
+  const int lane = threadIdx.x & 63, base = lane & ~(S - 1), me = lane & (S - 1);
+#pragma unroll
+  for (int o = 1; o < S; ++o) {
+    const int src = base | ((me + o) & (S - 1));
+#pragma unroll
+    for (int k = 0; k < KNN_K; ++k) {
+      const float d = __shfl(sd[k], src, 64);
+      const int id = __shfl(si[k], src, 64);
+      knn_insert_unique<KNN_K>(d, id, bd, bi);
+    }
+  }
+}
+
+// Pass B with S lanes per hard query (few hard queries, e.g. the 8192-ray training batches,
+// leave most CUs idle with one lane each): each lane scans its share of the ball's rows, the
+// lists are merged after each ball, lane 0 writes. Same survivors and neighbours as k_knn_pass_b8.
+template <int S>
+__global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_b8s(
+    const float4* __restrict__ q_pos, const int* __restrict__ cand, const int* __restrict__ hard,
+    const int* __restrict__ n_hard, const GridParams* __restrict__ gp, const int* __restrict__ cell_start,
+    const float4* __restrict__ sorted, int* __restrict__ flag, int* __restrict__ t_nbr) {
+  const int t = blockIdx.x * KNN_THREADS + threadIdx.x;
+  const int i = t / S, slice = t & (S - 1);
+  if (i >= *n_hard) return;   // uniform over the S lanes of a group
+  const GridParams g = *gp;
+  const int hc = hard[i];
+  const int c = hc >> 1;
+  const float4 q = q_pos[cand[c]];
+  float bd[KNN_K];
+  int bi[KNN_K];
+#pragma unroll
+  for (int k = 0; k < KNN_K; ++k) { bd[k] = INFINITY; bi[k] = 0x7fffffff; }
+  bool done = false;
+  if ((hc & 1) == 0) {
+    scan_ball_flat2<KNN_K, false, S>(g, cell_start, sorted, q.x, q.y, q.z, 0.25f * g.r2, bd, bi, nullptr, slice);
+    group_merge<S>(bd, bi);
+    done = bd[KNN_K - 1] < 0.25f * g.r2 * (1.f - 2e-4f);
+  }
+  if (!done) {
+    scan_ball_flat2<KNN_K, false, S>(g, cell_start, sorted, q.x, q.y, q.z, g.r2, bd, bi, nullptr, slice);
+    group_merge<S>(bd, bi);
+  }
+  if (slice != 0) return;
+  const bool surv = bd[KNN_K - 1] <= g.r2;
   flag[c] = surv;
   if (surv) {
     int4* nb = (int4*)(t_nbr + (int64_t)c * KNN_K);
@@ -1514,11 +1582,19 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
                        g.gp, g.cell_start, (const float4*)sorted_pts4, ccell, u1, u2, u4, flag, t_nbr, hard, n_hard,
                        hard_r, n_hard_r);
     static const bool stats = getenv("APN_KNN_STATS") != nullptr;   // profiling aid: apn_debug_knn_stats
-    auto pass_b = stats ? k_knn_pass_b8<true> : k_knn_pass_b8<false>;
-    hipLaunchKernelGGL(pass_b, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard, n_hard,
-                       g.gp, g.cell_start, (const float4*)sorted_pts4, flag, t_nbr);
-    hipLaunchKernelGGL(pass_b, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard_r,
-                       n_hard_r, g.gp, g.cell_start, (const float4*)sorted_pts4, flag, t_nbr);
+    if (!stats && n_queries <= KNN_SPLIT_MAX_QUERIES) {   // small batches: 4 lanes per hard query
+      const dim3 nb4(ceil_div(n_queries * 4, KNN_THREADS));
+      hipLaunchKernelGGL(k_knn_pass_b8s<4>, nb4, dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard, n_hard,
+                         g.gp, g.cell_start, (const float4*)sorted_pts4, flag, t_nbr);
+      hipLaunchKernelGGL(k_knn_pass_b8s<4>, nb4, dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard_r,
+                         n_hard_r, g.gp, g.cell_start, (const float4*)sorted_pts4, flag, t_nbr);
+    } else {
+      auto pass_b = stats ? k_knn_pass_b8<true> : k_knn_pass_b8<false>;
+      hipLaunchKernelGGL(pass_b, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard, n_hard,
+                         g.gp, g.cell_start, (const float4*)sorted_pts4, flag, t_nbr);
+      hipLaunchKernelGGL(pass_b, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard_r,
+                         n_hard_r, g.gp, g.cell_start, (const float4*)sorted_pts4, flag, t_nbr);
+    }
     hipLaunchKernelGGL(k_knn_flag_count, dim3(nb), dim3(KNN_THREADS), 0, s, flag, cblk_off + nb, blk_cnt);
     st = scan_exclusive_i32(blk_cnt, blk_off, nb, sws, s);
     if (st) return st;
