@@ -33,7 +33,7 @@ struct GridParams {
 
 constexpr int KNN_K = 8;
 constexpr int KNN_THREADS = 256;
-// launch bound (in-bbox samples) up to which pass B runs 4 lanes per hard query
+// launch bound (in-bbox samples) up to which pass B runs 8 lanes per hard query
 constexpr int64_t KNN_SPLIT_MAX_QUERIES = (int64_t)1 << 20;
 constexpr int KNN_SUBDIV = 8;   // fine cell side = r / KNN_SUBDIV (before the cell cap)
 
@@ -1582,11 +1582,11 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
                        g.gp, g.cell_start, (const float4*)sorted_pts4, ccell, u1, u2, u4, flag, t_nbr, hard, n_hard,
                        hard_r, n_hard_r);
     static const bool stats = getenv("APN_KNN_STATS") != nullptr;   // profiling aid: apn_debug_knn_stats
-    if (!stats && n_queries <= KNN_SPLIT_MAX_QUERIES) {   // small batches: 4 lanes per hard query
-      const dim3 nb4(ceil_div(n_queries * 4, KNN_THREADS));
-      hipLaunchKernelGGL(k_knn_pass_b8s<4>, nb4, dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard, n_hard,
+    if (!stats && n_queries <= KNN_SPLIT_MAX_QUERIES) {   // small batches: 8 lanes per hard query
+      const dim3 nb4(ceil_div(n_queries * 8, KNN_THREADS));
+      hipLaunchKernelGGL(k_knn_pass_b8s<8>, nb4, dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard, n_hard,
                          g.gp, g.cell_start, (const float4*)sorted_pts4, flag, t_nbr);
-      hipLaunchKernelGGL(k_knn_pass_b8s<4>, nb4, dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard_r,
+      hipLaunchKernelGGL(k_knn_pass_b8s<8>, nb4, dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard_r,
                          n_hard_r, g.gp, g.cell_start, (const float4*)sorted_pts4, flag, t_nbr);
     } else {
       auto pass_b = stats ? k_knn_pass_b8<true> : k_knn_pass_b8<false>;
