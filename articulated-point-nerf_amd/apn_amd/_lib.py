@@ -63,6 +63,8 @@ SIGNATURES = {
     "apn_nbr_tv_loss_backward": (C.c_int, [P, I64, I32, P, I32, P, P, P, P, P]),
     "apn_arap_loss": (C.c_int, [P, I64, P, I32, P, F32, P, P, P]),
     "apn_arap_loss_backward": (C.c_int, [P, I64, P, I32, P, F32, P, P, P, P, P]),
+    "apn_weight_sparsity_loss": (C.c_int, [P, I64, F32, P, P, P]),
+    "apn_weight_sparsity_loss_backward": (C.c_int, [P, I64, F32, P, P, P]),
     "apn_scan_workspace_bytes": (SZ, [I64]),
     "apn_scan_exclusive_i32": (C.c_int, [P, P, I64, P, P]),
     "apn_version": (C.c_char_p, []),

@@ -259,9 +259,9 @@ class TemporalPoints(torch.nn.Module):
         return NbrTVLoss.apply(self._last_weights, nn_i, rev_ptr, rev_edge)
 
     def get_weight_sparsity_loss(self):
-        eps = self.eps.to(self._last_weights.device)
-        return -(self._last_weights * torch.log(self._last_weights + eps)
-                 + (1 - self._last_weights) * torch.log(1 - self._last_weights + eps)).mean()
+        """temporalpoints.py:718-721 as the fused HIP SparsityLoss."""
+        from .train import SparsityLoss
+        return SparsityLoss.apply(self._last_weights, float(self.eps))
 
     def get_arap_loss(self, warped_pcd, c=0.03):
         """temporalpoints.py:723-725 as the fused HIP ArapLoss (gather-only backward)."""

@@ -30,7 +30,7 @@ from .tineuvox import poc_fre
 
 __all__ = ["forward_train", "LBSTrain", "lbs_train", "lbs_blend", "inv3x3", "radius_knn", "ordered_bbox",
            "reverse_csr", "NbrTVLoss", "ArapLoss",
-           "SplitKLinear", "feat_net_forward"]
+           "SplitKLinear", "feat_net_forward", "SparsityLoss"]
 
 
 def cloud_min_max(xyz: torch.Tensor):
@@ -185,6 +185,33 @@ class ArapLoss(torch.autograd.Function):
         call("apn_arap_loss_backward", ptr(xc), xc.shape[0], ptr(nn_i), nn_i.shape[1], ptr(d0c), ctx.eps,
              ptr(rev_ptr), ptr(rev_edge), ptr(dl), ptr(dx), stream_ptr(xc.device))
         return dx, None, None, None, None, None
+
+
+class SparsityLoss(torch.autograd.Function):
+    """get_weight_sparsity_loss (temporalpoints.py:718-721) as one HIP partial pass
+    (apn_weight_sparsity_loss) and one elementwise backward (apn_weight_sparsity_loss_backward)."""
+
+    @staticmethod
+    def forward(ctx, w, eps):
+        L.require_cuda(w, what="SparsityLoss")
+        wc = w.detach().float().contiguous()
+        dev = wc.device
+        loss = torch.empty((), device=dev)
+        ws = torch.empty(int(L.load().apn_nbr_loss_workspace_bytes()), dtype=torch.uint8, device=dev)
+        call("apn_weight_sparsity_loss", ptr(wc), wc.numel(), float(eps), ptr(loss), ptr(ws), stream_ptr(dev))
+        ctx.save_for_backward(wc)
+        ctx.eps = float(eps)
+        return loss
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, d_loss):
+        (wc,) = ctx.saved_tensors
+        dw = torch.empty_like(wc)
+        dl = d_loss.float().contiguous()
+        call("apn_weight_sparsity_loss_backward", ptr(wc), wc.numel(), ctx.eps, ptr(dl), ptr(dw),
+             stream_ptr(wc.device))
+        return dw, None
 
 
 SPLITK_ROWS = 4096   # rows per chunk of the split-K weight gradient

@@ -144,6 +144,36 @@ __global__ void __launch_bounds__(kLossThreads) k_arap_bwd(const float* __restri
   dx_out[3 * i] = gx; dx_out[3 * i + 1] = gy; dx_out[3 * i + 2] = gz;
 }
 
+// get_weight_sparsity_loss (temporalpoints.py:718-721): -mean(w log(w + eps) + (1 - w) log(1 - w + eps))
+// over the [N,J] skinning weights -- one partial pass instead of ~10 elementwise torch launches
+// forward and ~12 backward.
+__device__ __forceinline__ float sparsity_term(float w, float eps) {
+  const float a = w * logf(w + eps);
+  const float b = (1.f - w) * logf((1.f - w) + eps);
+  return a + b;
+}
+
+__global__ void __launch_bounds__(kLossThreads) k_sparsity_partial(const float* __restrict__ w, int64_t n, float eps,
+                                                                   float* __restrict__ partials) {
+  float acc = 0.f;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x)
+    acc += sparsity_term(w[t], eps);
+  const float s = block_sum(acc);
+  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+}
+
+// d w = -(dL / n) (log(w + eps) + w / (w + eps) - log(1 - w + eps) - (1 - w) / (1 - w + eps))
+__global__ void __launch_bounds__(kLossThreads) k_sparsity_bwd(const float* __restrict__ w, int64_t n, float eps,
+                                                               const float* __restrict__ d_loss, float inv_count,
+                                                               float* __restrict__ dw) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const float x = w[t];
+  const float a = x + eps, b = (1.f - x) + eps;
+  const float d = (logf(a) + x / a) - (logf(b) + (1.f - x) / b);
+  dw[t] = (-(d_loss[0] * inv_count)) * d;
+}
+
 }  // namespace apn
 
 using namespace apn;
@@ -207,5 +237,25 @@ extern "C" int apn_arap_loss_backward(const float* x, int64_t n_points, const in
   if (!fits32(n_points, 3, k)) return APN_ERR_ARG;
   APN_LAUNCH_K(k_arap_bwd, k, dim3(ceil_div(n_points, kLossThreads)), x, nn_i, nn_dist0, rev_ptr, rev_edge,
                (int)n_points, (int)k, eps, d_loss, dx);
+  return launch_status();
+}
+
+extern "C" int apn_weight_sparsity_loss(const float* w, int64_t n, float eps, float* loss_out, void* workspace,
+                                        void* stream) {
+  if (n <= 0 || !w || !loss_out || !workspace) return APN_ERR_ARG;
+  const int nb = partial_blocks(n);
+  hipLaunchKernelGGL(k_sparsity_partial, dim3(nb), dim3(kLossThreads), 0, (hipStream_t)stream, w, n, eps,
+                     (float*)workspace);
+  // loss = -(sum / n): the reduce kernel scales by -1/n
+  hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kLossThreads), 0, (hipStream_t)stream,
+                     (const float*)workspace, nb, (float)(-1.0 / (double)n), true, loss_out);
+  return launch_status();
+}
+
+extern "C" int apn_weight_sparsity_loss_backward(const float* w, int64_t n, float eps, const float* d_loss, float* dw,
+                                                 void* stream) {
+  if (n <= 0 || !w || !d_loss || !dw) return APN_ERR_ARG;
+  hipLaunchKernelGGL(k_sparsity_bwd, dim3(ceil_div(n, kLossThreads)), dim3(kLossThreads), 0, (hipStream_t)stream, w, n,
+                     eps, d_loss, (float)(1.0 / (double)n), dw);
   return launch_status();
 }

@@ -137,6 +137,11 @@ int apn_arap_loss(const float* x, int64_t n_points, const int64_t* nn_i, int32_t
 int apn_arap_loss_backward(const float* x, int64_t n_points, const int64_t* nn_i, int32_t k,
                            const float* nn_dist0, float eps, const int64_t* rev_ptr, const int64_t* rev_edge,
                            const float* d_loss, float* dx, void* stream);
+/* get_weight_sparsity_loss (temporalpoints.py:718-721) over w [n] (the [N,J] weights, flat):
+ * loss_out[0] = -mean(w log(w + eps) + (1 - w) log(1 - w + eps)); backward dw [n] (overwritten). */
+int apn_weight_sparsity_loss(const float* w, int64_t n, float eps, float* loss_out, void* workspace, void* stream);
+int apn_weight_sparsity_loss_backward(const float* w, int64_t n, float eps, const float* d_loss, float* dw,
+                                      void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Fused render pipeline stages (TemporalPoints.forward, temporalpoints.py:540-712).

@@ -146,3 +146,26 @@ def test_splitk_linear_vs_float64(M, K):
     for a, r, name in [(y, y64, "y")] + [(p.grad, q.grad, n) for p, q, n in zip(ps, ps64, "xwb")]:
         err = float((a.double() - r).abs().max() / r.abs().max().clamp_min(1e-30))
         assert err < 2e-6, (name, err)
+
+
+@pytest.mark.gpu
+@pytest.mark.autograd
+@pytest.mark.parametrize("n,J", [(1, 1), (777, 24), (300000, 24)])
+def test_weight_sparsity_loss_vs_float64(n, J):
+    """SparsityLoss (temporalpoints.py:718-721) vs the float64 autograd of the reference
+    expression, with exact 0 / 1 weights (log(eps) terms) included."""
+    from apn_amd.train import SparsityLoss
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(n)
+    w = torch.softmax(torch.randn(n, J, generator=g) * 4, -1)
+    w.view(-1)[:3] = torch.tensor([0.0, 1.0, 0.5])[: w.numel()]
+    eps = float(torch.tensor(1e-6))
+    w64 = w.double().requires_grad_(True)
+    ref = -(w64 * torch.log(w64 + eps) + (1 - w64) * torch.log(1 - w64 + eps)).mean()
+    ref.backward(torch.tensor(0.2, dtype=torch.float64))
+    wd = w.to(dev).requires_grad_(True)
+    loss = SparsityLoss.apply(wd, eps)
+    (0.2 * loss).backward()
+    assert abs(float(loss.detach()) - float(ref)) <= 2e-6 * max(1.0, abs(float(ref)))
+    err = (wd.grad.cpu().double() - w64.grad).abs() / w64.grad.abs().clamp_min(0.2 / w.numel())
+    assert float(err.max()) < 1e-5, float(err.max())
