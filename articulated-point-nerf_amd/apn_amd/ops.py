@@ -192,7 +192,7 @@ def segment_coo_sum(src, index, n_out):
 
 _LAYOUT = None
 _LAYOUT_NAMES = ["W1E", "B1", "W2", "B2", "W3", "B3", "W4", "B4", "WD", "BD", "WH", "BH", "WV2", "BV2", "W1F",
-                 "TOTAL", "KE", "KV", "H16"]
+                 "TOTAL", "KE", "KV", "H16", "FLAG"]
 
 
 def mlp_layout():
@@ -258,6 +258,14 @@ def pack_mlp_weights(feat_net_layers, densitynet, rgbnet, pose_embedding=None, o
     # (3-term split) apn_point_mlp kernel
     call("apn_mlp_split_weights", ptr(buf), stream_ptr(dev))
     return buf
+
+
+def mlp_range_fallback(wbuf) -> bool:
+    """True if the fp16-split MLP kernel met a value outside the fp16 range with these packed
+    weights (its range flag, apn_mlp_layout.h OFF_FLAG), so apn_point_mlp recomputed the launch on
+    the FP32 MFMA kernel. Reads one int from the device (a sync): for tests and diagnostics."""
+    off = mlp_layout()["FLAG"]
+    return bool(int(wbuf[off:off + 1].view(torch.int32).item()))
 
 
 def feat_project(canonical_feat, wbuf, out=None):

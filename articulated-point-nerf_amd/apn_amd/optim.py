@@ -29,11 +29,21 @@ def _check(*ts, what):
     return n
 
 
+def _bump(*ts):
+    """The kernels write through raw pointers, which torch cannot see: bump the version counters
+    so every cache keyed on ``(data_ptr, _version)`` (TemporalPoints' packed MLP weights and
+    feature projection, PointWarper's packed TransformNet) notices the in-place update, as it
+    would after a torch in-place op."""
+    for t in ts:
+        torch.autograd.graph.increment_version(t)
+
+
 def adam_upd(param, grad, exp_avg, exp_avg_sq, step, beta1, beta2, lr, eps):
     """adam_upd_kernel.cu:8-23, 62-82 (in place)."""
     n = _check(param, grad, exp_avg, exp_avg_sq, what="adam_upd")
     call("apn_adam_upd", ptr(param), ptr(grad), ptr(exp_avg), ptr(exp_avg_sq), n, int(step), float(beta1),
          float(beta2), float(lr), float(eps), stream_ptr(param.device))
+    _bump(param, exp_avg, exp_avg_sq)
 
 
 def masked_adam_upd(param, grad, exp_avg, exp_avg_sq, step, beta1, beta2, lr, eps):
@@ -41,6 +51,7 @@ def masked_adam_upd(param, grad, exp_avg, exp_avg_sq, step, beta1, beta2, lr, ep
     n = _check(param, grad, exp_avg, exp_avg_sq, what="masked_adam_upd")
     call("apn_masked_adam_upd", ptr(param), ptr(grad), ptr(exp_avg), ptr(exp_avg_sq), n, int(step), float(beta1),
          float(beta2), float(lr), float(eps), stream_ptr(param.device))
+    _bump(param, exp_avg, exp_avg_sq)
 
 
 def adam_upd_with_perlr(param, grad, exp_avg, exp_avg_sq, perlr, step, beta1, beta2, lr, eps):
@@ -48,6 +59,7 @@ def adam_upd_with_perlr(param, grad, exp_avg, exp_avg_sq, perlr, step, beta1, be
     n = _check(param, grad, exp_avg, exp_avg_sq, perlr, what="adam_upd_with_perlr")
     call("apn_adam_upd_with_perlr", ptr(param), ptr(grad), ptr(exp_avg), ptr(exp_avg_sq), ptr(perlr), n, int(step),
          float(beta1), float(beta2), float(lr), float(eps), stream_ptr(param.device))
+    _bump(param, exp_avg, exp_avg_sq)
 
 
 def total_variation_add_grad(param, grad, wx, wy, wz, dense_mode):
@@ -58,6 +70,7 @@ def total_variation_add_grad(param, grad, wx, wy, wz, dense_mode):
         raise RuntimeError("total_variation_add_grad: param must be [1, C, I, J, K]")
     call("apn_total_variation_add_grad", ptr(param), ptr(grad), float(wx), float(wy), float(wz), param.shape[2],
          param.shape[3], param.shape[4], n, int(bool(dense_mode)), stream_ptr(param.device))
+    _bump(grad)
 
 
 class MaskedAdam(torch.optim.Optimizer):

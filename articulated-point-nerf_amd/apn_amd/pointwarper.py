@@ -1,8 +1,9 @@
 """PointWarper / TransformNet with the reference's API and state-dict names
 (lib/pointwarper.py). The skeleton stage -- TransformNet (1x17 -> (J+1)x4), Rodrigues, the
-kinematic chain -- is a handful of J-sized tensor ops and runs as torch ops on the device;
-the per-point LBS blend + apply (the hot part, pointwarper.py:241-266) runs in the HIP kernel
-``apn_lbs_skin``.
+rotation/sibling masks, the recursive-halving kinematic chain -- runs as ONE HIP launch
+(``apn_skeleton_pose``, csrc/apn_skeleton.hip); ``pose_torch`` keeps the torch restatement the
+tests compare it with. The per-point LBS blend + apply (the hot part, pointwarper.py:241-266)
+runs in the HIP kernels ``apn_lbs_skin`` / ``k_lbs_skin_quad``.
 """
 from __future__ import annotations
 

@@ -36,8 +36,9 @@ def balanced_ray_split(offsets: torch.Tensor, world: int) -> list[int]:
 def pack_tile(out: dict, n_rays: int, device) -> torch.Tensor:
     """Per-ray outputs of TemporalPoints.forward -> [n_rays, 12] float32."""
     cols = []
+    get = getattr(out, "raw", out.get)   # RenderOutput.raw: the kernels' values, no survivor-count sync
     for key, w in TILE_KEYS:
-        v = out.get(key)
+        v = get(key)
         if v is None:
             v = torch.ones(n_rays, w, device=device)  # NoPoints fallback has no alphainv
         cols.append(v.reshape(n_rays, w).float())

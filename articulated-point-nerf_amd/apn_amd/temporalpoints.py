@@ -58,6 +58,90 @@ class FrameStats(dict):
         return dict(self)
 
 
+class RenderOutput(dict):
+    """The dict ``TemporalPoints.forward`` returns on the render path.
+
+    The fused pipeline keeps the kNN survivor count on the device (no host sync after the kNN
+    stage). When no sample survives, the reference raises NoPointsException inside
+    ``aggregate_pts`` and returns a different dict (temporalpoints.py:598-609): ``alphainv_last``
+    is None, there is no ``alphainv_last_direct``, and ``depth`` / ``weights`` are present
+    whatever ``render_depth`` / ``render_weights`` asked for. The colour values already agree
+    (the kernels composite nothing: rgb = bg, depth = 0, weights = bg), so only the key set and
+    ``alphainv_last`` differ -- they are resolved on the first access that can observe them,
+    with one read of the device count. Reading rgb_marched / depth / weights, as the
+    reference's render loops do (run.py:126-173), never syncs."""
+
+    _SENSITIVE = ("alphainv_last", "alphainv_last_direct", "depth", "weights")
+
+    def __init__(self, *a, nsurv=None, n_rays=0, bg=0.0, **kw):
+        super().__init__(*a, **kw)
+        self._nsurv = nsurv
+        self._n_rays = n_rays
+        self._bg = bg
+
+    def _resolve(self):
+        if self._nsurv is None:
+            return
+        nsurv, self._nsurv = self._nsurv, None
+        if int(nsurv.item()) > 0:
+            return
+        dev = nsurv.device
+        R, bg = self._n_rays, self._bg
+        super().pop("alphainv_last_direct", None)
+        super().__setitem__("alphainv_last", None)
+        if not dict.__contains__(self, "depth"):
+            super().__setitem__("depth", torch.zeros(R, device=dev))
+        if not dict.__contains__(self, "weights"):
+            super().__setitem__("weights", torch.ones(R, 3, device=dev) * bg)
+
+    def __getitem__(self, k):
+        if k in self._SENSITIVE:
+            self._resolve()
+        return super().__getitem__(k)
+
+    def get(self, k, default=None):
+        if k in self._SENSITIVE:
+            self._resolve()
+        return super().get(k, default)
+
+    def __contains__(self, k):
+        if k in self._SENSITIVE:
+            self._resolve()
+        return super().__contains__(k)
+
+    def keys(self):
+        self._resolve()
+        return super().keys()
+
+    def items(self):
+        self._resolve()
+        return super().items()
+
+    def values(self):
+        self._resolve()
+        return super().values()
+
+    def __iter__(self):
+        self._resolve()
+        return super().__iter__()
+
+    def __len__(self):
+        self._resolve()
+        return super().__len__()
+
+    def pop(self, k, *default):
+        self._resolve()
+        return super().pop(k, *default)
+
+    def copy(self):
+        self._resolve()
+        return dict(super().items())
+
+    def raw(self, k, default=None):
+        """The fused pipeline's own value (no resolution, no sync)."""
+        return super().get(k, default)
+
+
 def hls_palette(n, h=0.01, l=0.6, s=0.65):
     """seaborn.color_palette('hls', n) (temporalpoints.py:692)."""
     hues = np.linspace(0, 1, n + 1)[:-1]
@@ -496,8 +580,10 @@ class TemporalPoints(torch.nn.Module):
                     'depth': torch.zeros(R, device=dev), 'weights': torch.ones(R, 3, device=dev) * bg,
                     't_hat_pcd': t_hat_pcd, 'alphainv_last': None, 'grid': None, 'joints': joints, 'bones': bones}
         rgb, rgb_d, depth, wvis, last, last_d = out
-        ret = {'t_hat_pcd': t_hat_pcd, 'rgb_marched': rgb, 'alphainv_last': last, 'alphainv_last_direct': last_d,
-               'grid': None, 'rgb_marched_direct': rgb_d, 'joints': joints, 'bones': bones}
+        ret = RenderOutput({'t_hat_pcd': t_hat_pcd, 'rgb_marched': rgb, 'alphainv_last': last,
+                            'alphainv_last_direct': last_d, 'grid': None, 'rgb_marched_direct': rgb_d,
+                            'joints': joints, 'bones': bones},
+                           nsurv=self.last_stats._nsurv, n_rays=len(rgb), bg=float(render_kwargs['bg']))
         if render_depth:
             ret['depth'] = depth
         if render_weights:
@@ -576,8 +662,8 @@ class TemporalPoints(torch.nn.Module):
         self._mark("knn")
         # The survivor count stays on the device: the MLP and compositing kernels read it there and
         # n_bbox bounds it, so no sync here. (If no sample survives, the kernels produce the
-        # reference's NoPointsException values -- bg colour, depth 0 -- with alphainv_last = 1
-        # tensors instead of None.)
+        # reference's NoPointsException values -- bg colour, depth 0 -- and RenderOutput gives
+        # the reference's key set and alphainv_last=None when they are read.)
         S = n_bbox
         self.last_stats._nsurv = nsurv
         # neighbour MLP + heads + direct blend

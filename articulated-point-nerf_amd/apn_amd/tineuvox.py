@@ -1,6 +1,6 @@
 """The pieces of the reference's ``lib/tineuvox.py`` that the point render path uses
 (SURVEY.md §2 row 4): RGBNet, the density head holder, poc_fre, Raw2Alpha /
-Alphas2Weights (forward only, through libapn_hip.so) and ray generation.
+Alphas2Weights (re-exported from ``ops``: HIP forward and backward) and ray generation.
 
 The TiNeuVox voxel model itself (stage 1) is out of scope; ``TiNeuVoxHeads`` is the
 lightweight holder TemporalPoints takes as its ``tineuvox`` argument
@@ -16,6 +16,9 @@ import torch
 import torch.nn as nn
 
 from . import ops
+# tineuvox.py:627-670: the backward-capable autograd Functions over the HIP kernels (one
+# definition, shared with the render_utils drop-in)
+from .ops import Alphas2Weights, Raw2Alpha  # noqa: F401
 
 
 def poc_fre(input_data: torch.Tensor, poc_buf: torch.Tensor) -> torch.Tensor:
@@ -43,24 +46,6 @@ class RGBNet(nn.Module):
         else:
             assert self.input_ch_views == 0
         return self.views_linears(feature)
-
-
-class Raw2Alpha(torch.autograd.Function):
-    """tineuvox.py:646-670, forward only (training/backward is out of scope)."""
-
-    @staticmethod
-    def forward(ctx, density, shift, interval):
-        _, alpha = ops.raw2alpha(density, shift, interval)
-        return alpha
-
-
-class Alphas2Weights(torch.autograd.Function):
-    """tineuvox.py:627-643, forward only."""
-
-    @staticmethod
-    def forward(ctx, alpha, ray_id, N):
-        weights, _, alphainv_last, _, _ = ops.alpha2weight(alpha, ray_id, N)
-        return weights, alphainv_last
 
 
 class TiNeuVoxHeads(nn.Module):

@@ -148,7 +148,14 @@ __global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp(
     const float4* __restrict__ s_pos, const int* __restrict__ s_ray, const int* __restrict__ s_nbr,
     const int* __restrict__ n_samples_dev, const float4* __restrict__ recA, const float4* __restrict__ recB,
     const float4* __restrict__ pproj, const float* __restrict__ viewdirs, const float* __restrict__ vemb_const,
-    const float* __restrict__ wbuf, float eps, float shift, float interval, float4* __restrict__ out) {
+    const float* __restrict__ wbuf, float eps, float shift, float interval, float4* __restrict__ out,
+    const int* __restrict__ run_if) {
+  if (run_if) {  // range fallback of the fp16-split kernel: run only if it flagged this launch
+    __shared__ int s_run;
+    if (threadIdx.x == 0) s_run = __builtin_nontemporal_load(run_if);
+    __syncthreads();
+    if (!s_run) return;
+  }
   __shared__ __attribute__((aligned(16))) float X[TR * XS];
   __shared__ float sTo[TR];
   __shared__ int sNbr[TR];
@@ -490,7 +497,7 @@ using namespace apn;
 
 extern "C" int apn_mlp_weight_layout(int32_t* offsets) {
   const int32_t v[] = {OFF_W1E, OFF_B1, OFF_W2, OFF_B2, OFF_W3, OFF_B3, OFF_W4, OFF_B4, OFF_WD, OFF_BD,
-                       OFF_WH, OFF_BH, OFF_WV2, OFF_BV2, OFF_W1F, W_TOTAL, KE, KV, OFF_H16};
+                       OFF_WH, OFF_BH, OFF_WV2, OFF_BV2, OFF_W1F, W_TOTAL, KE, KV, OFF_H16, OFF_FLAG};
   for (int i = 0; i < (int)(sizeof(v) / sizeof(v[0])); ++i) offsets[i] = v[i];
   return (int)(sizeof(v) / sizeof(v[0]));
 }
@@ -548,19 +555,25 @@ extern "C" int apn_point_mlp(const float* s_pos4, const int32_t* s_ray, const in
   // while keeping the cross-tile index prefetch; one workgroup per tile is 12 % slower.
   int blocks = grid_blocks > 0 ? grid_blocks : 256 * 64;
   if (blocks > ntiles) blocks = (int)ntiles;
-  auto launch = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(MLP_THREADS), 0, (hipStream_t)stream, (const float4*)s_pos4, s_ray,
+  auto launch = [&](auto kern, int nblocks, const int* run_if) {
+    hipLaunchKernelGGL(kern, dim3(nblocks), dim3(MLP_THREADS), 0, (hipStream_t)stream, (const float4*)s_pos4, s_ray,
                        s_nbr, n_samples_dev, (const float4*)recA16, (const float4*)recB8, (const float4*)feat_proj,
-                       viewdirs, vemb_const, wbuf, eps, act_shift, interval, (float4*)out12);
+                       viewdirs, vemb_const, wbuf, eps, act_shift, interval, (float4*)out12, run_if);
   };
   if (variant == 1) {
-    launch(k_point_mlp<2, 2>);
+    launch(k_point_mlp<2, 2>, blocks, nullptr);
   } else if (variant == 2) {
-    launch(k_point_mlp<2, 2, true>);
+    launch(k_point_mlp<2, 2, true>, blocks, nullptr);
   } else {
     launch_point_mlp_h3(blocks, variant == 3, (hipStream_t)stream, (const float4*)s_pos4, s_ray, s_nbr,
                         n_samples_dev, (const float4*)recA16, (const float4*)recB8, (const float4*)feat_proj,
                         viewdirs, vemb_const, wbuf, eps, act_shift, interval, (float4*)out12);
+    // range fallback (apn_mlp_layout.h OFF_FLAG): the FP32 MFMA kernel redoes the launch iff the
+    // split kernel flagged an out-of-fp16-range value; otherwise its workgroups exit at once
+    // (8 per CU: a few microseconds). Stream order makes the flag visible; no host sync.
+    int fb = 256 * 8;
+    if (fb > blocks) fb = blocks;
+    launch(k_point_mlp<2, 2>, fb, (const int*)(wbuf + OFF_FLAG));
   }
   return launch_status();
 }

@@ -6,7 +6,11 @@
 // drops only lo(a) lo(b) (<= 2^-22 |a b|) and the fp16 rounding of the residual (<= 2^-22 |x|):
 // ~2e-7 relative per product, the size of fp32's own rounding. v_mfma_f32_16x16x32_f16 runs
 // 16x the FLOP rate of v_mfma_f32_16x16x4_f32, so the three terms cost 3/16 of the fp32 MFMA time.
-// Range: |activations|, |weights| < 65504 (fp16 max); the tests compare against the fp32 oracle.
+// Range: |activations|, |weights| < 65504 (fp16 max). Guarded on the device: an activation or
+// weight beyond it becomes inf/NaN in its hi half, and inf/NaN propagates through every later
+// MFMA, ReLU and the IDW sum, so checking the IDW sums h (the last values split) catches all of
+// them; the kernel then sets the range flag in wbuf and apn_point_mlp's FP32 MFMA launch redoes
+// the samples (no host sync). The tests compare against the fp32 oracle.
 //
 // Same algebra as apn_mlp.hip (layer-1 projection P = canonical_feat W1f^T added to the
 // accumulator, rgbnet feature_linears folded into views_linears.0); differences in structure:
@@ -19,7 +23,8 @@
 //   * the P rows are gathered straight into the layer-1 accumulators (global -> VGPR).
 //
 // Tile = 8 samples x 8 neighbours = 64 MLP rows per 256-thread workgroup (4 waves, wave w owns
-// output features 32w..32w+31 of every layer), 2 workgroups per CU.
+// output features 32w..32w+31 of every layer), 3 workgroups per CU (APN_MLP_OCC=2: the ping-pong
+// build at 2 per CU).
 #include "apn_mlp_layout.h"
 
 namespace apn {
@@ -366,6 +371,14 @@ __global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
   char* const X0 = Xs;
   char* const X1 = PP ? Xs + XBUF : Xs;
   char* const HX = PP ? X1 : Hs;     // head input rows
+  int* const range_flag = (int*)(wbuf + OFF_FLAG);
+  {  // a launch with the flag already set (these weights overflowed before): leave the samples
+     // to the FP32 kernel. Block-uniform decision (one read, broadcast through LDS).
+    __shared__ int s_skip;
+    if (threadIdx.x == 0) s_skip = __builtin_nontemporal_load(range_flag);
+    __syncthreads();
+    if (s_skip) return;
+  }
 
   const int nS = *n_samples_dev;
   const int ntiles = (nS + TS - 1) / TS;
@@ -513,6 +526,8 @@ __global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
 #pragma unroll
         for (int r = 0; r < 4; ++r) h[r] = h[r] + w * v[r];
       }
+      // range guard (see the header comment): false for NaN too
+      if (!(fmaxf(fmaxf(fabsf(h[0]), fabsf(h[1])), fmaxf(fabsf(h[2]), fabsf(h[3]))) <= H3_RANGE)) *range_flag = 1;
       // densitynet Linear(128 -> 1) (tineuvox.py:158) over this thread's 4 features, then the half-wave
       const f32x4 wd = *(const f32x4*)(sW + SW_WD + 4 * oq);
       float d = ((h[0] * wd[0] + h[1] * wd[1]) + h[2] * wd[2]) + h[3] * wd[3];
@@ -635,6 +650,7 @@ __global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
 // (matrix, o-tile, chunk, lane).
 __global__ void k_split_weights(float* __restrict__ wbuf) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t == 0) *(int*)(wbuf + OFF_FLAG) = 0;   // new weights: clear the range flag
   // fragment-lanes per matrix: W1E 8x2x64, W2..W4 8x4x64, WH 4x5x64
   constexpr int n1 = 8 * 2 * 64, n2 = 8 * 4 * 64, nh = 4 * 5 * 64;
   int mat, i;

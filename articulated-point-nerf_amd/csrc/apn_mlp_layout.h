@@ -43,7 +43,12 @@ constexpr int H_W3 = H_W2 + 8 * 4 * 2 * FRAG_HALVES;
 constexpr int H_W4 = H_W3 + 8 * 4 * 2 * FRAG_HALVES;
 constexpr int H_WH = H_W4 + 8 * 4 * 2 * FRAG_HALVES;
 constexpr int H_TOTAL = H_WH + 4 * 5 * 2 * FRAG_HALVES;
-constexpr int W_TOTAL = OFF_H16 + H_TOTAL / 2;
+// Range flag (one int32, 4 floats reserved): the fp16-split kernel sets it when a value it must
+// split into fp16 hi/lo halves is out of the fp16 range (or not finite); the FP32 MFMA kernel
+// then re-runs the launch (apn_point_mlp). Sticky until the weights are re-split
+// (apn_mlp_split_weights clears it), so later launches with the same weights go straight to FP32.
+constexpr int OFF_FLAG = OFF_H16 + H_TOTAL / 2;
+constexpr int W_TOTAL = OFF_FLAG + 4;
 
 // Column order of the positional encoding inside the fp16 kernel's layer-1 operand (64 columns):
 // gather thread p (4 per MLP row) owns columns 16p..16p+15 = sin(arg a_j), j = 0..7, then
@@ -68,6 +73,8 @@ void launch_point_mlp_h3(int blocks, bool timed, hipStream_t stream, const float
                          const int* s_nbr, const int* n_samples_dev, const float4* recA, const float4* recB,
                          const float4* pproj, const float* viewdirs, const float* vemb_const, const float* wbuf,
                          float eps, float shift, float interval, float4* out);
+// Largest magnitude the fp16-split kernel carries through its hi/lo halves (fp16 max finite).
+constexpr float H3_RANGE = 65504.f;
 // Adds (and resets) the phase-timed fp16-split kernel's cycle sums into out6.
 int debug_phase_cycles_h3(uint64_t* out6);
 

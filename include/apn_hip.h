@@ -249,16 +249,18 @@ int apn_knn_points(const float* q, int64_t n_queries, const float* pts, int64_t 
                    int32_t cell_cap, float* sorted_pts4, int32_t* bbox_ord, void* grid_workspace,
                    int64_t* idx_out, float* d2_out, void* stream);
 
-/* Packed MLP weight layout: writes 19 int32 offsets (W1E,B1,W2,B2,W3,B3,W4,B4,WD,BD,WH,BH,
- * WV2,BV2,W1F,TOTAL,KE,KV,H16) and returns their count (float offsets; TOTAL = buffer length).
- * W1E = feat_net.0 columns 0..62 (posenc), W1F = feat_net.0 columns 63..190 (features),
+/* Packed MLP weight layout: writes 20 int32 offsets (W1E,B1,W2,B2,W3,B3,W4,B4,WD,BD,WH,BH,
+ * WV2,BV2,W1F,TOTAL,KE,KV,H16,FLAG) and returns their count (float offsets; TOTAL = buffer
+ * length). W1E = feat_net.0 columns 0..62 (posenc), W1F = feat_net.0 columns 63..190 (features),
  * WH/BH = rgbnet feature_linears folded into views_linears.0 (no activation between them),
- * see apn_mlp.hip; H16 = start of the fp16 hi/lo fragment region (apn_mlp_layout.h). */
+ * see apn_mlp.hip; H16 = start of the fp16 hi/lo fragment region (apn_mlp_layout.h); FLAG = the
+ * int32 range flag of the split kernel (non-zero: an out-of-fp16-range value was met and the
+ * launch was recomputed on FP32 MFMA; cleared by apn_mlp_split_weights). */
 int apn_mlp_weight_layout(int32_t* offsets);
 
 /* Fill the fp16 hi/lo fragment region of a packed weight buffer from its fp32 region
- * (hi = fp16(w), lo = fp16(w - hi), MFMA fragment order). Call after every change of the fp32
- * region and before apn_point_mlp with the default (split) kernel. */
+ * (hi = fp16(w), lo = fp16(w - hi), MFMA fragment order) and clear its range flag. Call after
+ * every change of the fp32 region and before apn_point_mlp with the default (split) kernel. */
 int apn_mlp_split_weights(float* wbuf, void* stream);
 
 /* Per-point layer-1 feature projection proj [N,128] = canonical_feat [N,128] x W1F^T
@@ -271,7 +273,10 @@ int apn_feat_project(const float* canonical_feat, int64_t n_points, int32_t feat
  * samples; out12 [S,12] = {r,g,b,alpha, r_d,g_d,b_d,alpha_d, wr,wg,wb,0}. feat_proj is the
  * apn_feat_project output (feat_dim 128). vemb_const [27] (frozen_view_dir) or NULL to embed
  * viewdirs[ray]. Default kernel: fp32 contraction as 3 fp16 MFMA terms (hi*hi + hi*lo + lo*hi,
- * fp32 accumulate; wbuf prepared by apn_mlp_split_weights); variant 1 = the FP32-MFMA kernel. */
+ * fp32 accumulate; wbuf prepared by apn_mlp_split_weights), followed by an FP32-MFMA launch that
+ * recomputes every sample only if the split kernel set the range flag (a weight or activation
+ * beyond the fp16 range; see FLAG above) -- decided on the device, no host sync; variant 1 = the
+ * FP32-MFMA kernel alone. */
 int apn_point_mlp(const float* s_pos4, const int32_t* s_ray, const int32_t* s_nbr,
                   int64_t max_samples, const int32_t* n_samples_dev, const float* recA16,
                   const float* recB8, const float* feat_proj, int32_t feat_dim,

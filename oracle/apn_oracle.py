@@ -559,10 +559,12 @@ class OracleModel:
 
     # temporalpoints.py:416-521
     def aggregate_pts(self, t_hat_pcd, Rinv, query_radius, render_kwargs, pose_embedding,
-                      calc_min_max=True, knn_tree=None):
+                      calc_min_max=True, knn_tree=None, bbox=None):
         R = len(render_kwargs["rays_o"])
         K = self.K
-        if calc_min_max:
+        if bbox is not None:   # calc_min_max=False: the model's xyz_min / xyz_max (temporalpoints.py:425-426)
+            xyz_min, xyz_max = (torch.as_tensor(b).float() for b in bbox)
+        elif calc_min_max:
             xyz_min = torch.min(t_hat_pcd, dim=0)[0] - query_radius
             xyz_max = torch.max(t_hat_pcd, dim=0)[0] + query_radius
         else:
@@ -620,9 +622,10 @@ class OracleModel:
     @torch.no_grad()
     def forward(self, t, render_depth=False, render_kwargs=None, query_radius=0.01,
                 render_weights=False, rot_params=None, poses=None, Ks=None, get_skeleton=False,
-                calc_min_max=True, perm=None, knn_tree=None, t_hat_override=None):
+                calc_min_max=True, perm=None, knn_tree=None, t_hat_override=None, bbox=None):
         """``t_hat_override``: render against a given warped cloud (e.g. the GPU's) so that a
-        1-ulp difference in the warp cannot flip a borderline kNN-radius decision."""
+        1-ulp difference in the warp cannot flip a borderline kNN-radius decision. ``bbox`` =
+        (xyz_min, xyz_max): the sampling bbox of calc_min_max=False (the model's stored bbox)."""
         assert (t is None) ^ (rot_params is None)
         rk = {k: (v.detach().cpu() if torch.is_tensor(v) else v) for k, v in render_kwargs.items()}
         weights, (t_hat, joints_rel, G, joints_w, bone_Ts, global_t) = self.warp(t, rot_params)
@@ -642,7 +645,7 @@ class OracleModel:
             bones = self.bones
         R = len(rk["rays_o"])
         bg = rk["bg"]
-        res = self.aggregate_pts(t_hat, Rinv, query_radius, rk, pose_embedding, calc_min_max, knn_tree)
+        res = self.aggregate_pts(t_hat, Rinv, query_radius, rk, pose_embedding, calc_min_max, knn_tree, bbox)
         if res is None:  # NoPointsException fallback (598-609)
             return {"rgb_marched": torch.ones(R, 3) * bg, "rgb_marched_direct": torch.ones(R, 3) * bg,
                     "depth": torch.zeros(R), "weights": torch.ones(R, 3) * bg, "t_hat_pcd": t_hat,

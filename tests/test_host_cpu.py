@@ -50,7 +50,7 @@ def test_workspace_queries_need_no_gpu():
     assert lib.apn_knn_workspace_bytes(8_000_000) > 8_000_000 * 32
     arr = (ctypes.c_int32 * 32)()
     n = lib.apn_mlp_weight_layout(arr)
-    assert n == 19 and arr[16] == 64 and arr[17] == 160 and arr[18] % 4 == 0 and arr[15] > arr[18]
+    assert n == 20 and arr[16] == 64 and arr[17] == 160 and arr[18] % 4 == 0 and arr[15] > arr[19] > arr[18]
 
 
 def test_invalid_arguments_rejected_without_gpu():

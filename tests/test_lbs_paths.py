@@ -1,0 +1,113 @@
+"""GPU parity of the LBS paths the golden render tests do not reach:
+
+* ``get_weights`` with a non-trivial merge (temporalpoints.py:401-414; the state after
+  ``simplify_skeleton``): the fused softmax + merge-by-rule of ``apn_lbs_skin`` on the render path
+  and on the record-free repose path, against the reference's own ``get_weights_merged`` fixture
+  and the oracle's merged LBS;
+* the C5 configuration at full size (BASELINE configs[4]: 1M points, 48 bones, the repose sweep
+  of run.py:1364-1377) through ``k_lbs_skin_quad``'s persistent grid-stride loop: several trips
+  per lane, the next-row prefetch clamp ``min(n + stride, N - 1)`` and the ``n_end`` tail. The
+  oracle (CPU) checks a strided 50k-point subset plus the last point -- LBS is per point, so a
+  subset model is exact."""
+import numpy as np
+import pytest
+import torch
+
+from golden_io import CASES, Golden
+from oracle import apn_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch.device("cuda")
+
+
+def _merged_model(g, dev):
+    from model_io import model_from_golden
+    m = model_from_golden(g, dev)
+    rules = g.t("merge_rules")
+    J = m.weights.shape[1]
+    assert not torch.equal(rules, torch.arange(J))
+    m.flat_merging_rules.copy_(rules.to(dev))
+    m.merging_mat = torch.zeros(J, J, J)   # simplify_skeleton's marker (temporalpoints.py:405-410)
+    return m, rules
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_merge_rules_render_path_vs_reference(dev, name):
+    g = Golden(name)
+    m, rules = _merged_model(g, dev)
+    ref_w = g.t("get_weights_merged")
+    with torch.no_grad():
+        assert (m.get_weights().cpu() - ref_w).abs().max() < 1e-6
+        out = m(g.t("in_t").to(dev), render_depth=True, render_kwargs=g.render_kwargs(dev), render_weights=True)
+    torch.cuda.synchronize()
+    # the fused kernel's merged softmax (written for the training losses' _last_weights)
+    assert (m._last_weights.cpu() - ref_w).abs().max() < 1e-6
+    orc = g.oracle(mean_min_distance_value=g.t("in_mean_min_distance"), merging_rules=rules)
+    assert (orc.get_weights() - ref_w).abs().max() < 1e-6
+    _, (xyz, *_rest) = orc.warp(g.t("in_t"))
+    assert (out["t_hat_pcd"].cpu() - xyz).abs().max() < 2e-6
+    assert torch.isfinite(out["rgb_marched"]).all()
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_merge_rules_repose_vs_oracle(dev, name):
+    """repose with merge rules takes k_lbs_skin's record-free branch (the quad kernel needs the
+    identity rules)."""
+    g = Golden(name)
+    m, rules = _merged_model(g, dev)
+    orc = g.oracle(mean_min_distance_value=0.0, merging_rules=rules)
+    rp = g.t("repose_rot_params")
+    with torch.no_grad():
+        xyz, jr = m.repose(rp.to(dev))
+    xo, jo = orc.repose(rp)
+    assert (xyz.cpu() - xo).abs().max() < 2e-6
+    assert (jr.cpu() - jo).abs().max() < 1e-6
+
+
+def _subset_oracle(model, idx):
+    st = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    for k in ("weights", "canonical_feat", "canonical_alpha", "canonical_rgbs", "direct_eps", "gammas"):
+        st[k] = st[k][idx]
+    return O.OracleModel(st, model.canonical_pcd.cpu()[idx], model.bones, mean_min_distance_value=0.0)
+
+
+def test_c5_full_size_repose_vs_oracle_subset(dev):
+    from apn_amd import harness, synthetic as S
+    scene = S.make_scene("C5")
+    N, J = scene.cfg.N, scene.cfg.J
+    assert (N, J) == (1_000_000, 48)
+    model = harness.build_model(scene, dev)
+    idx = torch.cat([torch.arange(0, N, 20), torch.tensor([N - 1])])
+    orc = _subset_oracle(model, idx)
+    poses = S.repose_sweep(J)
+    assert len(poses) == 60
+    for k in (3, 29, 47):
+        with torch.no_grad():
+            xyz, jr = model.repose(poses[k].to(dev))
+        xyz = xyz.cpu()
+        assert xyz.shape == (N, 3) and torch.isfinite(xyz).all()
+        xo, jo = orc.repose(poses[k])
+        err = (xyz[idx] - xo).abs().max()
+        print(f"C5 pose {k}: max|d xyz| on {len(idx)} points = {float(err):.2e}")
+        assert err < 2e-6
+        assert (jr.cpu() - jo).abs().max() < 1e-6
+
+
+def test_c5_repose_is_order_independent(dev):
+    """Every lane of the persistent loop writes only its own points: the full-size result does not
+    depend on the grid (two launches with different pose histories agree bit for bit)."""
+    from apn_amd import harness, synthetic as S
+    scene = S.make_scene("C5")
+    model = harness.build_model(scene, dev)
+    poses = S.repose_sweep(scene.cfg.J)
+    with torch.no_grad():
+        a = model.repose(poses[10].to(dev))[0].clone()
+        model.repose(poses[50].to(dev))
+        b = model.repose(poses[10].to(dev))[0]
+    assert torch.equal(a, b)
+    assert np.isfinite(b.cpu().numpy()).all()
