@@ -30,6 +30,26 @@ def build_model(scene: S.Scene, device="cuda") -> TemporalPoints:
     return model.to(device)
 
 
+PER_POINT_CTOR = ("canonical_pcd", "canonical_alpha", "canonical_feat", "canonical_rgbs")
+
+
+def shard_scene_points(scene: S.Scene, rank: int, world: int) -> S.Scene:
+    """The scene restricted to rank's contiguous point range [N*rank/world, N*(rank+1)/world)
+    (LBS is per point, so the shards skin independently; the skeleton,
+    joints and networks are replicated). Per-point parameters derived in the constructor (the
+    bone-distance LBS weights, direct_eps, gammas) are per point as well."""
+    import copy
+    N = len(scene.ctor["canonical_pcd"])
+    r0, r1 = N * rank // world, N * (rank + 1) // world
+    ctor = dict(scene.ctor)
+    for k in PER_POINT_CTOR:
+        ctor[k] = scene.ctor[k][r0:r1]
+    out = copy.copy(scene)
+    out.ctor = ctor
+    out.extra = dict(scene.extra, point_range=(r0, r1))
+    return out
+
+
 def render_kwargs_for(scene: S.Scene, device="cuda"):
     return scene.render_kwargs(device)
 

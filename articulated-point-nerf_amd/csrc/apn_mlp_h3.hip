@@ -40,7 +40,7 @@ constexpr int HB = 800;            // bytes per head-input row: hi 160 | lo 160 
 constexpr int HLO = 320;           // lo offset inside a head-input row
 
 constexpr int SW_B1 = 0, SW_B2 = 128, SW_B3 = 256, SW_B4 = 384, SW_WD = 512, SW_BD = 640, SW_BH = 644,
-              SW_WV2 = 708, SW_BV2 = 900, SW_TOTAL = 904;
+              SW_WV2 = 708, SW_BV2 = 900, SW_SC = 904, SW_DS = 912, SW_MODE = 920, SW_TOTAL = 924;
 
 // sin and cos of x for the positional encoding, |x| < ~1e6 (arguments are rel_c * 2^f, f <= 9):
 // quadrant reduction k = rint(2x/pi), r = x - k pi/2 with pi/2 in two floats (fma, so k C1 is
@@ -212,8 +212,17 @@ __device__ __forceinline__ void layer_mfma(const char* __restrict__ X, rsrc_t rs
 // lrelu(acc [+ bias]) -> hi/lo halves of the next layer's input rows (transposed C layout: lane
 // (li, g) of (mt, j) holds features 16(2w+j) + 4g + r of row 16 mt + li). Layers 2-4 start their
 // accumulators from the bias (bias == nullptr here).
+// Wave-uniform scaled-weights mode (apn_mlp_layout.h OFF_SCALE), read from the LDS copy.
+__device__ __forceinline__ bool mode_scaled(const float* sW) {
+  return __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, sW[SW_MODE])) != 0;
+}
+
+// Scaled weights (apn_mlp_layout.h OFF_SCALE): the accumulators hold 2^s (W x + b); `dsc` = 2^-s.
+// Layer 1 adds its (unscaled) bias with one fma(acc, 2^-s, b) -- fma(a, 1, b) == a + b, so the
+// unscaled mode is the plain sum; layers 2-4 (bias in the accumulator) multiply only when scaled
+// (a wave-uniform branch).
 __device__ __forceinline__ void store_act(char* __restrict__ X, int ot0, const float* __restrict__ bias,
-                                          const f32x4 (&acc)[4][2]) {
+                                          const f32x4 (&acc)[4][2], bool scaled, float dsc) {
   const int lane = threadIdx.x & 63;
   const int li = lane & 15, g = lane >> 4;
 #pragma unroll
@@ -224,7 +233,9 @@ __device__ __forceinline__ void store_act(char* __restrict__ X, int ot0, const f
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       const f32x4 a = acc[mt][j];
-      const f32x4 v = lrelu4(bias ? f32x4{a[0] + bb[0], a[1] + bb[1], a[2] + bb[2], a[3] + bb[3]} : a);
+      const f32x4 v = lrelu4(bias ? f32x4{fmaf(a[0], dsc, bb[0]), fmaf(a[1], dsc, bb[1]), fmaf(a[2], dsc, bb[2]),
+                                          fmaf(a[3], dsc, bb[3])}
+                                  : (scaled ? f32x4{a[0] * dsc, a[1] * dsc, a[2] * dsc, a[3] * dsc} : a));
       h4 hi, lo;
       split4(v, hi, lo);
       char* p = X + act_off(16 * mt + li, c) + sub;
@@ -371,11 +382,10 @@ __global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
   char* const X0 = Xs;
   char* const X1 = PP ? Xs + XBUF : Xs;
   char* const HX = PP ? X1 : Hs;     // head input rows
-  int* const range_flag = (int*)(wbuf + OFF_FLAG);
   {  // a launch with the flag already set (these weights overflowed before): leave the samples
      // to the FP32 kernel. Block-uniform decision (one read, broadcast through LDS).
     __shared__ int s_skip;
-    if (threadIdx.x == 0) s_skip = __builtin_nontemporal_load(range_flag);
+    if (threadIdx.x == 0) s_skip = __builtin_nontemporal_load((const int*)(wbuf + OFF_FLAG));
     __syncthreads();
     if (s_skip) return;
   }
@@ -387,16 +397,26 @@ __global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
   // scalar, or every buffer load becomes a readfirstlane waterfall loop
   const int lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, g = lane >> 4;
-  const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(wbuf + OFF_H16), 0, H_TOTAL * 2, 0x00020000);
+  // buffer resource over the fp16 fragments and the range flag right after them (written with a
+  // buffer store: no extra 64-bit pointer live across the tile loop)
+  const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(wbuf + OFF_H16), 0, H_TOTAL * 2 + 4, 0x00020000);
   const int ot0 = 2 * wid;
+  // per-matrix weight scales 2^s (W1E, W2, W3, W4, WH), kept in LDS with their inverses (exact:
+  // powers of two) and read where used, so they hold no registers across the tile loop
+  const float* const scp = wbuf + OFF_SCALE;
   for (int i = tid; i < 128; i += MLP_THREADS) {
     sW[SW_B1 + i] = wbuf[OFF_B1 + i];
-    sW[SW_B2 + i] = wbuf[OFF_B2 + i];
-    sW[SW_B3 + i] = wbuf[OFF_B3 + i];
-    sW[SW_B4 + i] = wbuf[OFF_B4 + i];
+    sW[SW_B2 + i] = wbuf[OFF_B2 + i] * scp[1];   // accumulator initial values: 2^s b
+    sW[SW_B3 + i] = wbuf[OFF_B3 + i] * scp[2];
+    sW[SW_B4 + i] = wbuf[OFF_B4 + i] * scp[3];
     sW[SW_WD + i] = wbuf[OFF_WD + i];
   }
-  if (tid < 64) sW[SW_BH + tid] = wbuf[OFF_BH + tid];
+  if (tid < 5) {
+    sW[SW_SC + tid] = scp[tid];
+    sW[SW_DS + tid] = 1.f / scp[tid];
+  }
+  if (tid == 5) sW[SW_MODE] = scp[5];
+  if (tid < 64) sW[SW_BH + tid] = wbuf[OFF_BH + tid] * scp[4];
   if (tid < 192) sW[SW_WV2 + tid] = wbuf[OFF_WV2 + tid];
   if (tid < 3) sW[SW_BV2 + tid] = wbuf[OFF_BV2 + tid];
   if (tid == 0) sW[SW_BD] = wbuf[OFF_BD];
@@ -463,6 +483,13 @@ __global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
         acc[mt][j] = f32x4{v.x, v.y, v.z, v.w};
       }
     }
+    if (mode_scaled(sW)) {   // layer-1 accumulators in the W1E scale: 2^s1 P
+      const float sc1 = sW[SW_SC];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[mt][j] = acc[mt][j] * sc1;
+    }
     fetch(tile + per_xcd);
     // ------------------------------------------------ gather + posenc + direct-blend terms
     ws_gather(tid, nb, q, gregs, X0, sTo, sRow, sV, vemb_const);
@@ -490,18 +517,18 @@ __global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
     // ------------------------------------------------ feat_net: 4 x (Linear + LeakyReLU)
     layer_mfma<2, 4, 2, PP>(X0, rs, H_W1E, ot0, H_W2, ot0, acc, a);
     if (!PP) __syncthreads();
-    store_act(X1, ot0, sW + SW_B1, acc);
+    store_act(X1, ot0, sW + SW_B1, acc, mode_scaled(sW), sW[SW_DS + 0]);
     __syncthreads();
     APN_PHASE(1)
     init_bias(acc, ot0, sW + SW_B2);
     layer_mfma<4, 4, 2, PP>(X1, rs, H_W2, ot0, H_W3, ot0, acc, a);
     if (!PP) __syncthreads();
-    store_act(X0, ot0, nullptr, acc);
+    store_act(X0, ot0, nullptr, acc, mode_scaled(sW), sW[SW_DS + 1]);
     __syncthreads();
     init_bias(acc, ot0, sW + SW_B3);
     layer_mfma<4, 4, 2, PP>(X0, rs, H_W3, ot0, H_W4, ot0, acc, a);
     if (!PP) __syncthreads();
-    store_act(X1, ot0, nullptr, acc);
+    store_act(X1, ot0, nullptr, acc, mode_scaled(sW), sW[SW_DS + 2]);
     __syncthreads();
     init_bias(acc, ot0, sW + SW_B4);
     layer_mfma<4, 5, 1, PP>(X1, rs, H_W4, ot0, H_WH, wid, acc, a);
@@ -511,7 +538,9 @@ __global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
     for (int j = 0; j < 2; ++j) {
       const int o0 = 16 * (ot0 + j) + 4 * g;
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) *(f32x4*)(X0 + out32_off(16 * mt + li, o0 >> 2)) = lrelu4(acc[mt][j]);
+      for (int mt = 0; mt < 4; ++mt)
+        *(f32x4*)(X0 + out32_off(16 * mt + li, o0 >> 2)) =
+            lrelu4(mode_scaled(sW) ? acc[mt][j] * sW[SW_DS + 3] : acc[mt][j]);
     }
     __syncthreads();
     APN_PHASE(2)
@@ -527,7 +556,8 @@ __global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
         for (int r = 0; r < 4; ++r) h[r] = h[r] + w * v[r];
       }
       // range guard (see the header comment): false for NaN too
-      if (!(fmaxf(fmaxf(fabsf(h[0]), fabsf(h[1])), fmaxf(fabsf(h[2]), fabsf(h[3]))) <= H3_RANGE)) *range_flag = 1;
+      if (!(fmaxf(fmaxf(fabsf(h[0]), fabsf(h[1])), fmaxf(fabsf(h[2]), fabsf(h[3]))) <= H3_RANGE))
+        __builtin_amdgcn_raw_buffer_store_b32(1, rs, 0, H_TOTAL * 2, 0);   // the range flag (OFF_FLAG)
       // densitynet Linear(128 -> 1) (tineuvox.py:158) over this thread's 4 features, then the half-wave
       const f32x4 wd = *(const f32x4*)(sW + SW_WD + 4 * oq);
       float d = ((h[0] * wd[0] + h[1] * wd[1]) + h[2] * wd[2]) + h[3] * wd[3];
@@ -612,7 +642,7 @@ __global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
       float pc[3] = {0.f, 0.f, 0.f};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float v = fmaxf(ah[r], 0.f);
+        const float v = fmaxf(mode_scaled(sW) ? ah[r] * sW[SW_DS + 4] : ah[r], 0.f);
 #pragma unroll
         for (int c = 0; c < 3; ++c) pc[c] += v * sW[SW_WV2 + 64 * c + o0 + r];
       }
@@ -646,8 +676,53 @@ __global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
     out[(size_t)prev_s0 * 3 + tid] = *(const float4*)(sOut + 4 * tid);
 }
 
-// fp32 region of wbuf -> fp16 hi/lo fragments (layout: apn_mlp_layout.h). One thread per
-// (matrix, o-tile, chunk, lane).
+// Per-matrix scales (apn_mlp_layout.h OFF_SCALE) from max|w| of W1E, W2, W3, W4, WH: one
+// workgroup, one pass over the fp32 region (67 584 weights).
+__global__ __launch_bounds__(256) void k_weight_scales(float* __restrict__ wbuf) {
+  __shared__ float red[5][256];
+  const int tid = threadIdx.x;
+  const int offs[5] = {OFF_W1E, OFF_W2, OFF_W3, OFF_W4, OFF_WH};
+  const int lens[5] = {128 * KE, 128 * 128, 128 * 128, 128 * 128, 64 * KV};
+#pragma unroll
+  for (int m = 0; m < 5; ++m) {
+    float mx = 0.f;
+    for (int i = tid; i < lens[m]; i += 256) mx = fmaxf(mx, fabsf(wbuf[offs[m] + i]));
+    red[m][tid] = mx;
+  }
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (tid < w)
+#pragma unroll
+      for (int m = 0; m < 5; ++m) red[m][tid] = fmaxf(red[m][tid], red[m][tid + w]);
+    __syncthreads();
+  }
+  if (tid == 0) {
+    bool scaled = false;
+    float mx[5];
+#pragma unroll
+    for (int m = 0; m < 5; ++m) {
+      mx[m] = red[m][0];
+      // all-zero (or non-finite: left to the range guard) matrices keep scale 1
+      if (mx[m] > 0.f && mx[m] <= 3.0e38f && (mx[m] < SCALE_LO || mx[m] > SCALE_HI)) scaled = true;
+    }
+#pragma unroll
+    for (int m = 0; m < 5; ++m) {
+      float sc = 1.f;
+      if (scaled && mx[m] > 0.f && mx[m] <= 3.0e38f) {
+        int e;
+        frexpf(mx[m], &e);                        // mx = f 2^e, f in [0.5, 1)
+        sc = ldexpf(1.f, SCALE_TARGET_EXP - e);   // mx * sc in [2^12, 2^13)
+      }
+      wbuf[OFF_SCALE + m] = sc;
+    }
+    wbuf[OFF_SCALE + 5] = scaled ? 1.f : 0.f;
+    wbuf[OFF_SCALE + 6] = 0.f;
+    wbuf[OFF_SCALE + 7] = 0.f;
+  }
+}
+
+// fp32 region of wbuf -> fp16 hi/lo fragments of w * 2^s (layout: apn_mlp_layout.h). One thread
+// per (matrix, o-tile, chunk, lane).
 __global__ void k_split_weights(float* __restrict__ wbuf) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t == 0) *(int*)(wbuf + OFF_FLAG) = 0;   // new weights: clear the range flag
@@ -663,6 +738,7 @@ __global__ void k_split_weights(float* __restrict__ wbuf) {
   const int o = 16 * ot + (lane & 15), k0 = 32 * q + 8 * (lane >> 4);
   const int hbase = mat == 0 ? H_W1E : (mat == 1 ? H_W2 : (mat == 2 ? H_W3 : (mat == 3 ? H_W4 : H_WH)));
   _Float16* dst = (_Float16*)(wbuf + OFF_H16) + hbase + (size_t)((ot * nq + q) * 2) * FRAG_HALVES + lane * 8;
+  const float sc = wbuf[OFF_SCALE + mat];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int k = k0 + j;
@@ -676,6 +752,7 @@ __global__ void k_split_weights(float* __restrict__ wbuf) {
       const int off = mat == 1 ? OFF_W2 : (mat == 2 ? OFF_W3 : OFF_W4);
       w = wbuf[off + o * 128 + k];
     }
+    w *= sc;   // exact (power of two)
     const _Float16 hi = (_Float16)w;
     dst[j] = hi;
     dst[FRAG_HALVES + j] = (_Float16)(w - (float)hi);
@@ -720,6 +797,7 @@ using namespace apn;
 extern "C" int apn_mlp_split_weights(float* wbuf, void* stream) {
   if (!wbuf) return APN_ERR_ARG;
   constexpr int n = 8 * 2 * 64 + 3 * 8 * 4 * 64 + 4 * 5 * 64;
+  hipLaunchKernelGGL(h3::k_weight_scales, dim3(1), dim3(256), 0, (hipStream_t)stream, wbuf);
   hipLaunchKernelGGL(h3::k_split_weights, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, wbuf);
   return launch_status();
 }

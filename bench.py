@@ -5,10 +5,14 @@ Workload (BASELINE.json configs[1]): dnerf/jumpingjacks-like s
 A step = one full frame: TemporalPoints.forward over all 640k rays (skeleton, LBS, grid,
 sampling, radius kNN, neighbour MLP, compositing), inputs resident in HBM.
 
-Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process per GPU, each
-rank renders its own frame (different time t) per step -- frames are independent units, no
-data-path collective (weak scaling); the timing is barrier + synchronize bracketed and the
-max over ranks (RCCL all-reduce MAX of the elapsed time).
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process per GPU. By
+default (``--shard rays``) the N ranks render ONE frame together (BASELINE
+configs C3/C4): every rank replicates the cheap per-frame stages, renders the contiguous ray
+range holding ~1/N of the in-bbox samples, and the per-ray tiles are assembled with one RCCL
+all-gather over xGMI -- strong scaling, ``value`` = frame rays / step time. ``--shard frames``
+has every rank render its own frame instead (weak scaling, no data-path collective). C5
+(LBS-only) shards the points N/W per rank with no collective (strong scaling). The timing is
+barrier + synchronize bracketed and the max over ranks (all-reduce MAX of the elapsed time).
 
 Rank 0 prints ONE JSON line. Diagnostics go to stderr.
 """
@@ -63,6 +67,18 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def cpu_model_name():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
 def cpu_baseline(model, scene, rows, threads):
     """The oracle (CPU restatement, pure PyTorch + scipy cKDTree kNN) on a bounded sample:
     ``rows`` image rows spread evenly over the same frame (every H/rows-th row), so the
@@ -92,9 +108,29 @@ def cpu_baseline(model, scene, rows, threads):
             break
     dt = (time.perf_counter() - t0) / n_rep
     nrays = rows * W
-    return {"value": nrays / dt, "unit": "rays/s", "cores": threads, "kind": "port",
+    return {"value": nrays / dt, "unit": "rays/s", "cores": threads, "cpu_model": cpu_model_name(), "kind": "port",
             "sample": f"{rows} evenly spaced rows x {W} = {nrays} rays of the same frame, {n_rep} timed repeats "
-                      f"(oracle: torch-CPU MLP, scipy cKDTree kNN), {dt:.2f} s/band"}, ref, sel
+                      f"(oracle: torch-CPU MLP, scipy cKDTree kNN), {dt:.2f} s/band"}, ref, sel, (orc, sub, t)
+
+
+def same_cloud_error(gpu_out, orc, sub, t, sel):
+    """The oracle re-rendering the band against the GPU's own warped cloud (identical sample
+    positions and neighbour lists): max |rgb - oracle| over all band rays, and over the rays whose
+    oracle compositing is not within 1e-6 of a discontinuity (fast_color_thres on alpha/weight,
+    T = 1e-3; oracle/flips.py) -- the arithmetic error of the GPU path at the bench size."""
+    from oracle.flips import near_discontinuity, ray_errors, PATH_OF_KEY
+    ref = orc.forward(t, render_depth=True, render_kwargs=sub, render_weights=True, knn_tree=True,
+                      t_hat_override=gpu_out["t_hat_pcd"].detach().cpu())
+    res = {"rays": int(sel.numel())}
+    for key in ("rgb_marched", "rgb_marched_direct"):
+        a = gpu_out[key].detach().float().cpu()[sel].numpy()
+        b = ref[key].numpy()
+        err = ray_errors(a, b)
+        near = near_discontinuity(orc.trace, len(b), PATH_OF_KEY[key])
+        res[key] = {"max_abs": float(err.max()), "max_abs_off_discontinuities": float(err[~near].max()),
+                    "rays_over_1e-5": int((err > 1e-5).sum()),
+                    "rays_over_1e-5_unexplained": int(((err > 1e-5) & ~near).sum())}
+    return res
 
 
 def psnr_vs_oracle(gpu_out, ref, sel):
@@ -113,13 +149,17 @@ def psnr_vs_oracle(gpu_out, ref, sel):
 def lbs_sweep(args, rank, world, dev):
     """C5: LBS-only repose throughput (BASELINE.json configs[4]; run.py:1364-1377 sweep). One step
     = one pose of the sweep through TemporalPoints.repose (skeleton + fused LBS, 1M points, 48
-    bones); every rank sweeps its own poses (weak scaling). Roofline: k_lbs_skin against HBM with
-    B_alg = N*(24 + 4J) bytes per pose."""
+    bones). With N>1 GPUs the points are sharded N/W per rank (SURVEY.md §8(e): LBS is per point;
+    the skeleton stage is replicated, no collective) and every rank runs the same poses -- strong
+    scaling. Roofline: k_lbs_skin_quad against HBM with B_alg = N*(24 + 4J) bytes per pose
+    (SURVEY.md 8(d)), per rank N_r points."""
     scene = S.make_scene(args.config)
+    N_total = scene.cfg.N
+    if world > 1:
+        scene = harness.shard_scene_points(scene, rank, world)
     model = harness.build_model(scene, dev)
-    N, J = scene.cfg.N, scene.cfg.J
+    N, J = len(scene.ctor["canonical_pcd"]), scene.cfg.J
     poses = S.repose_sweep(J).to(dev)
-    poses = poses.roll(rank, 0)
     for i in range(args.warmup):
         model.repose(poses[i % len(poses)])
     model.timing = {}
@@ -157,26 +197,31 @@ def lbs_sweep(args, rank, world, dev):
                 orc.repose(pc[n_rep % len(pc)])
                 n_rep += 1
             dt = (time.perf_counter() - c0) / n_rep
-            cpu = {"value": N / dt, "unit": "points/s", "cores": torch.get_num_threads(), "kind": "port",
+            cpu = {"value": N / dt, "unit": "points/s", "cores": torch.get_num_threads(),
+                   "cpu_model": cpu_model_name(), "kind": "port",
                    "sample": f"{n_rep} poses of the same sweep, full 1M-point cloud (oracle: torch-CPU get_weights + "
                              f"LBS), {dt:.2f} s/pose"}
         except Exception as e:  # never lose the GPU line over the baseline leg
             log(f"cpu baseline failed: {e!r}")
-    value = world * args.steps * N / elapsed
+    value = args.steps * N_total / elapsed
     line = {
         "metric": "LBS-only repose throughput, 1M pts, 48 bones (points/s)",
         "value": value, "unit": "points/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "strong" if world > 1 else "weak",
         "vs_baseline": None, "dtype": "fp32", "data": "synthetic (procedural 48-joint capsule cloud, repose sweep)",
-        "config": {"workload": S.CONFIGS[args.config].name + f" ({args.config})", "points": N, "bones": J,
-                   "poses_per_s": world * args.steps / elapsed, "parallelism": f"poses x{world}" if world > 1 else "single"},
-        "roofline": {"bound": "hbm", "kernel": "k_lbs_skin", "achieved": b_alg / (lbs_ms * 1e-3) / 1e9 if lbs_ms > 0 else 0.0,
+        "config": {"workload": S.CONFIGS[args.config].name + f" ({args.config})", "points": N_total, "bones": J,
+                   "points_per_rank": N, "poses_per_s": args.steps / elapsed,
+                   "parallelism": f"points x{world} (no collective)" if world > 1 else "single"},
+        "roofline": {"bound": "hbm", "kernel": "k_lbs_skin_quad",
+                     "achieved": b_alg / (lbs_ms * 1e-3) / 1e9 if lbs_ms > 0 else 0.0,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": b_alg / (lbs_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if lbs_ms > 0 else 0.0,
                      "traffic": (read_traffic(os.path.join(ROOT, "profiles", "r01_lbs_traffic_c5.json")) or {}).get(
                          "bytes_per_launch"), "bytes_per_launch": b_alg, "avg_launch_ms": lbs_ms,
-                     "note": "achieved = B_alg = N*(24+4J) bytes per pose (SURVEY.md 8(d) C5) / avg k_lbs_skin time "
-                             "(HIP events on the launch stream); the step also runs the skeleton kernel"},
+                     "note": "achieved = B_alg = N_r*(24+4J) bytes per pose (SURVEY.md 8(d) C5; N_r = this rank's "
+                             "points) / avg LBS kernel time (HIP events on the launch stream); the step also runs "
+                             "the skeleton kernel"},
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)
@@ -198,10 +243,10 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--cpu-rows", type=int, default=16, help="image rows in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--shard", choices=["frames", "rays"], default="frames",
-                    help="N>1: 'frames' = every rank renders its own frame (weak scaling, no data-path "
-                         "collective); 'rays' = the ranks split one frame's rays and all-gather the tiles "
-                         "over RCCL (strong scaling)")
+    ap.add_argument("--shard", choices=["frames", "rays"], default="rays",
+                    help="N>1: 'rays' (default) = the ranks split one frame's rays and all-gather the tiles "
+                         "over RCCL (strong scaling, SURVEY.md 8(e)); 'frames' = every rank renders its own "
+                         "frame (weak scaling, no data-path collective)")
     args = ap.parse_args()
     torch.set_grad_enabled(False)   # a render benchmark: the reference renders under no_grad (run.py:80, 241)
 
@@ -210,10 +255,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one process per GPU; APN_DIST_BACKEND=gloo rehearses N>1 with several ranks on one card
     local = local % max(torch.cuda.device_count(), 1)
+    backend = os.environ.get("APN_DIST_BACKEND", "nccl")   # nccl = RCCL over xGMI
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group(os.environ.get("APN_DIST_BACKEND", "nccl"))   # nccl = RCCL over xGMI
+        dist.init_process_group(backend)
+    backend = "RCCL (xGMI)" if backend == "nccl" else backend
     dev = torch.device("cuda", local)
 
     if args.config == "C5":
@@ -332,11 +379,12 @@ def main():
     traffic = read_traffic(os.path.join(ROOT, "profiles", "r01_point_mlp_traffic.json"))
     ms_per_step = elapsed / args.steps * 1e3
     value = (1 if shard_rays else world) * args.steps * R / elapsed
-    cpu = psnr = None
+    cpu = psnr = same = None
     if world == 1 and not args.no_cpu_baseline:
         try:
-            cpu, ref, sel = cpu_baseline(model, scene, args.cpu_rows, torch.get_num_threads())
+            cpu, ref, sel, (orc, sub, t_cpu) = cpu_baseline(model, scene, args.cpu_rows, torch.get_num_threads())
             psnr = psnr_vs_oracle(out, ref, sel)
+            same = same_cloud_error(out, orc, sub, t_cpu, sel)
         except Exception as e:  # never lose the GPU line over the baseline leg
             log(f"cpu baseline failed: {e!r}")
     line = {
@@ -349,7 +397,9 @@ def main():
                            "oracle <= 3e-7 on alpha/rgb" if variant in (0, 3) else "fp32 MFMA (v_mfma_f32_16x16x4_f32)"),
         "config": {"workload": S.CONFIGS[args.config].name + f" ({args.config})", "rays_per_frame": R,
                    "points": scene.cfg.N, "bones": scene.cfg.J, "inbbox_samples": stats.get("inbbox_samples"),
-                   "kept_samples": S_kept, "parallelism": (f"rays x{world} + RCCL tile all-gather" if shard_rays else f"frames x{world}")
+                   "kept_samples": S_kept,
+                   "parallelism": (f"rays x{world} + {backend} all_gather_into_tensor of the per-ray tiles"
+                                   if shard_rays else f"frames x{world} (no data-path collective)")
                    if world > 1 else "single"},
         "roofline": {"bound": "mfma", "kernel": kernel, "achieved": achieved, "peak": peak,
                      "unit": "TFLOP/s", "frac": achieved / peak,
@@ -364,6 +414,7 @@ def main():
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
         "cpu_baseline": cpu,
         "psnr_vs_oracle": psnr,
+        "same_cloud_vs_oracle": same,
     }
     print(json.dumps(line), flush=True)
     if world > 1:

@@ -1,4 +1,4 @@
-"""Explained flips: the reference's compositing has three discontinuities, and a ray whose oracle
+"""TEST INFRASTRUCTURE ONLY (tests/ and bench.py's cpu_baseline leg). Explained flips: the reference's compositing has three discontinuities, and a ray whose oracle
 values sit on one of them may legitimately differ from the oracle by more than the fp tolerance
 when an input moves by an ulp:
 

@@ -1,0 +1,71 @@
+"""Ray-sharded rendering across real processes (apn_amd/shard.py).
+
+Two fresh child processes (torch.multiprocessing ``spawn``) each render their ray range of one
+frame through ``render_sharded`` and assemble the frame with the tile all-gather over ``gloo``
+(RCCL needs one GPU per rank; this box has one). Rank 0 also renders the frame in one process.
+The assembled frames of both ranks must equal the single-process frame bit for bit.
+
+The file name sorts first so that pytest runs this test before any other GPU test touches the
+device in the parent: the parent never initialises the GPU before the children are spawned (it
+does not touch it at all here)."""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+WORLD = 2
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    from apn_amd import harness, synthetic as S
+    from apn_amd.shard import pack_tile, render_sharded
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda", 0)
+        scene = S.make_scene(S.SceneConfig("spawn shard 200x200 50k pts 24 bones", 50_000, 24, 200, 200))
+        model = harness.build_model(scene, dev)
+        rk = scene.render_kwargs(dev)
+        t = torch.tensor([scene.cfg.t], device=dev)
+        poses, Ks = scene.c2w[None].to(dev), scene.K[None].to(dev)
+        with torch.no_grad():
+            out = render_sharded(model, t, rk, rank, world, poses=poses, Ks=Ks, get_skeleton=True)
+            R = rk["rays_o"].shape[0]
+            tiles = {"assembled": pack_tile(out, R, dev).cpu(),
+                     "range": torch.tensor(model.last_ray_range),
+                     "bounds": torch.tensor(model.last_ray_bounds)}
+            if rank == 0:
+                single = model(t, render_depth=True, render_kwargs=rk, render_weights=True, poses=poses, Ks=Ks,
+                               get_skeleton=True)
+                tiles["single"] = pack_tile(single, R, dev).cpu()
+        torch.cuda.synchronize()
+        torch.save(tiles, os.path.join(outdir, f"rank{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_render_sharded_two_processes_bit_identical():
+    import torch.multiprocessing as mp
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(WORLD, _free_port(), d), nprocs=WORLD, join=True)
+        res = [torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=True) for r in range(WORLD)]
+    single = res[0]["single"]
+    bounds = res[0]["bounds"].tolist()
+    assert bounds[0] == 0 and bounds[-1] == single.shape[0]
+    assert torch.equal(res[1]["bounds"], res[0]["bounds"])
+    for r in range(WORLD):
+        assert tuple(res[r]["range"].tolist()) == (bounds[r], bounds[r + 1])
+        assert torch.equal(res[r]["assembled"], single), r
+    # both ranks did real work (the object is hit by rays of both halves of the split)
+    assert 0 < bounds[1] < single.shape[0]

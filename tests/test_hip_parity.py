@@ -458,7 +458,7 @@ def test_forward_vs_oracle_same_cloud(golden_model, dev, key):
     within 1e-5 (depth: 1e-5 of its step-unit range) unless the oracle's compositing of that ray
     sits within 1e-6 of a discontinuity (fast_color_thres on alpha / weight, T = 1e-3), see
     tests/flips.py."""
-    from flips import assert_flips_explained
+    from oracle.flips import assert_flips_explained
     g, m = golden_model
     out = _forward(g, m, dev)
     orc, ref = _oracle_on_cloud(g, out["t_hat_pcd"].cpu(), perm=m.last_palette_perm)
@@ -488,7 +488,7 @@ def test_forward_vs_reference_golden_same_bbox(golden_model, dev, key):
     # and every ray over 1e-5 is explained by the oracle's compositing of the reference's own
     # cloud and bbox sitting on a discontinuity; the oracle matches the reference to ~1.5e-6
     # (MKL summation order, tests/test_oracle_golden.py), hence the wider 3e-6 band
-    from flips import assert_flips_explained
+    from oracle.flips import assert_flips_explained
     orc = g.oracle(mean_min_distance_value=g.t("in_mean_min_distance"))
     orc.forward(g.t("in_t"), render_depth=True, render_kwargs=g.render_kwargs(), render_weights=True,
                 t_hat_override=g.t("out_t_hat_pcd"), bbox=(g.t("trace_xyz_min"), g.t("trace_xyz_max")),
@@ -812,8 +812,8 @@ def test_full_size_band_vs_oracle(dev, config):
         sub[k] = rkc[k][sel].contiguous()
     # the full frame's bbox (from the whole cloud) -> pass it explicitly to the band
     ref = orc.forward(torch.tensor([scene.cfg.t]), render_depth=True, render_kwargs=sub, render_weights=True,
-                      t_hat_override=out["t_hat_pcd"].cpu(), knn_tree=True)
-    from flips import assert_flips_explained
+                      t_hat_override=out["t_hat_pcd"].cpu(), knn_tree=True, perm=model.last_palette_perm)
+    from oracle.flips import assert_flips_explained
     for key in KEYS:
         assert_flips_explained(key, out[key].cpu()[sel].numpy(), ref[key].numpy(), orc.trace)
 

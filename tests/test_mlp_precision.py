@@ -92,18 +92,60 @@ def run_mlp_stage(dev, m, orc, variant, render_kwargs, t):
     return o, tr, mlp_range_fallback(wbuf)
 
 
-def check_stage(o, tr, tag):
+def mlp_stage_f64(orc, tr, viewdirs):
+    """alpha / rgb of the kept samples in float64 from the reference's own fp32 inputs: rel_p,
+    to_nn and rel_c = Rinv[s_i] rel_p exactly as the (fp32) reference forms them
+    (temporalpoints.py:446-447, 478-480), then the posenc, feat_net, IDW sum, densitynet,
+    raw2alpha and rgbnet (temporalpoints.py:481-515) in float64."""
+    d = torch.float64
+    s_i = torch.from_numpy(tr["s_i"])
+    K = s_i.shape[1]
+    rel_p = torch.from_numpy(tr["pts"])[:, None, :] - tr["t_hat_pcd"][s_i, :]
+    to_nn = (rel_p ** 2).sum(-1)
+    Rk = tr["Rinv"][s_i, :, :][..., :3, :3]
+    rel_c = torch.bmm(Rk.reshape(-1, 3, 3), rel_p.reshape(-1, 3).unsqueeze(-1)).squeeze(-1)
+    st = {k: v.to(d) for k, v in orc.nets.items()}
+    w = 1 / (to_nn.to(d) + 1e-6)
+    w = (w / w.sum(-1, keepdim=True)).unsqueeze(-1)
+    x = [O.poc_fre(rel_c.to(d), orc.pos_poc.to(d)), orc.feat[s_i].reshape(-1, orc.feat.shape[-1]).to(d)]
+    if tr["pose_embedding"] is not None:
+        x.append(tr["pose_embedding"].to(d).expand(len(x[0]), -1))
+    h = (O.feat_net(torch.cat(x, -1), st).reshape(len(s_i), K, -1) * w).sum(1)
+    dens = O._lin(h, st, "densitynet").squeeze(-1)
+    alpha = 1 - (1 + torch.exp(dens + orc.act_shift)) ** (-0.5)
+    views = O.poc_fre(viewdirs.to(d), orc.view_poc.to(d))[torch.from_numpy(tr["ray_id"])]
+    rgb = torch.sigmoid(O.rgbnet(h, views, st))
+    return alpha, rgb
+
+
+def check_stage(o, tr, tag, f64=None):
+    """alpha/rgb: within 1e-5 of the fp32 oracle -- or, when the fp32 oracle itself is further
+    than 5e-6 from the float64 evaluation (ill-conditioned scaled networks), within
+    max(1e-5, 2x the fp32 oracle's own error) of float64: as accurate as the reference's own fp32
+    torch arithmetic. Direct blend (no MLP) 1e-6, weight-vis colour 1e-5 vs the fp32 oracle."""
     da = float((o[:, 3] - tr["alpha"]).abs().max())
     dr = float((o[:, 0:3] - tr["rgbs"]).abs().max())
     dad = float((o[:, 7] - tr["alpha_direct"]).abs().max())
     drd = float((o[:, 4:7] - tr["rgbs_direct"]).abs().max())
     dc = float((o[:, 8:11] - torch.from_numpy(tr["col"])).abs().max())
-    print(f"{tag}: max|d alpha| {da:.2e} max|d rgb| {dr:.2e} direct {dad:.1e}/{drd:.1e} col {dc:.1e} "
-          f"(alpha range {float(tr['alpha'].min()):.3g}..{float(tr['alpha'].max()):.3g})")
+    msg = (f"{tag}: vs fp32 oracle max|d alpha| {da:.2e} max|d rgb| {dr:.2e} direct {dad:.1e}/{drd:.1e} "
+           f"col {dc:.1e} (alpha range {float(tr['alpha'].min()):.3g}..{float(tr['alpha'].max()):.3g})")
     assert torch.isfinite(o).all()
-    assert da < 1e-5 and dr < 1e-5
-    assert dad < 1e-6 and drd < 1e-6
-    assert dc < 1e-5
+    if f64 is not None:
+        a64, r64 = f64
+        ga = float((o[:, 3].double() - a64).abs().max()); oa = float((tr["alpha"].double() - a64).abs().max())
+        gr = float((o[:, 0:3].double() - r64).abs().max()); orr = float((tr["rgbs"].double() - r64).abs().max())
+        msg += f"; vs float64: gpu alpha {ga:.2e} rgb {gr:.2e}, fp32 oracle alpha {oa:.2e} rgb {orr:.2e}"
+        print(msg)
+        if max(oa, orr) > 5e-6:
+            assert ga <= max(1e-5, 2 * oa) and gr <= max(1e-5, 2 * orr), msg
+        else:
+            assert da < 1e-5 and dr < 1e-5, msg
+    else:
+        print(msg)
+        assert da < 1e-5 and dr < 1e-5, msg
+    assert dad < 1e-6 and drd < 1e-6, msg
+    assert dc < 1e-5, msg
 
 
 @pytest.fixture(scope="module")
@@ -130,9 +172,11 @@ def test_mlp_stage_non_fp16_exact(dev, camera, mode, variant):
                         act_shift=float(m.tineuvox.act_shift), voxel_size_ratio=float(m.tineuvox.voxel_size_ratio),
                         mean_min_distance_value=float(m.mean_min_distance))
     t = torch.tensor([scene.cfg.t])
+    rk = scene.render_kwargs("cpu")
     with torch.no_grad():
-        o, tr, fallback = run_mlp_stage(dev, m, orc, variant, scene.render_kwargs("cpu"), t)
-    check_stage(o, tr, f"{camera}/{mode}/v{variant} fallback={fallback}")
+        o, tr, fallback = run_mlp_stage(dev, m, orc, variant, rk, t)
+        f64 = mlp_stage_f64(orc, tr, rk["viewdirs"])
+    check_stage(o, tr, f"{camera}/{mode}/v{variant} fallback={fallback}", f64)
     if variant == 0:
         # the guard fires exactly when a split value leaves the fp16 range
         assert fallback == (mode == "overflow"), fallback

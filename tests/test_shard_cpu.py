@@ -92,3 +92,25 @@ def test_gather_tiles_gloo_world2(counts):
     for rank, ok, tmax in res:
         assert ok, rank
         assert tmax == float(world)
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_point_shards_partition_the_cloud(world):
+    """C5 point sharding (bench.py --config C5 with N>1): the ranks' point ranges partition the
+    cloud, and the per-point LBS parameters the constructor derives (bone-distance weights) of
+    the shards concatenate to the full model's -- so the sharded sweep skins exactly the full
+    cloud."""
+    from apn_amd import harness, synthetic as S
+    scene = S.make_scene(S.SceneConfig("shard test", 3001, 24, 0, 0))
+    full = harness.build_model(scene, "cpu")
+    parts, ranges = [], []
+    for r in range(world):
+        sc = harness.shard_scene_points(scene, r, world)
+        ranges.append(sc.extra["point_range"])
+        m = harness.build_model(sc, "cpu")
+        parts.append((m.canonical_pcd, m.weights.detach(), m.canonical_feat.detach()))
+    assert ranges[0][0] == 0 and ranges[-1][1] == 3001
+    assert all(ranges[i][1] == ranges[i + 1][0] for i in range(world - 1))
+    assert torch.equal(torch.cat([p[0] for p in parts]), full.canonical_pcd)
+    assert torch.equal(torch.cat([p[1] for p in parts]), full.weights.detach())
+    assert torch.equal(torch.cat([p[2] for p in parts]), full.canonical_feat.detach())
