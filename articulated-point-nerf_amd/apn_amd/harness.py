@@ -39,6 +39,7 @@ def shard_scene_points(scene: S.Scene, rank: int, world: int) -> S.Scene:
     joints and networks are replicated). Per-point parameters derived in the constructor (the
     bone-distance LBS weights, direct_eps, gammas) are per point as well."""
     import copy
+    from .temporalpoints import weights_from_bones
     N = len(scene.ctor["canonical_pcd"])
     r0, r1 = N * rank // world, N * (rank + 1) // world
     ctor = dict(scene.ctor)
@@ -46,6 +47,11 @@ def shard_scene_points(scene: S.Scene, rank: int, world: int) -> S.Scene:
         ctor[k] = scene.ctor[k][r0:r1]
     out = copy.copy(scene)
     out.ctor = ctor
+    # the raw LBS weights of the full cloud, sliced (the vectorised bone-distance pass is not
+    # bit-stable under a change of N); loaded over the constructor's own by build_model
+    full_w = weights_from_bones(torch.as_tensor(scene.ctor["joints"]).float(), scene.ctor["bones"],
+                                torch.as_tensor(scene.ctor["canonical_pcd"]).float(), torch.tensor(1e-6))
+    out.params = dict(scene.params, weights=full_w[r0:r1].contiguous())
     out.extra = dict(scene.extra, point_range=(r0, r1))
     return out
 

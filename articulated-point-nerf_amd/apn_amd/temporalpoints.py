@@ -175,6 +175,16 @@ def _bone_distances(p, a, b):
     return torch.where(lower, d_lo, torch.where(upper, d_hi, d_in))
 
 
+def weights_from_bones(joints, bones, pcd, eps):
+    """Initial raw LBS weights (temporalpoints.py:235-254 with add_noise=True, noise_var=0,
+    add_zero_weight=True): [N, J] = [0 | 1 / (0.5 e^d + eps)] over the bone distances d."""
+    a = torch.stack([joints[b[0]] for b in bones])
+    b = torch.stack([joints[b[1]] for b in bones])
+    d = _bone_distances(pcd, a, b)
+    w = (1 / (0.5 * torch.e ** d + eps)).T.contiguous()
+    return torch.cat([torch.zeros((len(w), 1)), w], dim=-1)
+
+
 class TemporalPoints(torch.nn.Module):
     def __init__(self, canonical_pcd, canonical_alpha, canonical_feat, canonical_rgbs, skeleton_pcd, joints, bones,
                  xyz_min, xyz_max, tineuvox, neighbours=8, timebase_pe=8, eps=1e-6, stepsize=None, voxel_size=None,
@@ -277,12 +287,7 @@ class TemporalPoints(torch.nn.Module):
 
     # ------------------------------------------------------------------ construction helpers
     def _weights_from_bones(self, joints, bones, pcd, soft_weights=True):
-        """temporalpoints.py:235-254 with add_noise=True, noise_var=0, add_zero_weight=True."""
-        a = torch.stack([joints[b[0]] for b in bones])
-        b = torch.stack([joints[b[1]] for b in bones])
-        d = _bone_distances(pcd, a, b)
-        w = (1 / (0.5 * torch.e ** d + self.eps)).T.contiguous()
-        return torch.cat([torch.zeros((len(w), 1)), w], dim=-1)
+        return weights_from_bones(joints, bones, pcd, self.eps)
 
     def get_kwargs(self):
         """temporalpoints.py:176-200."""
