@@ -65,6 +65,12 @@ SIGNATURES = {
     "apn_arap_loss_backward": (C.c_int, [P, I64, P, I32, P, F32, P, P, P, P, P]),
     "apn_weight_sparsity_loss": (C.c_int, [P, I64, F32, P, P, P]),
     "apn_weight_sparsity_loss_backward": (C.c_int, [P, I64, F32, P, P, P]),
+    "apn_tnv_grid_bytes": (I64, [I32, I32, I32, I32]),
+    "apn_tnv_grid_pack": (C.c_int, [P, I32, I32, I32, I32, P, P]),
+    "apn_tnv_mult_dist_interp": (C.c_int, [P, I64, P, I32, I32, I32, P, P, P, P]),
+    "apn_tnv_weight_layout": (C.c_int, [I32, P]),
+    "apn_tnv_field": (C.c_int, [P, P, P, I64, P, P, I32, I32, I32, P, P, P, I32, P, P, P, I32, F32, F32, P, P, P,
+                                P, P]),
     "apn_scan_workspace_bytes": (SZ, [I64]),
     "apn_scan_exclusive_i32": (C.c_int, [P, P, I64, P, P]),
     "apn_version": (C.c_char_p, []),

@@ -40,7 +40,8 @@ constexpr int HB = 800;            // bytes per head-input row: hi 160 | lo 160 
 constexpr int HLO = 320;           // lo offset inside a head-input row
 
 constexpr int SW_B1 = 0, SW_B2 = 128, SW_B3 = 256, SW_B4 = 384, SW_WD = 512, SW_BD = 640, SW_BH = 644,
-              SW_WV2 = 708, SW_BV2 = 900, SW_SC = 904, SW_DS = 912, SW_MODE = 920, SW_TOTAL = 924;
+              SW_WV2 = 708, SW_BV2 = 900, SW_SC = 904, SW_DS = 912, SW_MODE = 920, SW_HSC = 921,
+              SW_TOTAL = 924;
 
 // sin and cos of x for the positional encoding, |x| < ~1e6 (arguments are rel_c * 2^f, f <= 9):
 // quadrant reduction k = rint(2x/pi), r = x - k pi/2 with pi/2 in two floats (fma, so k C1 is
@@ -411,12 +412,13 @@ __global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
     sW[SW_B4 + i] = wbuf[OFF_B4 + i] * scp[3];
     sW[SW_WD + i] = wbuf[OFF_WD + i];
   }
-  if (tid < 5) {
+  if (tid < 6) {   // 0-3: W1E, W2, W3, W4; 4: WH h-columns (2^a); 5: WH view columns (2^b)
     sW[SW_SC + tid] = scp[tid];
     sW[SW_DS + tid] = 1.f / scp[tid];
   }
-  if (tid == 5) sW[SW_MODE] = scp[5];
-  if (tid < 64) sW[SW_BH + tid] = wbuf[OFF_BH + tid] * scp[4];
+  if (tid == 6) sW[SW_MODE] = scp[6];
+  if (tid == 7) sW[SW_HSC] = scp[5] / scp[4];   // h' = h 2^(b-a): WH_h' h' = 2^b WH_h h
+  if (tid < 64) sW[SW_BH + tid] = wbuf[OFF_BH + tid] * scp[5];
   if (tid < 192) sW[SW_WV2 + tid] = wbuf[OFF_WV2 + tid];
   if (tid < 3) sW[SW_BV2 + tid] = wbuf[OFF_BV2 + tid];
   if (tid == 0) sW[SW_BD] = wbuf[OFF_BD];
@@ -555,12 +557,14 @@ __global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
 #pragma unroll
         for (int r = 0; r < 4; ++r) h[r] = h[r] + w * v[r];
       }
-      // range guard (see the header comment): false for NaN too
-      if (!(fmaxf(fmaxf(fabsf(h[0]), fabsf(h[1])), fmaxf(fabsf(h[2]), fabsf(h[3]))) <= H3_RANGE))
-        __builtin_amdgcn_raw_buffer_store_b32(1, rs, 0, H_TOTAL * 2, 0);   // the range flag (OFF_FLAG)
       // densitynet Linear(128 -> 1) (tineuvox.py:158) over this thread's 4 features, then the half-wave
       const f32x4 wd = *(const f32x4*)(sW + SW_WD + 4 * oq);
       float d = ((h[0] * wd[0] + h[1] * wd[1]) + h[2] * wd[2]) + h[3] * wd[3];
+      // the head's h input in the head's column scale (scaled mode): h' = h 2^(b-a), exact
+      if (mode_scaled(sW)) h = h * sW[SW_HSC];
+      // range guard (see the header comment) on the last values split: false for NaN too
+      if (!(fmaxf(fmaxf(fabsf(h[0]), fabsf(h[1])), fmaxf(fabsf(h[2]), fabsf(h[3]))) <= H3_RANGE))
+        __builtin_amdgcn_raw_buffer_store_b32(1, rs, 0, H_TOTAL * 2, 0);   // the range flag (OFF_FLAG)
       d += __shfl_xor(d, 16, 64);
       d += __shfl_xor(d, 8, 64);
       d += __shfl_xor(d, 4, 64);
@@ -642,7 +646,7 @@ __global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
       float pc[3] = {0.f, 0.f, 0.f};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float v = fmaxf(mode_scaled(sW) ? ah[r] * sW[SW_DS + 4] : ah[r], 0.f);
+        const float v = fmaxf(mode_scaled(sW) ? ah[r] * sW[SW_DS + 5] : ah[r], 0.f);
 #pragma unroll
         for (int c = 0; c < 3; ++c) pc[c] += v * sW[SW_WV2 + 64 * c + o0 + r];
       }
@@ -676,37 +680,48 @@ __global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
     out[(size_t)prev_s0 * 3 + tid] = *(const float4*)(sOut + 4 * tid);
 }
 
-// Per-matrix scales (apn_mlp_layout.h OFF_SCALE) from max|w| of W1E, W2, W3, W4, WH: one
+// Per-group scales (apn_mlp_layout.h OFF_SCALE) from max|w| of W1E, W2, W3, W4 and the two
+// column groups of the folded head WH (h columns 0..127, view columns 128..159 -- their
+// magnitudes are unrelated: feature_linears is folded into the first group only): one
 // workgroup, one pass over the fp32 region (67 584 weights).
 __global__ __launch_bounds__(256) void k_weight_scales(float* __restrict__ wbuf) {
-  __shared__ float red[5][256];
+  constexpr int NG = 6;
+  __shared__ float red[NG][256];
   const int tid = threadIdx.x;
-  const int offs[5] = {OFF_W1E, OFF_W2, OFF_W3, OFF_W4, OFF_WH};
-  const int lens[5] = {128 * KE, 128 * 128, 128 * 128, 128 * 128, 64 * KV};
 #pragma unroll
-  for (int m = 0; m < 5; ++m) {
-    float mx = 0.f;
-    for (int i = tid; i < lens[m]; i += 256) mx = fmaxf(mx, fabsf(wbuf[offs[m] + i]));
-    red[m][tid] = mx;
+  for (int m = 0; m < NG; ++m) red[m][tid] = 0.f;
+  for (int i = tid; i < 128 * KE; i += 256) red[0][tid] = fmaxf(red[0][tid], fabsf(wbuf[OFF_W1E + i]));
+  for (int i = tid; i < 128 * 128; i += 256) {
+    red[1][tid] = fmaxf(red[1][tid], fabsf(wbuf[OFF_W2 + i]));
+    red[2][tid] = fmaxf(red[2][tid], fabsf(wbuf[OFF_W3 + i]));
+    red[3][tid] = fmaxf(red[3][tid], fabsf(wbuf[OFF_W4 + i]));
+  }
+  for (int i = tid; i < 64 * KV; i += 256) {
+    const int g = (i % KV) < 128 ? 4 : 5;
+    red[g][tid] = fmaxf(red[g][tid], fabsf(wbuf[OFF_WH + i]));
   }
   __syncthreads();
   for (int w = 128; w > 0; w >>= 1) {
     if (tid < w)
 #pragma unroll
-      for (int m = 0; m < 5; ++m) red[m][tid] = fmaxf(red[m][tid], red[m][tid + w]);
+      for (int m = 0; m < NG; ++m) red[m][tid] = fmaxf(red[m][tid], red[m][tid + w]);
     __syncthreads();
   }
   if (tid == 0) {
     bool scaled = false;
-    float mx[5];
+    float mx[NG];
 #pragma unroll
-    for (int m = 0; m < 5; ++m) {
+    for (int m = 0; m < NG; ++m) {
       mx[m] = red[m][0];
-      // all-zero (or non-finite: left to the range guard) matrices keep scale 1
+      // all-zero (or non-finite: left to the range guard) groups keep scale 1
       if (mx[m] > 0.f && mx[m] <= 3.0e38f && (mx[m] < SCALE_LO || mx[m] > SCALE_HI)) scaled = true;
     }
 #pragma unroll
-    for (int m = 0; m < 5; ++m) {
+    // the folded head is scaled as one matrix (both column groups share the accumulator): its
+    // max over both groups; the groups only decide whether scaling is needed at all
+    mx[4] = mx[5] = fmaxf(mx[4], mx[5]);
+#pragma unroll
+    for (int m = 0; m < NG; ++m) {
       float sc = 1.f;
       if (scaled && mx[m] > 0.f && mx[m] <= 3.0e38f) {
         int e;
@@ -715,8 +730,7 @@ __global__ __launch_bounds__(256) void k_weight_scales(float* __restrict__ wbuf)
       }
       wbuf[OFF_SCALE + m] = sc;
     }
-    wbuf[OFF_SCALE + 5] = scaled ? 1.f : 0.f;
-    wbuf[OFF_SCALE + 6] = 0.f;
+    wbuf[OFF_SCALE + 6] = scaled ? 1.f : 0.f;
     wbuf[OFF_SCALE + 7] = 0.f;
   }
 }
@@ -738,7 +752,7 @@ __global__ void k_split_weights(float* __restrict__ wbuf) {
   const int o = 16 * ot + (lane & 15), k0 = 32 * q + 8 * (lane >> 4);
   const int hbase = mat == 0 ? H_W1E : (mat == 1 ? H_W2 : (mat == 2 ? H_W3 : (mat == 3 ? H_W4 : H_WH)));
   _Float16* dst = (_Float16*)(wbuf + OFF_H16) + hbase + (size_t)((ot * nq + q) * 2) * FRAG_HALVES + lane * 8;
-  const float sc = wbuf[OFF_SCALE + mat];
+  const float sc_mat = wbuf[OFF_SCALE + mat], sc_view = wbuf[OFF_SCALE + 5];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int k = k0 + j;
@@ -752,7 +766,7 @@ __global__ void k_split_weights(float* __restrict__ wbuf) {
       const int off = mat == 1 ? OFF_W2 : (mat == 2 ? OFF_W3 : OFF_W4);
       w = wbuf[off + o * 128 + k];
     }
-    w *= sc;   // exact (power of two)
+    w *= (mat == 4 && k >= 128) ? sc_view : sc_mat;   // exact (powers of two)
     const _Float16 hi = (_Float16)w;
     dst[j] = hi;
     dst[FRAG_HALVES + j] = (_Float16)(w - (float)hi);

@@ -48,13 +48,16 @@ constexpr int H_TOTAL = H_WH + 4 * 5 * 2 * FRAG_HALVES;
 // then re-runs the launch (apn_point_mlp). Sticky until the weights are re-split
 // (apn_mlp_split_weights clears it), so later launches with the same weights go straight to FP32.
 constexpr int OFF_FLAG = OFF_H16 + H_TOTAL / 2;
-// Per-matrix power-of-two scales of the fp16 hi/lo region (written by apn_mlp_split_weights):
-// [W1E, W2, W3, W4, WH, mode, 0, 0]. fp16 has 5 exponent bits: the lo halves of weights below
-// ~2^-3 are subnormal and lose relative precision. If every matrix's max|w| lies in
-// [2^-5, 2^12] (all reference-initialised or trained networks seen), mode = 0 and every scale is
-// 1 (the kernel then runs exactly the unscaled arithmetic). Otherwise mode = 1 and each matrix is
-// stored as w * 2^s with max|w 2^s| in [2^12, 2^13) -- exact in fp32 -- and the kernel multiplies
-// the layer's accumulators by 2^-s (biases / projections pre-scaled by 2^s).
+// Power-of-two weight scales of the fp16 hi/lo region (written by apn_mlp_split_weights):
+// [W1E, W2, W3, W4, WH h-columns, WH view-columns, mode, 0]. fp16 has 5 exponent bits: the lo
+// halves of weights below ~2^-3 are subnormal and lose relative precision. If every group's
+// max|w| lies in [2^-5, 2^12] (all reference-initialised or trained networks seen), mode = 0 and
+// every scale is 1 (the kernel then runs exactly the unscaled arithmetic). Otherwise mode = 1
+// and each group is stored as w * 2^s with max|w 2^s| in [2^12, 2^13) -- exact in fp32 -- and
+// the kernel multiplies the layer's accumulators by 2^-s (biases / projections pre-scaled by
+// 2^s). The head's two column groups are tested separately (their magnitudes are unrelated:
+// rgbnet.feature_linears folds into the h columns only) but scaled together, by the head's max
+// (slots 4 and 5 are equal; the kernel's h-input factor 2^(s5 - s4) is then 1).
 constexpr int OFF_SCALE = OFF_FLAG + 4;
 constexpr int W_TOTAL = OFF_SCALE + 8;
 constexpr float SCALE_LO = 0.03125f, SCALE_HI = 4096.f;   // unscaled range of max|w|

@@ -113,14 +113,19 @@ def cpu_baseline(model, scene, rows, threads):
                       f"(oracle: torch-CPU MLP, scipy cKDTree kNN), {dt:.2f} s/band"}, ref, sel, (orc, sub, t)
 
 
-def same_cloud_error(gpu_out, orc, sub, t, sel):
+def same_cloud_error(gpu_out, gpu_rk, perm, orc, sub, t, sel):
     """The oracle re-rendering the band against the GPU's own warped cloud (identical sample
     positions and neighbour lists): max |rgb - oracle| over all band rays, and over the rays whose
     oracle compositing is not within 1e-6 of a discontinuity (fast_color_thres on alpha/weight,
     T = 1e-3; oracle/flips.py) -- the arithmetic error of the GPU path at the bench size."""
     from oracle.flips import near_discontinuity, ray_errors, PATH_OF_KEY
+    # the GPU's own rays (device and host torch may round a ray direction differently in the
+    # last ulp, which moves that ray's samples)
+    sub = dict(sub)
+    for k in ("rays_o", "rays_d", "viewdirs"):
+        sub[k] = gpu_rk[k][sel].detach().cpu().contiguous()
     ref = orc.forward(t, render_depth=True, render_kwargs=sub, render_weights=True, knn_tree=True,
-                      t_hat_override=gpu_out["t_hat_pcd"].detach().cpu())
+                      t_hat_override=gpu_out["t_hat_pcd"].detach().cpu(), perm=perm)
     res = {"rays": int(sel.numel())}
     for key in ("rgb_marched", "rgb_marched_direct"):
         a = gpu_out[key].detach().float().cpu()[sel].numpy()
@@ -384,7 +389,7 @@ def main():
         try:
             cpu, ref, sel, (orc, sub, t_cpu) = cpu_baseline(model, scene, args.cpu_rows, torch.get_num_threads())
             psnr = psnr_vs_oracle(out, ref, sel)
-            same = same_cloud_error(out, orc, sub, t_cpu, sel)
+            same = same_cloud_error(out, rk, model.last_palette_perm, orc, sub, t_cpu, sel)
         except Exception as e:  # never lose the GPU line over the baseline leg
             log(f"cpu baseline failed: {e!r}")
     line = {

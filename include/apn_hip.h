@@ -301,6 +301,46 @@ int apn_composite(const float* smp12, const float* s_pos4, const int32_t* s_ray,
  * workgroups since the last call; resets them. */
 int apn_debug_mlp_phase_cycles(uint64_t* out6);
 
+/* ---------------------------------------------------------------------------------------------
+ * TiNeuVox stage 1: the voxel model the point cloud is exported from
+ * (lib/tineuvox.py:91-625). voxel_dim must be 12, net_width 128, posbase_pe 10, viewbase_pe 4,
+ * gridbase_pe 2 (the reference configuration); the deformation depth is a parameter.
+ * ------------------------------------------------------------------------------------------- */
+
+/* Bytes of the repacked 3-scale feature grid for a [1, C, X, Y, Z] feature (C must be 12), or -1. */
+int64_t apn_tnv_grid_bytes(int32_t C, int32_t X, int32_t Y, int32_t Z);
+
+/* feature [C][X][Y][Z] fp32 (TiNeuVox.feature) -> channels-last grids of the zero-padded feature
+ * at scales 1, 1/2, 1/4 (tineuvox.py:402-411: F.pad to (size-1) % 4 == 0, views [::2], [::4]). */
+int apn_tnv_grid_pack(const float* feature, int32_t C, int32_t X, int32_t Y, int32_t Z, float* grid,
+                      void* stream);
+
+/* TiNeuVox.mult_dist_interp (tineuvox.py:402-419, grid_sampler 379-394): trilinear
+ * grid_sample (align_corners=True, zero padding) of the three scales at pts [n,3] ->
+ * out [n,36] = [scale 1 | 1/2 | 1/4] x 12 channels. xyz_min/xyz_max: device [3]. */
+int apn_tnv_mult_dist_interp(const float* pts, int64_t n_pts, const float* grid, int32_t X, int32_t Y,
+                             int32_t Z, const float* xyz_min, const float* xyz_max, float* out, void* stream);
+
+/* Packed TiNeuVox network layout for a deformation depth: writes 14 int32 (float offsets
+ * D0E, DH, DOUT, FW, WD, BD, WH, BH, WV2, BV2, TOTAL, then KE, KF, KV) and returns the count. */
+int apn_tnv_weight_layout(int32_t defor_depth, int32_t* offsets);
+
+/* The TiNeuVox field at query points (tineuvox.py:479-532; get_grid_as_point_cloud 286-342):
+ * posenc -> Deformation (if deform; tineuvox.py:28-62) -> 3-scale trilinear grid sample ->
+ * posenc -> featurenet -> densitynet + raw2alpha, and rgbnet + sigmoid.
+ * pos4 [S,4] {x,y,z,*}, s_ray [S] (index into time_idx / viewdirs), time_idx [R] (row of tproj
+ * per ray; NULL = row 0), tproj [U,256] per-time projections (time columns of deformation
+ * layer 0 and of featurenet applied to timenet(poc_fre(t)), plus their biases), viewdirs [R,3] or
+ * vemb_const [27]. out12 [S,12] = {r,g,b,alpha, 0...} (the apn_composite layout); optional
+ * delta_out [S,3] (deformed positions), h_out [S,128], vox_out [S,36]. The sample count is read
+ * on the device (n_samples_dev <= max_samples). */
+int apn_tnv_field(const float* pos4, const int32_t* s_ray, const int32_t* time_idx, int64_t max_samples,
+                  const int32_t* n_samples_dev, const float* grid, int32_t X, int32_t Y, int32_t Z,
+                  const float* xyz_min, const float* xyz_max, const float* wbuf, int32_t defor_depth,
+                  const float* tproj, const float* viewdirs, const float* vemb_const, int32_t deform,
+                  float act_shift, float interval, float* out12, float* delta_out, float* h_out,
+                  float* vox_out, void* stream);
+
 /* Utilities */
 size_t apn_scan_workspace_bytes(int64_t n);
 int apn_scan_exclusive_i32(const int32_t* in, int32_t* out, int64_t n, void* workspace, void* stream);

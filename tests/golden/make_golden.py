@@ -15,7 +15,11 @@ What it does:
 * runs ``TemporalPoints.forward`` (the ``run.py --render_pcd`` call, run.py:149-151),
   ``repose`` (run.py:287 / temporalpoints.py:370), ``get_weights`` with a non-trivial
   merge, and ``PointWarper.forward`` on the t-path and the rot_params path;
-* stores inputs + outputs as compressed .npz next to this script.
+* stores inputs + outputs as compressed .npz next to this script;
+* T1: the stage-1 TiNeuVox model itself (lib/tineuvox.py:91-625) -- forward,
+  mult_dist_interp, get_grid_as_point_cloud -- and get_rays_of_a_view (a-22).
+
+Usage: ``python tests/golden/make_golden.py [G1 G2 G3 T1]`` (default: all).
 
 The reference never travels: only the .npz data files are committed.
 """
@@ -224,12 +228,100 @@ def rtn_poc(x, f):
     return poc_fre(x, f)
 
 
+# ------------------------------------------------------------------ TiNeuVox stage 1 + get_rays
+T1 = dict(xyz_min=[-0.8, -0.9, -1.0], xyz_max=[0.8, 0.9, 1.0], num_voxels=16000, voxel_dim=12, defor_depth=5,
+          net_width=128, alpha_init=1e-3, fast_color_thres=1e-4, no_view_dir=False, posbase_pe=10, viewbase_pe=4,
+          timebase_pe=8, gridbase_pe=2, H=32, W=32, near=1.0, far=6.0, stepsize=0.5, bg=1.0)
+
+
+def gen_tineuvox_case(name="T1"):
+    """The reference's TiNeuVox (stage 1, lib/tineuvox.py:91-625) on a small random model: forward
+    (tineuvox.py:458-564) with per-ray times, mult_dist_interp on random points inside and outside
+    the grid (379-419), get_grid_as_point_cloud on the full grid and on a point subset (253-363,
+    the run.py:1152-1194 export query); plus get_rays_of_a_view (675-738) for both camera
+    conventions, both pixel modes and the flips."""
+    from lib import tineuvox as rtn
+    c = T1
+    torch.manual_seed(7)
+    model = rtn.TiNeuVox(xyz_min=c["xyz_min"], xyz_max=c["xyz_max"], num_voxels=c["num_voxels"],
+                         num_voxels_base=c["num_voxels"], voxel_dim=c["voxel_dim"], defor_depth=c["defor_depth"],
+                         net_width=c["net_width"], alpha_init=c["alpha_init"], fast_color_thres=c["fast_color_thres"],
+                         no_view_dir=c["no_view_dir"], posbase_pe=c["posbase_pe"], viewbase_pe=c["viewbase_pe"],
+                         timebase_pe=c["timebase_pe"], gridbase_pe=c["gridbase_pe"])
+    g = torch.Generator().manual_seed(11)
+    with torch.no_grad():
+        model.feature.copy_(torch.randn(model.feature.shape, generator=g) * 0.5)
+        model.densitynet.weight.mul_(40.0)     # densities over a wide range: both fast_color_thres
+        model.densitynet.bias.fill_(1.0)       # masks and the T < 1e-3 early exit are exercised
+    c2w = S.pose_spherical(30.0, -30.0, 3.5)
+    H, W = c["H"], c["W"]
+    focal = 0.5 * W / np.tan(0.5 * 0.6911112)
+    K = S.intrinsics(H, W, focal)
+    data = {}
+    # get_rays_of_a_view (tineuvox.py:733-738), every option combination used by the loaders
+    for inv_y in (False, True):
+        for mode in ("center", "lefttop"):
+            for fx, fy in ((False, False), (True, False), (False, True)):
+                ro, rd, vd = rtn.get_rays_of_a_view(H, W, K, c2w, False, inverse_y=inv_y, flip_x=fx, flip_y=fy,
+                                                    mode=mode)
+                tag = f"rays_{int(inv_y)}{mode[0]}{int(fx)}{int(fy)}"
+                data[tag + "_o"], data[tag + "_d"], data[tag + "_v"] = ro, rd, vd
+    ro, rd, vd = rtn.get_rays_of_a_view(H, W, K, c2w, False, inverse_y=False, mode="center")
+    ro, rd, vd = ro.reshape(-1, 3), rd.reshape(-1, 3), vd.reshape(-1, 3)
+    N = len(ro)
+    times = torch.where(torch.arange(N) < N // 2, torch.tensor(0.2), torch.tensor(0.7))[:, None]
+    rk = dict(near=c["near"], far=c["far"], stepsize=c["stepsize"], bg=c["bg"])
+    with torch.no_grad():
+        out = model(ro, rd, vd, times, **rk)
+        pts = torch.rand(3000, 3, generator=g) * 2.2 - 1.1      # inside and outside the grid
+        vox = model.mult_dist_interp(pts)
+        gp = model.get_grid_as_point_cloud(stepsize=c["stepsize"], time_sel=torch.tensor([[0.0]]),
+                                           viewdir=vd.mean(0, keepdim=True), sampling_freq=1,
+                                           alpha_xyz_only=False)
+        sub = (torch.rand(700, 3, generator=g) * 2 - 1) * torch.tensor(c["xyz_max"])
+        gs = model.get_grid_as_point_cloud(stepsize=c["stepsize"], time_sel=torch.tensor([[0.4]]),
+                                           viewdir=vd.mean(0, keepdim=True), alpha_xyz_only=False, grid_xyz=sub)
+    state = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    for k, v in state.items():
+        data["in_" + k] = v
+    data.update({"in_c2w": c2w, "in_K": K, "in_rays_o": ro, "in_rays_d": rd, "in_viewdirs": vd, "in_times": times,
+                 "in_pts": pts, "in_sub_xyz": sub})
+    for k, v in c.items():
+        data["cfg_" + k] = torch.tensor(v)
+    data["cfg_act_shift"] = torch.tensor(float(model.act_shift), dtype=torch.float64)
+    data["cfg_voxel_size"] = model.voxel_size.detach().clone()
+    data["cfg_voxel_size_ratio"] = torch.as_tensor(model.voxel_size_ratio).detach().clone()
+    data["cfg_world_size"] = model.world_size.detach().clone()
+    for k in ("alphainv_last", "weights", "rgb_marched", "raw_alpha", "raw_rgb", "ray_id", "s", "ray_pts_delta",
+              "depth"):
+        data["out_" + k] = out[k]
+    data["out_n_max"] = torch.tensor(out["n_max"])
+    data["out_vox"] = vox
+    names = ["points", "alphas", "rgbs", "h_feature", "vox_feature", "binary_volume", "grid_xyz", "alpha_volume"]
+    for nm, v in zip(names, gp):
+        if nm in ("alphas", "rgbs", "grid_xyz", "alpha_volume"):
+            data["grid_" + nm] = v
+    for nm, v in zip(names, gs):
+        if nm in ("alphas", "rgbs", "h_feature", "vox_feature"):
+            data["sub_" + nm] = v
+    arrs = {k: (v.detach().cpu().numpy() if torch.is_tensor(v) else np.asarray(v)) for k, v in data.items()}
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), f"golden_{name}.npz")
+    np.savez_compressed(path, **arrs)
+    print(f"{name}: wrote {path} ({os.path.getsize(path) / 1e6:.2f} MB); world_size {model.world_size.tolist()}, "
+          f"in-bbox samples {len(out['ray_pts_delta'])}, kept {len(out['ray_id'])}, "
+          f"hit rays {int((out['alphainv_last'] < 1).sum())}")
+
+
 def main():
     install_stubs()
     sys.path.insert(0, REF)
     torch.set_num_threads(min(8, os.cpu_count() or 1))
-    for name in ("G1", "G2", "G3"):
-        gen_case(name)
+    which = sys.argv[1:] or ["G1", "G2", "G3", "T1"]
+    for name in which:
+        if name.startswith("T"):
+            gen_tineuvox_case(name)
+        else:
+            gen_case(name)
 
 
 if __name__ == "__main__":

@@ -137,3 +137,29 @@ def test_bench_psnr_and_flop_accounting():
     r = bench.psnr_vs_oracle(a, b, sel)
     assert r["rgb_marched"] == 200.0 and r["rgb_marched_frac_rays_within_1e-4"] == 1.0
     assert abs(r["rgb_marched_direct"] - 20.0) < 1e-3 and r["rgb_marched_direct_frac_rays_within_1e-4"] == 0.0
+
+
+def test_get_rays_of_a_view_pinned_to_reference():
+    """tineuvox.get_rays_of_a_view (a-22; tineuvox.py:675-738) against the reference's own output
+    for both camera conventions (inverse_y), both pixel modes and the flips (golden_T1.npz,
+    written by tests/golden/make_golden.py from lib/tineuvox.py): bit-exact."""
+    import numpy as np
+    from apn_amd.tineuvox import get_rays_of_a_view
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "golden_T1.npz"))
+    c2w, K = torch.from_numpy(z["in_c2w"]), torch.from_numpy(z["in_K"])
+    H, W = int(z["cfg_H"]), int(z["cfg_W"])
+    n = 0
+    for inv_y in (False, True):
+        for mode in ("center", "lefttop"):
+            for fx, fy in ((False, False), (True, False), (False, True)):
+                tag = f"rays_{int(inv_y)}{mode[0]}{int(fx)}{int(fy)}"
+                ro, rd, vd = get_rays_of_a_view(H, W, K, c2w, False, inverse_y=inv_y, flip_x=fx, flip_y=fy, mode=mode)
+                for got, key in ((ro, "_o"), (rd, "_d"), (vd, "_v")):
+                    assert np.array_equal(got.numpy(), z[tag + key]), tag + key
+                n += 1
+    assert n == 12
+    # the synthetic scenes' generator (apn_amd.synthetic.get_rays) is the same function flattened
+    from apn_amd import synthetic as S
+    ro, rd, vd = S.get_rays(H, W, K, c2w)
+    assert np.array_equal(rd.numpy(), z["rays_0c00_d"].reshape(-1, 3))
+    assert np.array_equal(vd.numpy(), z["rays_0c00_v"].reshape(-1, 3))

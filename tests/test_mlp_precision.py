@@ -128,6 +128,9 @@ def check_stage(o, tr, tag, f64=None):
     dad = float((o[:, 7] - tr["alpha_direct"]).abs().max())
     drd = float((o[:, 4:7] - tr["rgbs_direct"]).abs().max())
     dc = float((o[:, 8:11] - torch.from_numpy(tr["col"])).abs().max())
+    worst = int((o[:, 0:3] - tr["rgbs"]).abs().max(-1)[0].argmax())
+    tag += (f" [worst rgb sample {worst}: gpu {o[worst, 0:3].tolist()} oracle {tr['rgbs'][worst].tolist()} "
+            f"ray {int(tr['ray_id'][worst])}]")
     msg = (f"{tag}: vs fp32 oracle max|d alpha| {da:.2e} max|d rgb| {dr:.2e} direct {dad:.1e}/{drd:.1e} "
            f"col {dc:.1e} (alpha range {float(tr['alpha'].min()):.3g}..{float(tr['alpha'].max()):.3g})")
     assert torch.isfinite(o).all()

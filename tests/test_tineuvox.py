@@ -1,0 +1,125 @@
+"""TiNeuVox stage 1 on the GPU against the reference's own outputs
+(tests/golden/golden_T1.npz, written by tests/golden/make_golden.py from lib/tineuvox.py):
+
+* mult_dist_interp (tineuvox.py:402-419): the 3-scale trilinear feature lookup at random points
+  inside and outside the grid (zero padding);
+* forward (tineuvox.py:458-564) with per-ray times: deformed sample positions, per-sample alpha /
+  rgb after both fast_color_thres masks, and the composited rgb / depth / transmittance;
+* get_grid_as_point_cloud (tineuvox.py:253-363), the canonical export query of run.py:1152-1194,
+  on the whole grid and on a point subset (alpha, rgb, featurenet features, grid features).
+
+Bars: grid features 1e-6 (same IEEE trilinear arithmetic; the reference's CPU kernel may
+contract a multiply-add), everything downstream of the MLPs 1e-5 (fp32 reassociation)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+NON_STATE = ("c2w", "K", "rays_o", "rays_d", "viewdirs", "times", "pts", "sub_xyz")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch.device("cuda")
+
+
+@pytest.fixture(scope="module")
+def golden():
+    import os
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "golden_T1.npz"))
+    return {k: z[k] for k in z.files}
+
+
+def model_from_golden(z, dev):
+    from apn_amd.tineuvox import TiNeuVox
+    c = lambda k: z["cfg_" + k].item()
+    m = TiNeuVox(z["cfg_xyz_min"].tolist(), z["cfg_xyz_max"].tolist(), num_voxels=int(c("num_voxels")),
+                 num_voxels_base=int(c("num_voxels")), voxel_dim=int(c("voxel_dim")),
+                 defor_depth=int(c("defor_depth")), net_width=int(c("net_width")), alpha_init=c("alpha_init"),
+                 fast_color_thres=c("fast_color_thres"), no_view_dir=bool(c("no_view_dir")),
+                 posbase_pe=int(c("posbase_pe")), viewbase_pe=int(c("viewbase_pe")),
+                 timebase_pe=int(c("timebase_pe")), gridbase_pe=int(c("gridbase_pe")))
+    st = {k[3:]: torch.from_numpy(v) for k, v in z.items() if k.startswith("in_") and k[3:] not in NON_STATE}
+    m.load_state_dict(st, strict=True)
+    assert m.world_size.tolist() == z["cfg_world_size"].tolist()
+    return m.to(dev)
+
+
+def t(z, k, dev):
+    return torch.from_numpy(z[k]).to(dev)
+
+
+def test_mult_dist_interp_vs_reference(dev, golden):
+    m = model_from_golden(golden, dev)
+    with torch.no_grad():
+        vox = m.mult_dist_interp(t(golden, "in_pts", dev)).cpu().numpy()
+    ref = golden["out_vox"]
+    assert vox.shape == ref.shape
+    # points outside the grid hit the zero padding exactly
+    outside = np.any((golden["in_pts"] < golden["cfg_xyz_min"] - 0.2) | (golden["in_pts"] > golden["cfg_xyz_max"] + 0.2), 1)
+    assert np.all(ref[outside] == 0) and np.all(vox[outside] == 0)
+    err = np.abs(vox - ref).max()
+    print(f"mult_dist_interp max|d| {err:.2e} over {len(vox)} points ({int(outside.sum())} far outside)")
+    assert err < 1e-6
+
+
+def test_forward_vs_reference(dev, golden):
+    z = golden
+    m = model_from_golden(z, dev)
+    rk = dict(near=z["cfg_near"].item(), far=z["cfg_far"].item(), stepsize=z["cfg_stepsize"].item(),
+              bg=z["cfg_bg"].item())
+    with torch.no_grad():
+        out = m(t(z, "in_rays_o", dev), t(z, "in_rays_d", dev), t(z, "in_viewdirs", dev), t(z, "in_times", dev), **rk)
+    torch.cuda.synchronize()
+    d = float((out["ray_pts_delta"].cpu() - torch.from_numpy(z["out_ray_pts_delta"])).abs().max())
+    print(f"deformed positions max|d| {d:.2e} over {len(z['out_ray_pts_delta'])} samples")
+    assert out["ray_pts_delta"].shape == z["out_ray_pts_delta"].shape and d < 1e-5
+    # the same samples survive both fast_color_thres masks
+    assert np.array_equal(out["ray_id"].cpu().numpy(), z["out_ray_id"])
+    assert out["n_max"] == int(z["out_n_max"])
+    assert np.array_equal(out["s"].cpu().numpy(), z["out_s"])
+    for k, tol in (("raw_alpha", 1e-5), ("raw_rgb", 1e-5), ("weights", 1e-5), ("alphainv_last", 1e-5),
+                   ("rgb_marched", 1e-5)):
+        e = float(np.abs(out[k].cpu().numpy() - z["out_" + k]).max())
+        print(f"{k}: max|d| {e:.2e}")
+        assert e < tol, k
+    dep = out["depth"].cpu().numpy()
+    assert np.abs(dep - z["out_depth"]).max() < 1e-5 * (np.abs(z["out_depth"]).max() + 1)
+
+
+def test_grid_as_point_cloud_vs_reference(dev, golden):
+    z = golden
+    m = model_from_golden(z, dev)
+    vd = torch.from_numpy(z["in_viewdirs"]).mean(0, keepdim=True)
+    with torch.no_grad():
+        pts, alphas, rgbs, h, vox, _, grid_xyz, alpha_vol = m.get_grid_as_point_cloud(
+            stepsize=z["cfg_stepsize"].item(), time_sel=torch.tensor([[0.0]]), viewdir=vd, sampling_freq=1,
+            alpha_xyz_only=False)
+    assert np.array_equal(grid_xyz.cpu().numpy(), z["grid_grid_xyz"])
+    ea = float(np.abs(alpha_vol.cpu().numpy() - z["grid_alpha_volume"]).max())
+    er = float(np.abs(rgbs.cpu().numpy() - z["grid_rgbs"]).max())
+    print(f"grid export: alpha max|d| {ea:.2e} rgb {er:.2e} over {alpha_vol.numel()} grid points")
+    assert ea < 1e-5 and er < 1e-5
+    with torch.no_grad():
+        _, a2, r2, h2, v2, *_ = m.get_grid_as_point_cloud(
+            stepsize=z["cfg_stepsize"].item(), time_sel=torch.tensor([[0.4]]), viewdir=vd, alpha_xyz_only=False,
+            grid_xyz=torch.from_numpy(z["in_sub_xyz"]))
+    for k, v, tol in (("alphas", a2, 1e-5), ("rgbs", r2, 1e-5), ("h_feature", h2, 1e-5), ("vox_feature", v2, 1e-5)):
+        e = float(np.abs(v.cpu().numpy() - z["sub_" + k]).max())
+        print(f"subset {k}: max|d| {e:.2e}")
+        assert e < tol, k
+
+
+def test_canonical_query_skips_deformation(dev, golden):
+    """canonical=True (tineuvox.py:292-293) samples the grid at the query points themselves:
+    the grid features equal mult_dist_interp at those points."""
+    z = golden
+    m = model_from_golden(z, dev)
+    sub = torch.from_numpy(z["in_sub_xyz"])
+    with torch.no_grad():
+        _, _, _, _, vox, *_ = m.get_grid_as_point_cloud(stepsize=0.5, canonical=True, alpha_xyz_only=False,
+                                                        grid_xyz=sub)
+        ref = m.mult_dist_interp(sub.to(dev))
+    assert torch.equal(vox, ref)

@@ -26,10 +26,9 @@ orc = O.OracleModel(st, model.canonical_pcd.cpu(), model.bones, stepsize=S.STEPS
                     fast_color_thres=S.FAST_COLOR_THRES, pose_embedding_dim=model.pose_embedding_dim,
                     act_shift=float(model.tineuvox.act_shift), voxel_size_ratio=float(model.tineuvox.voxel_size_ratio),
                     mean_min_distance_value=float(model.mean_min_distance))
-rkc = scene.render_kwargs("cpu")
-sub = dict(rkc)
+sub = dict(rk)
 for k in ("rays_o", "rays_d", "viewdirs"):
-    sub[k] = rkc[k][sel].contiguous()
+    sub[k] = rk[k][sel].cpu().contiguous()
 ref = orc.forward(torch.tensor([scene.cfg.t]), render_depth=True, render_kwargs=sub, render_weights=True,
                   t_hat_override=out["t_hat_pcd"].cpu(), knn_tree=True, perm=model.last_palette_perm)
 a = out[key].cpu()[sel].numpy(); b = ref[key].numpy()
@@ -56,3 +55,21 @@ for r in worst:
     print("  oracle rgb_d  ", tr["rgbs_direct"].numpy()[oi])
     print("  gpu    rgb_d  ", o12[gi, 4:7])
     print("  nbr equal", np.array_equal(np.sort(tr["s_i"][oi], 1), np.sort(s_nbr[gi], 1)) if len(oi) == len(gi) else "n/a")
+
+# exact brute force for the samples whose neighbour lists differ
+t_hat = out["t_hat_pcd"].cpu().numpy()
+s_pos = ws["s_pos"][:ns * 4].reshape(ns, 4).cpu().numpy()
+for r in worst[:2]:
+    g = int(sel[r])
+    oi = np.nonzero(tr["ray_id"] == r)[0]
+    gi = np.nonzero(s_ray == g)[0]
+    for a_, b_ in zip(oi, gi):
+        on, gn = np.sort(tr["s_i"][a_]), np.sort(s_nbr[b_])
+        if not np.array_equal(on, gn):
+            q = s_pos[b_, :3].astype(np.float32)
+            d = ((q[0] - t_hat[:, 0]) * (q[0] - t_hat[:, 0]) + (q[1] - t_hat[:, 1]) * (q[1] - t_hat[:, 1])) \
+                + (q[2] - t_hat[:, 2]) * (q[2] - t_hat[:, 2])
+            order = np.lexsort((np.arange(len(d)), d))[:12]
+            print(f"ray {r} sample: q {q} oracle-pts {tr['pts'][a_]}")
+            print("  oracle nbr", tr["s_i"][a_], "\n  gpu nbr   ", s_nbr[b_])
+            print("  brute top12", order, d[order])
