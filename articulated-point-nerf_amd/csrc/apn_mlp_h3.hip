@@ -716,7 +716,6 @@ __global__ __launch_bounds__(256) void k_weight_scales(float* __restrict__ wbuf)
       // all-zero (or non-finite: left to the range guard) groups keep scale 1
       if (mx[m] > 0.f && mx[m] <= 3.0e38f && (mx[m] < SCALE_LO || mx[m] > SCALE_HI)) scaled = true;
     }
-#pragma unroll
     // the folded head is scaled as one matrix (both column groups share the accumulator): its
     // max over both groups; the groups only decide whether scaling is needed at all
     mx[4] = mx[5] = fmaxf(mx[4], mx[5]);
