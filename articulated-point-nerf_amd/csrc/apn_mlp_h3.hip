@@ -40,7 +40,7 @@ constexpr int HB = 800;            // bytes per head-input row: hi 160 | lo 160 
 constexpr int HLO = 320;           // lo offset inside a head-input row
 
 constexpr int SW_B1 = 0, SW_B2 = 128, SW_B3 = 256, SW_B4 = 384, SW_WD = 512, SW_BD = 640, SW_BH = 644,
-              SW_WV2 = 708, SW_BV2 = 900, SW_SC = 904, SW_DS = 912, SW_MODE = 920, SW_HSC = 921,
+              SW_WV2 = 708, SW_BV2 = 900, SW_SC = 904, SW_DS = 912, SW_HSC = 921,
               SW_TOTAL = 924;
 
 // sin and cos of x for the positional encoding, |x| < ~1e6 (arguments are rel_c * 2^f, f <= 9):
@@ -213,10 +213,6 @@ __device__ __forceinline__ void layer_mfma(const char* __restrict__ X, rsrc_t rs
 // lrelu(acc [+ bias]) -> hi/lo halves of the next layer's input rows (transposed C layout: lane
 // (li, g) of (mt, j) holds features 16(2w+j) + 4g + r of row 16 mt + li). Layers 2-4 start their
 // accumulators from the bias (bias == nullptr here).
-// Wave-uniform scaled-weights mode (apn_mlp_layout.h OFF_SCALE), read from the LDS copy.
-__device__ __forceinline__ bool mode_scaled(const float* sW) {
-  return __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, sW[SW_MODE])) != 0;
-}
 
 // Scaled weights (apn_mlp_layout.h OFF_SCALE): the accumulators hold 2^s (W x + b); `dsc` = 2^-s.
 // Layer 1 adds its (unscaled) bias with one fma(acc, 2^-s, b) -- fma(a, 1, b) == a + b, so the
@@ -364,32 +360,21 @@ __device__ __forceinline__ void ws_gather(int vt, int nb, float4 q, const Gather
 // OCC = workgroups per CU: 2 = activations ping-pong between two LDS buffers (one barrier per
 // layer); 3 = one activation buffer + a separate head-input buffer (45 KB of LDS, an extra barrier
 // per layer, 12 waves per CU to hide the phases' latencies).
-template <bool TIMED, int OCC>
-__global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
+//
+// SCALED: the weight-scale mode of wbuf (apn_mlp_layout.h OFF_SCALE), a block-uniform choice
+// between two instantiations of the tile loop (the unscaled one carries no scale arithmetic).
+template <bool TIMED, int OCC, bool SCALED>
+__device__ __forceinline__ void mlp_tiles(
     const float4* __restrict__ s_pos, const int* __restrict__ s_ray, const int* __restrict__ s_nbr,
     const int* __restrict__ n_samples_dev, const float4* __restrict__ recA, const float4* __restrict__ recB,
     const float4* __restrict__ pproj, const float* __restrict__ viewdirs, const float* __restrict__ vemb_const,
-    const float* __restrict__ wbuf, float eps, float shift, float interval, float4* __restrict__ out) {
+    const float* __restrict__ wbuf, float eps, float shift, float interval, float4* __restrict__ out,
+    char* const Xs, char* const Hs, float* const sTo, float* const sIdw, float* const sRow, float* const sOut,
+    float* const sV, float* const sW, float* const sPart) {
   constexpr bool PP = OCC == 2;
-  __shared__ __attribute__((aligned(16))) char Xs[PP ? 2 * XBUF : XBUF];
-  __shared__ __attribute__((aligned(16))) char Hs[PP ? 16 : TS * HB];
-  __shared__ float sTo[TR];
-  __shared__ float sIdw[TR];
-  __shared__ float sRow[TR * 8];     // direct blend per row: wdir, alpha_c, rgb_c(3), pcol(3)
-  __shared__ __attribute__((aligned(16))) float sOut[TS * 12];
-  __shared__ float sV[TS * 32];      // view embedding per sample (27 + zero pad)
-  __shared__ __attribute__((aligned(16))) float sW[SW_TOTAL];
-  __shared__ float sPart[4 * TS * 4];
   char* const X0 = Xs;
   char* const X1 = PP ? Xs + XBUF : Xs;
   char* const HX = PP ? X1 : Hs;     // head input rows
-  {  // a launch with the flag already set (these weights overflowed before): leave the samples
-     // to the FP32 kernel. Block-uniform decision (one read, broadcast through LDS).
-    __shared__ int s_skip;
-    if (threadIdx.x == 0) s_skip = __builtin_nontemporal_load((const int*)(wbuf + OFF_FLAG));
-    __syncthreads();
-    if (s_skip) return;
-  }
 
   const int nS = *n_samples_dev;
   const int ntiles = (nS + TS - 1) / TS;
@@ -407,18 +392,17 @@ __global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
   const float* const scp = wbuf + OFF_SCALE;
   for (int i = tid; i < 128; i += MLP_THREADS) {
     sW[SW_B1 + i] = wbuf[OFF_B1 + i];
-    sW[SW_B2 + i] = wbuf[OFF_B2 + i] * scp[1];   // accumulator initial values: 2^s b
-    sW[SW_B3 + i] = wbuf[OFF_B3 + i] * scp[2];
-    sW[SW_B4 + i] = wbuf[OFF_B4 + i] * scp[3];
+    sW[SW_B2 + i] = SCALED ? wbuf[OFF_B2 + i] * scp[1] : wbuf[OFF_B2 + i];   // accumulator initial values: 2^s b
+    sW[SW_B3 + i] = SCALED ? wbuf[OFF_B3 + i] * scp[2] : wbuf[OFF_B3 + i];
+    sW[SW_B4 + i] = SCALED ? wbuf[OFF_B4 + i] * scp[3] : wbuf[OFF_B4 + i];
     sW[SW_WD + i] = wbuf[OFF_WD + i];
   }
-  if (tid < 6) {   // 0-3: W1E, W2, W3, W4; 4: WH h-columns (2^a); 5: WH view columns (2^b)
+  if (SCALED && tid < 6) {   // 0-3: W1E, W2, W3, W4; 4: WH h-columns (2^a); 5: WH view columns (2^b)
     sW[SW_SC + tid] = scp[tid];
     sW[SW_DS + tid] = 1.f / scp[tid];
   }
-  if (tid == 6) sW[SW_MODE] = scp[6];
-  if (tid == 7) sW[SW_HSC] = scp[5] / scp[4];   // h' = h 2^(b-a): WH_h' h' = 2^b WH_h h
-  if (tid < 64) sW[SW_BH + tid] = wbuf[OFF_BH + tid] * scp[5];
+  if (SCALED && tid == 7) sW[SW_HSC] = scp[5] / scp[4];   // h' = h 2^(b-a): WH_h' h' = 2^b WH_h h
+  if (tid < 64) sW[SW_BH + tid] = SCALED ? wbuf[OFF_BH + tid] * scp[5] : wbuf[OFF_BH + tid];
   if (tid < 192) sW[SW_WV2 + tid] = wbuf[OFF_WV2 + tid];
   if (tid < 3) sW[SW_BV2 + tid] = wbuf[OFF_BV2 + tid];
   if (tid == 0) sW[SW_BD] = wbuf[OFF_BD];
@@ -485,7 +469,7 @@ __global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
         acc[mt][j] = f32x4{v.x, v.y, v.z, v.w};
       }
     }
-    if (mode_scaled(sW)) {   // layer-1 accumulators in the W1E scale: 2^s1 P
+    if (SCALED) {   // layer-1 accumulators in the W1E scale: 2^s1 P
       const float sc1 = sW[SW_SC];
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
@@ -519,18 +503,18 @@ __global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
     // ------------------------------------------------ feat_net: 4 x (Linear + LeakyReLU)
     layer_mfma<2, 4, 2, PP>(X0, rs, H_W1E, ot0, H_W2, ot0, acc, a);
     if (!PP) __syncthreads();
-    store_act(X1, ot0, sW + SW_B1, acc, mode_scaled(sW), sW[SW_DS + 0]);
+    store_act(X1, ot0, sW + SW_B1, acc, SCALED, SCALED ? sW[SW_DS + 0] : 1.f);
     __syncthreads();
     APN_PHASE(1)
     init_bias(acc, ot0, sW + SW_B2);
     layer_mfma<4, 4, 2, PP>(X1, rs, H_W2, ot0, H_W3, ot0, acc, a);
     if (!PP) __syncthreads();
-    store_act(X0, ot0, nullptr, acc, mode_scaled(sW), sW[SW_DS + 1]);
+    store_act(X0, ot0, nullptr, acc, SCALED, SCALED ? sW[SW_DS + 1] : 1.f);
     __syncthreads();
     init_bias(acc, ot0, sW + SW_B3);
     layer_mfma<4, 4, 2, PP>(X0, rs, H_W3, ot0, H_W4, ot0, acc, a);
     if (!PP) __syncthreads();
-    store_act(X1, ot0, nullptr, acc, mode_scaled(sW), sW[SW_DS + 2]);
+    store_act(X1, ot0, nullptr, acc, SCALED, SCALED ? sW[SW_DS + 2] : 1.f);
     __syncthreads();
     init_bias(acc, ot0, sW + SW_B4);
     layer_mfma<4, 5, 1, PP>(X1, rs, H_W4, ot0, H_WH, wid, acc, a);
@@ -542,7 +526,7 @@ __global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
         *(f32x4*)(X0 + out32_off(16 * mt + li, o0 >> 2)) =
-            lrelu4(mode_scaled(sW) ? acc[mt][j] * sW[SW_DS + 3] : acc[mt][j]);
+            lrelu4(SCALED ? acc[mt][j] * sW[SW_DS + 3] : acc[mt][j]);
     }
     __syncthreads();
     APN_PHASE(2)
@@ -561,7 +545,7 @@ __global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
       const f32x4 wd = *(const f32x4*)(sW + SW_WD + 4 * oq);
       float d = ((h[0] * wd[0] + h[1] * wd[1]) + h[2] * wd[2]) + h[3] * wd[3];
       // the head's h input in the head's column scale (scaled mode): h' = h 2^(b-a), exact
-      if (mode_scaled(sW)) h = h * sW[SW_HSC];
+      if (SCALED) h = h * sW[SW_HSC];
       // range guard (see the header comment) on the last values split: false for NaN too
       if (!(fmaxf(fmaxf(fabsf(h[0]), fabsf(h[1])), fmaxf(fabsf(h[2]), fabsf(h[3]))) <= H3_RANGE))
         __builtin_amdgcn_raw_buffer_store_b32(1, rs, 0, H_TOTAL * 2, 0);   // the range flag (OFF_FLAG)
@@ -646,7 +630,7 @@ __global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
       float pc[3] = {0.f, 0.f, 0.f};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float v = fmaxf(mode_scaled(sW) ? ah[r] * sW[SW_DS + 5] : ah[r], 0.f);
+        const float v = fmaxf(SCALED ? ah[r] * sW[SW_DS + 5] : ah[r], 0.f);
 #pragma unroll
         for (int c = 0; c < 3; ++c) pc[c] += v * sW[SW_WV2 + 64 * c + o0 + r];
       }
@@ -678,6 +662,36 @@ __global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
   __syncthreads();
   if (prev_s0 >= 0 && tid < TS * 3 && prev_s0 + tid / 3 < nS)
     out[(size_t)prev_s0 * 3 + tid] = *(const float4*)(sOut + 4 * tid);
+}
+
+// One instantiation per weight-scale mode (separate register allocation); apn_point_mlp launches
+// both and the one that does not match wbuf's mode exits at once (a launch with the range flag
+// already set -- these weights overflowed before -- leaves every sample to the FP32 kernel).
+// Block-uniform decisions: one read each, broadcast through LDS.
+template <bool TIMED, int OCC, bool SCALED>
+__global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
+    const float4* __restrict__ s_pos, const int* __restrict__ s_ray, const int* __restrict__ s_nbr,
+    const int* __restrict__ n_samples_dev, const float4* __restrict__ recA, const float4* __restrict__ recB,
+    const float4* __restrict__ pproj, const float* __restrict__ viewdirs, const float* __restrict__ vemb_const,
+    const float* __restrict__ wbuf, float eps, float shift, float interval, float4* __restrict__ out) {
+  constexpr bool PP = OCC == 2;
+  __shared__ __attribute__((aligned(16))) char Xs[PP ? 2 * XBUF : XBUF];
+  __shared__ __attribute__((aligned(16))) char Hs[PP ? 16 : TS * HB];
+  __shared__ float sTo[TR];
+  __shared__ float sIdw[TR];
+  __shared__ float sRow[TR * 8];     // direct blend per row: wdir, alpha_c, rgb_c(3), pcol(3)
+  __shared__ __attribute__((aligned(16))) float sOut[TS * 12];
+  __shared__ float sV[TS * 32];      // view embedding per sample (27 + zero pad)
+  __shared__ __attribute__((aligned(16))) float sW[SW_TOTAL];
+  __shared__ float sPart[4 * TS * 4];
+  __shared__ int s_skip;
+  if (threadIdx.x == 0)
+    s_skip = __builtin_nontemporal_load((const int*)(wbuf + OFF_FLAG)) != 0 ||
+             (wbuf[OFF_SCALE + 6] != 0.f) != SCALED;
+  __syncthreads();
+  if (s_skip) return;
+  mlp_tiles<TIMED, OCC, SCALED>(s_pos, s_ray, s_nbr, n_samples_dev, recA, recB, pproj, viewdirs, vemb_const, wbuf,
+                                eps, shift, interval, out, Xs, Hs, sTo, sIdw, sRow, sOut, sV, sW, sPart);
 }
 
 // Per-group scales (apn_mlp_layout.h OFF_SCALE) from max|w| of W1E, W2, W3, W4 and the two
@@ -782,14 +796,19 @@ void launch_point_mlp_h3(int blocks, bool timed, hipStream_t stream, const float
     const char* e = getenv("APN_MLP_OCC");
     return e ? atoi(e) : 3;
   }();
-  auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(MLP_THREADS), 0, stream, s_pos, s_ray, s_nbr, n_samples_dev, recA,
-                       recB, pproj, viewdirs, vemb_const, wbuf, eps, shift, interval, out);
+  auto go = [&](auto kern, int nb) {
+    hipLaunchKernelGGL(kern, dim3(nb), dim3(MLP_THREADS), 0, stream, s_pos, s_ray, s_nbr, n_samples_dev, recA, recB,
+                       pproj, viewdirs, vemb_const, wbuf, eps, shift, interval, out);
   };
+  // the scaled-weights instantiation runs on a smaller grid (a rare mode: weight magnitudes outside
+  // [2^-5, 2^12]); when it does not match, its 8 workgroups per CU exit at once
+  const int nb_scaled = blocks < 256 * 8 ? blocks : 256 * 8;
   if (occ == 3) {
-    if (timed) go(h3::k_point_mlp_h3<true, 3>); else go(h3::k_point_mlp_h3<false, 3>);
+    if (timed) { go(h3::k_point_mlp_h3<true, 3, false>, blocks); go(h3::k_point_mlp_h3<true, 3, true>, nb_scaled); }
+    else { go(h3::k_point_mlp_h3<false, 3, false>, blocks); go(h3::k_point_mlp_h3<false, 3, true>, nb_scaled); }
   } else {
-    if (timed) go(h3::k_point_mlp_h3<true, 2>); else go(h3::k_point_mlp_h3<false, 2>);
+    if (timed) { go(h3::k_point_mlp_h3<true, 2, false>, blocks); go(h3::k_point_mlp_h3<true, 2, true>, nb_scaled); }
+    else { go(h3::k_point_mlp_h3<false, 2, false>, blocks); go(h3::k_point_mlp_h3<false, 2, true>, nb_scaled); }
   }
 }
 
