@@ -57,11 +57,12 @@ def test_mult_dist_interp_vs_reference(dev, golden):
         vox = m.mult_dist_interp(t(golden, "in_pts", dev)).cpu().numpy()
     ref = golden["out_vox"]
     assert vox.shape == ref.shape
-    # points outside the grid hit the zero padding exactly
-    outside = np.any((golden["in_pts"] < golden["cfg_xyz_min"] - 0.2) | (golden["in_pts"] > golden["cfg_xyz_max"] + 0.2), 1)
-    assert np.all(ref[outside] == 0) and np.all(vox[outside] == 0)
+    # points outside the bbox: their corners are partly out of bounds (the zero padding of
+    # grid_sample), at the coarse scale a point up to one coarse voxel outside still interpolates
+    outside = np.any((golden["in_pts"] < golden["cfg_xyz_min"]) | (golden["in_pts"] > golden["cfg_xyz_max"]), 1)
+    assert outside.sum() > 100 and np.any(ref[outside] == 0) and np.any(ref[outside] != 0)
     err = np.abs(vox - ref).max()
-    print(f"mult_dist_interp max|d| {err:.2e} over {len(vox)} points ({int(outside.sum())} far outside)")
+    print(f"mult_dist_interp max|d| {err:.2e} over {len(vox)} points ({int(outside.sum())} outside the bbox)")
     assert err < 1e-6
 
 
