@@ -134,14 +134,14 @@ class PointWarper(torch.nn.Module):
         self.sibling_mask = sibling_mask.long()
 
     def _tn_packed(self, dev):
-        """TransformNet weights packed for apn_skeleton_pose ([W0, b0, W1, b1, ..., W_last]),
+        """TransformNet weights packed for apn_skeleton_pose ([W0^T, b0, W1^T, b1, ..., W_last^T]),
         cached on the parameters' versions."""
         lins = [m for m in self.transform_net.net if isinstance(m, torch.nn.Linear)]
         key = (str(dev),) + tuple((p.data_ptr(), p._version) for m in lins for p in m.parameters())
         if getattr(self, "_tn_key", None) != key:
             parts = []
-            for m in lins:
-                parts.append(m.weight.detach().float().reshape(-1))
+            for m in lins:   # W^T [in][out] per layer: coalesced GEMV loads (apn_skeleton.hip)
+                parts.append(m.weight.detach().float().t().contiguous().reshape(-1))
                 if m.bias is not None:
                     parts.append(m.bias.detach().float().reshape(-1))
             self._tn_buf = torch.cat(parts).to(dev).contiguous()

@@ -441,6 +441,33 @@ class TemporalPoints(torch.nn.Module):
         self._mark("lbs")
         return [xyz, joints_rel]
 
+    def capture_repose(self, rot_dim=4):
+        """The repose step (skeleton launch + fused LBS launch, run.py:1355-1396 sweeps it per pose)
+        captured once in a HIP graph: returns ``step(rot_params) -> (xyz, joints_rel)``, which
+        copies rot_params [J, rot_dim] into the graph's input and replays it -- no per-pose host
+        work besides one copy and one graph launch. The outputs are the graph's static buffers
+        (overwritten by the next step). Capture again after changing the model."""
+        dev = self.canonical_pcd.device
+        J = self.weights.shape[1]
+        rp = torch.zeros(J, rot_dim, device=dev)
+        with torch.no_grad():
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):   # warm-up: caches, workspaces, packed buffers
+                self.repose(rp)
+            torch.cuda.current_stream(dev).wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                xyz, joints_rel = self.repose(rp)
+
+        def step(rot_params):
+            rp.copy_(rot_params.reshape(J, rot_dim))
+            graph.replay()
+            return xyz, joints_rel
+
+        step.graph, step.inputs = graph, rp
+        return step
+
     def sample_ray(self, rays_o, rays_d, near, far, stepsize, xyz_min=None, xyz_max=None, **render_kwargs):
         """temporalpoints.py:373-399 through the render_utils drop-in."""
         from .ops import sample_pts_on_rays
@@ -504,8 +531,8 @@ class TemporalPoints(torch.nn.Module):
              ptr(self.canonical_alpha.detach().contiguous()) if records else None,
              ptr(self.canonical_rgbs.detach().contiguous()) if records else None,
              ptr(self.direct_eps.detach().contiguous()) if records else None, mmd, 0, ptr(xyz), ptr(wout), None,
-             ptr(recA), ptr(recB), ptr(bbox), ptr(ws.bytes("lbs_ws", L.load().apn_lbs_workspace_bytes(N), dev)),
-             stream_ptr(dev))
+             ptr(recA), ptr(recB), ptr(bbox) if records else None,   # the bbox only feeds the render's sampling
+             ptr(ws.bytes("lbs_ws", L.load().apn_lbs_workspace_bytes(N), dev)), stream_ptr(dev))
         return xyz, wout, (recA, recB, bbox)
 
     def _packed_weights(self, pose_embedding, dev):

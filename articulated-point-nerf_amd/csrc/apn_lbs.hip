@@ -275,6 +275,7 @@ void k_lbs_skin_quad(
   for (int e = tid; e < J * 12; e += LBS_THREADS) sT[e] = boneT12[e];
   for (int e = tid; e < J * 3; e += LBS_THREADS) sC[e] = colors ? colors[e] : 0.f;
   const float th = weights_final ? 1.f : fmaxf(eps, theta_weight[0]);
+  const float rth = 1.f / th;   // IEEE reciprocal, once per thread
   const int64_t stride = (int64_t)gridDim.x * PPB;
   int64_t n = (int64_t)blockIdx.x * PPB + (tid >> 2);
   // the next row is in flight while the current one is processed (grid-stride, one step ahead)
@@ -290,21 +291,24 @@ void k_lbs_skin_quad(
     for (int j = 0; j < JL; ++j) row[j] = nrow[j];
     quad_load_row<JL>(W + min(n + stride, N - 1) * J + sub * JL, nrow);
     if (!weights_final) {   // softmax(W / th) over J (temporalpoints.py:403)
+      // W / th as the reciprocal product plus one fma residual correction (3 VALU instead of the
+      // ~10 of an IEEE division; the corrected quotient is the correctly rounded one)
       float m = -INFINITY;
 #pragma unroll
       for (int j = 0; j < JL; ++j) {
-        row[j] = row[j] / th;
+        const float q = row[j] * rth;
+        row[j] = fmaf(fmaf(-q, th, row[j]), rth, q);
         m = fmaxf(m, row[j]);
-        if (j & 1) __builtin_amdgcn_sched_barrier(0);
       }
       m = fmaxf(m, quad_swap<QX1>(m));
       m = fmaxf(m, quad_swap<QX2>(m));
+      // exp(x - m) on the transcendental unit (v_exp_f32 = 2^x): x - m <= 0, so the argument
+      // rounding costs w |x - m| 2^-24 log2(e) absolute per weight (<= 3e-8, as w e^-d d <= 1/e)
       float sum = 0.f;
 #pragma unroll
       for (int j = 0; j < JL; ++j) {
-        row[j] = expf(row[j] - m);
+        row[j] = __builtin_amdgcn_exp2f((row[j] - m) * 1.4426950408889634f);
         sum += row[j];
-        if (j & 1) __builtin_amdgcn_sched_barrier(0);
       }
       sum += quad_swap<QX1>(sum);
       sum += quad_swap<QX2>(sum);

@@ -4,8 +4,8 @@
 //   -> M_j = [R_j | p - R_j p] about the parent joint p (167-172)
 //   -> kinematic chain as the reference's recursive-halving matrix product (145-153, 173-175)
 //   -> joints_rel = T_j [joint_j; 1] (258-260).
-// The reference runs this as ~100 tiny torch launches per frame; here it is one launch of
-// ~10 us (GEMV layers read 0.9 MB of weights once), so the per-point kernels start right away.
+// The reference runs this as ~100 tiny torch launches per frame; here it is one launch (GEMV
+// layers read 0.9 MB of transposed, coalesced weights once; the chain products run from LDS).
 #include "apn_common.h"
 
 namespace apn {
@@ -13,6 +13,7 @@ namespace apn {
 constexpr int SK_THREADS = 256;
 constexpr int SK_MAX_J = 64;
 constexpr int SK_MAX_DEPTH = 32;
+constexpr int SK_STACK = 8;   // recursion depth of the halving tree for chains <= 32 factors: ceil(log2 32) + 1
 
 // C = A B for row-major 4x4, the sum in k order.
 __device__ __forceinline__ void mm4(const float* A, const float* B, float* C) {
@@ -23,47 +24,28 @@ __device__ __forceinline__ void mm4(const float* A, const float* B, float* C) {
       C[4 * i + k] = ((A[4 * i] * B[k] + A[4 * i + 1] * B[4 + k]) + A[4 * i + 2] * B[8 + k]) + A[4 * i + 3] * B[12 + k];
 }
 
-// matrix_chain_product over chain[lo, hi) (pointwarper.py:145-153): prod(left half) @ prod(right
-// half), left = first floor(L/2) factors. Iterative post-order with an explicit stack.
-__device__ void chain_product(const float (*chain)[16], int n, float* out) {
-  struct Frame { int lo, hi, state; };
-  Frame st[12];
-  float res[12][16];   // result of each pending level's left half
-  float cur[16];
-  int sp = 0;
-  st[0] = {0, n, 0};
-  bool have = false;
+// matrix_chain_product (pointwarper.py:145-153) = prod(left half) @ prod(right half), left =
+// first floor(L/2) factors, recursively. The recursion tree depends only on the chain length, so
+// it is flattened once per launch into a postfix program (SK_LEAF | d = push factor d, SK_MUL =
+// pop two, push their product) that every joint's thread then runs with its stack in LDS.
+constexpr int SK_MUL = -1;
+__device__ int chain_program(int n, int* prog, int (*st)[3]) {
+  int sp = 0, np = 0;
+  st[0][0] = 0; st[0][1] = n; st[0][2] = 0;
   while (sp >= 0) {
-    Frame& f = st[sp];
-    const int L = f.hi - f.lo;
-    if (L == 1) {
-      for (int e = 0; e < 16; ++e) cur[e] = chain[f.lo][e];
-      have = true;
-      --sp;
-      continue;
-    }
-    if (f.state == 0) {            // descend into the left half
-      f.state = 1;
-      st[sp + 1] = {f.lo, f.lo + L / 2, 0};
-      ++sp;
-    } else if (f.state == 1) {     // left done (in cur): keep it, descend right
-      for (int e = 0; e < 16; ++e) res[sp][e] = cur[e];
-      f.state = 2;
-      st[sp + 1] = {f.lo + L / 2, f.hi, 0};
-      ++sp;
-    } else {                       // right done: combine
-      float t[16];
-      mm4(res[sp], cur, t);
-      for (int e = 0; e < 16; ++e) cur[e] = t[e];
-      --sp;
-    }
+    int* f = st[sp];
+    const int L = f[1] - f[0];
+    if (L == 1) { prog[np++] = f[0]; --sp; continue; }
+    if (f[2] == 0) { f[2] = 1; st[sp + 1][0] = f[0]; st[sp + 1][1] = f[0] + L / 2; st[sp + 1][2] = 0; ++sp; }
+    else if (f[2] == 1) { f[2] = 2; st[sp + 1][0] = f[0] + L / 2; st[sp + 1][1] = f[1]; st[sp + 1][2] = 0; ++sp; }
+    else { prog[np++] = SK_MUL; --sp; }
   }
-  (void)have;
-  for (int e = 0; e < 16; ++e) out[e] = cur[e];
+  return np;
 }
 
-// Packed TransformNet weights (floats): W0 [H][T], b0 [H], then for l = 1..NL-2: Wl [H][H], bl [H],
-// then W_last [(J+1)*4][H] (no bias). NL = num_layers (5 in the reference).
+// Packed TransformNet weights (floats), each layer transposed so that thread o's loads over k are
+// coalesced across the block: W0^T [T][H], b0 [H], then for l = 1..NL-2: Wl^T [H][H], bl [H], then
+// W_last^T [H][(J+1)*4] (no bias). NL = num_layers (5 in the reference).
 __global__ __launch_bounds__(SK_THREADS) void k_skeleton_pose(
     const float* __restrict__ t_embed, int t_dim, const float* __restrict__ rot_params, int rot_dim, int J,
     const float* __restrict__ tnw, int hidden, int n_layers, const float* __restrict__ joints,
@@ -75,10 +57,15 @@ __global__ __launch_bounds__(SK_THREADS) void k_skeleton_pose(
   __shared__ float sP[SK_MAX_J + 1][4];
   __shared__ float sR[SK_MAX_J][9];
   __shared__ float sM[SK_MAX_J + 1][16];
+  __shared__ int sProg[2 * SK_MAX_DEPTH];
+  __shared__ int sFrames[SK_MAX_DEPTH + 2][3];
+  __shared__ int sNProg;
+  __shared__ float sStk[SK_MAX_J][SK_STACK][16];
   const int tid = threadIdx.x;
   const bool tpath = rot_params == nullptr;
+  if (tid == SK_THREADS - 1) sNProg = chain_program(depth, sProg, sFrames);   // overlaps the GEMVs
   if (tpath) {
-    // TransformNet: one output feature per thread (hidden <= 256)
+    // TransformNet: one output feature per thread (hidden <= 256), k summed in order
     if (tid < t_dim) h[0][tid] = t_embed[tid];
     __syncthreads();
     const float* w = tnw;
@@ -87,9 +74,10 @@ __global__ __launch_bounds__(SK_THREADS) void k_skeleton_pose(
       const bool last = l == n_layers - 1;
       const int out_dim = last ? (J + 1) * 4 : hidden;
       if (tid < out_dim) {
-        const float* wr = w + (size_t)tid * in_dim;
+        const float* wc = w + tid;
         float a = 0.f;
-        for (int k = 0; k < in_dim; ++k) a += wr[k] * h[cur][k];
+#pragma unroll 8
+        for (int k = 0; k < in_dim; ++k) a += wc[(size_t)k * out_dim] * h[cur][k];
         if (!last) {
           a += w[(size_t)out_dim * in_dim + tid];
           h[cur ^ 1][tid] = fmaxf(a, 0.f);
@@ -154,15 +142,33 @@ __global__ __launch_bounds__(SK_THREADS) void k_skeleton_pose(
     }
   }
   __syncthreads();
-  // kinematic chain per joint (pointwarper.py:173-175), joints_rel (258-260)
+  // kinematic chain per joint (pointwarper.py:173-175): the postfix program over the joint's
+  // factors (parent_indices, -1 -> identity), top of stack in registers, the rest in LDS
   if (tid < J) {
-    float chain[SK_MAX_DEPTH][16];
-    for (int d = 0; d < depth; ++d) {
-      const int idx = parent_indices[tid * depth + d] + 1;   // -1 -> identity (slot 0)
-      for (int e = 0; e < 16; ++e) chain[d][e] = sM[idx][e];
+    const int np = sNProg;
+    const int* pidx = parent_indices + (size_t)tid * depth;
+    float cur[16];
+    int sp = -1;   // LDS stack entries below the top: sStk[tid][0..sp]
+    for (int i = 0; i < np; ++i) {
+      const int op = sProg[i];
+      if (op == SK_MUL) {
+        float t[16];
+        mm4(sStk[tid][sp], cur, t);   // (left) @ (right = top)
+        --sp;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) cur[e] = t[e];
+      } else {
+        if (i > 0) {
+          ++sp;
+#pragma unroll
+          for (int e = 0; e < 16; ++e) sStk[tid][sp][e] = cur[e];
+        }
+        const float* f = sM[pidx[op] + 1];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) cur[e] = f[e];
+      }
     }
-    float T[16];
-    chain_product(chain, depth, T);
+    const float* T = cur;
     for (int e = 0; e < 16; ++e) bone_T16[16 * tid + e] = T[e];
     for (int e = 0; e < 12; ++e) bone_T34[12 * tid + e] = T[e];
     const float jx = joints[3 * tid], jy = joints[3 * tid + 1], jz = joints[3 * tid + 2];
@@ -191,7 +197,7 @@ extern "C" int apn_skeleton_pose(const float* t_embed, int32_t t_dim, const floa
                 hidden > SK_THREADS || n_layers < 2 || (n_joints + 1) * 4 > SK_THREADS))
     return APN_ERR_ARG;
   if (!tpath && rot_dim != 3 && rot_dim != 4) return APN_ERR_ARG;
-  if (depth > (1 << 11)) return APN_ERR_ARG;
+
   hipLaunchKernelGGL(k_skeleton_pose, dim3(1), dim3(SK_THREADS), 0, (hipStream_t)stream, t_embed, t_dim, rot_params,
                      rot_dim, n_joints, tn_weights, hidden, n_layers, joints, parent_indices, depth, parent_joint_ex,
                      sibling_mask, rot_mask, params_out, thetas_out, bone_T16, bone_T34, global_t_out,

@@ -165,15 +165,27 @@ def lbs_sweep(args, rank, world, dev):
     model = harness.build_model(scene, dev)
     N, J = len(scene.ctor["canonical_pcd"]), scene.cfg.J
     poses = S.repose_sweep(J).to(dev)
-    for i in range(args.warmup):
+    # LBS kernel time for the roofline: HIP events around the LBS launch, eager steps
+    for i in range(2):
         model.repose(poses[i % len(poses)])
     model.timing = {}
+    for i in range(args.steps):
+        model.repose(poses[i % len(poses)])
+    torch.cuda.synchronize(dev)
+    marks = model.timing.get("marks", [])
+    lbs_ms = sum(a.elapsed_time(b) for (_, a), (nm, b) in zip(marks[:-1], marks[1:]) if nm == "lbs") / args.steps
+    model.timing = None
+    # throughput: every pose of the sweep through the captured repose step (skeleton + LBS in one
+    # HIP graph; per pose one device copy of rot_params + one graph launch)
+    step = model.capture_repose(rot_dim=poses.shape[-1])
+    for i in range(args.warmup):
+        step(poses[i % len(poses)])
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        model.repose(poses[i % len(poses)])
+        step(poses[i % len(poses)])
     torch.cuda.synchronize(dev)
     if world > 1:
         torch.distributed.barrier()
@@ -182,9 +194,6 @@ def lbs_sweep(args, rank, world, dev):
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t)
-    marks = model.timing.get("marks", [])
-    lbs_ms = sum(a.elapsed_time(b) for (_, a), (nm, b) in zip(marks[:-1], marks[1:]) if nm == "lbs") / args.steps
-    model.timing = None
     if rank != 0:
         return
     b_alg = N * (24 + 4 * J)
@@ -217,6 +226,8 @@ def lbs_sweep(args, rank, world, dev):
         "vs_baseline": None, "dtype": "fp32", "data": "synthetic (procedural 48-joint capsule cloud, repose sweep)",
         "config": {"workload": S.CONFIGS[args.config].name + f" ({args.config})", "points": N_total, "bones": J,
                    "points_per_rank": N, "poses_per_s": args.steps / elapsed,
+                   "step": "skeleton + LBS captured in one HIP graph (TemporalPoints.capture_repose)",
+                   "lbs_kernel_ms": lbs_ms,
                    "parallelism": f"points x{world} (no collective)" if world > 1 else "single"},
         "roofline": {"bound": "hbm", "kernel": "k_lbs_skin_quad",
                      "achieved": b_alg / (lbs_ms * 1e-3) / 1e9 if lbs_ms > 0 else 0.0,

@@ -167,8 +167,9 @@ int apn_lbs_skin(const float* canonical_pcd, const float* raw_weights, int64_t n
  * input, pointwarper.py:213) -- softmax/merge skipped. G_out [N,16] (weighted_G_tw) or NULL. */
 
 /* Skeleton stage of PointWarper.forward (pointwarper.py:213-239, 118-193) in one launch:
- * TransformNet (t path: t_embed [t_dim] through tn_weights = [W0 [hidden][t_dim], b0, W1, b1, ...,
- * W_last [(J+1)*4][hidden]] with ReLU between, n_layers Linear layers) or rot_params [J, rot_dim]
+ * TransformNet (t path: t_embed [t_dim] through tn_weights = [W0^T [t_dim][hidden], b0, W1^T, b1,
+ * ..., W_last^T [hidden][(J+1)*4]] -- nn.Linear weights transposed, for coalesced loads -- with
+ * ReLU between, n_layers Linear layers) or rot_params [J, rot_dim]
  * (rot_dim 3 or 4; t_embed = NULL) -> Rodrigues -> sibling_mask [J] / rot_mask [J] (int32, NULL =
  * identity / none) -> local transforms about parent_joint_ex [J] -> recursive-halving chain
  * product over parent_indices [J, depth] (-1 = identity). Outputs: params_out [(J+1)*4] (t path),

@@ -111,3 +111,19 @@ def test_c5_repose_is_order_independent(dev):
         b = model.repose(poses[10].to(dev))[0]
     assert torch.equal(a, b)
     assert np.isfinite(b.cpu().numpy()).all()
+
+
+def test_captured_repose_graph_equals_eager(dev):
+    """TemporalPoints.capture_repose (skeleton + LBS in one HIP graph, the C5 bench step) replays
+    the eager repose bit for bit over several poses of the sweep."""
+    from apn_amd import harness, synthetic as S
+    scene = S.make_scene(S.SceneConfig("graph repose", 50_000, 48, 0, 0))
+    model = harness.build_model(scene, dev)
+    poses = S.repose_sweep(48).to(dev)
+    step = model.capture_repose(rot_dim=4)
+    for k in (0, 7, 31, 59):
+        with torch.no_grad():
+            xe, je = (v.clone() for v in model.repose(poses[k]))
+        xg, jg = step(poses[k])
+        torch.cuda.synchronize()
+        assert torch.equal(xg, xe) and torch.equal(jg, je), k
