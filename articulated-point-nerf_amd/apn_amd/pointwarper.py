@@ -155,7 +155,8 @@ class PointWarper(torch.nn.Module):
             self._tree = (self.parent_indices.to(dev, torch.int32).contiguous(),
                           self.parent_joint_ex.to(dev, torch.int32).contiguous(),
                           self.sibling_mask.to(dev, torch.int32).contiguous(),
-                          None if self.rot_mask is None else self.rot_mask.to(dev, torch.int32).contiguous())
+                          None if self.rot_mask is None else self.rot_mask.to(dev, torch.int32).contiguous(),
+                          torch.tensor(chain_program(self.parent_indices.shape[1]), dtype=torch.int32, device=dev))
             self._tree_key = key
         return self._tree
 
@@ -168,7 +169,7 @@ class PointWarper(torch.nn.Module):
         dev = joints.device
         L.require_cuda(joints, what="PointWarper.pose")
         J = joints.shape[0]
-        pi, pjx, sib, rmask = self._tree_buffers(dev)
+        pi, pjx, sib, rmask, prog = self._tree_buffers(dev)
         jts = joints.detach().float().contiguous()
         thetas = torch.empty(J, device=dev)
         bone_Ts = torch.empty(J, 4, 4, device=dev)
@@ -182,14 +183,14 @@ class PointWarper(torch.nn.Module):
             params = torch.empty(J + 1, 4, device=dev)
             call("apn_skeleton_pose", ptr(te), te.numel(), None, 4, J, ptr(tn), hidden, n_layers, ptr(jts), ptr(pi),
                  pi.shape[1], ptr(pjx), ptr(sib), ptr(rmask), ptr(params), ptr(thetas), ptr(bone_Ts), ptr(T34),
-                 ptr(gt), ptr(joints_rel), s)
+                 ptr(gt), ptr(joints_rel), ptr(prog), s)
             self.prev_params = params
             self.prev_global_t = gt
         else:
             rp = rot_params.detach().float().contiguous()
             call("apn_skeleton_pose", None, 0, ptr(rp), rp.shape[-1], J, None, 0, 0, ptr(jts), ptr(pi), pi.shape[1],
                  ptr(pjx), ptr(sib), ptr(rmask), None, ptr(thetas), ptr(bone_Ts), ptr(T34), ptr(gt), ptr(joints_rel),
-                 s)
+                 ptr(prog), s)
             if global_t is not None:
                 gt = global_t
         self.prev_thetas = thetas
@@ -233,6 +234,24 @@ class PointWarper(torch.nn.Module):
             out.append(joints_rel + global_t)
             out.append(self.bones)
         return out
+
+
+def chain_program(n):
+    """matrix_chain_product (pointwarper.py:145-153: prod(left floor(n/2)) @ prod(rest),
+    recursively) as a postfix program over factor indices 0..n-1: d = push factor d, -1 =
+    multiply the top two (left below right). Consumed by apn_skeleton_pose."""
+    prog = []
+
+    def rec(lo, hi):
+        if hi - lo == 1:
+            prog.append(lo)
+            return
+        mid = lo + (hi - lo) // 2
+        rec(lo, mid)
+        rec(mid, hi)
+        prog.append(-1)
+    rec(0, n)
+    return prog
 
 
 def lbs_apply(pcd, weights, bone_Ts, global_t, get_frames=False):

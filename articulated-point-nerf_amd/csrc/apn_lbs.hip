@@ -324,8 +324,10 @@ void k_lbs_skin_quad(
       const float4* T4 = (const float4*)(sT + 12 * (sub * JL + j));
       const float4 t0 = T4[0], t1 = T4[1], t2 = T4[2];
       const float T[12] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w, t2.x, t2.y, t2.z, t2.w};
+      // fused multiply-add (v_pk_fma_f32: two per instruction); the record-free kernel's bar is
+      // fp32 reassociation, not the render path's bit-exact skinned cloud
 #pragma unroll
-      for (int e = 0; e < 12; ++e) G[e] = G[e] + row[j] * T[e];
+      for (int e = 0; e < 12; ++e) G[e] = fmaf(row[j], T[e], G[e]);
       __builtin_amdgcn_sched_barrier(0);   // one joint's bone row live at a time
     }
 #pragma unroll

@@ -547,8 +547,10 @@ __device__ __forceinline__ void mlp_tiles(
       // the head's h input in the head's column scale (scaled mode): h' = h 2^(b-a), exact
       if (SCALED) h = h * sW[SW_HSC];
       // range guard (see the header comment) on the last values split: false for NaN too
+#ifndef APN_H3_AB_NO_GUARD   // A/B builds only (tools/ab_build.sh): the guard's cost
       if (!(fmaxf(fmaxf(fabsf(h[0]), fabsf(h[1])), fmaxf(fabsf(h[2]), fabsf(h[3]))) <= H3_RANGE))
         __builtin_amdgcn_raw_buffer_store_b32(1, rs, 0, H_TOTAL * 2, 0);   // the range flag (OFF_FLAG)
+#endif
       d += __shfl_xor(d, 16, 64);
       d += __shfl_xor(d, 8, 64);
       d += __shfl_xor(d, 4, 64);
@@ -684,12 +686,16 @@ __global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
   __shared__ float sV[TS * 32];      // view embedding per sample (27 + zero pad)
   __shared__ __attribute__((aligned(16))) float sW[SW_TOTAL];
   __shared__ float sPart[4 * TS * 4];
+#ifndef APN_H3_AB_NO_GUARD
   __shared__ int s_skip;
   if (threadIdx.x == 0)
     s_skip = __builtin_nontemporal_load((const int*)(wbuf + OFF_FLAG)) != 0 ||
              (wbuf[OFF_SCALE + 6] != 0.f) != SCALED;
   __syncthreads();
   if (s_skip) return;
+#else
+  if (SCALED) return;
+#endif
   mlp_tiles<TIMED, OCC, SCALED>(s_pos, s_ray, s_nbr, n_samples_dev, recA, recB, pproj, viewdirs, vemb_const, wbuf,
                                 eps, shift, interval, out, Xs, Hs, sTo, sIdw, sRow, sOut, sV, sW, sPart);
 }

@@ -52,7 +52,7 @@ __global__ __launch_bounds__(SK_THREADS) void k_skeleton_pose(
     const int* __restrict__ parent_indices, int depth, const int* __restrict__ parent_joint_ex,
     const int* __restrict__ sibling_mask, const int* __restrict__ rot_mask, float* __restrict__ params_out,
     float* __restrict__ thetas_out, float* __restrict__ bone_T16, float* __restrict__ bone_T34,
-    float* __restrict__ global_t_out, float* __restrict__ joints_rel_out) {
+    float* __restrict__ global_t_out, float* __restrict__ joints_rel_out, const int* __restrict__ chain_prog) {
   __shared__ float h[2][SK_THREADS];
   __shared__ float sP[SK_MAX_J + 1][4];
   __shared__ float sR[SK_MAX_J][9];
@@ -63,7 +63,12 @@ __global__ __launch_bounds__(SK_THREADS) void k_skeleton_pose(
   __shared__ float sStk[SK_MAX_J][SK_STACK][16];
   const int tid = threadIdx.x;
   const bool tpath = rot_params == nullptr;
-  if (tid == SK_THREADS - 1) sNProg = chain_program(depth, sProg, sFrames);   // overlaps the GEMVs
+  if (chain_prog) {   // the host's program for this depth (2 depth - 1 ops)
+    if (tid < 2 * depth - 1) sProg[tid] = chain_prog[tid];
+    if (tid == 0) sNProg = 2 * depth - 1;
+  } else if (tid == SK_THREADS - 1) {
+    sNProg = chain_program(depth, sProg, sFrames);   // overlaps the GEMVs
+  }
   if (tpath) {
     // TransformNet: one output feature per thread (hidden <= 256), k summed in order
     if (tid < t_dim) h[0][tid] = t_embed[tid];
@@ -188,7 +193,8 @@ extern "C" int apn_skeleton_pose(const float* t_embed, int32_t t_dim, const floa
                                  const float* joints, const int32_t* parent_indices, int32_t depth,
                                  const int32_t* parent_joint_ex, const int32_t* sibling_mask, const int32_t* rot_mask,
                                  float* params_out, float* thetas_out, float* bone_T16, float* bone_T34,
-                                 float* global_t_out, float* joints_rel_out, void* stream) {
+                                 float* global_t_out, float* joints_rel_out, const int32_t* chain_prog,
+                                 void* stream) {
   const bool tpath = rot_params == nullptr;
   if (n_joints <= 0 || n_joints > SK_MAX_J || depth <= 0 || depth > SK_MAX_DEPTH || !joints || !parent_indices ||
       !parent_joint_ex || !thetas_out || !bone_T16 || !bone_T34 || !global_t_out || !joints_rel_out)
@@ -201,6 +207,6 @@ extern "C" int apn_skeleton_pose(const float* t_embed, int32_t t_dim, const floa
   hipLaunchKernelGGL(k_skeleton_pose, dim3(1), dim3(SK_THREADS), 0, (hipStream_t)stream, t_embed, t_dim, rot_params,
                      rot_dim, n_joints, tn_weights, hidden, n_layers, joints, parent_indices, depth, parent_joint_ex,
                      sibling_mask, rot_mask, params_out, thetas_out, bone_T16, bone_T34, global_t_out,
-                     joints_rel_out);
+                     joints_rel_out, chain_prog);
   return launch_status();
 }

@@ -67,6 +67,15 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def emit(line, args):
+    """The one JSON line on stdout (the driver's contract), optionally also to --out."""
+    text = json.dumps(line)
+    print(text, flush=True)
+    if getattr(args, "out", None):
+        with open(args.out, "w") as f:
+            f.write(text + "\n")
+
+
 def cpu_model_name():
     try:
         with open("/proc/cpuinfo") as f:
@@ -240,7 +249,7 @@ def lbs_sweep(args, rank, world, dev):
                              "the skeleton kernel"},
         "cpu_baseline": cpu,
     }
-    print(json.dumps(line), flush=True)
+    emit(line, args)
 
 
 def read_traffic(path):
@@ -259,6 +268,7 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--cpu-rows", type=int, default=16, help="image rows in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("-o", "--out", default=None, help="also write the JSON line to this file")
     ap.add_argument("--shard", choices=["frames", "rays"], default="rays",
                     help="N>1: 'rays' (default) = the ranks split one frame's rays and all-gather the tiles "
                          "over RCCL (strong scaling, SURVEY.md 8(e)); 'frames' = every rank renders its own "
@@ -432,7 +442,7 @@ def main():
         "psnr_vs_oracle": psnr,
         "same_cloud_vs_oracle": same,
     }
-    print(json.dumps(line), flush=True)
+    emit(line, args)
     if world > 1:
         torch.distributed.destroy_process_group()
 

@@ -174,13 +174,16 @@ int apn_lbs_skin(const float* canonical_pcd, const float* raw_weights, int64_t n
  * identity / none) -> local transforms about parent_joint_ex [J] -> recursive-halving chain
  * product over parent_indices [J, depth] (-1 = identity). Outputs: params_out [(J+1)*4] (t path),
  * thetas [J], bone_T16 [J,16], bone_T34 [J,12] (rows 0..2), global_t [3] (params[J][:3]; 0 for
- * rot_params), joints_rel [J,3]. J <= 64, depth <= 32, hidden <= 256. */
+ * rot_params), joints_rel [J,3]. J <= 64, depth <= 32, hidden <= 256. chain_prog: the
+ * recursive-halving product over `depth` factors as a postfix program (2 depth - 1 int32: factor
+ * index d = push factor d, -1 = multiply the top two), e.g. precomputed once by the host
+ * (PointWarper._tree_buffers); NULL = the kernel derives it. */
 int apn_skeleton_pose(const float* t_embed, int32_t t_dim, const float* rot_params, int32_t rot_dim,
                       int32_t n_joints, const float* tn_weights, int32_t hidden, int32_t n_layers,
                       const float* joints, const int32_t* parent_indices, int32_t depth,
                       const int32_t* parent_joint_ex, const int32_t* sibling_mask,
                       const int32_t* rot_mask, float* params_out, float* thetas_out, float* bone_T16,
-                      float* bone_T34, float* global_t_out, float* joints_rel_out, void* stream);
+                      float* bone_T34, float* global_t_out, float* joints_rel_out, const int32_t* chain_prog, void* stream);
 
 /* Padded sampling bbox = bbox_ord -/+ query_radius (temporalpoints.py:424) as 6 floats. */
 int apn_bbox_unpack(const int32_t* bbox_ord, float query_radius, float* out6, void* stream);

@@ -1,0 +1,19 @@
+#!/bin/bash
+# Build A/B variants of libapn_hip.so into ab/<name>/libapn_hip.so (select with APN_HIP_LIB).
+# Usage: tools/ab_build.sh <name> "<extra hipcc flags>"
+set -e
+name=$1; flags=$2
+root=$(cd "$(dirname "$0")/.." && pwd)
+out=$root/ab/$name; mkdir -p $out/build
+src=$root/articulated-point-nerf_amd/csrc
+objs=""
+for f in $src/*.hip $src/apn_version.cpp; do
+  b=$(basename $f); o=$out/build/${b%.*}.o
+  extra=""; [ "$b" = "apn_mlp_h3.hip" ] && extra="-fno-slp-vectorize"
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off $extra $flags -c $f -o $o &
+  objs="$objs $o"
+done
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $objs -o $out/libapn_hip.so
+rm -rf $out/build
+echo "built $out/libapn_hip.so ($flags)"
