@@ -48,18 +48,22 @@ constexpr int SW_B1 = 0, SW_B2 = 128, SW_B3 = 256, SW_B4 = 384, SW_WD = 512, SW_
 // exact), minimax polynomials on |r| <= pi/4 (Cephes sinf/cosf coefficients). Max error ~1e-7
 // absolute (fp32 sinf: ~7e-8), about a third of the VALU work of the library sincosf and no
 // large-argument branch (whose registers the library path keeps live).
+// k comes from the 1.5 2^23 rounding trick (one fma + one subtract, |2x/pi| < 2^22), which also
+// leaves k mod 4 in the low mantissa bits: the quadrant's swap and sign flips are bit operations.
 __device__ __forceinline__ void sincos_pe(float x, float& sn, float& cs) {
-  const float k = rintf(x * 0.636619772367581343f);
+  const float kf = fmaf(x, 0.636619772367581343f, 12582912.f);
+  const float k = kf - 12582912.f;
+  const uint32_t qb = __float_as_uint(kf);
   float r = fmaf(k, -0x1.921fb6p+0f, x);
   r = fmaf(k, 0x1.777a5cp-25f, r);
   const float z = r * r;
   const float sp = fmaf(r * z, fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f), r);
   const float cp = fmaf(z * z, fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f),
                         fmaf(-0.5f, z, 1.f));
-  const int q = (int)k;
-  const float ss = (q & 1) ? cp : sp, cc = (q & 1) ? sp : cp;
-  sn = (q & 2) ? -ss : ss;
-  cs = ((q + 1) & 2) ? -cc : cc;
+  const bool odd = qb & 1u;
+  const float ss = odd ? cp : sp, cc = odd ? sp : cp;
+  sn = __uint_as_float(__float_as_uint(ss) ^ ((qb << 30) & 0x80000000u));          // q & 2: -sin
+  cs = __uint_as_float(__float_as_uint(cc) ^ (((qb + 1u) << 30) & 0x80000000u));   // (q + 1) & 2: -cos
 }
 
 // Byte offset of logical 16-B chunk c (8 halves, 0..15) of the hi part of activation row m.
@@ -83,11 +87,17 @@ __device__ __forceinline__ void split4(const f32x4& v, h4& hi, h4& lo) {
   const u32x2 hb = __builtin_bit_cast(u32x2, hi);
   lo = __builtin_bit_cast(h4, (u32x2){split_lo2(hb[0], v[0], v[1]), split_lo2(hb[1], v[2], v[3])});
 }
-// LeakyReLU(0.01) as med3(x, 0.01x, +inf) with scalar multiplies (packed f32 VALU beside MFMAs
-// costs more than two plain ops, MI355X_MICROARCH.md constants table).
+// LeakyReLU(0.01) = max(x, 0.01x) with scalar multiplies (packed f32 VALU beside MFMAs costs
+// more than two plain ops, MI355X_MICROARCH.md constants table). The max is written as asm: the
+// compiler's fmaxf/fmed3f first canonicalise an MFMA result (an extra v_max_f32 x, x, x per
+// value, IEEE mode), a third of the epilogue's VALU. A NaN x gives NaN either way (both operands).
+__device__ __forceinline__ float lrelu_asm(float x) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(x * 0.01f));
+  return r;
+}
 __device__ __forceinline__ f32x4 lrelu4(const f32x4& v) {
-  return f32x4{__builtin_amdgcn_fmed3f(v[0], v[0] * 0.01f, INFINITY), __builtin_amdgcn_fmed3f(v[1], v[1] * 0.01f, INFINITY),
-               __builtin_amdgcn_fmed3f(v[2], v[2] * 0.01f, INFINITY), __builtin_amdgcn_fmed3f(v[3], v[3] * 0.01f, INFINITY)};
+  return f32x4{lrelu_asm(v[0]), lrelu_asm(v[1]), lrelu_asm(v[2]), lrelu_asm(v[3])};
 }
 
 __device__ __forceinline__ f32x4 mfma3(const h8& ahi, const h8& alo, const h8& bhi, const h8& blo, f32x4 acc) {
@@ -102,18 +112,21 @@ __device__ __forceinline__ f32x4 mfma3(const h8& ahi, const h8& alo, const h8& b
 // would be hoisted out of the tile loop by the compiler (~80 live VGPR pairs).
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
-// Fragment (o-tile ot, chunk q, part) of the matrix at half offset hbase with NQ chunks.
-__device__ __forceinline__ h8 frag(rsrc_t rs, int hbase, int nq, int ot, int q, int part) {
-  const int lane = threadIdx.x & 63;
-  const int soff = hbase * 2 + ((ot * nq + q) * 2 + part) * (FRAG_HALVES * 2);
-  return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, soff, 0));
+// Fragment f of this wave's block (apn_mlp_layout.h, wave-major): the per-lane VGPR offset
+// vb = wave block + lane * 16 B is the only register; f is a compile-time constant after
+// unrolling, so the scalar offset is an immediate / rematerialised constant.
+__device__ __forceinline__ h8 frag(rsrc_t rs, int vb, int f) {
+#ifdef APN_H3_PROBE_L1W   // timing probe only (wrong results): 4 fragments shared by every wave, L1-resident
+  return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rs, (threadIdx.x & 63) * 16, (f & 3) * (FRAG_HALVES * 2), 0));
+#endif
+  return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rs, vb, f * (FRAG_HALVES * 2), 0));
 }
 
 // acc[mt][j] += W[o-tile 2w+j] X^T over NQ chunks of 32. `a` carries chunk 0 of this matrix's
-// fragments in and chunk 0 of the next matrix (Wn, NQN chunks, o-tiles otn0, otn0+1) out.
-template <int NQ, int NQN, int NTN, bool BPF = true>
-__device__ __forceinline__ void layer_mfma(const char* __restrict__ X, rsrc_t rs, int W, int ot0, int Wn, int otn0,
-                                           f32x4 (&acc)[4][2], h8 (&a)[2][2]) {
+// fragments (block FB) in and chunk 0 of the next matrix (block FBN, NQN chunks, NTN o-tiles) out.
+template <int NQ, int NQN, int NTN, int FB, int FBN, bool BPF = true>
+__device__ __forceinline__ void layer_mfma(const char* __restrict__ X, rsrc_t rs, int vb, f32x4 (&acc)[4][2],
+                                           h8 (&a)[2][2]) {
   const int lane = threadIdx.x & 63;
   const int li = lane & 15, g = lane >> 4;
   if constexpr (!BPF) {
@@ -126,12 +139,12 @@ __device__ __forceinline__ void layer_mfma(const char* __restrict__ X, rsrc_t rs
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
-          for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, W, NQ, ot0 + j, q + 1, pt);
+          for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, vb, FB + (j * NQ + q + 1) * 2 + pt);
       } else {
 #pragma unroll
         for (int j = 0; j < NTN; ++j)
 #pragma unroll
-          for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, Wn, NQN, otn0 + j, 0, pt);
+          for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, vb, FBN + j * NQN * 2 + pt);
       }
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
@@ -170,7 +183,7 @@ __device__ __forceinline__ void layer_mfma(const char* __restrict__ X, rsrc_t rs
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, W, NQ, ot0 + j, q + 1, pt);
+        for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, vb, FB + (j * NQ + q + 1) * 2 + pt);
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
         const char* p = X + act_off(16 * mt + li, 4 * (q + 1) + g);
@@ -181,7 +194,7 @@ __device__ __forceinline__ void layer_mfma(const char* __restrict__ X, rsrc_t rs
 #pragma unroll
       for (int j = 0; j < NTN; ++j)
 #pragma unroll
-        for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, Wn, NQN, otn0 + j, 0, pt);
+        for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, vb, FBN + j * NQN * 2 + pt);
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -207,6 +220,63 @@ __device__ __forceinline__ void layer_mfma(const char* __restrict__ X, rsrc_t rs
         a[j][1] = an[j][1];
       }
     }
+  }
+}
+
+// Two-deep weight prefetch (the single-buffer OCC = 3 build): chunk q + 2's fragments are in flight
+// while chunk q's MFMAs run -- the L2 latency of the 1-KB fragment loads is the MFMA phases' main
+// wait (a probe with L1-resident weights ran 12 % faster), and the MFMA phases sit below the
+// kernel's register peak (the gather), so the extra 16 VGPRs cost no occupancy. a0 / a1 carry
+// chunks 0 / 1 of this matrix in (IN2 = false: chunk 1 is loaded here) and chunks 0 / 1 of the
+// next matrix (block FBN, NQN chunks, NTN o-tiles) out (OUT2 = false: chunk 0 only).
+#ifdef APN_H3_D2
+constexpr bool kD2 = true;
+#else
+constexpr bool kD2 = false;   // measured: no gain over the one-deep prefetch (A/B builds only)
+#endif
+template <int NQ, int NQN, int NTN, int FB, int FBN, bool IN2, bool OUT2>
+__device__ __forceinline__ void layer_mfma_d2(const char* __restrict__ X, rsrc_t rs, int vb, f32x4 (&acc)[4][2],
+                                              h8 (&a0)[2][2], h8 (&a1)[2][2]) {
+  static_assert(NQ >= 2, "two-deep prefetch needs two chunks");
+  const int lane = threadIdx.x & 63;
+  const int li = lane & 15, g = lane >> 4;
+  if constexpr (!IN2) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int pt = 0; pt < 2; ++pt) a1[j][pt] = frag(rs, vb, FB + (j * NQ + 1) * 2 + pt);
+  }
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    h8 an[2][2];
+    if (q + 2 < NQ) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, vb, FB + (j * NQ + q + 2) * 2 + pt);
+    } else if (q + 2 == NQ || OUT2) {
+      const int qn = q + 2 - NQ;   // chunk of the next matrix
+#pragma unroll
+      for (int j = 0; j < NTN; ++j)
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, vb, FBN + (j * NQN + qn) * 2 + pt);
+    }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const char* p = X + act_off(16 * mt + li, 4 * q + g);
+      const h8 bh = *(const h8*)p, bl = *(const h8*)(p + 256);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[mt][j] = mfma3(a0[j][0], a0[j][1], bh, bl, acc[mt][j]);
+    }
+    // rotate (only the o-tiles each chunk holds)
+    const int nt1 = q + 1 < NQ ? 2 : NTN;   // a1 holds chunk q + 1 of this matrix or chunk 0 of the next
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      if (j < nt1) { a0[j][0] = a1[j][0]; a0[j][1] = a1[j][1]; }
+    const int nt2 = q + 2 < NQ ? 2 : NTN;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      if (j < nt2 && (q + 2 <= NQ || OUT2)) { a1[j][0] = an[j][0]; a1[j][1] = an[j][1]; }
   }
 }
 
@@ -256,10 +326,13 @@ __device__ __forceinline__ void init_bias(f32x4 (&acc)[4][2], int ot0, const flo
 
 __device__ unsigned long long g_phase[6];
 
-// Gather of one tile by the 256 V-threads (vt): row r = vt >> 2 (sample r >> 3, neighbour r & 7),
-// quarter p = vt & 3 of the row. Split in two: ws_gather_load issues the neighbour-record and
-// view-direction loads (a segment ahead), ws_gather writes the posenc hi/lo into PE (X layout,
-// chunks 0..7) and the row records into sTo/sRow/sV.
+// Gather of one tile: lane r of every wave owns MLP row r (sample r >> 3, neighbour r & 7), and
+// wave p computes quarter p of the row's posenc columns -- the quarter is wave-uniform, so the
+// argument indices, frequency scales and which-coordinate choices below are compile-time
+// constants (one instantiation per wave) instead of per-lane selects. Split in two:
+// ws_gather_load issues the neighbour-record and view-direction loads (a segment ahead),
+// ws_gather writes the posenc hi/lo into PE (X layout, chunks 0..7) and the row records into
+// sTo/sRow/sV.
 struct GatherRegs {
   float4 a0, a1, a2, a3, b0, b1;
   float vv;
@@ -268,12 +341,18 @@ struct GatherRegs {
 // Loads are unconditional (clamped indices; invalid rows read row 0 and are discarded later):
 // a load under a divergent branch makes the compiler drain vmcnt(0) at the join, which would
 // expose the latency of every load in flight.
-__device__ __forceinline__ void ws_gather_load(int vt, int nb, int ray, GatherRegs& G,
+__device__ __forceinline__ void ws_gather_load(int p, int nb, int ray, GatherRegs& G,
                                                const float4* __restrict__ recA, const float4* __restrict__ recB,
                                                const float* __restrict__ viewdirs,
                                                const float* __restrict__ vemb_const) {
-  const int r = vt >> 2, p = vt & 3, k = r & 7;
+  const int k = threadIdx.x & 7;
   const size_t n = (size_t)max(nb, 0);
+#ifdef APN_H3_PROBE_NOREC   // timing probe only (wrong results): no neighbour-record loads
+  G.a0 = make_float4(0.f, 0.f, 0.f, 1.f + (float)n);
+  G.a1 = G.a2 = G.a3 = G.b0 = G.b1 = make_float4(0.01f, 0.f, 0.f, 0.f);
+  G.vv = 0.f;
+  return;
+#endif
   G.a0 = recA[4 * n + 0];
   G.a1 = recA[4 * n + 1];
   G.a2 = recA[4 * n + 2];
@@ -285,22 +364,22 @@ __device__ __forceinline__ void ws_gather_load(int vt, int nb, int ray, GatherRe
   G.vv = vemb_const ? 0.f : viewdirs[3 * (size_t)ray + (e < 3 ? e : ee >> 2)];
 }
 
-__device__ __forceinline__ void ws_gather(int vt, int nb, float4 q, const GatherRegs& G, char* __restrict__ PE,
-                                          float* __restrict__ sTo, float* __restrict__ sRow, float* __restrict__ sV,
-                                          const float* __restrict__ vemb_const) {
-  const int r = vt >> 2, p = vt & 3, s = r >> 3, k = r & 7;
+template <int P>
+__device__ __forceinline__ void ws_gather_q(int nb, float4 q, const GatherRegs& G, char* __restrict__ PE,
+                                            float* __restrict__ sTo, float* __restrict__ sRow,
+                                            float* __restrict__ sV, const float* __restrict__ vemb_const) {
+  const int r = threadIdx.x & 63, s = r >> 3, k = r & 7;
   char* xr = PE + r * XB;
-  const int c_sin = (2 * p) ^ (r & 15), c_cos = (2 * p + 1) ^ (r & 15);
+  const int c_sin = (2 * P) ^ (r & 15), c_cos = (2 * P + 1) ^ (r & 15);
   if (nb >= 0) {
     const float4 a0 = G.a0, a1 = G.a1, a2 = G.a2, a3 = G.a3;
     const float dx = q.x - a0.x, dy = q.y - a0.y, dz = q.z - a0.z;
-    const float rc0 = (a1.x * dx + a1.y * dy) + a1.z * dz;
-    const float rc1 = (a1.w * dx + a2.x * dy) + a2.y * dz;
-    const float rc2 = (a2.z * dx + a2.w * dy) + a3.x * dz;
-    const float tn = (dx * dx + dy * dy) + dz * dz;
-    if (p == 0) {
-      sTo[r] = tn;
-    } else if (p == 1) {
+    const float rc[3] = {(a1.x * dx + a1.y * dy) + a1.z * dz, (a1.w * dx + a2.x * dy) + a2.y * dz,
+                         (a2.z * dx + a2.w * dy) + a3.x * dz};
+    if constexpr (P == 0) {
+      sTo[r] = (dx * dx + dy * dy) + dz * dz;
+    } else if constexpr (P == 1) {
+      const float tn = (dx * dx + dy * dy) + dz * dz;
       float* rw = sRow + 8 * r;
       rw[0] = expf(-(tn * tn) / a0.w);   // temporalpoints.py:461 (to_nn is already squared)
       rw[1] = a3.y;
@@ -310,15 +389,13 @@ __device__ __forceinline__ void ws_gather(int vt, int nb, float4 q, const Gather
     f32x4 sv0, sv1, cv0, cv1;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int aa = p + 4 * j;
+      const int aa = P + 4 * j;   // reference argument index a = 10 i + f (apn_mlp_layout.h pe_col_to_ref)
       float sv, cv;
       if (aa < 30) {
-        const int ci = aa / 10;
-        const float v = (ci == 0 ? rc0 : (ci == 1 ? rc1 : rc2)) * (float)(1 << (aa - 10 * ci));
-        sincos_pe(v, sv, cv);
+        sincos_pe(rc[aa / 10] * (float)(1 << (aa % 10)), sv, cv);
       } else {
-        sv = p == 2 ? rc0 : rc2;
-        cv = p == 2 ? rc1 : 0.f;
+        sv = P == 2 ? rc[0] : rc[2];
+        cv = P == 2 ? rc[1] : 0.f;
       }
       if (j < 4) { sv0[j] = sv; cv0[j] = cv; } else { sv1[j - 4] = sv; cv1[j - 4] = cv; }
     }
@@ -329,7 +406,7 @@ __device__ __forceinline__ void ws_gather(int vt, int nb, float4 q, const Gather
     *(h8*)(xr + (c_sin << 4) + 256) = __builtin_shufflevector(ls0, ls1, 0, 1, 2, 3, 4, 5, 6, 7);
     *(h8*)(xr + (c_cos << 4)) = __builtin_shufflevector(hc0, hc1, 0, 1, 2, 3, 4, 5, 6, 7);
     *(h8*)(xr + (c_cos << 4) + 256) = __builtin_shufflevector(lc0, lc1, 0, 1, 2, 3, 4, 5, 6, 7);
-    const int e = 4 * k + p;   // view embedding element e of this sample
+    const int e = 4 * k + P;   // view embedding element e of this sample
     float v = 0.f;
     if (e < 27) {
       if (vemb_const) {
@@ -348,12 +425,27 @@ __device__ __forceinline__ void ws_gather(int vt, int nb, float4 q, const Gather
     *(h8*)(xr + (c_sin << 4) + 256) = z;
     *(h8*)(xr + (c_cos << 4)) = z;
     *(h8*)(xr + (c_cos << 4) + 256) = z;
-    sV[s * 32 + 4 * k + p] = 0.f;
-    if (p == 0) {
+    sV[s * 32 + 4 * k + P] = 0.f;
+    if constexpr (P == 0) {
       sTo[r] = 1.f;
-    } else if (p == 1) {
+    } else if constexpr (P == 1) {
       for (int c = 0; c < 8; ++c) sRow[8 * r + c] = 0.f;
     }
+  }
+}
+
+// Wave-uniform dispatch (p = the SGPR wave index).
+__device__ __forceinline__ void ws_gather(int p, int nb, float4 q, const GatherRegs& G, char* __restrict__ PE,
+                                          float* __restrict__ sTo, float* __restrict__ sRow, float* __restrict__ sV,
+                                          const float* __restrict__ vemb_const) {
+#ifdef APN_COUNT_ONE_QUARTER
+  p = 0;
+#endif
+  switch (p) {
+    case 0: ws_gather_q<0>(nb, q, G, PE, sTo, sRow, sV, vemb_const); break;
+    case 1: ws_gather_q<1>(nb, q, G, PE, sTo, sRow, sV, vemb_const); break;
+    case 2: ws_gather_q<2>(nb, q, G, PE, sTo, sRow, sV, vemb_const); break;
+    default: ws_gather_q<3>(nb, q, G, PE, sTo, sRow, sV, vemb_const); break;
   }
 }
 
@@ -387,6 +479,7 @@ __device__ __forceinline__ void mlp_tiles(
   // buffer store: no extra 64-bit pointer live across the tile loop)
   const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(wbuf + OFF_H16), 0, H_TOTAL * 2 + 4, 0x00020000);
   const int ot0 = 2 * wid;
+  const int vb = (wid * FR_WAVE * FRAG_HALVES + lane * 8) * 2;   // this wave's fragment block + lane
   // per-matrix weight scales 2^s (W1E, W2, W3, W4, WH), kept in LDS with their inverses (exact:
   // powers of two) and read where used, so they hold no registers across the tile loop
   const float* const scp = wbuf + OFF_SCALE;
@@ -428,10 +521,10 @@ __device__ __forceinline__ void mlp_tiles(
   float4 pf_q = make_float4(0.f, 0.f, 0.f, 0.f);
   auto fetch = [&](int tl) {
     const int tc = min(tl, t_end - 1);
-    const int gs = tc * TS + (tid >> 5);
+    const int gs = tc * TS + (lane >> 3);   // this lane's gather row: sample lane >> 3, neighbour lane & 7
     const int gc = min(gs, nS - 1);
     pf_ok = tl < t_end && gs < nS;
-    pf_nb = s_nbr[(size_t)gc * 8 + ((tid >> 2) & 7)];
+    pf_nb = s_nbr[(size_t)gc * 8 + (lane & 7)];
     pf_q = s_pos[gc];
     pf_ray = s_ray[gc];
 #pragma unroll
@@ -443,13 +536,34 @@ __device__ __forceinline__ void mlp_tiles(
   };
   int tile = t_beg + blockIdx.x / nx;
   if (tile < t_end) fetch(tile);
-  h8 a[2][2];   // carried A-fragment prefetch (chunk 0 of the next weight matrix)
+  h8 a[2][2];    // carried A-fragment prefetch (chunk 0 of the next weight matrix)
+  h8 a1[2][2];   // and chunk 1 (two-deep prefetch of the OCC = 3 build)
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int pt = 0; pt < 2; ++pt) a[j][pt] = frag(rs, H_W1E, 2, ot0 + j, 0, pt);
-  int prev_s0 = -1;
+    for (int pt = 0; pt < 2; ++pt) a[j][pt] = frag(rs, vb, FR_W1E + j * 4 + pt);
+  // layer-1 accumulators = P[nbr] (global -> VGPR; validity pok: rows past the last sample read
+  // row 0, zeroed before layer 1)
+  f32x4 acc[4][2];
+  bool pok[4];
+  auto load_p = [&]() {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      pok[mt] = pf_pok[mt];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+#ifdef APN_H3_PROBE_NOP   // timing probe only (wrong results): no P-row gather
+        const float4 v = make_float4(0.f, 0.f, 0.f, pf_pn[mt] < 0 ? 1.f : 0.f);
+#else
+        const float4 v = pproj[(size_t)max(pf_pn[mt], 0) * (FEAT / 4) + 4 * (ot0 + j) + g];
+#endif
+        acc[mt][j] = f32x4{v.x, v.y, v.z, v.w};
+      }
+    }
+  };
   GatherRegs gregs;
+  int prev_s0 = -1;
+  bool range_bad = false;
   for (; tile < t_end; tile += per_xcd) {
     const int s0 = tile * TS;
     if (TIMED) { tk = clock64(); ph[4] += 1; }
@@ -457,18 +571,12 @@ __device__ __forceinline__ void mlp_tiles(
     // then the layer-1 accumulators = P[nbr] (global -> VGPR), then the next tile's indices
     const int nb = pf_ok ? pf_nb : -1;
     const float4 q = pf_q;
-    ws_gather_load(tid, nb, pf_ray, gregs, recA, recB, viewdirs, vemb_const);
-    f32x4 acc[4][2];
-    bool pok[4];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      pok[mt] = pf_pok[mt];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const float4 v = pproj[(size_t)max(pf_pn[mt], 0) * (FEAT / 4) + 4 * (ot0 + j) + g];
-        acc[mt][j] = f32x4{v.x, v.y, v.z, v.w};
-      }
-    }
+    // loads in consumption order -- the gather's records, then the layer-1 accumulators = P[nbr],
+    // then the next tile's indices. vmcnt is an in-order counter: a wait for a load also waits for
+    // every load issued before it, so loads issued earlier (e.g. the next tile's P after layer 4,
+    // measured +1.6 %) hold up the weight-fragment waits in between.
+    ws_gather_load(wid, nb, pf_ray, gregs, recA, recB, viewdirs, vemb_const);
+    load_p();
     if (SCALED) {   // layer-1 accumulators in the W1E scale: 2^s1 P
       const float sc1 = sW[SW_SC];
 #pragma unroll
@@ -478,7 +586,7 @@ __device__ __forceinline__ void mlp_tiles(
     }
     fetch(tile + per_xcd);
     // ------------------------------------------------ gather + posenc + direct-blend terms
-    ws_gather(tid, nb, q, gregs, X0, sTo, sRow, sV, vemb_const);
+    ws_gather(wid, nb, q, gregs, X0, sTo, sRow, sV, vemb_const);
     __syncthreads();
     APN_PHASE(0)
     // ------------------------------------------------ outputs of the previous tile
@@ -495,29 +603,35 @@ __device__ __forceinline__ void mlp_tiles(
 #pragma unroll
       for (int k = 0; k < 8; ++k) sIdw[tid * 8 + k] = w[k] * inv;
     }
+    if (s0 + TS > nS) {   // the last tile only (block-uniform): rows past the last sample loaded P rows of point 0
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)   // rows past the last sample: P rows of point 0 were loaded
+      for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        if (!pok[mt]) acc[mt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < 2; ++j)
+          if (!pok[mt]) acc[mt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
     // ------------------------------------------------ feat_net: 4 x (Linear + LeakyReLU)
-    layer_mfma<2, 4, 2, PP>(X0, rs, H_W1E, ot0, H_W2, ot0, acc, a);
+    if constexpr (PP || !kD2) layer_mfma<2, 4, 2, FR_W1E, FR_W2, PP>(X0, rs, vb, acc, a);
+    else layer_mfma_d2<2, 4, 2, FR_W1E, FR_W2, false, true>(X0, rs, vb, acc, a, a1);
     if (!PP) __syncthreads();
     store_act(X1, ot0, sW + SW_B1, acc, SCALED, SCALED ? sW[SW_DS + 0] : 1.f);
     __syncthreads();
     APN_PHASE(1)
     init_bias(acc, ot0, sW + SW_B2);
-    layer_mfma<4, 4, 2, PP>(X1, rs, H_W2, ot0, H_W3, ot0, acc, a);
+    if constexpr (PP || !kD2) layer_mfma<4, 4, 2, FR_W2, FR_W3, PP>(X1, rs, vb, acc, a);
+    else layer_mfma_d2<4, 4, 2, FR_W2, FR_W3, true, true>(X1, rs, vb, acc, a, a1);
     if (!PP) __syncthreads();
     store_act(X0, ot0, nullptr, acc, SCALED, SCALED ? sW[SW_DS + 1] : 1.f);
     __syncthreads();
     init_bias(acc, ot0, sW + SW_B3);
-    layer_mfma<4, 4, 2, PP>(X0, rs, H_W3, ot0, H_W4, ot0, acc, a);
+    if constexpr (PP || !kD2) layer_mfma<4, 4, 2, FR_W3, FR_W4, PP>(X0, rs, vb, acc, a);
+    else layer_mfma_d2<4, 4, 2, FR_W3, FR_W4, true, true>(X0, rs, vb, acc, a, a1);
     if (!PP) __syncthreads();
     store_act(X1, ot0, nullptr, acc, SCALED, SCALED ? sW[SW_DS + 2] : 1.f);
     __syncthreads();
     init_bias(acc, ot0, sW + SW_B4);
-    layer_mfma<4, 5, 1, PP>(X1, rs, H_W4, ot0, H_WH, wid, acc, a);
+    if constexpr (PP || !kD2) layer_mfma<4, 5, 1, FR_W4, FR_WH, PP>(X1, rs, vb, acc, a);
+    else layer_mfma_d2<4, 5, 1, FR_W4, FR_WH, true, true>(X1, rs, vb, acc, a, a1);
     if (!PP) __syncthreads();
     // layer-4 output lrelu(acc) (bias in the accumulator) as fp32 rows (for the IDW sum)
 #pragma unroll
@@ -528,6 +642,7 @@ __device__ __forceinline__ void mlp_tiles(
         *(f32x4*)(X0 + out32_off(16 * mt + li, o0 >> 2)) =
             lrelu4(SCALED ? acc[mt][j] * sW[SW_DS + 3] : acc[mt][j]);
     }
+
     __syncthreads();
     APN_PHASE(2)
     // ------------------------------------------------ IDW sum (temporalpoints.py:493-494), density head
@@ -539,17 +654,18 @@ __device__ __forceinline__ void mlp_tiles(
         const f32x4 v = *(const f32x4*)(X0 + out32_off(8 * s + k, oq));
         const float w = sIdw[8 * s + k];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) h[r] = h[r] + w * v[r];
+        for (int r = 0; r < 4; ++r) h[r] = fmaf(w, v[r], h[r]);
       }
       // densitynet Linear(128 -> 1) (tineuvox.py:158) over this thread's 4 features, then the half-wave
       const f32x4 wd = *(const f32x4*)(sW + SW_WD + 4 * oq);
       float d = ((h[0] * wd[0] + h[1] * wd[1]) + h[2] * wd[2]) + h[3] * wd[3];
       // the head's h input in the head's column scale (scaled mode): h' = h 2^(b-a), exact
       if (SCALED) h = h * sW[SW_HSC];
-      // range guard (see the header comment) on the last values split: false for NaN too
+      // range guard (see the header comment) on the last values split: false for NaN too. The
+      // flag store waits for the end of the tile loop (a store under a divergent branch inside the
+      // loop makes every later vmcnt wait conservative)
 #ifndef APN_H3_AB_NO_GUARD   // A/B builds only (tools/ab_build.sh): the guard's cost
-      if (!(fmaxf(fmaxf(fabsf(h[0]), fabsf(h[1])), fmaxf(fabsf(h[2]), fabsf(h[3]))) <= H3_RANGE))
-        __builtin_amdgcn_raw_buffer_store_b32(1, rs, 0, H_TOTAL * 2, 0);   // the range flag (OFF_FLAG)
+      range_bad |= !(fmaxf(fmaxf(fabsf(h[0]), fabsf(h[1])), fmaxf(fabsf(h[2]), fabsf(h[3]))) <= H3_RANGE);
 #endif
       d += __shfl_xor(d, 16, 64);
       d += __shfl_xor(d, 8, 64);
@@ -557,8 +673,10 @@ __device__ __forceinline__ void mlp_tiles(
       d += __shfl_xor(d, 2, 64);
       d += __shfl_xor(d, 1, 64);
       if (oq == 0) {  // Raw2Alpha (render_utils_kernel.cu:357-369)
+        // (1 + e)^-interval as exp2(-interval log2(1 + e)) on v_log_f32 / v_exp_f32 (1 ulp each; the
+        // alpha error stays below 1e-7 absolute: |y| 2^-|y| <= 0.53 scales the exponent's error)
         const float e = expf((d + sW[SW_BD]) + shift);
-        sOut[12 * s + 3] = 1.f - powf(1.f + e, -interval);
+        sOut[12 * s + 3] = 1.f - __builtin_amdgcn_exp2f(-interval * __builtin_amdgcn_logf(1.f + e));
       }
       // head input row s: [h (128) | view embedding (27) | 0] as hi/lo halves
       char* hr = HX + s * HB;
@@ -600,31 +718,68 @@ __device__ __forceinline__ void mlp_tiles(
     {
       const int o0 = 16 * wid + 4 * g;
       f32x4 ah = *(const f32x4*)(sW + SW_BH + o0);   // views_linears.0 (folded) bias
-      const char* hr = HX + li * HB;
-      const h8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+      // B columns 8..15 of the 16-wide MFMA tile repeat rows 0..7: their outputs are never read
+      // (each output column depends on its own B column only), so no zero fill or select
+      const char* hr = HX + (li & (TS - 1)) * HB;
+      if constexpr (PP || !kD2) {
 #pragma unroll
-      for (int q = 0; q < KV / 32; ++q) {
-        h8 an[2][2];
-        if (q + 1 < KV / 32) {
+        for (int q = 0; q < KV / 32; ++q) {
+          h8 an[2][2];
+          if (q + 1 < KV / 32) {
 #pragma unroll
-          for (int pt = 0; pt < 2; ++pt) an[0][pt] = frag(rs, H_WH, KV / 32, wid, q + 1, pt);
-        } else {  // chunk 0 of the next tile's layer 1
+            for (int pt = 0; pt < 2; ++pt) an[0][pt] = frag(rs, vb, FR_WH + (q + 1) * 2 + pt);
+          } else {  // chunk 0 of the next tile's layer 1
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
+            for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, H_W1E, 2, ot0 + j, 0, pt);
+              for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, vb, FR_W1E + j * 4 + pt);
+          }
+          const h8 bh = *(const h8*)(hr + 16 * (4 * q + g));
+          const h8 bl = *(const h8*)(hr + HLO + 16 * (4 * q + g));
+          ah = mfma3(a[0][0], a[0][1], bh, bl, ah);
+          if (q + 1 < KV / 32) {
+            a[0][0] = an[0][0];
+            a[0][1] = an[0][1];
+          } else {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              a[j][0] = an[j][0];
+              a[j][1] = an[j][1];
+            }
+          }
         }
-        const h8 bh = li < TS ? *(const h8*)(hr + 16 * (4 * q + g)) : z;
-        const h8 bl = li < TS ? *(const h8*)(hr + HLO + 16 * (4 * q + g)) : z;
-        ah = mfma3(a[0][0], a[0][1], bh, bl, ah);
-        if (q + 1 < KV / 32) {
-          a[0][0] = an[0][0];
-          a[0][1] = an[0][1];
-        } else {
+      } else {
+        // two-deep: a / a1 hold head chunks 0 / 1 (layer 4 carried them); chunk q + 2 in flight; the
+        // next tile's W1E chunk 0 is the last prefetch (one deep across the gather, the register peak)
+        constexpr int NQH = KV / 32;
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            a[j][0] = an[j][0];
-            a[j][1] = an[j][1];
+        for (int q = 0; q < NQH; ++q) {
+          h8 an[2][2];
+          if (q + 2 < NQH) {
+#pragma unroll
+            for (int pt = 0; pt < 2; ++pt) an[0][pt] = frag(rs, vb, FR_WH + (q + 2) * 2 + pt);
+          } else if (q + 2 == NQH) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+              for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, vb, FR_W1E + j * 4 + pt);
+          }
+          const h8 bh = *(const h8*)(hr + 16 * (4 * q + g));
+          const h8 bl = *(const h8*)(hr + HLO + 16 * (4 * q + g));
+          ah = mfma3(a[0][0], a[0][1], bh, bl, ah);
+          // rotate: a <- a1 (chunk q + 1, or the W1E chunk 0 with both o-tiles), a1 <- an
+          if (q + 2 <= NQH) {
+            const int nt1 = q + 1 < NQH ? 1 : 2;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              if (j < nt1) { a[j][0] = a1[j][0]; a[j][1] = a1[j][1]; }
+            const int nt2 = q + 2 < NQH ? 1 : 2;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              if (j < nt2) { a1[j][0] = an[j][0]; a1[j][1] = an[j][1]; }
+          } else {   // q = NQH - 1: a1 holds the W1E chunk 0
+#pragma unroll
+            for (int j = 0; j < 2; ++j) { a[j][0] = a1[j][0]; a[j][1] = a1[j][1]; }
           }
         }
       }
@@ -664,6 +819,7 @@ __device__ __forceinline__ void mlp_tiles(
   __syncthreads();
   if (prev_s0 >= 0 && tid < TS * 3 && prev_s0 + tid / 3 < nS)
     out[(size_t)prev_s0 * 3 + tid] = *(const float4*)(sOut + 4 * tid);
+  if (range_bad) __builtin_amdgcn_raw_buffer_store_b32(1, rs, 0, H_TOTAL * 2, 0);   // the range flag (OFF_FLAG)
 }
 
 // One instantiation per weight-scale mode (separate register allocation); apn_point_mlp launches
@@ -769,8 +925,11 @@ __global__ void k_split_weights(float* __restrict__ wbuf) {
   const int nq = mat == 0 ? 2 : (mat == 4 ? 5 : 4);
   const int lane = i & 63, q = (i >> 6) % nq, ot = (i >> 6) / nq;
   const int o = 16 * ot + (lane & 15), k0 = 32 * q + 8 * (lane >> 4);
-  const int hbase = mat == 0 ? H_W1E : (mat == 1 ? H_W2 : (mat == 2 ? H_W3 : (mat == 3 ? H_W4 : H_WH)));
-  _Float16* dst = (_Float16*)(wbuf + OFF_H16) + hbase + (size_t)((ot * nq + q) * 2) * FRAG_HALVES + lane * 8;
+  // wave-major block (apn_mlp_layout.h): W1E..W4 o-tile ot -> wave ot / 2, j = ot & 1; head -> wave ot
+  const int fb = mat == 0 ? FR_W1E : (mat == 1 ? FR_W2 : (mat == 2 ? FR_W3 : (mat == 3 ? FR_W4 : FR_WH)));
+  const int wave = mat == 4 ? ot : ot >> 1, j16 = mat == 4 ? 0 : ot & 1;
+  const int fidx = wave * FR_WAVE + fb + (j16 * nq + q) * 2;
+  _Float16* dst = (_Float16*)(wbuf + OFF_H16) + (size_t)fidx * FRAG_HALVES + lane * 8;
   const float sc_mat = wbuf[OFF_SCALE + mat], sc_view = wbuf[OFF_SCALE + 5];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {

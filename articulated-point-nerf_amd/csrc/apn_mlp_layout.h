@@ -32,17 +32,22 @@ constexpr int OFF_W1F = OFF_BV2 + 4;              // [128][128] feat_net.0 colum
 constexpr int W_F32_TOTAL = OFF_W1F + 128 * 128;
 
 // fp16 hi/lo region (written by apn_mlp_split_weights from the fp32 region): every matrix
-// W [O][K] in MFMA fragment order -- for o-tile ot (16 rows), k-chunk q (32 columns), part
+// W [O][K] in MFMA fragments -- for o-tile ot (16 rows), k-chunk q (32 columns), part
 // (0 = hi = fp16(w), 1 = lo = fp16(w - hi)), lane l: 8 halves W[16 ot + (l & 15)][32 q + 8 (l >> 4) + j].
 // One 16-byte load per lane fetches a whole 1 KB fragment, coalesced.
+// Wave-major: wave w of the kernel's workgroup owns o-tiles 2w, 2w+1 of W1E..W4 (j = ot & 1) and
+// o-tile w of the head, and its 66 fragments are one contiguous block, fragment index
+// FR_<matrix> + (j nq + q) 2 + part inside it -- the kernel's load offsets are then a per-wave
+// VGPR base plus compile-time constants (no wave-dependent scalar offsets to keep live).
 constexpr int OFF_H16 = (W_F32_TOTAL + 3) & ~3;   // float offset (16-B aligned)
 constexpr int FRAG_HALVES = 64 * 8;               // one fragment part
-constexpr int H_W1E = 0;                          // halves, relative to OFF_H16
-constexpr int H_W2 = H_W1E + 8 * 2 * 2 * FRAG_HALVES;
-constexpr int H_W3 = H_W2 + 8 * 4 * 2 * FRAG_HALVES;
-constexpr int H_W4 = H_W3 + 8 * 4 * 2 * FRAG_HALVES;
-constexpr int H_WH = H_W4 + 8 * 4 * 2 * FRAG_HALVES;
-constexpr int H_TOTAL = H_WH + 4 * 5 * 2 * FRAG_HALVES;
+constexpr int FR_W1E = 0;                         // fragment index inside a wave's block
+constexpr int FR_W2 = FR_W1E + 2 * 2 * 2;
+constexpr int FR_W3 = FR_W2 + 2 * 4 * 2;
+constexpr int FR_W4 = FR_W3 + 2 * 4 * 2;
+constexpr int FR_WH = FR_W4 + 2 * 4 * 2;
+constexpr int FR_WAVE = FR_WH + 5 * 2;            // 66 fragments per wave
+constexpr int H_TOTAL = 4 * FR_WAVE * FRAG_HALVES;   // halves, relative to OFF_H16
 // Range flag (one int32, 4 floats reserved): the fp16-split kernel sets it when a value it must
 // split into fp16 hi/lo halves is out of the fp16 range (or not finite); the FP32 MFMA kernel
 // then re-runs the launch (apn_point_mlp). Sticky until the weights are re-split

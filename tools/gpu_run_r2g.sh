@@ -1,0 +1,4 @@
+source tools/gpu_steps.sh
+export AB_STEPS=10
+step ab 900 bash tools/ab.sh "APN_AB=cur" "APN_HIP_LIB=ab/l1w/libapn_hip.so" "APN_HIP_LIB=ab/nop/libapn_hip.so" "APN_HIP_LIB=ab/both/libapn_hip.so" "APN_MLP_VARIANT=3"
+grep -h "mlp phases" gpurun_out/ab/run5.err || true
