@@ -941,6 +941,139 @@ __device__ __forceinline__ void scan_ball_flat2(const GridParams& g, const int* 
   }
 }
 
+// ---- mode 9: pass B on a second, anisotropic grid. A hard query's r-ball scan on the fine grid
+// (h = r/8) walks ~220 (z, y) rows but reads only ~80 points: rows dominate. The second grid keeps
+// the fine x cells (row chords stay tight) and merges AG_F x AG_F fine cells in y and z, so the
+// r-ball has ~AG_F^2 fewer rows, each covering AG_F^2 fine rows. Its cell boundaries coincide with
+// fine ones (AG_F a power of two: the products below are exact), and each point's cell is derived
+// from its fine cell, so the cell-box distance bounds of the scan hold exactly as on the fine grid.
+// Built per frame from the fine grid's sorted points (atomic counting sort: the order inside a
+// cell is arbitrary, the top-K is not -- distance then index).
+struct AGrid {
+  float ox, oy, oz, hx;
+  float hy, hz, ihx, ihy;
+  float ihz, r, r2, pad0;
+  int dx, dy, dz, nf;
+};
+
+__global__ void k_agrid_params(const GridParams* __restrict__ gp, int f, AGrid* __restrict__ ag) {
+  if (threadIdx.x != 0) return;
+  const GridParams g = *gp;
+  AGrid a;
+  a.ox = g.ox; a.oy = g.oy; a.oz = g.oz;
+  a.hx = g.h; a.hy = a.hz = g.h * (float)f;
+  a.ihx = g.inv_h; a.ihy = a.ihz = g.inv_h / (float)f;
+  a.r = g.r; a.r2 = g.r2; a.pad0 = 0.f;
+  a.dx = g.dx; a.dy = (g.dy + f - 1) / f; a.dz = (g.dz + f - 1) / f;
+  a.nf = a.dx * a.dy * a.dz;
+  *ag = a;
+}
+
+__global__ void k_agrid_count(const float4* __restrict__ sorted, int64_t N, const GridParams* __restrict__ gp, int f,
+                              int* __restrict__ counts, int* __restrict__ pcell) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const GridParams g = *gp;
+  const float4 P = sorted[i];
+  const int cx = cell_coord(P.x, g.ox, g.inv_h, g.dx);
+  const int cy = cell_coord(P.y, g.oy, g.inv_h, g.dy) / f;
+  const int cz = cell_coord(P.z, g.oz, g.inv_h, g.dz) / f;
+  const int dy2 = (g.dy + f - 1) / f;
+  const int cell = (cz * dy2 + cy) * g.dx + cx;
+  pcell[i] = cell;
+  atomicAdd(counts + cell, 1);
+}
+
+__global__ void k_agrid_scatter(const float4* __restrict__ sorted, int64_t N, const int* __restrict__ pcell,
+                                const int* __restrict__ cell_start, int* __restrict__ cursor,
+                                float4* __restrict__ sorted2) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const int cell = pcell[i];
+  sorted2[cell_start[cell] + atomicAdd(cursor + cell, 1)] = sorted[i];
+}
+
+// scan_ball_flat2 on the anisotropic grid (cell sides hx, hy, hz): the same lock-step row/point
+// state machine, nearest-first slabs, running K-th-best culling with 1e-4 slack.
+// PTS points per point step (2 or 4).
+template <int K, bool STATS = false, int PTS = 2>
+__device__ __forceinline__ void scan_ball_aniso(const AGrid& g, const int* __restrict__ cell_start,
+                                                const float4* __restrict__ sorted, float qx, float qy, float qz,
+                                                float R2, float (&bd)[K], int (&bi)[K], unsigned* ctr = nullptr) {
+  const float R = sqrtf(R2) * 1.0001f;
+  const int z0 = max((int)floorf((qz - R - g.oz) * g.ihz), 0), z1 = min((int)floorf((qz + R - g.oz) * g.ihz), g.dz - 1);
+  const int y0 = max((int)floorf((qy - R - g.oy) * g.ihy), 0), y1 = min((int)floorf((qy + R - g.oy) * g.ihy), g.dy - 1);
+  const int fz = min(max((int)floorf((qz - g.oz) * g.ihz), z0), z1);
+  const int fy = min(max((int)floorf((qy - g.oy) * g.ihy), y0), y1);
+  const int nz = (z1 < z0 || y1 < y0) ? 0 : 2 * max(fz - z0, z1 - fz) + 1;
+  const int ny = 2 * max(fy - y0, y1 - fy) + 1;
+  int iz = -1, iy = 0, nyz = 0;
+  int z = 0;
+  float dz2 = 0.f;
+  int b = 0, e = 0, pb = 0, pe = 0;
+  bool pend = false;
+  for (;;) {
+    const bool has_pts = b < e;
+    const bool rows_left = iz < nz && (iy < nyz || iz + 1 < nz);
+    if (!has_pts && !pend && !rows_left) break;
+    if (STATS) ctr[has_pts ? 1 : 0]++;
+    if (has_pts) {
+      float4 P[PTS];
+      int id[PTS];
+#pragma unroll
+      for (int u = 0; u < PTS; ++u) {
+        P[u] = sorted[min(b + u, e - 1)];
+        id[u] = __float_as_int(P[u].w);
+      }
+#pragma unroll
+      for (int u = 0; u < PTS; ++u) asm("" : "+v"(id[u]));
+#pragma unroll
+      for (int u = 0; u < PTS; ++u) {
+        const float dx = qx - P[u].x, dy = qy - P[u].y, dz = qz - P[u].z;
+        const float d = (dx * dx + dy * dy) + dz * dz;
+        if (b + u < e && d <= g.r2) knn_insert_unique<K>(d, id[u], bd, bi);
+      }
+      b += PTS;
+      if (b > e) b = e;
+    } else {
+      if (pend) { b = pb; e = pe; pend = false; }
+      const float tau = fminf(bd[K - 1], R2) * 1.0001f;
+      if (iy >= nyz) {
+        ++iz;
+        iy = 0;
+        nyz = 0;
+        if (iz < nz) {
+          z = fz + nf_offset(iz);
+          if (z >= z0 && z <= z1) {
+            dz2 = slab_d2(qz, g.oz, g.hz, z, z);
+            if (dz2 <= tau) {
+              const int my = (int)floorf(sqrtf(tau - dz2) * g.ihy * 1.0001f) + 1;
+              nyz = min(2 * my + 1, ny);
+            }
+          }
+        }
+      } else {
+        const int y = fy + nf_offset(iy);
+        ++iy;
+        if (y >= y0 && y <= y1) {
+          const float dyz2 = dz2 + slab_d2(qy, g.oy, g.hy, y, y);
+          if (dyz2 <= tau) {
+            const float w = sqrtf(tau - dyz2) * 1.0001f;
+            const int x0 = max((int)floorf((qx - w - g.ox) * g.ihx), 0);
+            const int x1 = min((int)floorf((qx + w - g.ox) * g.ihx), g.dx - 1);
+            if (x0 <= x1) {
+              const int row = (z * g.dy + y) * g.dx;
+              pb = cell_start[row + x0];
+              pe = cell_start[row + x1 + 1];
+              pend = true;
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
 // ---- mode 6: per-cell rejection bound. For every fine cell C holding a candidate, U(C) = number
 // of points in cells whose box lies within r of C's box -- an upper bound on the points within r of
 // ANY query in C (also of a query just outside the grid, clamped into C: its distance to a point
@@ -1037,12 +1170,14 @@ __global__ __launch_bounds__(KNN_THREADS) void k_cell_bound3(const GridParams* _
 
 // Pass A of mode 8: reject on u1 < 8; the r/4 ball (flat scan) only where u4 >= 8; the rest go to
 // the hard list tagged with their first useful level (r/2 if u2 >= 8, else r).
+template <bool ANISO>
 __global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_a8(
     const float4* __restrict__ q_pos, const int* __restrict__ cand, const int* __restrict__ n_cand_dev,
     const GridParams* __restrict__ gp, const int* __restrict__ cell_start, const float4* __restrict__ sorted,
     const int* __restrict__ ccell, const int* __restrict__ u1, const int* __restrict__ u2,
     const int* __restrict__ u4, int* __restrict__ flag, int* __restrict__ t_nbr, int* __restrict__ hard,
-    int* __restrict__ n_hard, int* __restrict__ hard_r, int* __restrict__ n_hard_r) {
+    int* __restrict__ n_hard, int* __restrict__ hard_r, int* __restrict__ n_hard_r, const AGrid* __restrict__ agp,
+    const int* __restrict__ cell_start2, const float4* __restrict__ sorted2) {
   const int nc = *n_cand_dev;
   const int c = blockIdx.x * KNN_THREADS + threadIdx.x;
   const GridParams g = *gp;
@@ -1060,7 +1195,8 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_a8(
 #pragma unroll
         for (int k = 0; k < KNN_K; ++k) { bd[k] = INFINITY; bi[k] = 0x7fffffff; }
         const float R2 = coarse ? g.r2 : 0.0625f * g.r2;
-        scan_ball_flat2<KNN_K>(g, cell_start, sorted, q.x, q.y, q.z, R2, bd, bi);
+        if (ANISO) scan_ball_aniso<KNN_K>(*agp, cell_start2, sorted2, q.x, q.y, q.z, R2, bd, bi);
+        else scan_ball_flat2<KNN_K>(g, cell_start, sorted, q.x, q.y, q.z, R2, bd, bi);
         if (R2 == g.r2 || bd[KNN_K - 1] < R2 * (1.f - 2e-4f)) {
           surv = bd[KNN_K - 1] <= g.r2;
           if (surv) {
@@ -1402,6 +1538,49 @@ __global__ void k_knn_points(const float* __restrict__ q, int64_t M, const GridP
   }
 }
 
+// Pass B of mode 9: k_knn_pass_b8 with the r/2 and r balls on the anisotropic grid.
+template <bool STATS, int PTS>
+__global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_b9(
+    const float4* __restrict__ q_pos, const int* __restrict__ cand, const int* __restrict__ hard,
+    const int* __restrict__ n_hard, const AGrid* __restrict__ agp, const int* __restrict__ cell_start2,
+    const float4* __restrict__ sorted2, int* __restrict__ flag, int* __restrict__ t_nbr) {
+  const int i = blockIdx.x * KNN_THREADS + threadIdx.x;
+  if (i >= *n_hard) return;
+  const AGrid g = *agp;
+  unsigned c2[2] = {0, 0}, cr[2] = {0, 0};
+  const int hc = hard[i];
+  const int c = hc >> 1;
+  const float4 q = q_pos[cand[c]];
+  float bd[KNN_K];
+  int bi[KNN_K];
+#pragma unroll
+  for (int k = 0; k < KNN_K; ++k) { bd[k] = INFINITY; bi[k] = 0x7fffffff; }
+  bool done = false;
+  if ((hc & 1) == 0) {
+    scan_ball_aniso<KNN_K, STATS, PTS>(g, cell_start2, sorted2, q.x, q.y, q.z, 0.25f * g.r2, bd, bi, c2);
+    done = bd[KNN_K - 1] < 0.25f * g.r2 * (1.f - 2e-4f);
+  }
+  if (!done) scan_ball_aniso<KNN_K, STATS, PTS>(g, cell_start2, sorted2, q.x, q.y, q.z, g.r2, bd, bi, cr);
+  const bool surv = bd[KNN_K - 1] <= g.r2;
+  if (STATS) {
+    unsigned long long* st = g_knn_stats + 10 * (hc & 1);
+    atomicAdd(&st[0], 1ull);
+    if (done) atomicAdd(&st[1], 1ull);
+    if (surv) atomicAdd(&st[2], 1ull);
+    atomicAdd(&st[3], (unsigned long long)c2[0]);
+    atomicAdd(&st[4], (unsigned long long)c2[1]);
+    atomicAdd(&st[5], (unsigned long long)cr[0]);
+    atomicAdd(&st[6], (unsigned long long)cr[1]);
+    if (!done && !surv) { atomicAdd(&st[7], 1ull); atomicAdd(&st[8], (unsigned long long)(cr[0] + cr[1])); }
+  }
+  flag[c] = surv;
+  if (surv) {
+    int4* nb = (int4*)(t_nbr + (int64_t)c * KNN_K);
+    nb[0] = make_int4(bi[0], bi[1], bi[2], bi[3]);
+    nb[1] = make_int4(bi[4], bi[5], bi[6], bi[7]);
+  }
+}
+
 __global__ void k_bbox_from_points(const float* __restrict__ xyz, int64_t N, int* __restrict__ bbox_ord) {
   const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -1431,19 +1610,19 @@ using namespace apn;
 
 static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// Search strategy (apn_set_knn_mode / APN_KNN_MODE; default 7, see include/apn_hip.h). All are
+// Search strategy (apn_set_knn_mode / APN_KNN_MODE; default 9, see include/apn_hip.h). All are
 // exact; the others stay for A/B measurements and as cross-checks in the tests.
 static int& knn_mode() {
   static int m = [] {
     const char* e = getenv("APN_KNN_MODE");
-    return e ? atoi(e) : 8;
+    return e ? atoi(e) : 9;
   }();
   return m;
 }
 
 extern "C" int apn_set_knn_mode(int32_t mode) {
   const int prev = knn_mode();
-  if (mode >= 0 && mode <= 8) knn_mode() = mode;
+  if (mode >= 0 && mode <= 9) knn_mode() = mode;
   return prev;
 }
 
@@ -1462,16 +1641,20 @@ extern "C" int apn_debug_knn_stats(uint64_t* out20) {
 //   GridParams | counts[cap] | cell_start[cap+1] | cursor[cap] | pcell[N] | ccount[cap] | scan ws |
 //   tile_cnt[cap] | tile_start[cap+1] | tile_cursor[cap] | tile_list[cap] | n_tile_list[1]
 // (tiles of KT^3 cells never outnumber cells, so cap bounds the tile arrays).
+//   | AGrid | counts2[cap] | cursor2[cap] | cell_start2[cap+1] | pcell2[N] | sorted2[N] float4
+// (the anisotropic second grid of kNN mode 9; its cells never outnumber the fine ones).
 extern "C" size_t apn_grid_workspace_bytes(int64_t n_points, int32_t cell_cap) {
   return al256(sizeof(GridParams)) + al256((size_t)cell_cap * 4) + al256((size_t)(cell_cap + 1) * 4) +
          al256((size_t)cell_cap * 4) + al256((size_t)n_points * 4) + al256((size_t)cell_cap * 4) +
          al256(scan_workspace_bytes(cell_cap)) + al256((size_t)cell_cap * 4) * 3 +
-         al256((size_t)(cell_cap + 1) * 4) + al256(4);
+         al256((size_t)(cell_cap + 1) * 4) + al256(4) + al256(sizeof(AGrid)) + al256((size_t)cell_cap * 4) * 2 +
+         al256((size_t)(cell_cap + 1) * 4) + al256((size_t)n_points * 4) + al256((size_t)n_points * 16);
 }
 
 struct GridWs {
   GridParams* gp; int* counts; int* cell_start; int* cursor; int* pcell; int* ccount; void* scan;
   int* tile_cnt; int* tile_start; int* tile_cursor; int* tile_list; int* n_tile_list;
+  AGrid* ag; int* counts2; int* cursor2; int* cell_start2; int* pcell2; float4* sorted2;
 };
 static GridWs grid_ws(void* ws, int64_t N, int cap) {
   char* p = (char*)ws;
@@ -1487,7 +1670,13 @@ static GridWs grid_ws(void* ws, int64_t N, int cap) {
   w.tile_start = (int*)p; p += al256((size_t)(cap + 1) * 4);
   w.tile_cursor = (int*)p; p += al256((size_t)cap * 4);
   w.tile_list = (int*)p; p += al256((size_t)cap * 4);
-  w.n_tile_list = (int*)p;
+  w.n_tile_list = (int*)p; p += al256(4);
+  w.ag = (AGrid*)p; p += al256(sizeof(AGrid));
+  w.counts2 = (int*)p; p += al256((size_t)cap * 4);
+  w.cursor2 = (int*)p; p += al256((size_t)cap * 4);
+  w.cell_start2 = (int*)p; p += al256((size_t)(cap + 1) * 4);
+  w.pcell2 = (int*)p; p += al256((size_t)N * 4);
+  w.sorted2 = (float4*)p;
   return w;
 }
 
@@ -1557,7 +1746,26 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
   if (st) return st;
   hipLaunchKernelGGL(k_compact_i32, dim3(nb), dim3(KNN_THREADS), 0, s, cand_blk, cblk_cnt, cblk_off, cand);
   // candidates: count at cblk_off[nb]; launch over the upper bound nb blocks
-  if (knn_mode() == 8) {
+  if (knn_mode() == 8 || knn_mode() == 9) {
+    static const bool stats = getenv("APN_KNN_STATS") != nullptr;   // profiling aid: apn_debug_knn_stats
+    const bool small = !stats && n_queries <= KNN_SPLIT_MAX_QUERIES;   // small batches: 8 lanes per hard query
+    const bool aniso = knn_mode() == 9 && !small;
+    if (aniso) {   // the anisotropic second grid for pass B (built from the fine grid's sorted points)
+      static const int f = [] {
+        const char* e = getenv("APN_KNN_ANISO");
+        const int v = e ? atoi(e) : 2;
+        return (v == 1 || v == 2 || v == 4) ? v : 2;
+      }();
+      APN_HIP_TRY(hipMemsetAsync(g.counts2, 0, (size_t)cell_cap * 4, s));
+      APN_HIP_TRY(hipMemsetAsync(g.cursor2, 0, (size_t)cell_cap * 4, s));
+      hipLaunchKernelGGL(k_agrid_params, dim3(1), dim3(64), 0, s, g.gp, f, g.ag);
+      hipLaunchKernelGGL(k_agrid_count, dim3(ceil_div(n_points, 256)), dim3(256), 0, s, (const float4*)sorted_pts4,
+                         n_points, g.gp, f, g.counts2, g.pcell2);
+      st = scan_exclusive_i32(g.counts2, g.cell_start2, cell_cap, g.scan, s);
+      if (st) return st;
+      hipLaunchKernelGGL(k_agrid_scatter, dim3(ceil_div(n_points, 256)), dim3(256), 0, s, (const float4*)sorted_pts4,
+                         n_points, g.pcell2, g.cell_start2, g.cursor2, g.sorted2);
+    }
     int* flag = t_ray;
     int* hard = cand_blk;
     int* n_hard = cblk_cnt + nb + 1;
@@ -1578,16 +1786,27 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
     int* hard_r = ccell + slots;          // second quarter of the t_pos region
     int* n_hard_r = cblk_off + nb + 1;    // cblk_off has nb + 2 entries
     APN_HIP_TRY(hipMemsetAsync(n_hard_r, 0, 4, s));
-    hipLaunchKernelGGL(k_knn_pass_a8, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, cblk_off + nb,
-                       g.gp, g.cell_start, (const float4*)sorted_pts4, ccell, u1, u2, u4, flag, t_nbr, hard, n_hard,
-                       hard_r, n_hard_r);
-    static const bool stats = getenv("APN_KNN_STATS") != nullptr;   // profiling aid: apn_debug_knn_stats
-    if (!stats && n_queries <= KNN_SPLIT_MAX_QUERIES) {   // small batches: 8 lanes per hard query
+    static const bool a_aniso = getenv("APN_KNN_A_ANISO") != nullptr;   // A/B: pass A's r/4 ball on the second grid
+    hipLaunchKernelGGL((aniso && a_aniso) ? k_knn_pass_a8<true> : k_knn_pass_a8<false>, dim3(nb), dim3(KNN_THREADS), 0,
+                       s, (const float4*)q_pos4, cand, cblk_off + nb, g.gp, g.cell_start, (const float4*)sorted_pts4,
+                       ccell, u1, u2, u4, flag, t_nbr, hard, n_hard, hard_r, n_hard_r, g.ag, g.cell_start2, g.sorted2);
+    if (small) {
       const dim3 nb4(ceil_div(n_queries * 8, KNN_THREADS));
       hipLaunchKernelGGL(k_knn_pass_b8s<8>, nb4, dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard, n_hard,
                          g.gp, g.cell_start, (const float4*)sorted_pts4, flag, t_nbr);
       hipLaunchKernelGGL(k_knn_pass_b8s<8>, nb4, dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard_r,
                          n_hard_r, g.gp, g.cell_start, (const float4*)sorted_pts4, flag, t_nbr);
+    } else if (aniso) {
+      static const int pts = [] {   // points per step of the scan (A/B: APN_KNN_PTS=2)
+        const char* e = getenv("APN_KNN_PTS");
+        return e && atoi(e) == 2 ? 2 : 4;
+      }();
+      auto pass_b = stats ? (pts == 4 ? k_knn_pass_b9<true, 4> : k_knn_pass_b9<true, 2>)
+                          : (pts == 4 ? k_knn_pass_b9<false, 4> : k_knn_pass_b9<false, 2>);
+      hipLaunchKernelGGL(pass_b, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard, n_hard,
+                         g.ag, g.cell_start2, g.sorted2, flag, t_nbr);
+      hipLaunchKernelGGL(pass_b, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard_r,
+                         n_hard_r, g.ag, g.cell_start2, g.sorted2, flag, t_nbr);
     } else {
       auto pass_b = stats ? k_knn_pass_b8<true> : k_knn_pass_b8<false>;
       hipLaunchKernelGGL(pass_b, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard, n_hard,

@@ -367,7 +367,7 @@ def main():
             n = st[4 * i] or 1
             log(f"[knn {nm}] queries/frame {st[4 * i] / args.steps:.0f} cycles share {100 * st[4 * i + 1] / tot_cyc:.1f}% "
                 f"cycles/query {st[4 * i + 1] / n:.0f} rows/query {st[4 * i + 2] / n:.1f} pts/query {st[4 * i + 3] / n:.1f}")
-    if os.environ.get("APN_KNN_STATS"):   # mode-8 pass-B counters (per hard list)
+    if os.environ.get("APN_KNN_STATS"):   # mode-8/9 pass-B counters (per hard list)
         import ctypes
         from apn_amd import _lib
         st = (ctypes.c_uint64 * 20)()

@@ -570,7 +570,7 @@ def test_no_points_fallback(dev):
     assert torch.all(out["rgb_marched"] == g.cfg("bg")) and torch.all(out["depth"] == 0)
 
 
-@pytest.mark.parametrize("mode", [1, 2, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("mode", [1, 2, 4, 5, 6, 7, 8, 9])
 def test_knn_modes_identical_full_scene(dev, mode):
     """Full C2 frame (300k points, 640k rays, ~8M in-bbox samples): every kNN search strategy
     gives bit-identical renders and survivor counts to the default one (size-independent
