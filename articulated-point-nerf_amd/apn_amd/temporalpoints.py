@@ -199,7 +199,7 @@ class TemporalPoints(torch.nn.Module):
         self.bone_arap_mask = torch.tensor(bones).reshape(-1)
         self.register_buffer("xyz_min", torch.Tensor(np.asarray(xyz_min, dtype=np.float32)))
         self.register_buffer("xyz_max", torch.Tensor(np.asarray(xyz_max, dtype=np.float32)))
-        self.eps = torch.tensor(eps)
+        self.eps = torch.as_tensor(eps, dtype=torch.float32).clone()
         self._eps = float(eps)
         self.feat_depth = feat_depth
         self.timebase_pe = timebase_pe

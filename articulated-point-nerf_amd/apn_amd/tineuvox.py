@@ -55,6 +55,11 @@ class TiNeuVoxHeads(nn.Module):
                  net_width=128, alpha_init=1e-3, posbase_pe=10, viewbase_pe=4, timebase_pe=8,
                  gridbase_pe=2, no_view_dir=False, **kwargs):
         super().__init__()
+        self._kwargs = dict(xyz_min=np.asarray(xyz_min, dtype=np.float32), xyz_max=np.asarray(xyz_max, dtype=np.float32),
+                            num_voxels=num_voxels, num_voxels_base=num_voxels_base, voxel_dim=voxel_dim,
+                            net_width=net_width, alpha_init=alpha_init, posbase_pe=posbase_pe,
+                            viewbase_pe=viewbase_pe, timebase_pe=timebase_pe, gridbase_pe=gridbase_pe,
+                            no_view_dir=no_view_dir)
         self.no_view_dir = no_view_dir
         self.posbase_pe, self.viewbase_pe, self.timebase_pe, self.gridbase_pe = posbase_pe, viewbase_pe, timebase_pe, gridbase_pe
         self.register_buffer("xyz_min", torch.tensor(np.asarray(xyz_min, dtype=np.float32)))
@@ -76,6 +81,10 @@ class TiNeuVoxHeads(nn.Module):
         self.register_buffer("grid_poc", torch.FloatTensor([(2 ** i) for i in range(gridbase_pe)]))
         self.register_buffer("pos_poc", torch.FloatTensor([(2 ** i) for i in range(posbase_pe)]))
         self.register_buffer("view_poc", torch.FloatTensor([(2 ** i) for i in range(viewbase_pe)]))
+
+    def get_kwargs(self):
+        """Constructor arguments (the TiNeuVox.get_kwargs subset this holder takes)."""
+        return dict(self._kwargs)
 
     def activate_density(self, density, interval=None, act_shift=None):
         """tineuvox.py:396-400 -> Raw2Alpha (HIP raw2alpha)."""

@@ -237,7 +237,13 @@ __device__ __forceinline__ void quad_load_row(const float* __restrict__ src, flo
   if constexpr (JL % 4 == 0) {
 #pragma unroll
     for (int q = 0; q < JL / 4; ++q) {
+#ifdef APN_LBS_NT   // A/B: streamed once, non-temporal
+      typedef float f4v __attribute__((ext_vector_type(4)));
+      const f4v w = __builtin_nontemporal_load((const f4v*)src + q);
+      const float4 v = make_float4(w[0], w[1], w[2], w[3]);
+#else
       const float4 v = ((const float4*)src)[q];
+#endif
       row[4 * q] = v.x; row[4 * q + 1] = v.y; row[4 * q + 2] = v.z; row[4 * q + 3] = v.w;
     }
   } else if constexpr (JL % 2 == 0) {

@@ -223,6 +223,33 @@ def gen_case(name, t=0.3):
           f"{int((out['alphainv_last'] < 1).sum())}")
 
 
+def gen_checkpoint_case(name="G3"):
+    """A TemporalPoints checkpoint in the reference layout -- {'model_kwargs': get_kwargs() (with
+    the reference TiNeuVox *module*), 'model_state_dict'} as run.py saves it -- converted by
+    apn_amd.checkpoint.to_weights_only into the weights-only file the loader reads
+    (ckpt_<name>.pt). Float tensors that are fp16-exact by construction are stored as fp16
+    (lossless; load_state_dict casts them back)."""
+    sys.path.insert(0, os.path.join(ROOT, "articulated-point-nerf_amd"))
+    from apn_amd import checkpoint as C
+    scene = S.make_scene(name)
+    torch.manual_seed(1234)
+    model, tnv = build_reference_model(scene)
+    ck = C.to_weights_only({"model_kwargs": model.get_kwargs(), "model_state_dict": model.state_dict()})
+    assert ck["tineuvox_class"] == "TiNeuVox" and type(tnv).__module__ == "lib.tineuvox"
+
+    def small(v):
+        if torch.is_tensor(v) and v.dtype == torch.float32 and v.numel() > 1024 and torch.equal(v.half().float(), v):
+            return v.half()
+        if isinstance(v, dict):
+            return {k: small(x) for k, x in v.items()}
+        return v
+    ck = {k: small(v) for k, v in ck.items()}
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), f"ckpt_{name}.pt")
+    torch.save(ck, path)
+    print(f"ckpt {name}: wrote {path} ({os.path.getsize(path) / 1e6:.2f} MB); "
+          f"{len(ck['model_state_dict'])} state keys, tineuvox kwargs {sorted(ck['tineuvox_kwargs'])}")
+
+
 def rtn_poc(x, f):
     from lib.tineuvox import poc_fre
     return poc_fre(x, f)
@@ -318,7 +345,9 @@ def main():
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     which = sys.argv[1:] or ["G1", "G2", "G3", "T1"]
     for name in which:
-        if name.startswith("T"):
+        if name.startswith("ckpt_"):
+            gen_checkpoint_case(name[5:])
+        elif name.startswith("T"):
             gen_tineuvox_case(name)
         else:
             gen_case(name)
