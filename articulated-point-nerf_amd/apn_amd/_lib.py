@@ -36,6 +36,7 @@ SIGNATURES = {
     "apn_bbox_unpack": (C.c_int, [P, F32, P, P]),
     "apn_inbbox_count": (C.c_int, [P, P, P, F32, F32, F32, I64, P, P, P]),
     "apn_inbbox_fill": (C.c_int, [P, P, P, F32, F32, F32, I64, P, P, P, P]),
+    "apn_inbbox_fill_capped": (C.c_int, [P, P, P, F32, F32, F32, I64, P, I64, P, P, P, P]),
     "apn_grid_workspace_bytes": (SZ, [I64, I32]),
     "apn_grid_build": (C.c_int, [P, I64, P, F32, I32, P, P, P]),
     "apn_knn_workspace_bytes": (SZ, [I64]),

@@ -33,14 +33,20 @@ class NoPointsException(Exception):
 
 
 class FrameStats(dict):
-    """Per-frame counts. 'kept_samples' (kNN survivors) stays on the device until asked for, so
-    rendering a frame needs no device->host sync after the kNN stage."""
+    """Per-frame counts. 'kept_samples' (kNN survivors) -- and on the capacity-bounded path
+    'inbbox_samples' too -- stay on the device until asked for, so rendering a frame needs no
+    device->host sync."""
 
-    def __init__(self, *args, nsurv=None, **kw):
+    def __init__(self, *args, nsurv=None, info=None, **kw):
         super().__init__(*args, **kw)
         self._nsurv = nsurv
+        self._info = info   # apn_inbbox_fill_capped frame_info {queries, in-bbox total, overflow, survivors}
 
     def __missing__(self, key):
+        if self._info is not None and key in ("inbbox_samples", "kept_samples"):
+            v = self._info.tolist()
+            self["inbbox_samples"], self["kept_samples"] = v[1], v[3]
+            return self[key]
         if key == "kept_samples" and self._nsurv is not None:
             v = int(self._nsurv.item())
             self[key] = v
@@ -55,6 +61,7 @@ class FrameStats(dict):
 
     def resolved(self):
         self.get("kept_samples")
+        self.get("inbbox_samples")
         return dict(self)
 
 
@@ -69,23 +76,43 @@ class RenderOutput(dict):
     (the kernels composite nothing: rgb = bg, depth = 0, weights = bg), so only the key set and
     ``alphainv_last`` differ -- they are resolved on the first access that can observe them,
     with one read of the device count. Reading rgb_marched / depth / weights, as the
-    reference's render loops do (run.py:126-173), never syncs."""
+    reference's render loops do (run.py:126-173), never syncs.
+
+    On the capacity-bounded path (no host read of the in-bbox sample count, see
+    TemporalPoints._render) the frame is validated on the first access of any key: one read of
+    the device frame_info; a frame whose samples overflowed the capacity is rendered again on the
+    exact path (``rerender``) and its values replace these."""
 
     _SENSITIVE = ("alphainv_last", "alphainv_last_direct", "depth", "weights")
 
-    def __init__(self, *a, nsurv=None, n_rays=0, bg=0.0, **kw):
+    def __init__(self, *a, nsurv=None, n_rays=0, bg=0.0, info=None, rerender=None, **kw):
         super().__init__(*a, **kw)
         self._nsurv = nsurv
         self._n_rays = n_rays
         self._bg = bg
+        self._info = info
+        self._rerender = rerender
 
     def _resolve(self):
-        if self._nsurv is None:
+        if self._info is not None:
+            info, self._info = self._info, None
+            v = info.tolist()   # {queries, in-bbox total, overflow, survivors}
+            if v[2]:
+                fresh = self._rerender()
+                dict.clear(self)
+                dict.update(self, {k: dict.__getitem__(fresh, k) for k in dict.keys(fresh)})
+                self._nsurv, self._n_rays, self._bg = fresh._nsurv, fresh._n_rays, fresh._bg
+                self._rerender = None
+                return self._resolve()
+            self._nsurv = None
+            n_surv, dev = v[3], info.device
+        elif self._nsurv is not None:
+            nsurv, self._nsurv = self._nsurv, None
+            n_surv, dev = int(nsurv.item()), nsurv.device
+        else:
             return
-        nsurv, self._nsurv = self._nsurv, None
-        if int(nsurv.item()) > 0:
+        if n_surv > 0:
             return
-        dev = nsurv.device
         R, bg = self._n_rays, self._bg
         super().pop("alphainv_last_direct", None)
         super().__setitem__("alphainv_last", None)
@@ -95,17 +122,17 @@ class RenderOutput(dict):
             super().__setitem__("weights", torch.ones(R, 3, device=dev) * bg)
 
     def __getitem__(self, k):
-        if k in self._SENSITIVE:
+        if self._info is not None or k in self._SENSITIVE:
             self._resolve()
         return super().__getitem__(k)
 
     def get(self, k, default=None):
-        if k in self._SENSITIVE:
+        if self._info is not None or k in self._SENSITIVE:
             self._resolve()
         return super().get(k, default)
 
     def __contains__(self, k):
-        if k in self._SENSITIVE:
+        if self._info is not None or k in self._SENSITIVE:
             self._resolve()
         return super().__contains__(k)
 
@@ -183,6 +210,11 @@ def weights_from_bones(joints, bones, pcd, eps):
     d = _bone_distances(pcd, a, b)
     w = (1 / (0.5 * torch.e ** d + eps)).T.contiguous()
     return torch.cat([torch.zeros((len(w), 1)), w], dim=-1)
+
+
+def _grow_capacity(n):
+    """In-bbox sample capacity for a frame of n samples: 25 % headroom, 64k granules."""
+    return max(65536, (int(n * 1.25) + 65535) // 65536 * 65536)
 
 
 class TemporalPoints(torch.nn.Module):
@@ -274,6 +306,9 @@ class TemporalPoints(torch.nn.Module):
         self.palette_perm_device = None   # None: the weights' device (reference behaviour)
         self.timing = None          # set to {} to record HIP-event timings of the MLP launch
         self.last_stats = FrameStats()
+        self._capacity = {}         # ray count -> in-bbox sample capacity of the sync-free render path
+        self._force_exact = False
+        self._last_info = None
 
     # view_poc / pos_poc alias the TiNeuVox buffers (temporalpoints.py:148-150); as properties
     # they follow .to(device) (the reference relies on a CUDA default tensor type instead).
@@ -468,6 +503,53 @@ class TemporalPoints(torch.nn.Module):
         step.graph, step.inputs = graph, rp
         return step
 
+    def capture_frame(self, t, render_kwargs, render_depth=True, render_weights=True, query_radius=0.01):
+        """The render frame for a fixed ray set (skeleton, LBS, grid, sampling, kNN, MLP,
+        compositing: the whole no-grad forward) captured once in a HIP graph: returns
+        ``step(t) -> RenderOutput``, which copies the time into the graph's input and replays it.
+        The outputs are the graph's static buffers (overwritten by the next step); like an eager
+        frame they are validated on first read (one read of the device frame_info) and a frame
+        whose samples overflowed the capacity is rendered again eagerly. Needs no host sync inside
+        the frame: the capacity is set by the warm-up frames. Capture again after changing the
+        model or the rays."""
+        dev = self.canonical_feat.device
+        t_in = torch.as_tensor(t, dtype=torch.float32, device=dev).reshape(-1).clone()
+        rk = dict(render_kwargs)
+        R = len(rk['rays_o'])
+        args = (render_depth, rk, query_radius, render_weights, None, None, None, True, False, None)
+        with torch.no_grad():
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):   # warm-up: capacity (first frame), caches, workspaces
+                self._forward_render(t_in, *args)
+                warm = self._forward_render(t_in, *args)
+            torch.cuda.current_stream(dev).wait_stream(side)
+            warm.keys()   # validate: an overflow renders again and grows the capacity
+            if self._capacity.get(R) is None:
+                raise RuntimeError("capture_frame: no sample capacity for this ray set (empty frame?)")
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                out = self._forward_render(t_in, *args)
+        static = {k: dict.__getitem__(out, k) for k in dict.keys(out)}
+        info, n_rays, bg = out._info, out._n_rays, out._bg
+
+        def step(t):
+            t_in.copy_(torch.as_tensor(t, dtype=torch.float32, device=dev).reshape(-1))
+            graph.replay()
+            tt = t_in.clone()
+
+            def rerender():
+                self._force_exact = True
+                try:
+                    with torch.no_grad():
+                        return self._forward_render(tt, *args)
+                finally:
+                    self._force_exact = False
+            return RenderOutput(dict(static), n_rays=n_rays, bg=bg, info=info, rerender=rerender)
+
+        step.graph, step.inputs = graph, t_in
+        return step
+
     def sample_ray(self, rays_o, rays_d, near, far, stepsize, xyz_min=None, xyz_max=None, **render_kwargs):
         """temporalpoints.py:373-399 through the render_utils drop-in."""
         from .ops import sample_pts_on_rays
@@ -612,10 +694,21 @@ class TemporalPoints(torch.nn.Module):
                     'depth': torch.zeros(R, device=dev), 'weights': torch.ones(R, 3, device=dev) * bg,
                     't_hat_pcd': t_hat_pcd, 'alphainv_last': None, 'grid': None, 'joints': joints, 'bones': bones}
         rgb, rgb_d, depth, wvis, last, last_d = out
+        info = self._last_info
+
+        def rerender():   # the exact path (the frame overflowed its sample capacity)
+            self._force_exact = True
+            try:
+                with torch.no_grad():
+                    return self._forward_render(t, render_depth, render_kwargs, query_radius, render_weights,
+                                                rot_params, poses, Ks, calc_min_max, get_skeleton, ray_shard)
+            finally:
+                self._force_exact = False
         ret = RenderOutput({'t_hat_pcd': t_hat_pcd, 'rgb_marched': rgb, 'alphainv_last': last,
                             'alphainv_last_direct': last_d, 'grid': None, 'rgb_marched_direct': rgb_d,
                             'joints': joints, 'bones': bones},
-                           nsurv=self.last_stats._nsurv, n_rays=len(rgb), bg=float(render_kwargs['bg']))
+                           nsurv=self.last_stats._nsurv, n_rays=len(rgb), bg=float(render_kwargs['bg']),
+                           info=info, rerender=rerender if info is not None else None)
         if render_depth:
             ret['depth'] = depth
         if render_weights:
@@ -674,30 +767,53 @@ class TemporalPoints(torch.nn.Module):
             ro, rd, vd = ro[r0:r1], rd[r0:r1], vd[r0:r1]
             offs = (offs[r0:r1 + 1] - offs[r0]).contiguous()
             R = r1 - r0
-        n_bbox = int(offs[R].item())
-        self.last_stats = FrameStats({"rays": R, "inbbox_samples": n_bbox})
-        if n_bbox == 0:
-            raise NoPointsException("No points.")
-        q_pos = ws.get("q_pos", n_bbox * 4, torch.float32, dev)
-        q_ray = ws.get("q_ray", n_bbox, torch.int32, dev)
-        call("apn_inbbox_fill", ptr(ro), ptr(rd), ptr(bbox6), near, far, stepdist, R, ptr(offs), ptr(q_pos),
-             ptr(q_ray), s)
+        # In-bbox sample count: the first frame of a ray count reads it (one host sync) and sizes
+        # a capacity from it; later frames keep the count on the device -- buffers and launch
+        # bounds use the capacity, apn_inbbox_fill_capped drops samples past it and reports an
+        # overflow, which RenderOutput checks when the frame is first read (and then renders the
+        # frame again on this exact path). A ray shard reads its split on the host anyway.
+        cap = self._capacity.get(R) if (shard is None and not self._force_exact) else None
+        info = None
+        if cap is None:
+            n_bbox = int(offs[R].item())
+            self.last_stats = FrameStats({"rays": R, "inbbox_samples": n_bbox})
+            if n_bbox == 0:
+                raise NoPointsException("No points.")
+            if shard is None:
+                self._capacity[R] = max(self._capacity.get(R, 0), _grow_capacity(n_bbox))
+            Q = n_bbox
+            q_pos = ws.get("q_pos", Q * 4, torch.float32, dev)
+            q_ray = ws.get("q_ray", Q, torch.int32, dev)
+            call("apn_inbbox_fill", ptr(ro), ptr(rd), ptr(bbox6), near, far, stepdist, R, ptr(offs), ptr(q_pos),
+                 ptr(q_ray), s)
+            nq_dev = C.c_void_p(offs.data_ptr() + 4 * R)
+            nsurv = torch.empty(1, dtype=torch.int32, device=dev)   # per frame: FrameStats may read it later
+        else:
+            Q = cap
+            q_pos = ws.get("q_pos", Q * 4, torch.float32, dev)
+            q_ray = ws.get("q_ray", Q, torch.int32, dev)
+            info = torch.empty(4, dtype=torch.int32, device=dev)   # {queries, total, overflow, survivors}
+            call("apn_inbbox_fill_capped", ptr(ro), ptr(rd), ptr(bbox6), near, far, stepdist, R, ptr(offs), Q,
+                 ptr(q_pos), ptr(q_ray), ptr(info), s)
+            nq_dev = ptr(info)
+            nsurv = info[3:]
+            self.last_stats = FrameStats({"rays": R}, info=info)
         self._mark("sampling")
         # radius kNN + compaction of survivors
-        s_pos = ws.get("s_pos", n_bbox * 4, torch.float32, dev)
-        s_ray = ws.get("s_ray", n_bbox, torch.int32, dev)
-        s_nbr = ws.get("s_nbr", n_bbox * 8, torch.int32, dev)
-        nsurv = torch.empty(1, dtype=torch.int32, device=dev)   # per frame: FrameStats may read it later
-        kws = ws.bytes("knn_ws", lib.apn_knn_workspace_bytes(n_bbox), dev)
-        call("apn_knn_radius", ptr(q_pos), ptr(q_ray), n_bbox, C.c_void_p(offs.data_ptr() + 4 * R), ptr(gws), N,
+        s_pos = ws.get("s_pos", Q * 4, torch.float32, dev)
+        s_ray = ws.get("s_ray", Q, torch.int32, dev)
+        s_nbr = ws.get("s_nbr", Q * 8, torch.int32, dev)
+        kws = ws.bytes("knn_ws", lib.apn_knn_workspace_bytes(Q), dev)
+        call("apn_knn_radius", ptr(q_pos), ptr(q_ray), Q, nq_dev, ptr(gws), N,
              CELL_CAP, ptr(sorted4), qr, ptr(s_pos), ptr(s_ray), ptr(s_nbr), ptr(nsurv), ptr(kws), s)
         self._mark("knn")
         # The survivor count stays on the device: the MLP and compositing kernels read it there and
-        # n_bbox bounds it, so no sync here. (If no sample survives, the kernels produce the
+        # Q bounds it, so no sync here. (If no sample survives, the kernels produce the
         # reference's NoPointsException values -- bg colour, depth 0 -- and RenderOutput gives
         # the reference's key set and alphainv_last=None when they are read.)
-        S = n_bbox
+        S = Q
         self.last_stats._nsurv = nsurv
+        self._last_info = info
         # neighbour MLP + heads + direct blend
         wbuf, proj = self._packed_weights(pose_embedding, dev)
         out12 = ws.get("out12", S * 12, torch.float32, dev)

@@ -6,6 +6,8 @@
 // are bit-identical to the CPU oracle (oracle/apn_oracle.py).
 #include "apn_common.h"
 
+#include <climits>
+
 namespace apn {
 
 struct RayGeom {
@@ -208,17 +210,19 @@ __global__ void k_inbbox_count(const float* __restrict__ ro, const float* __rest
 }
 
 // q_pos[i] = (x, y, z, bits(step_id)); q_ray[i] = ray id. Sorted by ray, then step.
+// cap: samples at positions >= cap are not written (the capacity-bounded, sync-free render path:
+// apn_inbbox_fill_capped); INT_MAX = every sample.
 __global__ void k_inbbox_fill(const float* __restrict__ ro, const float* __restrict__ rd,
                               const float* __restrict__ bbox6, float near, float far,
                               float stepdist, int64_t n_rays, const int* __restrict__ off,
-                              float4* __restrict__ q_pos, int* __restrict__ q_ray) {
+                              float4* __restrict__ q_pos, int* __restrict__ q_ray, int cap) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n_rays) return;
   int o = off[r];
-  if (off[r + 1] == o) return;
+  if (off[r + 1] == o || o >= cap) return;
   const float lo[3] = {bbox6[0], bbox6[1], bbox6[2]}, hi[3] = {bbox6[3], bbox6[4], bbox6[5]};
   RayGeom g = ray_geom(ro + 3 * r, rd + 3 * r, lo, hi, near, far, stepdist);
-  for (int k = 0; k < g.n; ++k) {
+  for (int k = 0; k < g.n && o < cap; ++k) {
     float px, py, pz;
     if (sample_at(g, k, stepdist, lo, hi, px, py, pz)) {
       q_pos[o] = make_float4(px, py, pz, __int_as_float(k));
@@ -226,6 +230,15 @@ __global__ void k_inbbox_fill(const float* __restrict__ ro, const float* __restr
       ++o;
     }
   }
+}
+
+// frame_info = {min(total, cap), total, total > cap} from the exclusive scan's last entry.
+__global__ void k_frame_info(const int* __restrict__ total, int cap, int* __restrict__ info) {
+  if (threadIdx.x != 0) return;
+  const int n = *total;
+  info[0] = n < cap ? n : cap;
+  info[1] = n;
+  info[2] = n > cap ? 1 : 0;
 }
 
 // bbox_ord: ordered-int encoded [min x,y,z, max x,y,z] of the warped cloud (apn_lbs.hip);
@@ -352,7 +365,19 @@ extern "C" int apn_inbbox_fill(const float* rays_o, const float* rays_d, const f
                                void* stream) {
   if (n_rays <= 0) return APN_ERR_ARG;
   hipLaunchKernelGGL(k_inbbox_fill, dim3(ceil_div(n_rays, 256)), dim3(256), 0, (hipStream_t)stream, rays_o, rays_d,
-                     bbox6, near, far, stepdist, n_rays, offsets, (float4*)q_pos4, q_ray);
+                     bbox6, near, far, stepdist, n_rays, offsets, (float4*)q_pos4, q_ray, INT_MAX);
+  return launch_status();
+}
+
+extern "C" int apn_inbbox_fill_capped(const float* rays_o, const float* rays_d, const float* bbox6, float near,
+                                      float far, float stepdist, int64_t n_rays, const int32_t* offsets,
+                                      int64_t capacity, float* q_pos4, int32_t* q_ray, int32_t* frame_info,
+                                      void* stream) {
+  if (n_rays <= 0 || capacity < 0 || capacity > INT_MAX || !frame_info) return APN_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_frame_info, dim3(1), dim3(64), 0, s, offsets + n_rays, (int)capacity, frame_info);
+  hipLaunchKernelGGL(k_inbbox_fill, dim3(ceil_div(n_rays, 256)), dim3(256), 0, s, rays_o, rays_d, bbox6, near, far,
+                     stepdist, n_rays, offsets, (float4*)q_pos4, q_ray, (int)capacity);
   return launch_status();
 }
 

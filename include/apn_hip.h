@@ -198,6 +198,15 @@ int apn_inbbox_count(const float* rays_o, const float* rays_d, const float* bbox
 int apn_inbbox_fill(const float* rays_o, const float* rays_d, const float* bbox6, float near,
                     float far, float stepdist, int64_t n_rays, const int32_t* offsets,
                     float* q_pos4, int32_t* q_ray, void* stream);
+/* apn_inbbox_fill with buffers sized `capacity` on the host: samples at positions >= capacity are
+ * dropped, and frame_info[3] (device) = {min(total, capacity), total, total > capacity}. Element
+ * 0 is the live query count apn_knn_radius reads on the device (n_queries = capacity), so the
+ * frame needs no device->host read of the sample count; an overflowed frame is recomputed by the
+ * caller (TemporalPoints: RenderOutput validation). */
+int apn_inbbox_fill_capped(const float* rays_o, const float* rays_d, const float* bbox6, float near,
+                           float far, float stepdist, int64_t n_rays, const int32_t* offsets,
+                           int64_t capacity, float* q_pos4, int32_t* q_ray, int32_t* frame_info,
+                           void* stream);
 
 /* Uniform grid over the warped cloud (cell >= sqrt(query_radius)): counting sort into
  * sorted_pts4 [N,4] {x,y,z,bits(idx)}. cell_cap bounds the number of cells. */

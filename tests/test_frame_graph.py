@@ -1,0 +1,79 @@
+"""The sync-free render frame and its HIP-graph capture.
+
+* after a ray count's first frame (which reads the in-bbox sample count once and sizes a
+  capacity), frames keep that count on the device (apn_inbbox_fill_capped): the result equals the
+  exact path bit for bit, and the frame statistics resolve lazily from the device frame_info;
+* a frame whose samples overflow the capacity is detected on first read and rendered again on
+  the exact path (same values as an exact frame), growing the capacity;
+* TemporalPoints.capture_frame replays the whole no-grad forward as one HIP graph: each replay
+  equals the eager frame at that time bit for bit."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+KEYS = ("rgb_marched", "rgb_marched_direct", "depth", "weights", "alphainv_last")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch.device("cuda")
+
+
+def _scene_model(dev, name="G3"):
+    from apn_amd import harness, synthetic as S
+    scene = S.make_scene(name)
+    return scene, harness.build_model(scene, dev)
+
+
+def _frame(model, t, rk):
+    with torch.no_grad():
+        o = model(t, render_depth=True, render_kwargs=rk, render_weights=True)
+    return {k: o[k].clone() for k in KEYS}
+
+
+def test_sync_free_frame_equals_exact(dev):
+    scene, model = _scene_model(dev)
+    rk = scene.render_kwargs(dev)
+    R = len(rk["rays_o"])
+    t = torch.tensor([scene.cfg.t], device=dev)
+    a = _frame(model, t, rk)
+    stats_a = model.last_stats.resolved()
+    assert R in model._capacity and model._capacity[R] >= stats_a["inbbox_samples"]
+    b = _frame(model, t, rk)
+    assert model._last_info is not None          # the second frame took the capacity path
+    stats_b = model.last_stats.resolved()
+    assert stats_a == stats_b
+    for k in KEYS:
+        assert torch.equal(a[k], b[k]), k
+
+
+def test_overflowing_frame_is_rendered_again(dev):
+    scene, model = _scene_model(dev)
+    rk = scene.render_kwargs(dev)
+    R = len(rk["rays_o"])
+    t = torch.tensor([scene.cfg.t], device=dev)
+    exact = _frame(model, t, rk)
+    n = model.last_stats["inbbox_samples"]
+    model._capacity[R] = 64                       # far below the frame's sample count
+    with torch.no_grad():
+        o = model(t, render_depth=True, render_kwargs=rk, render_weights=True)
+    assert model._last_info is not None and int(model._last_info[2]) == 1   # overflow flagged on the device
+    for k in KEYS:                                 # first read: validated, rendered again exactly
+        assert torch.equal(o[k], exact[k]), k
+    assert model._capacity[R] >= n
+
+
+def test_captured_frame_equals_eager(dev):
+    scene, model = _scene_model(dev)
+    rk = scene.render_kwargs(dev)
+    t0 = torch.tensor([scene.cfg.t], device=dev)
+    t1 = torch.tensor([scene.cfg.t + 0.15], device=dev)
+    step = model.capture_frame(t0, rk)
+    for t in (t0, t1, t0):
+        g = step(t)
+        got = {k: g[k].clone() for k in KEYS}
+        ref = _frame(model, t, rk)
+        for k in KEYS:
+            assert torch.equal(got[k], ref[k]), k
