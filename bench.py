@@ -273,6 +273,11 @@ def main():
                     help="N>1: 'rays' (default) = the ranks split one frame's rays and all-gather the tiles "
                          "over RCCL (strong scaling, SURVEY.md 8(e)); 'frames' = every rank renders its own "
                          "frame (weak scaling, no data-path collective)")
+    ap.add_argument("--graph", choices=["auto", "on", "off"], default="off",
+                    help="replay the frame as one HIP graph (TemporalPoints.capture_frame); auto = on unless "
+                         "the ranks split one frame's rays (the split is read on the host). Off by default: "
+                         "a C2 replay sequence faulted on the box (under investigation); the eager frame is "
+                         "already free of host syncs")
     args = ap.parse_args()
     torch.set_grad_enabled(False)   # a render benchmark: the reference renders under no_grad (run.py:80, 241)
 
@@ -308,31 +313,51 @@ def main():
     log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.2f}s, rays/frame {R}")
 
     poses, Ks = scene.c2w[None].to(dev), scene.K[None].to(dev)
+    use_graph = args.graph == "on" or (args.graph == "auto" and not shard_rays)
 
-    def step():
+    def eager_step():
         if shard_rays:
             from apn_amd.shard import render_sharded
             return render_sharded(model, t_arg, rk, rank, world, poses=poses, Ks=Ks, get_skeleton=True)
         return model(t_arg, render_depth=True, render_kwargs=rk, render_weights=True, poses=poses, Ks=Ks,
                      get_skeleton=True)
 
+    step = eager_step
     for _ in range(args.warmup):
-        step()
+        eager_step()
     torch.cuda.synchronize(dev)
     stats = model.last_stats.resolved()
     log(f"[rank {rank}] scene: {stats}")
+    if use_graph:   # the whole frame as one HIP graph replay (no per-kernel host launches, no host sync)
+        graph_step = model.capture_frame(t_arg, rk)
+        step = lambda: graph_step(t_arg)   # noqa: E731
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize(dev)
 
+    # stage / MLP-kernel timings come from HIP events on eager frames (events are not recorded
+    # inside a graph replay); the timed loop below runs the step as configured
     model.timing = {}
+    if use_graph:
+        for _ in range(min(args.steps, 10)):
+            eager_step()
+        torch.cuda.synchronize(dev)
+    timing, model.timing = model.timing, None
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     host_s = 0.0
+    if not use_graph:
+        model.timing = timing
     for _ in range(args.steps):
         h0 = time.perf_counter()
         out = step()
         host_s += time.perf_counter() - h0
     torch.cuda.synchronize(dev)
+    if not use_graph:
+        timing, model.timing = model.timing, None
+    n_timed = min(args.steps, 10) if use_graph else args.steps
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
@@ -350,12 +375,13 @@ def main():
                                         enumerate(["gather", "layer1", "layers2-4", "epilogue"]))
             + f"; cycles/tile {tot / max(ph[4], 1):.0f}, in-loop share {tot / max(ph[5], 1):.3f}")
     stage_ms = {}
-    marks = model.timing.get("marks", [])
+    marks = timing.get("marks", [])
     for (_, a), (name, b) in zip(marks[:-1], marks[1:]):
         if name != "frame":
-            stage_ms[name] = stage_ms.get(name, 0.0) + a.elapsed_time(b) / args.steps
-    log(f"[rank {rank}] stage ms/frame (HIP events): " + ", ".join(f"{k} {v:.3f}" for k, v in stage_ms.items()))
-    log(f"[rank {rank}] host time inside step() {1e3 * host_s / args.steps:.3f} ms/step (includes the n_bbox sync wait)")
+            stage_ms[name] = stage_ms.get(name, 0.0) + a.elapsed_time(b) / n_timed
+    log(f"[rank {rank}] stage ms/frame (HIP events, eager frames): " + ", ".join(f"{k} {v:.3f}" for k, v in stage_ms.items()))
+    log(f"[rank {rank}] host time inside step() {1e3 * host_s / args.steps:.3f} ms/step "
+        f"({'graph replay' if use_graph else 'eager launches'}; device {1e3 * elapsed / args.steps:.3f} ms/step)")
     if os.environ.get("APN_KNN_MODE") == "3":   # kNN query-class counters
         import ctypes
         from apn_amd import _lib
@@ -379,10 +405,9 @@ def main():
             log(f"[knn pass B {nm}] queries/frame {v[0] / n:.0f}, done at r/2 {v[1] / q:.3f}, survive {v[2] / q:.3f}, "
                 f"r/2 scan rows+pts iters/query {v[3] / q:.1f}+{v[4] / q:.1f}, r scan {v[5] / q:.1f}+{v[6] / q:.1f}, "
                 f"rejected after full r scan {v[7] / q:.3f} ({v[8] / max(v[7], 1):.1f} iters each)")
-    ev = model.timing.get("mlp_events", [])
+    ev = timing.get("mlp_events", [])
     mlp_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / max(len(ev), 1)
     S_kept = int(ev[-1][2].item()) if ev else stats.get("kept_samples", 0)
-    model.timing = None
 
     if rank != 0:
         if world > 1:
@@ -426,7 +451,9 @@ def main():
                    "kept_samples": S_kept,
                    "parallelism": (f"rays x{world} + {backend} all_gather_into_tensor of the per-ray tiles"
                                    if shard_rays else f"frames x{world} (no data-path collective)")
-                   if world > 1 else "single"},
+                   if world > 1 else "single",
+                   "step": ("whole frame replayed as one HIP graph (TemporalPoints.capture_frame)" if use_graph
+                            else "eager launches")},
         "roofline": {"bound": "mfma", "kernel": kernel, "achieved": achieved, "peak": peak,
                      "unit": "TFLOP/s", "frac": achieved / peak,
                      "traffic": traffic.get("bytes_per_launch") if traffic else None,
