@@ -608,6 +608,9 @@ class TemporalPoints(torch.nn.Module):
         if records:
             self.mean_min_distance
             mmd = self._mmd_f
+        if self.timing is not None:   # HIP events right around the LBS launch (bench: the C5 roofline)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
         call("apn_lbs_skin", ptr(pcd), ptr(self.weights.detach().contiguous()), N, J, ptr(self.theta_weight.detach()),
              self._eps, ptr(rules32), ptr(T34), ptr(gt), ptr(colors),
              ptr(self.canonical_alpha.detach().contiguous()) if records else None,
@@ -615,6 +618,9 @@ class TemporalPoints(torch.nn.Module):
              ptr(self.direct_eps.detach().contiguous()) if records else None, mmd, 0, ptr(xyz), ptr(wout), None,
              ptr(recA), ptr(recB), ptr(bbox) if records else None,   # the bbox only feeds the render's sampling
              ptr(ws.bytes("lbs_ws", L.load().apn_lbs_workspace_bytes(N), dev)), stream_ptr(dev))
+        if self.timing is not None:
+            e1.record()
+            self.timing.setdefault("lbs_events", []).append((e0, e1))
         return xyz, wout, (recA, recB, bbox)
 
     def _packed_weights(self, pose_embedding, dev):

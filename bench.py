@@ -181,8 +181,8 @@ def lbs_sweep(args, rank, world, dev):
     for i in range(args.steps):
         model.repose(poses[i % len(poses)])
     torch.cuda.synchronize(dev)
-    marks = model.timing.get("marks", [])
-    lbs_ms = sum(a.elapsed_time(b) for (_, a), (nm, b) in zip(marks[:-1], marks[1:]) if nm == "lbs") / args.steps
+    ev = model.timing.get("lbs_events", [])
+    lbs_ms = sum(a.elapsed_time(b) for a, b in ev) / max(len(ev), 1)   # events right around each LBS launch
     model.timing = None
     # throughput: every pose of the sweep through the captured repose step (skeleton + LBS in one
     # HIP graph; per pose one device copy of rot_params + one graph launch)
