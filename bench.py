@@ -174,16 +174,29 @@ def lbs_sweep(args, rank, world, dev):
     model = harness.build_model(scene, dev)
     N, J = len(scene.ctor["canonical_pcd"]), scene.cfg.J
     poses = S.repose_sweep(J).to(dev)
-    # LBS kernel time for the roofline: HIP events around the LBS launch, eager steps
-    for i in range(2):
-        model.repose(poses[i % len(poses)])
-    model.timing = {}
-    for i in range(args.steps):
-        model.repose(poses[i % len(poses)])
-    torch.cuda.synchronize(dev)
-    ev = model.timing.get("lbs_events", [])
-    lbs_ms = sum(a.elapsed_time(b) for a, b in ev) / max(len(ev), 1)   # events right around each LBS launch
-    model.timing = None
+    # LBS kernel time for the roofline: 20 back-to-back LBS launches of one pose captured in a HIP
+    # graph, HIP events around one replay (eager events around a single launch would also time
+    # the host's launch latency whenever the device runs dry)
+    with torch.no_grad():
+        bone_Ts, gt, _ = model.forward_warp.pose(model.joints, rot_params=poses[0])
+        T34 = model.forward_warp.last_T34
+        for _ in range(2):
+            model._lbs(bone_Ts, gt, records=False, T34=T34)
+        torch.cuda.synchronize(dev)
+        n_lbs = 20
+        g_lbs = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_lbs):
+            for _ in range(n_lbs):
+                model._lbs(bone_Ts, gt, records=False, T34=T34)
+        g_lbs.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(3):
+            g_lbs.replay()
+        e1.record()
+        torch.cuda.synchronize(dev)
+        lbs_ms = e0.elapsed_time(e1) / (3 * n_lbs)
+        del g_lbs
     # throughput: every pose of the sweep through the captured repose step (skeleton + LBS in one
     # HIP graph; per pose one device copy of rot_params + one graph launch)
     step = model.capture_repose(rot_dim=poses.shape[-1])
@@ -245,8 +258,8 @@ def lbs_sweep(args, rank, world, dev):
                      "traffic": (read_traffic(os.path.join(ROOT, "profiles", "r01_lbs_traffic_c5.json")) or {}).get(
                          "bytes_per_launch"), "bytes_per_launch": b_alg, "avg_launch_ms": lbs_ms,
                      "note": "achieved = B_alg = N_r*(24+4J) bytes per pose (SURVEY.md 8(d) C5; N_r = this rank's "
-                             "points) / avg LBS kernel time (HIP events on the launch stream); the step also runs "
-                             "the skeleton kernel"},
+                             "points) / avg LBS kernel time (HIP events around a graph of 20 back-to-back LBS "
+                             "launches on the launch stream); the step also runs the skeleton kernel"},
         "cpu_baseline": cpu,
     }
     emit(line, args)
@@ -427,7 +440,7 @@ def main():
     else:
         kernel, peak, mfma_peak = "k_point_mlp_h3 (3-term fp16-split MFMA)", SPLIT3_PEAK_TFLOPS, FP16_MFMA_PEAK_TFLOPS
         peak_note = "peak = fp16 dense MFMA peak / 3 (three fp16 MFMA terms per fp32-accurate product)"
-    traffic = read_traffic(os.path.join(ROOT, "profiles", "r01_point_mlp_traffic.json"))
+    traffic = read_traffic(os.path.join(ROOT, "profiles", "r02_point_mlp_traffic.json"))
     ms_per_step = elapsed / args.steps * 1e3
     value = (1 if shard_rays else world) * args.steps * R / elapsed
     cpu = psnr = same = None
