@@ -260,6 +260,19 @@ def pack_mlp_weights(feat_net_layers, densitynet, rgbnet, pose_embedding=None, o
     return buf
 
 
+def fold_pose_bias(l1, pose_embedding, buf):
+    """Per-frame update of a packed buffer whose weights are unchanged: only b1 depends on the
+    pose embedding (temporalpoints.py:487-488, folded as in pack_mlp_weights). Also clears the
+    range flag, as the full pack's split does, so the guard is judged per frame."""
+    lay = mlp_layout()
+    n_emb, n_feat = 63, 128
+    w1 = l1.weight.detach().float()
+    b1 = l1.bias.detach().float() + (w1[:, n_emb + n_feat:] @ pose_embedding.reshape(-1, 1).float()).reshape(-1)
+    buf[lay["B1"]:lay["B1"] + b1.numel()].copy_(b1)
+    buf[lay["FLAG"]:lay["FLAG"] + 1].view(torch.int32).zero_()
+    return buf
+
+
 def mlp_range_fallback(wbuf) -> bool:
     """True if the fp16-split MLP kernel met a value outside the fp16 range with these packed
     weights (its range flag, apn_mlp_layout.h OFF_FLAG), so apn_point_mlp recomputed the launch on

@@ -628,18 +628,19 @@ class TemporalPoints(torch.nn.Module):
         (only the pose-embedding bias fold changes per frame)."""
         if len(self.feat_net) != 6:
             raise NotImplementedError("the fused MLP kernel implements feat_depth=4 (the reference default)")
-        from .ops import feat_project, mlp_layout
+        from .ops import feat_project, fold_pose_bias, mlp_layout
         layers = [self.feat_net[0], self.feat_net[2][0], self.feat_net[3][0], self.feat_net[4]]
         params = [p for l in layers for p in (l.weight, l.bias)] + list(self.densitynet.parameters()) + \
             list(self.rgbnet.parameters()) + [self.canonical_feat]
         key = tuple((p.data_ptr(), p._version) for p in params)
         buf = self._ws.get("mlp_w", mlp_layout()["TOTAL"], torch.float32, dev)
-        if key != getattr(self, "_pack_key", None) or pose_embedding is not None:
-            pack_mlp_weights(layers, self.densitynet, self.rgbnet, pose_embedding, out=buf)
         if key != getattr(self, "_pack_key", None):
+            pack_mlp_weights(layers, self.densitynet, self.rgbnet, pose_embedding, out=buf)
             proj = self._ws.get("feat_proj", self.canonical_feat.shape[0] * 128, torch.float32, dev)
             feat_project(self.canonical_feat, buf, out=proj.view(-1, 128))
             self._pack_key = key
+        elif pose_embedding is not None:   # same weights: only b1 follows the pose embedding
+            fold_pose_bias(layers[0], pose_embedding, buf)
         return buf, self._ws.bufs["feat_proj"]
 
     def forward(self, t, render_depth=False, render_kwargs=None, query_radius=0.01, render_weights=False,

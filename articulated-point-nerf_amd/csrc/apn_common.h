@@ -21,6 +21,31 @@ inline int launch_status() {
 
 inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
+// Stream-ordered int32 fill and copy as plain kernels rather than hipMemsetAsync /
+// hipMemcpyAsync, so a captured render frame holds kernel nodes only (the same node kind as
+// the repose graph, which replays back to back without fault).
+__global__ static void __launch_bounds__(256) k_fill_i32(int* __restrict__ p, int v, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = v;
+}
+__global__ static void __launch_bounds__(64) k_copy_i32(const int* __restrict__ src, int* __restrict__ dst, int n) {
+  for (int i = threadIdx.x; i < n; i += 64) dst[i] = src[i];
+}
+inline int fill_i32(int* p, int v, int64_t n, hipStream_t s) {
+  if (n <= 0) return APN_OK;
+  const int64_t nb = (n + 255) / 256;
+  hipLaunchKernelGGL(k_fill_i32, dim3((unsigned)(nb < 2048 ? nb : 2048)), dim3(256), 0, s, p, v, n);
+  return hipPeekAtLastError() == hipSuccess ? APN_OK : APN_ERR_HIP;
+}
+inline int copy_i32(const int* src, int* dst, int n, hipStream_t s) {
+  hipLaunchKernelGGL(k_copy_i32, dim3(1), dim3(64), 0, s, src, dst, n);
+  return hipPeekAtLastError() == hipSuccess ? APN_OK : APN_ERR_HIP;
+}
+#define APN_TRY(x)              \
+  do {                          \
+    int st_ = (x);              \
+    if (st_) return st_;        \
+  } while (0)
+
 // Order-preserving float <-> int mapping for atomicMin/atomicMax on floats.
 __device__ __forceinline__ int float_to_ordered(float f) {
   int i = __float_as_int(f);

@@ -78,7 +78,7 @@ extern "C" int apn_composite(const float* smp12, const float* s_pos4, const int3
   hipStream_t s = (hipStream_t)stream;
   int* beg = ray_ws;
   int* end = ray_ws + n_rays;
-  APN_HIP_TRY(hipMemsetAsync(ray_ws, 0, (size_t)n_rays * 2 * sizeof(int), s));
+  APN_TRY(fill_i32(ray_ws, 0, n_rays * 2, s));
   if (max_samples > 0)
     hipLaunchKernelGGL(k_ray_bounds, dim3(ceil_div(max_samples, 256)), dim3(256), 0, s, s_ray, n_samples_dev, beg,
                        end);

@@ -1685,8 +1685,8 @@ extern "C" int apn_grid_build(const float* xyz, int64_t n_points, const int32_t*
   if (n_points <= 0 || cell_cap <= 0 || !xyz || !bbox_ord || !sorted_pts4 || !workspace) return APN_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   GridWs w = grid_ws(workspace, n_points, cell_cap);
-  APN_HIP_TRY(hipMemsetAsync(w.counts, 0, (size_t)cell_cap * 4, s));
-  APN_HIP_TRY(hipMemsetAsync(w.cursor, 0, (size_t)cell_cap * 4, s));
+  APN_TRY(fill_i32(w.counts, 0, cell_cap, s));
+  APN_TRY(fill_i32(w.cursor, 0, cell_cap, s));
   static const int subdiv = [] {
     const char* e = getenv("APN_KNN_SUBDIV");
     return e ? atoi(e) : KNN_SUBDIV;
@@ -1723,7 +1723,7 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
   if (n_queries < 0 || !grid_workspace || !workspace) return APN_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   if (n_queries == 0) {
-    APN_HIP_TRY(hipMemsetAsync(n_survivors_dev, 0, 4, s));
+    APN_TRY(fill_i32(n_survivors_dev, 0, 1, s));
     return launch_status();
   }
   GridWs g = grid_ws((void*)grid_workspace, n_points, cell_cap);
@@ -1756,8 +1756,8 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
         const int v = e ? atoi(e) : 2;
         return (v == 1 || v == 2 || v == 4) ? v : 2;
       }();
-      APN_HIP_TRY(hipMemsetAsync(g.counts2, 0, (size_t)cell_cap * 4, s));
-      APN_HIP_TRY(hipMemsetAsync(g.cursor2, 0, (size_t)cell_cap * 4, s));
+      APN_TRY(fill_i32(g.counts2, 0, cell_cap, s));
+      APN_TRY(fill_i32(g.cursor2, 0, cell_cap, s));
       hipLaunchKernelGGL(k_agrid_params, dim3(1), dim3(64), 0, s, g.gp, f, g.ag);
       hipLaunchKernelGGL(k_agrid_count, dim3(ceil_div(n_points, 256)), dim3(256), 0, s, (const float4*)sorted_pts4,
                          n_points, g.gp, f, g.counts2, g.pcell2);
@@ -1774,9 +1774,9 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
     int* u1 = g.counts;          // free after the grid build
     int* u2 = g.tile_cnt;
     int* u4 = g.tile_cursor;
-    APN_HIP_TRY(hipMemsetAsync(mark, 0, (size_t)cell_cap * 4, s));
-    APN_HIP_TRY(hipMemsetAsync(g.n_tile_list, 0, 4, s));
-    APN_HIP_TRY(hipMemsetAsync(n_hard, 0, 4, s));
+    APN_TRY(fill_i32(mark, 0, cell_cap, s));
+    APN_TRY(fill_i32(g.n_tile_list, 0, 1, s));
+    APN_TRY(fill_i32(n_hard, 0, 1, s));
     hipLaunchKernelGGL(k_mark_cells, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, cblk_off + nb,
                        g.gp, ccell, mark);
     hipLaunchKernelGGL(k_tile_list, dim3(ceil_div(cell_cap, LIST_THREADS)), dim3(LIST_THREADS), 0, s, mark, cell_cap,
@@ -1785,7 +1785,7 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
                        dim3(KNN_THREADS), 0, s, g.gp, g.cell_start, g.tile_list, g.n_tile_list, u1, u2, u4);
     int* hard_r = ccell + slots;          // second quarter of the t_pos region
     int* n_hard_r = cblk_off + nb + 1;    // cblk_off has nb + 2 entries
-    APN_HIP_TRY(hipMemsetAsync(n_hard_r, 0, 4, s));
+    APN_TRY(fill_i32(n_hard_r, 0, 1, s));
     static const bool a_aniso = getenv("APN_KNN_A_ANISO") != nullptr;   // A/B: pass A's r/4 ball on the second grid
     hipLaunchKernelGGL((aniso && a_aniso) ? k_knn_pass_a8<true> : k_knn_pass_a8<false>, dim3(nb), dim3(KNN_THREADS), 0,
                        s, (const float4*)q_pos4, cand, cblk_off + nb, g.gp, g.cell_start, (const float4*)sorted_pts4,
@@ -1819,7 +1819,7 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
     if (st) return st;
     hipLaunchKernelGGL(k_knn_flag_compact, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, q_ray, cand,
                        cblk_off + nb, flag, t_nbr, blk_off, (float4*)s_pos4, s_ray, s_nbr);
-    APN_HIP_TRY(hipMemcpyAsync(n_survivors_dev, blk_off + nb, 4, hipMemcpyDeviceToDevice, s));
+    APN_TRY(copy_i32(blk_off + nb, n_survivors_dev, 1, s));
     return launch_status();
   }
   if (knn_mode() == 6 || knn_mode() == 7) {
@@ -1829,9 +1829,9 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
     int* ccell = (int*)t_pos;
     int* mark = g.cursor;        // free after the grid build
     int* ubound = g.counts;      // free after the grid build
-    APN_HIP_TRY(hipMemsetAsync(mark, 0, (size_t)cell_cap * 4, s));
-    APN_HIP_TRY(hipMemsetAsync(g.n_tile_list, 0, 4, s));
-    APN_HIP_TRY(hipMemsetAsync(n_hard, 0, 4, s));
+    APN_TRY(fill_i32(mark, 0, cell_cap, s));
+    APN_TRY(fill_i32(g.n_tile_list, 0, 1, s));
+    APN_TRY(fill_i32(n_hard, 0, 1, s));
     hipLaunchKernelGGL(k_mark_cells, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, cblk_off + nb,
                        g.gp, ccell, mark);
     hipLaunchKernelGGL(k_tile_list, dim3(ceil_div(cell_cap, LIST_THREADS)), dim3(LIST_THREADS), 0, s, mark, cell_cap,
@@ -1851,16 +1851,16 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
     if (st) return st;
     hipLaunchKernelGGL(k_knn_flag_compact, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, q_ray, cand,
                        cblk_off + nb, flag, t_nbr, blk_off, (float4*)s_pos4, s_ray, s_nbr);
-    APN_HIP_TRY(hipMemcpyAsync(n_survivors_dev, blk_off + nb, 4, hipMemcpyDeviceToDevice, s));
+    APN_TRY(copy_i32(blk_off + nb, n_survivors_dev, 1, s));
     return launch_status();
   }
   if (knn_mode() == 5) {
     int* flag = t_ray;
     int* order = cand_blk;
     int* ctile = (int*)t_pos;
-    APN_HIP_TRY(hipMemsetAsync(g.tile_cnt, 0, (size_t)cell_cap * 4, s));
-    APN_HIP_TRY(hipMemsetAsync(g.tile_cursor, 0, (size_t)cell_cap * 4, s));
-    APN_HIP_TRY(hipMemsetAsync(g.n_tile_list, 0, 4, s));
+    APN_TRY(fill_i32(g.tile_cnt, 0, cell_cap, s));
+    APN_TRY(fill_i32(g.tile_cursor, 0, cell_cap, s));
+    APN_TRY(fill_i32(g.n_tile_list, 0, 1, s));
     hipLaunchKernelGGL(k_tile_count, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, cblk_off + nb,
                        g.gp, ctile, g.tile_cnt);
     st = scan_exclusive_i32(g.tile_cnt, g.tile_start, cell_cap, g.scan, s);
@@ -1877,14 +1877,14 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
     if (st) return st;
     hipLaunchKernelGGL(k_knn_flag_compact, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, q_ray, cand,
                        cblk_off + nb, flag, t_nbr, blk_off, (float4*)s_pos4, s_ray, s_nbr);
-    APN_HIP_TRY(hipMemcpyAsync(n_survivors_dev, blk_off + nb, 4, hipMemcpyDeviceToDevice, s));
+    APN_TRY(copy_i32(blk_off + nb, n_survivors_dev, 1, s));
     return launch_status();
   }
   if (knn_mode() == 4) {
     int* flag = t_ray;              // per candidate slot
     int* hard = cand_blk;           // free after the candidate compaction
     int* n_hard = cblk_cnt + nb + 1;
-    APN_HIP_TRY(hipMemsetAsync(n_hard, 0, 4, s));
+    APN_TRY(fill_i32(n_hard, 0, 1, s));
     hipLaunchKernelGGL(k_knn_pass_a, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, cblk_off + nb,
                        g.gp, g.cell_start, (const float4*)sorted_pts4, flag, t_nbr, hard, n_hard);
     hipLaunchKernelGGL(k_knn_pass_b, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard, n_hard,
@@ -1894,7 +1894,7 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
     if (st) return st;
     hipLaunchKernelGGL(k_knn_flag_compact, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, q_ray, cand,
                        cblk_off + nb, flag, t_nbr, blk_off, (float4*)s_pos4, s_ray, s_nbr);
-    APN_HIP_TRY(hipMemcpyAsync(n_survivors_dev, blk_off + nb, 4, hipMemcpyDeviceToDevice, s));
+    APN_TRY(copy_i32(blk_off + nb, n_survivors_dev, 1, s));
     return launch_status();
   }
   if (knn_mode() == 3)
@@ -1909,7 +1909,7 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
   if (st) return st;
   hipLaunchKernelGGL(k_knn_compact, dim3(nb), dim3(KNN_THREADS), 0, s, t_pos, t_ray, t_nbr, blk_cnt, blk_off,
                      (float4*)s_pos4, s_ray, s_nbr);
-  APN_HIP_TRY(hipMemcpyAsync(n_survivors_dev, blk_off + nb, 4, hipMemcpyDeviceToDevice, s));
+  APN_TRY(copy_i32(blk_off + nb, n_survivors_dev, 1, s));
   return launch_status();
 }
 

@@ -105,7 +105,7 @@ size_t scan_workspace_bytes(int64_t n) {
 
 int scan_exclusive_i32(const int* in, int* out, int64_t n, void* ws, hipStream_t s) {
   if (n <= 0) {
-    APN_HIP_TRY(hipMemsetAsync(out, 0, sizeof(int), s));
+    APN_TRY(fill_i32(out, 0, 1, s));
     return launch_status();
   }
   int nb = ceil_div(n, SCAN_TILE);
