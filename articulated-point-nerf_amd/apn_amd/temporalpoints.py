@@ -503,7 +503,8 @@ class TemporalPoints(torch.nn.Module):
         step.graph, step.inputs = graph, rp
         return step
 
-    def capture_frame(self, t, render_kwargs, render_depth=True, render_weights=True, query_radius=0.01):
+    def capture_frame(self, t, render_kwargs, render_depth=True, render_weights=True, query_radius=0.01, poses=None,
+                      Ks=None, get_skeleton=False):
         """The render frame for a fixed ray set (skeleton, LBS, grid, sampling, kNN, MLP,
         compositing: the whole no-grad forward) captured once in a HIP graph: returns
         ``step(t) -> RenderOutput``, which copies the time into the graph's input and replays it.
@@ -511,12 +512,15 @@ class TemporalPoints(torch.nn.Module):
         frame they are validated on first read (one read of the device frame_info) and a frame
         whose samples overflowed the capacity is rendered again eagerly. Needs no host sync inside
         the frame: the capacity is set by the warm-up frames. Capture again after changing the
-        model or the rays."""
+        model or the rays. ``get_skeleton`` (with fixed ``poses`` / ``Ks``) captures the joint
+        projection too, as the eager forward runs it."""
         dev = self.canonical_feat.device
         t_in = torch.as_tensor(t, dtype=torch.float32, device=dev).reshape(-1).clone()
         rk = dict(render_kwargs)
         R = len(rk['rays_o'])
-        args = (render_depth, rk, query_radius, render_weights, None, None, None, True, False, None)
+        if get_skeleton:
+            poses, Ks = poses.to(dev), Ks.to(dev, torch.float32)   # device-resident before the capture
+        args = (render_depth, rk, query_radius, render_weights, None, poses, Ks, True, get_skeleton, None)
         with torch.no_grad():
             side = torch.cuda.Stream(dev)
             side.wait_stream(torch.cuda.current_stream(dev))

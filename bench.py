@@ -286,11 +286,9 @@ def main():
                     help="N>1: 'rays' (default) = the ranks split one frame's rays and all-gather the tiles "
                          "over RCCL (strong scaling, SURVEY.md 8(e)); 'frames' = every rank renders its own "
                          "frame (weak scaling, no data-path collective)")
-    ap.add_argument("--graph", choices=["auto", "on", "off"], default="off",
+    ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                     help="replay the frame as one HIP graph (TemporalPoints.capture_frame); auto = on unless "
-                         "the ranks split one frame's rays (the split is read on the host). Off by default: "
-                         "a C2 replay sequence faulted on the box (under investigation); the eager frame is "
-                         "already free of host syncs")
+                         "the ranks split one frame's rays (the split is read on the host)")
     args = ap.parse_args()
     torch.set_grad_enabled(False)   # a render benchmark: the reference renders under no_grad (run.py:80, 241)
 
@@ -342,7 +340,7 @@ def main():
     stats = model.last_stats.resolved()
     log(f"[rank {rank}] scene: {stats}")
     if use_graph:   # the whole frame as one HIP graph replay (no per-kernel host launches, no host sync)
-        graph_step = model.capture_frame(t_arg, rk)
+        graph_step = model.capture_frame(t_arg, rk, poses=poses, Ks=Ks, get_skeleton=True)
         step = lambda: graph_step(t_arg)   # noqa: E731
         for _ in range(2):
             step()

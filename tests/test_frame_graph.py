@@ -77,3 +77,27 @@ def test_captured_frame_equals_eager(dev):
         ref = _frame(model, t, rk)
         for k in KEYS:
             assert torch.equal(got[k], ref[k]), k
+
+
+def test_captured_frame_back_to_back(dev):
+    """Consecutive replays with no eager frame in between (bench --graph on). Round 2 saw these
+    fault on the second replay while the captured frame still held memset / memcpy nodes and the
+    full per-frame weight repack; the frame now captures kernel nodes only (apn_common.h fill_i32 /
+    copy_i32) and repacks only the pose-folded b1."""
+    scene, model = _scene_model(dev)
+    rk = scene.render_kwargs(dev)
+    ts = [torch.tensor([scene.cfg.t + 0.05 * i], device=dev) for i in range(4)]
+    poses, Ks = scene.c2w[None].to(dev), scene.K[None].to(dev)
+    step = model.capture_frame(ts[0], rk, poses=poses, Ks=Ks, get_skeleton=True)   # the bench's frame
+    kept = []
+    for i in range(12):
+        g = step(ts[i % 4])
+        torch.cuda.synchronize()
+        if i >= 8:
+            kept.append({k: g[k].clone() for k in KEYS + ("joints",)})
+    for i, got in enumerate(kept):
+        with torch.no_grad():
+            ref = model(ts[(8 + i) % 4], render_depth=True, render_kwargs=rk, render_weights=True, poses=poses,
+                        Ks=Ks, get_skeleton=True)
+        for k in KEYS + ("joints",):
+            assert torch.equal(got[k], ref[k]), (i, k)
