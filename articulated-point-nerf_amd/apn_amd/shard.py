@@ -18,19 +18,63 @@ TILE_KEYS = (("rgb_marched", 3), ("rgb_marched_direct", 3), ("depth", 1), ("weig
 TILE_WIDTH = sum(w for _, w in TILE_KEYS)
 
 
-def balanced_ray_split(offsets: torch.Tensor, world: int) -> list[int]:
-    """Ray boundaries b[0]=0 <= ... <= b[world]=R such that rank k's rays [b[k], b[k+1]) hold
-    ~total/world in-bbox samples. ``offsets`` is the exclusive prefix sum of per-ray sample
-    counts ([R+1], offsets[R] = total), on any device; one small device->host copy."""
+def split_inner(offsets: torch.Tensor, world: int) -> torch.Tensor:
+    """The world - 1 inner ray boundaries of the balanced split, on the offsets' device (no host
+    read): rank k's rays [b[k], b[k+1]) hold ~total/world in-bbox samples."""
     R = offsets.numel() - 1
     total = offsets[R:R + 1].to(torch.int64)
     k = torch.arange(1, world, device=offsets.device, dtype=torch.int64)
     targets = (total * k + world // 2) // world
-    inner = torch.searchsorted(offsets[:R + 1].to(torch.int64).contiguous(), targets.contiguous())
-    b = [0] + [min(max(int(x), 0), R) for x in inner.cpu().tolist()] + [R]
-    for i in range(1, len(b)):  # monotone even for degenerate inputs
+    return torch.searchsorted(offsets[:R + 1].to(torch.int64).contiguous(), targets.contiguous())
+
+
+def bounds_from_inner(inner, R: int) -> list[int]:
+    """[0, *inner, R] clamped to [0, R] and made monotone (degenerate inputs)."""
+    b = [0] + [min(max(int(x), 0), R) for x in inner] + [R]
+    for i in range(1, len(b)):
         b[i] = max(b[i], b[i - 1])
     return b
+
+
+def balanced_ray_split(offsets: torch.Tensor, world: int) -> list[int]:
+    """Ray boundaries b[0]=0 <= ... <= b[world]=R such that rank k's rays [b[k], b[k+1]) hold
+    ~total/world in-bbox samples. ``offsets`` is the exclusive prefix sum of per-ray sample
+    counts ([R+1], offsets[R] = total), on any device; one small device->host copy."""
+    return bounds_from_inner(split_inner(offsets, world).cpu().tolist(), offsets.numel() - 1)
+
+
+class SplitTracker:
+    """Sync-free ray split for consecutive sharded frames of one (ray count, world): the first
+    frame reads its balanced split on the host; every frame then computes the split of its own
+    sample counts on the device and copies it to pinned host memory without waiting, and the next
+    frame uses it (one frame stale, which only moves the balance, never the result: any contiguous
+    split assembles the same frame). By the time the next frame asks, the device has long passed
+    that copy, so the event wait costs no device idle; every rank switches at the same frame, and
+    identical inputs give identical splits on every rank."""
+
+    def __init__(self):
+        self.bounds = None
+        self._host = None
+        self._event = None
+
+    def bounds_for(self, offsets: torch.Tensor, world: int, advance: bool = True) -> list[int]:
+        """advance=False (a frame rendered again after an overflow) keeps the current split, so the
+        re-rendered range is the one the frame was gathered with."""
+        R = offsets.numel() - 1
+        if self.bounds is None:
+            self.bounds = balanced_ray_split(offsets, world)
+        elif not advance:
+            return self.bounds
+        elif self._event is not None:
+            self._event.synchronize()
+            self.bounds = bounds_from_inner(self._host.tolist(), R)
+        if world > 1 and offsets.is_cuda:
+            if self._host is None:
+                self._host = torch.empty(world - 1, dtype=torch.int64, pin_memory=True)
+            self._host.copy_(split_inner(offsets, world), non_blocking=True)
+            self._event = torch.cuda.Event()
+            self._event.record()
+        return self.bounds
 
 
 def pack_tile(out: dict, n_rays: int, device) -> torch.Tensor:
@@ -54,34 +98,104 @@ def unpack_tile(tile: torch.Tensor) -> dict:
     return out
 
 
-def gather_tiles(tile: torch.Tensor, bounds: list[int], group=None) -> torch.Tensor:
+def gather_tiles(tile: torch.Tensor, bounds: list[int], group=None, info: torch.Tensor | None = None):
     """All-gather variable-length ray tiles (padded to the longest range) and concatenate
-    them in ray order -> [R, TILE_WIDTH] on every rank."""
+    them in ray order -> [R, TILE_WIDTH] on every rank. With ``info`` (this rank's int32 frame_info
+    [4], see apn_inbbox_fill_capped) one more row per rank carries it through the same
+    collective: returns (tiles, infos [world, 4] int32)."""
     import torch.distributed as dist
     world = len(bounds) - 1
     lens = [bounds[i + 1] - bounds[i] for i in range(world)]
     m = max(max(lens), 1)
-    padded = torch.zeros(m, tile.shape[1], device=tile.device, dtype=tile.dtype)
+    rows = m + (1 if info is not None else 0)
+    padded = torch.zeros(rows, tile.shape[1], device=tile.device, dtype=tile.dtype)
     padded[:tile.shape[0]] = tile
-    full = torch.empty(world * m, tile.shape[1], device=tile.device, dtype=tile.dtype)
+    if info is not None:
+        padded[m, :4] = info.to(torch.int32).view(torch.float32)
+    full = torch.empty(world * rows, tile.shape[1], device=tile.device, dtype=tile.dtype)
     if dist.get_backend(group) == "gloo":
-        dist.all_gather(list(full.view(world, m, -1).unbind(0)), padded, group=group)
+        dist.all_gather(list(full.view(world, rows, -1).unbind(0)), padded, group=group)
     else:
         dist.all_gather_into_tensor(full, padded, group=group)
-    return torch.cat([full[i * m:i * m + lens[i]] for i in range(world)], dim=0)
+    tiles = torch.cat([full[i * rows:i * rows + lens[i]] for i in range(world)], dim=0)
+    if info is None:
+        return tiles
+    return tiles, full.view(world, rows, -1)[:, m, :4].contiguous().view(torch.int32)
+
+
+class ShardedFrame(dict):
+    """The assembled frame of render_sharded. Ranks on the sync-free path may have dropped samples
+    past their capacity; every rank's frame_info rode along in the all-gather, and the first read
+    of any key checks them (one device read): if a rank overflowed, the frame is rendered again
+    on this rank alone, exactly (no collective, so it is safe whichever ranks read the frame)."""
+
+    def __init__(self, *a, infos=None, rerender=None, **kw):
+        super().__init__(*a, **kw)
+        self._infos = infos
+        self._rerender = rerender
+
+    def _resolve(self):
+        if self._infos is None:
+            return
+        infos, self._infos = self._infos, None
+        if bool((infos[:, 2] != 0).any()):
+            fresh = self._rerender(infos)
+            dict.update(self, fresh)
+
+    def __getitem__(self, k):
+        self._resolve()
+        return super().__getitem__(k)
+
+    def get(self, k, default=None):
+        self._resolve()
+        return super().get(k, default)
+
+    def keys(self):
+        self._resolve()
+        return super().keys()
+
+    def items(self):
+        self._resolve()
+        return super().items()
+
+    def __contains__(self, k):
+        self._resolve()
+        return super().__contains__(k)
+
+    def raw(self, k, default=None):
+        return super().get(k, default)
 
 
 @torch.no_grad()
 def render_sharded(model, t, render_kwargs, rank: int, world: int, group=None, **forward_kwargs) -> dict:
     """One frame rendered by ``world`` ranks: this rank's ray range through
     TemporalPoints.forward(ray_shard=(rank, world)), then the tile all-gather. Returns the
-    reference output keys for all rays on every rank."""
+    reference output keys for all rays on every rank (a ShardedFrame, validated on first read)."""
     out = model(t, render_kwargs=render_kwargs, ray_shard=(rank, world), render_depth=True,
                 render_weights=True, **forward_kwargs)
     r0, r1 = model.last_ray_range
-    tile = pack_tile(out, r1 - r0, render_kwargs["rays_o"].device)
-    full = gather_tiles(tile, model.last_ray_bounds, group) if world > 1 else tile
+    dev = render_kwargs["rays_o"].device
+    tile = pack_tile(out, r1 - r0, dev)
+    info = getattr(out, "_info", None)
+    if world > 1:
+        if info is None:   # exact path: nothing was dropped
+            info = torch.zeros(4, dtype=torch.int32, device=dev)
+        full, infos = gather_tiles(tile, model.last_ray_bounds, group, info=info)
+    else:
+        full, infos = tile, (info.view(1, 4) if info is not None else None)
     res = unpack_tile(full)
     for k in ("t_hat_pcd", "joints", "bones"):
-        res[k] = out.get(k)
-    return res
+        res[k] = out.raw(k) if hasattr(out, "raw") else out.get(k)
+
+    def rerender(infos):
+        # grow this rank's capacity from its in-bbox total (frame_info[1]) for the frames to come
+        from .temporalpoints import _grow_capacity
+        key = (render_kwargs["rays_o"].shape[0], rank, world)
+        model._capacity[key] = max(model._capacity.get(key, 0), _grow_capacity(int(infos[rank, 1])))
+        model._force_exact = True
+        try:
+            whole = model(t, render_kwargs=render_kwargs, render_depth=True, render_weights=True, **forward_kwargs)
+            return {k: whole.get(k) for k, _ in TILE_KEYS} | {k: whole.get(k) for k in ("t_hat_pcd", "joints", "bones")}
+        finally:
+            model._force_exact = False
+    return ShardedFrame(res, infos=infos, rerender=rerender)

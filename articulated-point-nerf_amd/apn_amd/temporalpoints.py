@@ -22,7 +22,7 @@ from . import _lib as L
 from ._lib import call, ptr, stream_ptr
 from .ops import Workspace, pack_mlp_weights
 from .pointwarper import PointWarper
-from .shard import balanced_ray_split
+from .shard import SplitTracker
 from .tineuvox import poc_fre
 
 CELL_CAP = int(os.environ.get("APN_CELL_CAP", 1 << 20))
@@ -306,7 +306,8 @@ class TemporalPoints(torch.nn.Module):
         self.palette_perm_device = None   # None: the weights' device (reference behaviour)
         self.timing = None          # set to {} to record HIP-event timings of the MLP launch
         self.last_stats = FrameStats()
-        self._capacity = {}         # ray count -> in-bbox sample capacity of the sync-free render path
+        self._capacity = {}         # ray count (or shard) -> in-bbox sample capacity of the sync-free render path
+        self._splits = {}           # (ray count, world) -> SplitTracker of the ray-sharded frames
         self._force_exact = False
         self._last_info = None
 
@@ -768,10 +769,13 @@ class TemporalPoints(torch.nn.Module):
         offs = ws.get("offs", R + 1, torch.int32, dev)
         sws = ws.bytes("samp_ws", lib.apn_sample_pts_on_rays_workspace_bytes(R), dev)
         call("apn_inbbox_count", ptr(ro), ptr(rd), ptr(bbox6), near, far, stepdist, R, ptr(offs), ptr(sws), s)
+        cap_key = R
         if shard is not None:
-            # contiguous ray range holding ~1/world of the in-bbox samples
+            # contiguous ray range holding ~1/world of the in-bbox samples; after
+            # the first frame, the split of the previous frame's counts (no host sync, shard.py)
             rank, world = shard
-            bounds = balanced_ray_split(offs, world)
+            bounds = self._splits.setdefault((R, world), SplitTracker()).bounds_for(offs, world, advance=not self._force_exact)
+            cap_key = (R, rank, world)
             r0, r1 = bounds[rank], bounds[rank + 1]
             self.last_ray_range = (r0, r1)
             self.last_ray_bounds = bounds
@@ -782,16 +786,15 @@ class TemporalPoints(torch.nn.Module):
         # a capacity from it; later frames keep the count on the device -- buffers and launch
         # bounds use the capacity, apn_inbbox_fill_capped drops samples past it and reports an
         # overflow, which RenderOutput checks when the frame is first read (and then renders the
-        # frame again on this exact path). A ray shard reads its split on the host anyway.
-        cap = self._capacity.get(R) if (shard is None and not self._force_exact) else None
+        # frame again on this exact path); a ray shard's capacity is keyed by its rank.
+        cap = None if self._force_exact else self._capacity.get(cap_key)
         info = None
         if cap is None:
             n_bbox = int(offs[R].item())
             self.last_stats = FrameStats({"rays": R, "inbbox_samples": n_bbox})
             if n_bbox == 0:
                 raise NoPointsException("No points.")
-            if shard is None:
-                self._capacity[R] = max(self._capacity.get(R, 0), _grow_capacity(n_bbox))
+            self._capacity[cap_key] = max(self._capacity.get(cap_key, 0), _grow_capacity(n_bbox))
             Q = n_bbox
             q_pos = ws.get("q_pos", Q * 4, torch.float32, dev)
             q_ray = ws.get("q_ray", Q, torch.int32, dev)

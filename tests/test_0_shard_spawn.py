@@ -26,6 +26,11 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def _assembled(out, R, dev):
+    from apn_amd.shard import TILE_KEYS
+    return torch.cat([out[k].reshape(R, w).float() for k, w in TILE_KEYS], dim=1).cpu()   # validated reads
+
+
 def _worker(rank, world, port, outdir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     import torch.distributed as dist
@@ -37,18 +42,27 @@ def _worker(rank, world, port, outdir):
         scene = S.make_scene(S.SceneConfig("spawn shard 200x200 50k pts 24 bones", 50_000, 24, 200, 200))
         model = harness.build_model(scene, dev)
         rk = scene.render_kwargs(dev)
-        t = torch.tensor([scene.cfg.t], device=dev)
+        R = rk["rays_o"].shape[0]
+        t0 = torch.tensor([scene.cfg.t], device=dev)
+        t1 = torch.tensor([scene.cfg.t + 0.1], device=dev)
         poses, Ks = scene.c2w[None].to(dev), scene.K[None].to(dev)
+        kw = dict(poses=poses, Ks=Ks, get_skeleton=True)
+        tiles = {}
         with torch.no_grad():
-            out = render_sharded(model, t, rk, rank, world, poses=poses, Ks=Ks, get_skeleton=True)
-            R = rk["rays_o"].shape[0]
-            tiles = {"assembled": pack_tile(out, R, dev).cpu(),
-                     "range": torch.tensor(model.last_ray_range),
-                     "bounds": torch.tensor(model.last_ray_bounds)}
+            # frame 0: exact path (split and sample count read on the host); frames 1-2: the
+            # sync-free path (previous frame's split, per-rank capacity); frame 3: rank 1 overflows
+            # its capacity, which every rank must detect through the gathered frame_info rows
+            for i, t in enumerate((t0, t1, t0, t1)):
+                if i == 3 and rank == 1:
+                    model._capacity[(R, rank, world)] = 64
+                out = render_sharded(model, t, rk, rank, world, **kw)
+                tiles[f"assembled{i}"] = _assembled(out, R, dev)
+                tiles[f"range{i}"] = torch.tensor(model.last_ray_range)
+                tiles[f"bounds{i}"] = torch.tensor(model.last_ray_bounds)
             if rank == 0:
-                single = model(t, render_depth=True, render_kwargs=rk, render_weights=True, poses=poses, Ks=Ks,
-                               get_skeleton=True)
-                tiles["single"] = pack_tile(single, R, dev).cpu()
+                for i, t in enumerate((t0, t1)):
+                    single = model(t, render_depth=True, render_kwargs=rk, render_weights=True, **kw)
+                    tiles[f"single{i}"] = pack_tile(single, R, dev).cpu()
         torch.cuda.synchronize()
         torch.save(tiles, os.path.join(outdir, f"rank{rank}.pt"))
     finally:
@@ -60,12 +74,13 @@ def test_render_sharded_two_processes_bit_identical():
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker, args=(WORLD, _free_port(), d), nprocs=WORLD, join=True)
         res = [torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=True) for r in range(WORLD)]
-    single = res[0]["single"]
-    bounds = res[0]["bounds"].tolist()
-    assert bounds[0] == 0 and bounds[-1] == single.shape[0]
-    assert torch.equal(res[1]["bounds"], res[0]["bounds"])
-    for r in range(WORLD):
-        assert tuple(res[r]["range"].tolist()) == (bounds[r], bounds[r + 1])
-        assert torch.equal(res[r]["assembled"], single), r
-    # both ranks did real work (the object is hit by rays of both halves of the split)
-    assert 0 < bounds[1] < single.shape[0]
+    for i in range(4):
+        single = res[0][f"single{i % 2}"]
+        bounds = res[0][f"bounds{i}"].tolist()
+        assert bounds[0] == 0 and bounds[-1] == single.shape[0]
+        assert torch.equal(res[1][f"bounds{i}"], res[0][f"bounds{i}"]), i   # every rank on the same split
+        for r in range(WORLD):
+            assert tuple(res[r][f"range{i}"].tolist()) == (bounds[r], bounds[r + 1])
+            assert torch.equal(res[r][f"assembled{i}"], single), (i, r)
+        # both ranks did real work (the object is hit by rays of both halves of the split)
+        assert 0 < bounds[1] < single.shape[0]

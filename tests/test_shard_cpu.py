@@ -114,3 +114,41 @@ def test_point_shards_partition_the_cloud(world):
     assert torch.equal(torch.cat([p[0] for p in parts]), full.canonical_pcd)
     assert torch.equal(torch.cat([p[1] for p in parts]), full.weights.detach())
     assert torch.equal(torch.cat([p[2] for p in parts]), full.canonical_feat.detach())
+
+
+def _worker_info(rank, world, port, result_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        bounds = [0, 3, 7]
+        full = torch.arange(7 * TILE_WIDTH, dtype=torch.float32).reshape(7, TILE_WIDTH)
+        info = torch.tensor([10 + rank, 20 + rank, rank, 30 + rank], dtype=torch.int32)
+        got, infos = gather_tiles(full[bounds[rank]:bounds[rank + 1]].clone(), bounds, info=info)
+        want = torch.tensor([[10, 20, 0, 30], [11, 21, 1, 31]], dtype=torch.int32)
+        result_q.put((rank, bool(torch.equal(got, full)), bool(torch.equal(infos, want))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_tiles_carries_frame_info_gloo_world2():
+    """The per-rank frame_info row rides in the same all-gather (ShardedFrame's overflow check)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_info, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert res == [(0, True, True), (1, True, True)]
+
+
+def test_split_tracker_cpu_keeps_first_split():
+    """Off the GPU there is no async copy: the tracker keeps the first frame's balanced split."""
+    from apn_amd.shard import SplitTracker
+    tr = SplitTracker()
+    a = tr.bounds_for(_offsets([5, 0, 3, 9, 1, 4]), 2)
+    b = tr.bounds_for(_offsets([0, 0, 0, 0, 30, 1]), 2)
+    assert a == b == balanced_ray_split(_offsets([5, 0, 3, 9, 1, 4]), 2)

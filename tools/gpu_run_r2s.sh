@@ -1,6 +1,3 @@
 source tools/gpu_steps.sh
-step bench 300 python -u bench.py --steps 20 --warmup 3 -o gpurun_out/bench20.json
-python3 -c "
-import json
-d=json.load(open('gpurun_out/bench20.json')); print(d['value']/1e6, d['ms_per_step'], d['config']['step'], d['stage_ms'], d['cpu_baseline'], d.get('same_cloud_vs_oracle'))"
-step ab_c5 300 bash tools/ab_c5.sh "APN_AB=cur" "APN_HIP_LIB=ab/nt/libapn_hip.so"
+step shard_tests 400 python -u -m pytest tests/test_0_shard_spawn.py tests/test_frame_graph.py -x -v --timeout 300 --timeout-method thread
+step bench_gloo2 400 env APN_DIST_BACKEND=gloo python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --no-cpu-baseline --steps 10 -o gpurun_out/r2s_gloo2.json
