@@ -1010,6 +1010,49 @@ def test_train_step_with_optimizer_reduces_loss(dev):
 
 
 @pytest.mark.autograd
+def test_render_after_hip_optimizer_steps_uses_new_weights(dev):
+    """The HIP Adam kernels write parameters in place; the render path caches packed weights on
+    (data_ptr, _version) -- the MLP pack + per-point projection (TemporalPoints._packed_weights)
+    and the TransformNet pack (PointWarper) -- so apn_amd.optim bumps the versions. After MaskedAdam
+    steps, a no_grad render must equal a freshly built model carrying the same weights bit for bit
+    (and differ from the render before the steps)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "articulated-point-nerf_amd"))
+    from apn_amd import harness, synthetic as S
+    from apn_amd.optim import MaskedAdam
+    scene = S.make_scene("C1")
+    model = harness.build_model(scene, dev)
+    rk = scene.render_kwargs(dev)
+    t = torch.tensor([scene.cfg.t], device=dev)
+    with torch.no_grad():
+        before = model(t, render_kwargs=rk)["rgb_marched"].clone()   # fills every packed-weight cache
+    params = list(model.feat_net.parameters()) + list(model.forward_warp.parameters())
+    if model.canonical_feat.requires_grad:
+        params.append(model.canonical_feat)
+    opt = MaskedAdam([{"params": params, "lr": 1e-2, "skip_zero_grad": False}])
+    gen = torch.Generator().manual_seed(1)
+    sel = torch.randint(0, len(rk["rays_o"]), (2048,), generator=gen).to(dev)
+    sub = dict(rk)
+    for k in ("rays_o", "rays_d", "viewdirs"):
+        sub[k] = rk[k][sel]
+    for _ in range(3):
+        opt.zero_grad(set_to_none=True)
+        out = model(t, False, sub, render_pcd_direct=False)
+        (out["rgb_marched"] - 0.5).pow(2).mean().backward()
+        opt.step()
+    with torch.no_grad():
+        after = model(t, render_kwargs=rk)["rgb_marched"].clone()
+    fresh = harness.build_model(scene, dev)
+    fresh.load_state_dict(model.state_dict())
+    with torch.no_grad():
+        ref = fresh(t, render_kwargs=rk)["rgb_marched"]
+    assert not torch.equal(after, before)
+    assert torch.equal(after, ref)
+
+
+@pytest.mark.autograd
 @pytest.mark.parametrize("J", [8, 24, 48])
 def test_lbs_train_kernel_vs_torch_autograd(dev, J):
     """apn_lbs_train_fwd/_bwd (LBSTrain) vs the torch autograd composition it replaces
