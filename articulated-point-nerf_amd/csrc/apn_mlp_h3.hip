@@ -368,7 +368,12 @@ template <int P>
 __device__ __forceinline__ void ws_gather_q(int nb, float4 q, const GatherRegs& G, char* __restrict__ PE,
                                             float* __restrict__ sTo, float* __restrict__ sRow,
                                             float* __restrict__ sV, const float* __restrict__ vemb_const) {
-  const int r = threadIdx.x & 63, s = r >> 3, k = r & 7;
+  // the lane index through an opaque asm: the per-lane LDS addresses below are then recomputed
+  // in each tile (a few VALU) instead of hoisted out of the loop for all four quarter cases and
+  // spilled to scratch (reloads that wait in vmcnt order behind the gather's loads)
+  int r_ = threadIdx.x & 63;
+  asm volatile("" : "+v"(r_));
+  const int r = r_, s = r >> 3, k = r & 7;
   char* xr = PE + r * XB;
   const int c_sin = (2 * P) ^ (r & 15), c_cos = (2 * P + 1) ^ (r & 15);
   if (nb >= 0) {
@@ -546,16 +551,16 @@ __device__ __forceinline__ void mlp_tiles(
   // row 0, zeroed before layer 1)
   f32x4 acc[4][2];
   bool pok[4];
-  auto load_p = [&]() {
+  auto load_p = [&](const int (&pn)[4], const bool (&pk)[4]) {
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
-      pok[mt] = pf_pok[mt];
+      pok[mt] = pk[mt];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
 #ifdef APN_H3_PROBE_NOP   // timing probe only (wrong results): no P-row gather
-        const float4 v = make_float4(0.f, 0.f, 0.f, pf_pn[mt] < 0 ? 1.f : 0.f);
+        const float4 v = make_float4(0.f, 0.f, 0.f, pn[mt] < 0 ? 1.f : 0.f);
 #else
-        const float4 v = pproj[(size_t)max(pf_pn[mt], 0) * (FEAT / 4) + 4 * (ot0 + j) + g];
+        const float4 v = pproj[(size_t)max(pn[mt], 0) * (FEAT / 4) + 4 * (ot0 + j) + g];
 #endif
         acc[mt][j] = f32x4{v.x, v.y, v.z, v.w};
       }
@@ -576,7 +581,17 @@ __device__ __forceinline__ void mlp_tiles(
     // every load issued before it, so loads issued earlier (e.g. the next tile's P after layer 4,
     // measured +1.6 %) hold up the weight-fragment waits in between.
     ws_gather_load(wid, nb, pf_ray, gregs, recA, recB, viewdirs, vemb_const);
-    load_p();
+    int pn_tile[4];   // this tile's P-row indices (fetch below overwrites pf_pn with the next tile's)
+    bool pok_tile[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) { pn_tile[mt] = pf_pn[mt]; pok_tile[mt] = pf_pok[mt]; }
+    fetch(tile + per_xcd);
+    // ------------------------------------------------ gather + posenc + direct-blend terms
+    ws_gather(wid, nb, q, gregs, X0, sTo, sRow, sV, vemb_const);
+    // layer-1 accumulators = P[nbr] (global -> VGPR), loaded after the gather's register peak:
+    // held across it they pushed the kernel past its 168-VGPR budget (20 VGPRs spilled, their
+    // reloads waiting in vmcnt order behind the gather's loads); measured 7.28 -> 6.92 ms
+    load_p(pn_tile, pok_tile);
     if (SCALED) {   // layer-1 accumulators in the W1E scale: 2^s1 P
       const float sc1 = sW[SW_SC];
 #pragma unroll
@@ -584,9 +599,6 @@ __device__ __forceinline__ void mlp_tiles(
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[mt][j] = acc[mt][j] * sc1;
     }
-    fetch(tile + per_xcd);
-    // ------------------------------------------------ gather + posenc + direct-blend terms
-    ws_gather(wid, nb, q, gregs, X0, sTo, sRow, sV, vemb_const);
     __syncthreads();
     APN_PHASE(0)
     // ------------------------------------------------ outputs of the previous tile

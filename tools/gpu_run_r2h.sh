@@ -1,8 +1,4 @@
 source tools/gpu_steps.sh
-export AB_STEPS=10
-step tests 600 python -u -m pytest tests/test_mlp_precision.py tests/test_hip_parity.py -m gpu -q -x -rf --timeout 300 --timeout-method thread -k "mlp or precision or same_cloud or golden" > gpurun_out/gpu_tests9.log 2>&1
-tail -2 gpurun_out/gpu_tests9.log
-step ab 900 bash tools/ab.sh "APN_AB=cur" "APN_MLP_VARIANT=3" "APN_MLP_OCC=2"
-grep -h "mlp phases" gpurun_out/ab/run2.err || true
-step bench_r1 300 bash -c 'cd ab/r1 && python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline > ../../gpurun_out/bench9_r1.json 2> ../../gpurun_out/bench9_r1.err'
-python3 -c "import json; d=json.load(open('gpurun_out/bench9_r1.json')); print('r1', d['ms_per_step'], d['stage_ms'])"
+export AB_STEPS=20
+step parity_nhpa 300 env APN_HIP_LIB=ab/nhpa/libapn_hip.so python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "mlp or forward_vs_oracle"
+step ab 900 bash tools/ab.sh "APN_AB=cur" "APN_HIP_LIB=ab/nh/libapn_hip.so" "APN_HIP_LIB=ab/nhp/libapn_hip.so" "APN_HIP_LIB=ab/nhpa/libapn_hip.so" "APN_AB=cur2" "APN_HIP_LIB=ab/nhp/libapn_hip.so" "APN_HIP_LIB=ab/nh/libapn_hip.so"
