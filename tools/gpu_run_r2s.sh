@@ -1,3 +1,7 @@
 source tools/gpu_steps.sh
-step shard_tests 400 python -u -m pytest tests/test_0_shard_spawn.py tests/test_frame_graph.py -x -v --timeout 300 --timeout-method thread
-step bench_gloo2 400 env APN_DIST_BACKEND=gloo python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --no-cpu-baseline --steps 10 -o gpurun_out/r2s_gloo2.json
+step tests 900 python -u -m pytest tests -m gpu -q -x -rf --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_s.log 2>&1
+tail -3 gpurun_out/gpu_tests_s.log
+step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+step bench 300 python -u bench.py -o gpurun_out/bench_s.json
+step bench_c5 300 python -u bench.py --config C5 --no-cpu-baseline -o gpurun_out/bench_s_c5.json
+step rocprof 400 bash tools/bench_rocprof.sh gpurun_out/prof_s

@@ -1,14 +1,19 @@
-# Helper for GPU calls: `step NAME TIMEOUT CMD...` runs one GPU step under its own time limit and
-# stops the whole call on a crash / abort / time limit (rc >= 124 or a signal); test failures
-# (rc 1) and usage errors (rc 2..) let the call continue. Source from a gpurun command script.
-set -o pipefail
+#!/bin/bash
+# Sourced by the tools/gpu_run_*.sh scripts on the GPU box.
+#   step <name> <seconds> <command...>
+# runs one GPU step under its own time limit and ends the script on any failure
+# (fault, abort, time limit): no further GPU step runs in that call.
+cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 mkdir -p gpurun_out
 step() {
-  local name=$1 lim=$2; shift 2
-  echo "== $name"
-  timeout -k 10 "$lim" "$@"
+  local name=$1 secs=$2; shift 2
+  local t0=$(date +%s)
+  echo "[step $name] start (limit ${secs}s)"
+  timeout -k 10 "$secs" "$@"
   local rc=$?
-  echo "== $name rc=$rc"
-  if [ $rc -ge 124 ]; then echo "== stopping after $name (rc=$rc)"; exit $rc; fi
-  return 0
+  echo "[step $name] rc=$rc after $(( $(date +%s) - t0 ))s"
+  if [ $rc -ne 0 ]; then
+    echo "[step $name] FAILED: stopping this call"
+    exit $rc
+  fi
 }
