@@ -160,11 +160,17 @@ class PointWarper(torch.nn.Module):
             self._tree_key = key
         return self._tree
 
-    def pose(self, joints, t=None, rot_params=None, global_t=None):
+    def pose(self, joints, t=None, rot_params=None, global_t=None, time_poc=None, proj=None):
         """Skeleton stage of forward (pointwarper.py:216-239) as one HIP launch
-        (apn_skeleton_pose): returns bone_Ts [J,4,4], global_t [3] and joints_rel [J,3]; the
+        (apn_skeleton_frame): returns bone_Ts [J,4,4], global_t [3] and joints_rel [J,3]; the
         bone rows [J,12] for apn_lbs_skin are kept in ``last_T34``. Sets prev_params /
-        prev_thetas / prev_global_t."""
+        prev_thetas / prev_global_t.
+
+        ``time_poc`` given: ``t`` is the raw time [1] and its embedding poc_fre(t, time_poc)
+        (tineuvox.py:872-878) is computed in the same launch. ``proj=(c2w [P,4,4], K [P,3,3])``:
+        the skeleton projection project_point_to_image_plane(joints_rel + global_t, c2w, K)
+        (temporalpoints.py:578-583) runs in the launch too, left in ``last_joints2d`` [P,J,2]
+        (None when not requested or beyond the kernel's limits: the caller projects in torch)."""
         assert (t is None) ^ (rot_params is None)
         dev = joints.device
         L.require_cuda(joints, what="PointWarper.pose")
@@ -177,24 +183,51 @@ class PointWarper(torch.nn.Module):
         gt = torch.empty(3, device=dev)
         joints_rel = torch.empty(J, 3, device=dev)
         s = stream_ptr(dev)
+        c2w = Km = j2d = None
+        n_views = 0
+        if proj is not None:
+            c2w, Km = proj
+            n_views = c2w.shape[0]
+            if 0 < n_views <= 16 and n_views * J <= 1024 and tuple(c2w.shape[1:]) == (4, 4) and \
+                    tuple(Km.shape) == (n_views, 3, 3):
+                c2w = c2w.to(dev, torch.float32).contiguous()
+                Km = Km.to(dev, torch.float32).contiguous()
+                j2d = torch.empty(n_views, J, 2, device=dev)
+            else:
+                c2w = Km = None
+                n_views = 0
+        params = None
         if rot_params is None:
             tn, t_dim, hidden, n_layers = self._tn_packed(dev)
-            te = t.detach().float().reshape(-1).contiguous()
             params = torch.empty(J + 1, 4, device=dev)
-            call("apn_skeleton_pose", ptr(te), te.numel(), None, 4, J, ptr(tn), hidden, n_layers, ptr(jts), ptr(pi),
-                 pi.shape[1], ptr(pjx), ptr(sib), ptr(rmask), ptr(params), ptr(thetas), ptr(bone_Ts), ptr(T34),
-                 ptr(gt), ptr(joints_rel), ptr(prog), s)
+            if time_poc is not None:
+                tr = torch.as_tensor(t, dtype=torch.float32, device=dev).reshape(-1)
+                if tr.numel() != 1 or 1 + 2 * time_poc.numel() != t_dim:
+                    raise ValueError("PointWarper.pose: raw t must be one time and match the TransformNet input")
+                poc = time_poc.detach().to(dev, torch.float32).contiguous()
+                call("apn_skeleton_frame", ptr(tr), ptr(poc), poc.numel(), None, 4, J, ptr(tn), hidden, n_layers,
+                     ptr(jts), ptr(pi), pi.shape[1], ptr(pjx), ptr(sib), ptr(rmask), ptr(params), ptr(thetas),
+                     ptr(bone_Ts), ptr(T34), ptr(gt), ptr(joints_rel), ptr(prog), ptr(c2w), ptr(Km), n_views, ptr(j2d),
+                     s)
+            else:
+                te = t.detach().float().reshape(-1).contiguous()   # t is already the time embedding
+                call("apn_skeleton_pose", ptr(te), te.numel(), None, 4, J, ptr(tn), hidden, n_layers, ptr(jts),
+                     ptr(pi), pi.shape[1], ptr(pjx), ptr(sib), ptr(rmask), ptr(params), ptr(thetas), ptr(bone_Ts),
+                     ptr(T34), ptr(gt), ptr(joints_rel), ptr(prog), s)
+                j2d = None
             self.prev_params = params
             self.prev_global_t = gt
         else:
             rp = rot_params.detach().float().contiguous()
-            call("apn_skeleton_pose", None, 0, ptr(rp), rp.shape[-1], J, None, 0, 0, ptr(jts), ptr(pi), pi.shape[1],
-                 ptr(pjx), ptr(sib), ptr(rmask), None, ptr(thetas), ptr(bone_Ts), ptr(T34), ptr(gt), ptr(joints_rel),
-                 ptr(prog), s)
+            call("apn_skeleton_frame", None, None, 0, ptr(rp), rp.shape[-1], J, None, 0, 0, ptr(jts), ptr(pi),
+                 pi.shape[1], ptr(pjx), ptr(sib), ptr(rmask), None, ptr(thetas), ptr(bone_Ts), ptr(T34), ptr(gt),
+                 ptr(joints_rel), ptr(prog), ptr(c2w), ptr(Km), n_views, ptr(j2d), s)
             if global_t is not None:
                 gt = global_t
+                j2d = None   # projected with the kernel's zero global_t: the caller projects in torch
         self.prev_thetas = thetas
         self.last_T34 = T34
+        self.last_joints2d = j2d
         return bone_Ts, gt, joints_rel
 
     def pose_torch(self, joints, t=None, rot_params=None, global_t=None):

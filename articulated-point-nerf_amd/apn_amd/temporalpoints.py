@@ -675,20 +675,31 @@ class TemporalPoints(torch.nn.Module):
                         calc_min_max, get_skeleton, ray_shard):
         dev = self.canonical_feat.device
         L.require_cuda(self.canonical_feat, what="TemporalPoints.forward")
-        t_embed = poc_fre(t, self.time_poc) if rot_params is None else None
-        bone_Ts, global_t, joints_rel = self.forward_warp.pose(self.joints, t_embed, rot_params)
+        # skeleton stage: time embedding, TransformNet, chain and (get_skeleton) the joint projection
+        # in one launch (apn_skeleton_frame)
+        proj = (poses, Ks) if get_skeleton else None
+        tt = None if rot_params is not None else torch.as_tensor(t, dtype=torch.float32, device=dev).reshape(-1)
+        if tt is not None and tt.numel() == 1:
+            bone_Ts, global_t, joints_rel = self.forward_warp.pose(self.joints, tt, None, time_poc=self.time_poc,
+                                                                   proj=proj)
+        else:
+            t_embed = poc_fre(t, self.time_poc) if rot_params is None else None
+            bone_Ts, global_t, joints_rel = self.forward_warp.pose(self.joints, t_embed, rot_params, proj=proj)
         colors = self._joint_colors(dev) if render_weights else None
         self._mark("frame")
         t_hat_pcd, weights, recs = self._lbs(bone_Ts, global_t, records=True, colors=colors,
                                              T34=self.forward_warp.last_T34)
         self._mark("lbs")
         self._last_weights = weights
-        delta_joint = (self.joints - joints_rel).clone().detach()
-        pose_embedding = (self.pose_embedding_net(poc_fre(delta_joint, self.pos_poc).view(1, -1))
-                          if self.pose_embedding_dim > 0 else None)
+        pose_embedding = None
+        if self.pose_embedding_dim > 0:
+            delta_joint = (self.joints - joints_rel).clone().detach()
+            pose_embedding = self.pose_embedding_net(poc_fre(delta_joint, self.pos_poc).view(1, -1))
         joints = bones = None
         if get_skeleton:
-            joints = project_point_to_image_plane(joints_rel + global_t, poses.to(dev), Ks.to(dev, torch.float32))
+            joints = self.forward_warp.last_joints2d
+            if joints is None:
+                joints = project_point_to_image_plane(joints_rel + global_t, poses.to(dev), Ks.to(dev, torch.float32))
             bones = self.bones
             if self.joints_to_keep is not None:
                 joints = joints[:, self.joints_to_keep]

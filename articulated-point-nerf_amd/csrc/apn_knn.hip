@@ -1538,17 +1538,21 @@ __global__ void k_knn_points(const float* __restrict__ q, int64_t M, const GridP
   }
 }
 
-// Pass B of mode 9: k_knn_pass_b8 with the r/2 and r balls on the anisotropic grid.
+// Pass B of mode 9: k_knn_pass_b8 with the r/2 and r balls on the anisotropic grid. One launch
+// over both hard lists (first list first: the host passes the heavier r list there, so the
+// longest waves start first and the two lists share one tail); hard2 == nullptr: one list.
 template <bool STATS, int PTS>
 __global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_b9(
     const float4* __restrict__ q_pos, const int* __restrict__ cand, const int* __restrict__ hard,
-    const int* __restrict__ n_hard, const AGrid* __restrict__ agp, const int* __restrict__ cell_start2,
-    const float4* __restrict__ sorted2, int* __restrict__ flag, int* __restrict__ t_nbr) {
+    const int* __restrict__ n_hard, const int* __restrict__ hard2, const int* __restrict__ n_hard2,
+    const AGrid* __restrict__ agp, const int* __restrict__ cell_start2, const float4* __restrict__ sorted2,
+    int* __restrict__ flag, int* __restrict__ t_nbr) {
   const int i = blockIdx.x * KNN_THREADS + threadIdx.x;
-  if (i >= *n_hard) return;
+  const int n1 = *n_hard, n2 = hard2 ? *n_hard2 : 0;
+  if (i >= n1 + n2) return;
   const AGrid g = *agp;
   unsigned c2[2] = {0, 0}, cr[2] = {0, 0};
-  const int hc = hard[i];
+  const int hc = i < n1 ? hard[i] : hard2[i - n1];
   const int c = hc >> 1;
   const float4 q = q_pos[cand[c]];
   float bd[KNN_K];
@@ -1803,10 +1807,19 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
       }();
       auto pass_b = stats ? (pts == 4 ? k_knn_pass_b9<true, 4> : k_knn_pass_b9<true, 2>)
                           : (pts == 4 ? k_knn_pass_b9<false, 4> : k_knn_pass_b9<false, 2>);
-      hipLaunchKernelGGL(pass_b, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard, n_hard,
-                         g.ag, g.cell_start2, g.sorted2, flag, t_nbr);
-      hipLaunchKernelGGL(pass_b, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard_r,
-                         n_hard_r, g.ag, g.cell_start2, g.sorted2, flag, t_nbr);
+      static const bool split = [] {   // A/B: APN_KNN_B_SPLIT=1 runs the two lists as two launches
+        const char* e = getenv("APN_KNN_B_SPLIT");
+        return e && atoi(e) == 1;
+      }();
+      if (split) {
+        hipLaunchKernelGGL(pass_b, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard, n_hard,
+                           nullptr, nullptr, g.ag, g.cell_start2, g.sorted2, flag, t_nbr);
+        hipLaunchKernelGGL(pass_b, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard_r,
+                           n_hard_r, nullptr, nullptr, g.ag, g.cell_start2, g.sorted2, flag, t_nbr);
+      } else {   // n_hard + n_hard_r <= candidates <= nb * KNN_THREADS
+        hipLaunchKernelGGL(pass_b, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard_r,
+                           n_hard_r, hard, n_hard, g.ag, g.cell_start2, g.sorted2, flag, t_nbr);
+      }
     } else {
       auto pass_b = stats ? k_knn_pass_b8<true> : k_knn_pass_b8<false>;
       hipLaunchKernelGGL(pass_b, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard, n_hard,

@@ -1,17 +1,25 @@
 // Skeleton stage of PointWarper.forward (pointwarper.py:213-239) in one workgroup:
+//   [time embedding poc_fre(t) (tineuvox.py:872-878), optional]
 //   TransformNet (pointwarper.py:5-37, 17 -> 256 x4 (ReLU) -> (J+1)*4, last layer without bias)
 //   -> Rodrigues (118-143) -> sibling / rotation masks (230-236)
 //   -> M_j = [R_j | p - R_j p] about the parent joint p (167-172)
 //   -> kinematic chain as the reference's recursive-halving matrix product (145-153, 173-175)
-//   -> joints_rel = T_j [joint_j; 1] (258-260).
-// The reference runs this as ~100 tiny torch launches per frame; here it is one launch (GEMV
-// layers read 0.9 MB of transposed, coalesced weights once; the chain products run from LDS).
+//   -> joints_rel = T_j [joint_j; 1] (258-260)
+//   -> [skeleton projection of joints_rel + global_t into the views (temporalpoints.py:578-583,
+//       utils.py:435-450), optional].
+// The reference runs this as ~100 tiny torch launches per frame; here it is one launch. The GEMV
+// layers read 0.9 MB of transposed, coalesced weights once, split over 4 K-slices (1024 threads:
+// a quarter of the dependent load batches per thread -- the stage is load-latency bound); the chain
+// products run from LDS.
 #include "apn_common.h"
 
 namespace apn {
 
-constexpr int SK_THREADS = 256;
+constexpr int SK_THREADS = 1024;
+constexpr int SK_OUT = 256;                      // max GEMV width (hidden, (J+1)*4, t_dim)
+constexpr int SK_SLICES = SK_THREADS / SK_OUT;   // K-slices per output feature
 constexpr int SK_MAX_J = 64;
+constexpr int SK_MAX_VIEWS = 16;
 constexpr int SK_MAX_DEPTH = 32;
 constexpr int SK_STACK = 8;   // recursion depth of the halving tree for chains <= 32 factors: ceil(log2 32) + 1
 
@@ -52,8 +60,13 @@ __global__ __launch_bounds__(SK_THREADS) void k_skeleton_pose(
     const int* __restrict__ parent_indices, int depth, const int* __restrict__ parent_joint_ex,
     const int* __restrict__ sibling_mask, const int* __restrict__ rot_mask, float* __restrict__ params_out,
     float* __restrict__ thetas_out, float* __restrict__ bone_T16, float* __restrict__ bone_T34,
-    float* __restrict__ global_t_out, float* __restrict__ joints_rel_out, const int* __restrict__ chain_prog) {
-  __shared__ float h[2][SK_THREADS];
+    float* __restrict__ global_t_out, float* __restrict__ joints_rel_out, const int* __restrict__ chain_prog,
+    const float* __restrict__ time_poc, int n_freq, const float* __restrict__ c2w, const float* __restrict__ Kmat,
+    int n_views, float* __restrict__ joints2d_out) {
+  __shared__ float h[2][SK_OUT];
+  __shared__ float sPart[SK_SLICES][SK_OUT];
+  __shared__ float sInv[SK_MAX_VIEWS][12];
+  __shared__ float sJw[SK_MAX_J][3];
   __shared__ float sP[SK_MAX_J + 1][4];
   __shared__ float sR[SK_MAX_J][9];
   __shared__ float sM[SK_MAX_J + 1][16];
@@ -70,25 +83,42 @@ __global__ __launch_bounds__(SK_THREADS) void k_skeleton_pose(
     sNProg = chain_program(depth, sProg, sFrames);   // overlaps the GEMVs
   }
   if (tpath) {
-    // TransformNet: one output feature per thread (hidden <= 256), k summed in order
-    if (tid < t_dim) h[0][tid] = t_embed[tid];
+    // time embedding (tineuvox.py:872-878): [t, sin(t f_0..f_F-1), cos(t f_0..f_F-1)]
+    if (tid < t_dim) {
+      if (time_poc) {
+        const float t = t_embed[0];
+        h[0][tid] = tid == 0 ? t : (tid <= n_freq ? sinf(t * time_poc[tid - 1]) : cosf(t * time_poc[tid - 1 - n_freq]));
+      } else {
+        h[0][tid] = t_embed[tid];
+      }
+    }
     __syncthreads();
+    // TransformNet: output feature o = tid % 256 over K-slice tid / 256 (each slice summed in k
+    // order), the slices added pairwise
     const float* w = tnw;
+    const int o = tid % SK_OUT, sl = tid / SK_OUT;
     int in_dim = t_dim, cur = 0;
     for (int l = 0; l < n_layers; ++l) {
       const bool last = l == n_layers - 1;
       const int out_dim = last ? (J + 1) * 4 : hidden;
+      const int kper = (in_dim + SK_SLICES - 1) / SK_SLICES;
+      const int k0 = sl * kper, k1 = min(in_dim, k0 + kper);
+      float a = 0.f;
+      if (o < out_dim) {
+        const float* wc = w + o;
+#pragma unroll 16
+        for (int k = k0; k < k1; ++k) a += wc[(size_t)k * out_dim] * h[cur][k];
+      }
+      sPart[sl][o] = a;
+      __syncthreads();
       if (tid < out_dim) {
-        const float* wc = w + tid;
-        float a = 0.f;
-#pragma unroll 8
-        for (int k = 0; k < in_dim; ++k) a += wc[(size_t)k * out_dim] * h[cur][k];
+        float v = (sPart[0][tid] + sPart[1][tid]) + (sPart[2][tid] + sPart[3][tid]);
         if (!last) {
-          a += w[(size_t)out_dim * in_dim + tid];
-          h[cur ^ 1][tid] = fmaxf(a, 0.f);
+          v += w[(size_t)out_dim * in_dim + tid];
+          h[cur ^ 1][tid] = fmaxf(v, 0.f);
         } else {
-          sP[tid >> 2][tid & 3] = a;
-          params_out[tid] = a;
+          sP[tid >> 2][tid & 3] = v;
+          params_out[tid] = v;
         }
       }
       w += (size_t)out_dim * in_dim + (last ? 0 : out_dim);
@@ -99,6 +129,33 @@ __global__ __launch_bounds__(SK_THREADS) void k_skeleton_pose(
   } else {
     if (tid < J * rot_dim) sP[tid / rot_dim][tid % rot_dim] = rot_params[tid];
     __syncthreads();
+  }
+  // inverse of each view's camera-to-world matrix (torch.inverse, utils.py:437), Gauss-Jordan with
+  // partial pivoting in double on threads the Rodrigues step leaves idle; rows 0-2 kept
+  if (tid >= SK_OUT && tid < SK_OUT + n_views) {
+    const int v = tid - SK_OUT;
+    double A[4][8];
+    for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < 4; ++j) {
+        A[i][j] = c2w[16 * v + 4 * i + j];
+        A[i][4 + j] = i == j ? 1.0 : 0.0;
+      }
+    for (int c = 0; c < 4; ++c) {
+      int p = c;
+      for (int i = c + 1; i < 4; ++i)
+        if (fabs(A[i][c]) > fabs(A[p][c])) p = i;
+      if (p != c)
+        for (int j = 0; j < 8; ++j) { const double tt = A[c][j]; A[c][j] = A[p][j]; A[p][j] = tt; }
+      const double inv = 1.0 / A[c][c];
+      for (int j = 0; j < 8; ++j) A[c][j] *= inv;
+      for (int i = 0; i < 4; ++i)
+        if (i != c) {
+          const double f = A[i][c];
+          for (int j = 0; j < 8; ++j) A[i][j] -= f * A[c][j];
+        }
+    }
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 4; ++j) sInv[v][4 * i + j] = (float)A[i][4 + j];
   }
   // Rodrigues (pointwarper.py:118-143), thetas = prev_thetas
   if (tid < J) {
@@ -177,16 +234,64 @@ __global__ __launch_bounds__(SK_THREADS) void k_skeleton_pose(
     for (int e = 0; e < 16; ++e) bone_T16[16 * tid + e] = T[e];
     for (int e = 0; e < 12; ++e) bone_T34[12 * tid + e] = T[e];
     const float jx = joints[3 * tid], jy = joints[3 * tid + 1], jz = joints[3 * tid + 2];
-    joints_rel_out[3 * tid + 0] = ((T[0] * jx + T[1] * jy) + T[2] * jz) + T[3];
-    joints_rel_out[3 * tid + 1] = ((T[4] * jx + T[5] * jy) + T[6] * jz) + T[7];
-    joints_rel_out[3 * tid + 2] = ((T[8] * jx + T[9] * jy) + T[10] * jz) + T[11];
+    float jr[3];
+    jr[0] = ((T[0] * jx + T[1] * jy) + T[2] * jz) + T[3];
+    jr[1] = ((T[4] * jx + T[5] * jy) + T[6] * jz) + T[7];
+    jr[2] = ((T[8] * jx + T[9] * jy) + T[10] * jz) + T[11];
+    for (int e = 0; e < 3; ++e) {
+      joints_rel_out[3 * tid + e] = jr[e];
+      sJw[tid][e] = jr[e] + (tpath ? sP[J][e] : 0.f);   // joints_rel + global_t (temporalpoints.py:580)
+    }
   }
   if (tid < 3) global_t_out[tid] = tpath ? sP[J][tid] : 0.f;
+  if (n_views > 0) {
+    // project_point_to_image_plane (utils.py:435-450): x_cam = inv(c2w)[:3,:3] x + inv(c2w)[:3,3],
+    // x_img = K x_cam, (u, v) = x_img[:2] / x_img[2]
+    __syncthreads();
+    if (tid < J * n_views) {
+      const int v = tid / J, j = tid % J;
+      const float* I = sInv[v];
+      const float* Kv = Kmat + 9 * v;
+      const float wx = sJw[j][0], wy = sJw[j][1], wz = sJw[j][2];
+      float pc[3], q[3];
+      for (int i = 0; i < 3; ++i) pc[i] = ((I[4 * i] * wx + I[4 * i + 1] * wy) + I[4 * i + 2] * wz) + I[4 * i + 3];
+      for (int i = 0; i < 3; ++i) q[i] = (Kv[3 * i] * pc[0] + Kv[3 * i + 1] * pc[1]) + Kv[3 * i + 2] * pc[2];
+      joints2d_out[2 * tid + 0] = q[0] / q[2];
+      joints2d_out[2 * tid + 1] = q[1] / q[2];
+    }
+  }
 }
 
 }  // namespace apn
 
 using namespace apn;
+
+extern "C" int apn_skeleton_frame(const float* t, const float* time_poc, int32_t n_freq, const float* rot_params,
+                                  int32_t rot_dim, int32_t n_joints, const float* tn_weights, int32_t hidden,
+                                  int32_t n_layers, const float* joints, const int32_t* parent_indices, int32_t depth,
+                                  const int32_t* parent_joint_ex, const int32_t* sibling_mask, const int32_t* rot_mask,
+                                  float* params_out, float* thetas_out, float* bone_T16, float* bone_T34,
+                                  float* global_t_out, float* joints_rel_out, const int32_t* chain_prog,
+                                  const float* c2w, const float* K, int32_t n_views, float* joints2d_out,
+                                  void* stream) {
+  const bool tpath = rot_params == nullptr;
+  const int t_dim = 1 + 2 * n_freq;
+  if (n_joints <= 0 || n_joints > SK_MAX_J || depth <= 0 || depth > SK_MAX_DEPTH || !joints || !parent_indices ||
+      !parent_joint_ex || !thetas_out || !bone_T16 || !bone_T34 || !global_t_out || !joints_rel_out)
+    return APN_ERR_ARG;
+  if (tpath && (!t || !time_poc || !tn_weights || !params_out || n_freq < 0 || t_dim > SK_OUT || hidden <= 0 ||
+                hidden > SK_OUT || n_layers < 2 || (n_joints + 1) * 4 > SK_OUT))
+    return APN_ERR_ARG;
+  if (!tpath && rot_dim != 3 && rot_dim != 4) return APN_ERR_ARG;
+  if (n_views < 0 || n_views > SK_MAX_VIEWS || n_joints * n_views > SK_THREADS ||
+      (n_views > 0 && (!c2w || !K || !joints2d_out)))
+    return APN_ERR_ARG;
+  hipLaunchKernelGGL(k_skeleton_pose, dim3(1), dim3(SK_THREADS), 0, (hipStream_t)stream, t, t_dim, rot_params,
+                     rot_dim, n_joints, tn_weights, hidden, n_layers, joints, parent_indices, depth, parent_joint_ex,
+                     sibling_mask, rot_mask, params_out, thetas_out, bone_T16, bone_T34, global_t_out,
+                     joints_rel_out, chain_prog, time_poc, n_freq, c2w, K, n_views, joints2d_out);
+  return launch_status();
+}
 
 extern "C" int apn_skeleton_pose(const float* t_embed, int32_t t_dim, const float* rot_params, int32_t rot_dim,
                                  int32_t n_joints, const float* tn_weights, int32_t hidden, int32_t n_layers,
@@ -199,14 +304,14 @@ extern "C" int apn_skeleton_pose(const float* t_embed, int32_t t_dim, const floa
   if (n_joints <= 0 || n_joints > SK_MAX_J || depth <= 0 || depth > SK_MAX_DEPTH || !joints || !parent_indices ||
       !parent_joint_ex || !thetas_out || !bone_T16 || !bone_T34 || !global_t_out || !joints_rel_out)
     return APN_ERR_ARG;
-  if (tpath && (!t_embed || !tn_weights || !params_out || t_dim <= 0 || t_dim > SK_THREADS || hidden <= 0 ||
-                hidden > SK_THREADS || n_layers < 2 || (n_joints + 1) * 4 > SK_THREADS))
+  if (tpath && (!t_embed || !tn_weights || !params_out || t_dim <= 0 || t_dim > SK_OUT || hidden <= 0 ||
+                hidden > SK_OUT || n_layers < 2 || (n_joints + 1) * 4 > SK_OUT))
     return APN_ERR_ARG;
   if (!tpath && rot_dim != 3 && rot_dim != 4) return APN_ERR_ARG;
 
   hipLaunchKernelGGL(k_skeleton_pose, dim3(1), dim3(SK_THREADS), 0, (hipStream_t)stream, t_embed, t_dim, rot_params,
                      rot_dim, n_joints, tn_weights, hidden, n_layers, joints, parent_indices, depth, parent_joint_ex,
                      sibling_mask, rot_mask, params_out, thetas_out, bone_T16, bone_T34, global_t_out,
-                     joints_rel_out, chain_prog);
+                     joints_rel_out, chain_prog, nullptr, 0, nullptr, nullptr, 0, nullptr);
   return launch_status();
 }

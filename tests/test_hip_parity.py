@@ -393,6 +393,43 @@ def test_skeleton_pose_vs_torch_with_masks(golden_model, dev, path):
     assert (th_a - th_b).abs().max() < 1e-6
 
 
+@pytest.mark.parametrize("path", ["t", "rot4"])
+def test_skeleton_frame_time_embedding_and_projection(golden_model, dev, path):
+    """apn_skeleton_frame: the time embedding poc_fre(t) computed in the launch (t path) and the
+    skeleton projection of joints_rel + global_t into 3 views (temporalpoints.py:578-583) vs the
+    torch expressions (torch sin/cos embedding -> apn_skeleton_pose; torch.inverse + bmm)."""
+    from apn_amd.temporalpoints import project_point_to_image_plane
+    from apn_amd.tineuvox import poc_fre
+    g, m = golden_model
+    pw = m.forward_warp
+    J = m.joints.shape[0]
+    gen = torch.Generator().manual_seed(3)
+    c2w = g.t("in_c2w")[None].repeat(3, 1, 1).clone()
+    c2w[1, :3, 3] += torch.tensor([0.1, -0.2, 0.05])
+    ang = 0.3
+    rz = torch.tensor([[np.cos(ang), -np.sin(ang), 0.0], [np.sin(ang), np.cos(ang), 0.0], [0.0, 0.0, 1.0]],
+                      dtype=torch.float32)
+    c2w[2, :3, :3] = rz @ c2w[2, :3, :3]
+    Ks = g.t("in_K")[None].repeat(3, 1, 1).clone()
+    Ks[2, 0, 0] *= 1.1
+    c2w, Ks = c2w.to(dev), Ks.to(dev)
+    if path == "t":
+        t = g.t("in_t").to(dev).reshape(1)
+        a = pw.pose(m.joints.detach(), t, time_poc=m.time_poc, proj=(c2w, Ks))
+        j2d = pw.last_joints2d.clone()
+        b = pw.pose(m.joints.detach(), poc_fre(t, m.time_poc))
+    else:
+        rp = (torch.randn(J, 4, generator=gen) * 0.3).to(dev)
+        a = pw.pose(m.joints.detach(), rot_params=rp, proj=(c2w, Ks))
+        j2d = pw.last_joints2d.clone()
+        b = pw.pose(m.joints.detach(), rot_params=rp)
+    for x, y in zip(a, b):
+        assert (x - y).abs().max() < 2e-6
+    ref = project_point_to_image_plane(b[2] + b[1], c2w, Ks)
+    assert j2d.shape == (3, J, 2)
+    assert (j2d - ref).abs().max() < 1e-3   # pixels (the golden joints bar)
+
+
 @torch.no_grad()
 def _forward(g, m, dev):
     return m(g.t("in_t").to(dev), render_depth=True, render_kwargs=g.render_kwargs(dev), render_weights=True,
