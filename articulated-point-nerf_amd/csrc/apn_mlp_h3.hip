@@ -504,6 +504,7 @@ __device__ __forceinline__ void mlp_tiles(
   if (tid < 192) sW[SW_WV2 + tid] = wbuf[OFF_WV2 + tid];
   if (tid < 3) sW[SW_BV2 + tid] = wbuf[OFF_BV2 + tid];
   if (tid == 0) sW[SW_BD] = wbuf[OFF_BD];
+  if (SCALED) __syncthreads();   // the first tile reads the layer-1 scale before its first barrier
   // XCD-aware tile order (as apn_mlp.hip): XCD x = block % 8 walks a contiguous tile range, so
   // neighbouring samples (which share neighbour points) gather through the same L2.
   const int nx = (gridDim.x % 8 == 0) ? 8 : 1;
