@@ -307,6 +307,9 @@ class TemporalPoints(torch.nn.Module):
         self.timing = None          # set to {} to record HIP-event timings of the MLP launch
         self.last_stats = FrameStats()
         self._capacity = {}         # ray count (or shard) -> in-bbox sample capacity of the sync-free render path
+        # kNN grid build on a side stream, concurrent with the sampling (APN_CONCURRENT_GRID=0: serial)
+        self.concurrent_grid = os.environ.get("APN_CONCURRENT_GRID", "1") != "0"
+        self._side_streams = {}
         self._splits = {}           # (ray count, world) -> SplitTracker of the ray-sharded frames
         self._force_exact = False
         self._last_info = None
@@ -771,10 +774,24 @@ class TemporalPoints(torch.nn.Module):
         else:
             bbox6 = torch.cat([self.xyz_min, self.xyz_max]).float().contiguous()
         self._mark("bbox")
-        # kNN grid over the warped cloud
+        # kNN grid over the warped cloud. Outside stage timing it runs on a side stream, concurrently
+        # with the in-bbox sampling below (neither reads the other's output; joined before the kNN),
+        # so the grid build's short launches overlap the sampling's (also inside a captured frame)
         gws = ws.bytes("grid_ws", lib.apn_grid_workspace_bytes(N, CELL_CAP), dev)
         sorted4 = ws.get("sorted4", N * 4, torch.float32, dev)
-        call("apn_grid_build", ptr(xyz), N, ptr(bbox_ord), qr, CELL_CAP, ptr(sorted4), ptr(gws), s)
+        side = None
+        if self.timing is None and self.concurrent_grid:
+            cur = torch.cuda.current_stream(dev)
+            side = self._side_streams.get(dev)
+            if side is None:
+                side = self._side_streams[dev] = torch.cuda.Stream(dev)
+            side.wait_stream(cur)
+            xyz.record_stream(side)
+            with torch.cuda.stream(side):
+                call("apn_grid_build", ptr(xyz), N, ptr(bbox_ord), qr, CELL_CAP, ptr(sorted4), ptr(gws),
+                     stream_ptr(dev))
+        else:
+            call("apn_grid_build", ptr(xyz), N, ptr(bbox_ord), qr, CELL_CAP, ptr(sorted4), ptr(gws), s)
         self._mark("grid")
         # in-bbox samples
         offs = ws.get("offs", R + 1, torch.int32, dev)
@@ -824,6 +841,8 @@ class TemporalPoints(torch.nn.Module):
             nsurv = info[3:]
             self.last_stats = FrameStats({"rays": R}, info=info)
         self._mark("sampling")
+        if side is not None:
+            cur.wait_stream(side)
         # radius kNN + compaction of survivors
         s_pos = ws.get("s_pos", Q * 4, torch.float32, dev)
         s_ray = ws.get("s_ray", Q, torch.int32, dev)

@@ -1,4 +1,4 @@
 source tools/gpu_steps.sh
-step bench_c5 300 python -u bench.py --config C5 --steps 60 --warmup 5 -o gpurun_out/bench23_c5.json
-python3 -c "
-import json; d=json.load(open('gpurun_out/bench23_c5.json')); print(d['ms_per_step'], d['roofline']['avg_launch_ms'], d['roofline']['frac'], d['cpu_baseline'])"
+step tests 600 python -u -m pytest tests/test_frame_graph.py tests/test_hip_parity.py tests/test_0_shard_spawn.py -m gpu -q -x -rf --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_v.log 2>&1
+tail -3 gpurun_out/gpu_tests_v.log
+AB_STEPS=20 step ab 600 bash tools/ab.sh "APN_AB=conc" "APN_CONCURRENT_GRID=0" "APN_AB=conc2" "APN_CONCURRENT_GRID=0"
