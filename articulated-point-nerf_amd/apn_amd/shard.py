@@ -7,7 +7,14 @@ box, gloo in the CPU tests). Rays are independent given the warped cloud, so the
 frame is bit-identical to a single-GPU render (chunk invariance, tests/test_hip_parity.py).
 
 Tile layout: [rays, 12] float32 = rgb_marched (3), rgb_marched_direct (3), depth (1),
-weights (3), alphainv_last (1), alphainv_last_direct (1).
+weights (3), alphainv_last (1), alphainv_last_direct (1); render_sharded appends one column, the
+ray's kNN survivor count, for the next frame's split.
+
+Load balance: a shard's time follows its kNN survivors (the MLP's rows) far more than its in-bbox
+samples -- at C2 with 8 ranks, equal in-bbox shards held 0.13M to 0.60M survivors and took 1.5 to
+3.5 ms (tools/shard_balance.py). The first frame splits the in-bbox samples; every later frame
+splits the previous frame's per-ray cost KEPT_WEIGHT * survivors + in-bbox samples (the survivor
+counts ride in the tile all-gather, so every rank computes the same split).
 """
 from __future__ import annotations
 
@@ -16,6 +23,15 @@ import torch
 TILE_KEYS = (("rgb_marched", 3), ("rgb_marched_direct", 3), ("depth", 1), ("weights", 3),
              ("alphainv_last", 1), ("alphainv_last_direct", 1))
 TILE_WIDTH = sum(w for _, w in TILE_KEYS)
+KEPT_WEIGHT = 10   # cost of a survivor (neighbour MLP + its kNN) in in-bbox-sample units: ~4.5 vs ~0.45 ns at C2
+
+
+def cost_offsets(offsets: torch.Tensor, kept: torch.Tensor) -> torch.Tensor:
+    """Exclusive prefix [R+1] (int64) of the per-ray cost KEPT_WEIGHT * kept + in-bbox samples."""
+    R = offsets.numel() - 1
+    o = offsets[:R + 1].to(torch.int64)
+    cost = (o[1:] - o[:-1]) + KEPT_WEIGHT * kept.reshape(-1).to(torch.int64)
+    return torch.cat([o.new_zeros(1), torch.cumsum(cost, 0)])
 
 
 def split_inner(offsets: torch.Tensor, world: int) -> torch.Tensor:
@@ -56,6 +72,7 @@ class SplitTracker:
         self.bounds = None
         self._host = None
         self._event = None
+        self.cost_mode = False   # set by the first submit_cost: later splits follow the survivors
 
     def bounds_for(self, offsets: torch.Tensor, world: int, advance: bool = True) -> list[int]:
         """advance=False (a frame rendered again after an overflow) keeps the current split, so the
@@ -68,13 +85,24 @@ class SplitTracker:
         elif self._event is not None:
             self._event.synchronize()
             self.bounds = bounds_from_inner(self._host.tolist(), R)
-        if world > 1 and offsets.is_cuda:
-            if self._host is None:
-                self._host = torch.empty(world - 1, dtype=torch.int64, pin_memory=True)
-            self._host.copy_(split_inner(offsets, world), non_blocking=True)
-            self._event = torch.cuda.Event()
-            self._event.record()
+        if world > 1 and offsets.is_cuda and not self.cost_mode:
+            self._launch(offsets, world)
         return self.bounds
+
+    def _launch(self, prefix: torch.Tensor, world: int):
+        if self._host is None:
+            self._host = torch.empty(world - 1, dtype=torch.int64, pin_memory=True)
+        self._host.copy_(split_inner(prefix, world), non_blocking=True)
+        self._event = torch.cuda.Event()
+        self._event.record()
+
+    def submit_cost(self, offsets: torch.Tensor, kept: torch.Tensor, world: int):
+        """After a frame's all-gather: the next frame's split from this frame's per-ray cost
+        (``offsets`` = the frame's in-bbox prefix over all rays, ``kept`` = survivors per ray),
+        computed and copied to the host without waiting."""
+        if world > 1 and offsets.is_cuda:
+            self._launch(cost_offsets(offsets, kept), world)
+            self.cost_mode = True
 
 
 def pack_tile(out: dict, n_rays: int, device) -> torch.Tensor:
@@ -176,11 +204,16 @@ def render_sharded(model, t, render_kwargs, rank: int, world: int, group=None, *
     r0, r1 = model.last_ray_range
     dev = render_kwargs["rays_o"].device
     tile = pack_tile(out, r1 - r0, dev)
+    kept = model.last_kept_per_ray(r1 - r0)
+    tile = torch.cat([tile, kept.float().reshape(-1, 1)], dim=1)   # survivors per ray (exact in f32)
     info = getattr(out, "_info", None)
     if world > 1:
         if info is None:   # exact path: nothing was dropped
             info = torch.zeros(4, dtype=torch.int32, device=dev)
         full, infos = gather_tiles(tile, model.last_ray_bounds, group, info=info)
+        tracker = model.last_split_tracker
+        if tracker is not None and not model._force_exact:
+            tracker.submit_cost(model.last_full_offsets, full[:, TILE_WIDTH].to(torch.int64), world)
     else:
         full, infos = tile, (info.view(1, 4) if info is not None else None)
     res = unpack_tile(full)

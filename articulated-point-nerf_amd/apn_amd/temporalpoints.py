@@ -311,6 +311,7 @@ class TemporalPoints(torch.nn.Module):
         self.concurrent_grid = os.environ.get("APN_CONCURRENT_GRID", "1") != "0"
         self._side_streams = {}
         self._splits = {}           # (ray count, world) -> SplitTracker of the ray-sharded frames
+        self.last_split_tracker = self.last_full_offsets = self._last_ray_ws = None
         self._force_exact = False
         self._last_info = None
 
@@ -678,6 +679,7 @@ class TemporalPoints(torch.nn.Module):
                         calc_min_max, get_skeleton, ray_shard):
         dev = self.canonical_feat.device
         L.require_cuda(self.canonical_feat, what="TemporalPoints.forward")
+        self._last_ray_ws = None
         # skeleton stage: time embedding, TransformNet, chain and (get_skeleton) the joint projection
         # in one launch (apn_skeleton_frame)
         proj = (poses, Ks) if get_skeleton else None
@@ -741,6 +743,15 @@ class TemporalPoints(torch.nn.Module):
             ret['weights'] = wvis
         return ret
 
+    def last_kept_per_ray(self, n_rays):
+        """kNN survivors per ray of the last fused render (its ray range), from the compositing
+        kernel's per-ray segment bounds [beg | end] (rays without survivors: 0, 0); int32 [n_rays]
+        (zeros if that frame composited nothing: no in-bbox sample)."""
+        if self._last_ray_ws is None or self._last_ray_ws[1] != n_rays:
+            return torch.zeros(n_rays, dtype=torch.int32, device=self.canonical_feat.device)
+        rws, R = self._last_ray_ws
+        return rws[R:2 * R] - rws[:R]
+
     def _mark(self, name):
         """HIP-event stage marker (only while self.timing is a dict): the time between consecutive
         markers is charged to the stage named by the later one."""
@@ -802,7 +813,9 @@ class TemporalPoints(torch.nn.Module):
             # contiguous ray range holding ~1/world of the in-bbox samples; after
             # the first frame, the split of the previous frame's counts (no host sync, shard.py)
             rank, world = shard
-            bounds = self._splits.setdefault((R, world), SplitTracker()).bounds_for(offs, world, advance=not self._force_exact)
+            tracker = self._splits.setdefault((R, world), SplitTracker())
+            bounds = tracker.bounds_for(offs, world, advance=not self._force_exact)
+            self.last_split_tracker, self.last_full_offsets = tracker, offs
             cap_key = (R, rank, world)
             r0, r1 = bounds[rank], bounds[rank + 1]
             self.last_ray_range = (r0, r1)
@@ -881,6 +894,7 @@ class TemporalPoints(torch.nn.Module):
         depth = torch.empty(R, device=dev); wvis = torch.empty(R, 3, device=dev)
         last = torch.empty(R, device=dev); last_d = torch.empty(R, device=dev)
         rws = ws.get("ray_ws", 2 * R, torch.int32, dev)
+        self._last_ray_ws = (rws, R)
         call("apn_composite", ptr(out12), ptr(s_pos), ptr(s_ray), S, ptr(nsurv), R, float(self.fast_color_thres), bg,
              ptr(rgb), ptr(rgb_d), ptr(depth), ptr(wvis), ptr(last), ptr(last_d), ptr(rws), s)
         self._mark("composite")

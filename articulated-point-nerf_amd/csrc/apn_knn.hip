@@ -34,7 +34,7 @@ struct GridParams {
 constexpr int KNN_K = 8;
 constexpr int KNN_THREADS = 256;
 // launch bound (in-bbox samples) up to which pass B runs 8 lanes per hard query
-constexpr int64_t KNN_SPLIT_MAX_QUERIES = (int64_t)1 << 20;
+constexpr int64_t KNN_SPLIT_MAX_QUERIES = (int64_t)1 << 18;
 constexpr int KNN_SUBDIV = 8;   // fine cell side = r / KNN_SUBDIV (before the cell cap)
 
 __device__ __forceinline__ int floor_div(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
@@ -1752,7 +1752,14 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
   // candidates: count at cblk_off[nb]; launch over the upper bound nb blocks
   if (knn_mode() == 8 || knn_mode() == 9) {
     static const bool stats = getenv("APN_KNN_STATS") != nullptr;   // profiling aid: apn_debug_knn_stats
-    const bool small = !stats && n_queries <= KNN_SPLIT_MAX_QUERIES;   // small batches: 8 lanes per hard query
+    // small batches (the 8192-ray training steps): 8 lanes per hard query. Up to 2^18 queries:
+    // a ray shard of a full frame (~0.5-1M in-bbox samples at C2 over 8 GPUs) ran its kNN 2.3x
+    // slower on the 8-lane pass than on mode 9's (tools/shard_balance.py); APN_KNN_SMALL_MAX overrides
+    static const int64_t small_max = [] {
+      const char* e = getenv("APN_KNN_SMALL_MAX");
+      return e ? (int64_t)atoll(e) : KNN_SPLIT_MAX_QUERIES;
+    }();
+    const bool small = !stats && n_queries <= small_max;
     const bool aniso = knn_mode() == 9 && !small;
     if (aniso) {   // the anisotropic second grid for pass B (built from the fine grid's sorted points)
       static const int f = [] {

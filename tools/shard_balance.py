@@ -3,7 +3,10 @@ shards for world = 2, 4, 8 rendered one after another (ray_shard=(k, world)), ea
 events, next to its in-bbox samples and kNN survivors (the MLP's work). The max over shards is
 what a strong-scaling step waits for. Diagnostic tool (not a test).
 
-    python tools/shard_balance.py [--config C2] [--reps 5] [--split inbbox|cost]
+    python tools/shard_balance.py [--config C2] [--reps 5] [--split inbbox,cost]
+
+--split cost: the split render_sharded uses from the second frame on (shard.cost_offsets of the
+previous frame's survivors and in-bbox samples), preset in the model's SplitTracker.
 """
 from __future__ import annotations
 
@@ -23,6 +26,8 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--worlds", default="2,4,8")
+    ap.add_argument("--split", default="inbbox,cost")
+    ap.add_argument("--kept-weights", default="", help="comma list of shard.KEPT_WEIGHT values to try (cost split)")
     args = ap.parse_args()
     torch.set_grad_enabled(False)
     dev = torch.device("cuda", 0)
@@ -32,6 +37,8 @@ def main():
     t = torch.tensor([scene.cfg.t], device=dev)
     poses, Ks = scene.c2w[None].to(dev), scene.K[None].to(dev)
     kw = dict(render_depth=True, render_kwargs=rk, render_weights=True, poses=poses, Ks=Ks, get_skeleton=True)
+
+    stages = {}
 
     def timed(fn, reps):
         for _ in range(2):
@@ -43,21 +50,49 @@ def main():
             out = fn()
         e1.record()
         torch.cuda.synchronize(dev)
-        return e0.elapsed_time(e1) / reps, out
+        ms = e0.elapsed_time(e1) / reps
+        model.timing = {}   # one more frame with HIP-event stage marks
+        fn()
+        torch.cuda.synchronize(dev)
+        marks = model.timing.get("marks", [])
+        model.timing = None
+        stages.clear()
+        for (_, a), (name, b) in zip(marks[:-1], marks[1:]):
+            if name != "frame":
+                stages[name] = stages.get(name, 0.0) + a.elapsed_time(b)
+        return ms, out
 
     full_ms, out = timed(lambda: model(t, **kw), args.reps)
     st = model.last_stats.resolved()
     print(f"full frame {full_ms:.3f} ms, {st}")
-    for world in [int(w) for w in args.worlds.split(",")]:
+    from apn_amd.shard import SplitTracker, bounds_from_inner, cost_offsets, split_inner
+    R = rk["rays_o"].shape[0]
+    kept = model.last_kept_per_ray(R).clone()
+    offs = model._ws.get("offs", R + 1, torch.int32, dev).clone()
+    import apn_amd.shard as SH
+    splits = args.split.split(",")
+    if args.kept_weights:
+        splits = [s for s in splits if s != "cost"] + [f"cost{w}" for w in args.kept_weights.split(",")]
+    for split, world in [(sp, int(w)) for sp in splits for w in args.worlds.split(",")]:
+        model._splits.clear()
+        model._capacity = {k: v for k, v in model._capacity.items() if not isinstance(k, tuple)}
+        if split.startswith("cost"):
+            if split != "cost":
+                SH.KEPT_WEIGHT = int(split[4:])
+            tr = SplitTracker()
+            tr.bounds = bounds_from_inner(split_inner(cost_offsets(offs, kept), world).cpu().tolist(), R)
+            tr.cost_mode = True
+            model._splits[(R, world)] = tr
         rows = []
         for k in range(world):
             ms, o = timed(lambda: model(t, ray_shard=(k, world), **kw), args.reps)
             s = model.last_stats.resolved()
             r0, r1 = model.last_ray_range
             rows.append((ms, s.get("inbbox_samples", -1), s.get("kept_samples", -1), r1 - r0))
+            print(f"   shard {k}: {ms:.3f} ms, stages " + " ".join(f"{n} {v:.3f}" for n, v in stages.items()))
         mx = max(r[0] for r in rows)
         mean = sum(r[0] for r in rows) / world
-        print(f"world {world}: shard ms " + " ".join(f"{r[0]:.3f}" for r in rows)
+        print(f"[{split}] world {world}: shard ms " + " ".join(f"{r[0]:.3f}" for r in rows)
               + f" | max {mx:.3f} mean {mean:.3f} (max/mean {mx / mean:.3f}); ideal full/world {full_ms / world:.3f}; "
               f"speedup bound {full_ms / mx:.2f}x")
         print("   kept per shard: " + " ".join(str(r[2]) for r in rows)
