@@ -61,17 +61,22 @@ def balanced_ray_split(offsets: torch.Tensor, world: int) -> list[int]:
 
 class SplitTracker:
     """Sync-free ray split for consecutive sharded frames of one (ray count, world): the first
-    frame reads its balanced split on the host; every frame then computes the split of its own
-    sample counts on the device and copies it to pinned host memory without waiting, and the next
-    frame uses it (one frame stale, which only moves the balance, never the result: any contiguous
-    split assembles the same frame). By the time the next frame asks, the device has long passed
-    that copy, so the event wait costs no device idle; every rank switches at the same frame, and
-    identical inputs give identical splits on every rank."""
+    frame reads its balanced split on the host; every frame then computes a split on the device
+    (of its in-bbox counts, or -- after submit_cost -- of its per-ray cost) and copies it to pinned
+    host memory without waiting. A frame uses the split computed two frames before it (kept in a
+    queue of pending copies): by then the device has finished that copy even when the host runs a
+    whole frame ahead, so the wait costs neither host nor device time (waiting on the previous
+    frame's copy would hold the host until the device drains, and the device would then idle
+    while the next frame's first launches are issued). Stale splits only move the balance, never
+    the result: any contiguous split assembles the same frame. Every rank makes the same calls, so
+    every rank switches at the same frame, and identical inputs give identical splits."""
+
+    DEPTH = 2
 
     def __init__(self):
         self.bounds = None
-        self._host = None
-        self._event = None
+        self._pending = []   # [(pinned host split, event)] oldest first
+        self._free = []      # pinned buffers to reuse
         self.cost_mode = False   # set by the first submit_cost: later splits follow the survivors
 
     def bounds_for(self, offsets: torch.Tensor, world: int, advance: bool = True) -> list[int]:
@@ -82,25 +87,30 @@ class SplitTracker:
             self.bounds = balanced_ray_split(offsets, world)
         elif not advance:
             return self.bounds
-        elif self._event is not None:
-            self._event.synchronize()
-            self.bounds = bounds_from_inner(self._host.tolist(), R)
+        elif len(self._pending) >= self.DEPTH:
+            host, ev = self._pending.pop(0)
+            ev.synchronize()
+            self.bounds = bounds_from_inner(host.tolist(), R)
+            self._free.append(host)
         if world > 1 and offsets.is_cuda and not self.cost_mode:
             self._launch(offsets, world)
         return self.bounds
 
     def _launch(self, prefix: torch.Tensor, world: int):
-        if self._host is None:
-            self._host = torch.empty(world - 1, dtype=torch.int64, pin_memory=True)
-        self._host.copy_(split_inner(prefix, world), non_blocking=True)
-        self._event = torch.cuda.Event()
-        self._event.record()
+        host = self._free.pop() if self._free else torch.empty(world - 1, dtype=torch.int64, pin_memory=True)
+        host.copy_(split_inner(prefix, world), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._pending.append((host, ev))
 
     def submit_cost(self, offsets: torch.Tensor, kept: torch.Tensor, world: int):
-        """After a frame's all-gather: the next frame's split from this frame's per-ray cost
-        (``offsets`` = the frame's in-bbox prefix over all rays, ``kept`` = survivors per ray),
-        computed and copied to the host without waiting."""
+        """After a frame's all-gather: a split from this frame's per-ray cost (``offsets`` = the
+        frame's in-bbox prefix over all rays, ``kept`` = survivors per ray), computed and copied to
+        the host without waiting; from the first call on, frames queue these instead of in-bbox
+        splits."""
         if world > 1 and offsets.is_cuda:
+            if not self.cost_mode:
+                self._pending.clear()   # in-bbox splits still queued: superseded
             self._launch(cost_offsets(offsets, kept), world)
             self.cost_mode = True
 
