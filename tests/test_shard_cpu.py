@@ -152,3 +152,20 @@ def test_split_tracker_cpu_keeps_first_split():
     a = tr.bounds_for(_offsets([5, 0, 3, 9, 1, 4]), 2)
     b = tr.bounds_for(_offsets([0, 0, 0, 0, 30, 1]), 2)
     assert a == b == balanced_ray_split(_offsets([5, 0, 3, 9, 1, 4]), 2)
+
+
+def test_cost_offsets_weights_survivors():
+    """shard.cost_offsets: exclusive prefix of KEPT_WEIGHT * survivors + in-bbox samples per ray;
+    the split of it puts equal cost (not equal samples) on each rank."""
+    from apn_amd.shard import KEPT_WEIGHT, cost_offsets, split_inner, bounds_from_inner
+    inb = [4, 4, 4, 4, 4, 4, 4, 4]
+    kept = torch.tensor([4, 4, 4, 4, 0, 0, 0, 0], dtype=torch.int32)
+    offs = _offsets(inb)
+    c = cost_offsets(offs, kept)
+    per = torch.tensor(inb) + KEPT_WEIGHT * kept.long()
+    assert c.dtype == torch.int64 and c.tolist() == [0] + torch.cumsum(per, 0).tolist()
+    b = bounds_from_inner(split_inner(c, 2).tolist(), len(inb))
+    # equal in-bbox halves would be [0, 4, 8]; equal cost puts the boundary inside the first half
+    assert b[0] == 0 and b[-1] == len(inb) and b[1] < 4
+    costs = [int(c[b[i + 1]] - c[b[i]]) for i in range(2)]
+    assert abs(costs[0] - costs[1]) <= 2 * int(per.max())   # a boundary lands within one ray of the target
