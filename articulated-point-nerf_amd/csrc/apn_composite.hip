@@ -20,6 +20,9 @@ __global__ void k_ray_bounds(const int* __restrict__ s_ray, const int* __restric
   if (i == n - 1 || s_ray[i + 1] != r) end[r] = i + 1;
 }
 
+// Both paths walk the ray's samples in one loop (each keeps its own T, mask and break -- the same
+// arithmetic as two separate walks), and sample i + 1's records are loaded before sample i is
+// accumulated: the per-ray chain of dependent loads is what a compositing thread waits on.
 __global__ void k_composite(const float4* __restrict__ smp, const float4* __restrict__ s_pos,
                             const int* __restrict__ beg, const int* __restrict__ end, int64_t n_rays, float thr,
                             int use_mask, float bg, float* __restrict__ rgb_out, float* __restrict__ rgb_d_out,
@@ -28,37 +31,47 @@ __global__ void k_composite(const float4* __restrict__ smp, const float4* __rest
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n_rays) return;
   const int b = beg[r], e = end[r];
-  // Point-NeRF path
+  // Point-NeRF path (a) and direct path (d)
   float T = 1.f, cr = 0.f, cg = 0.f, cb = 0.f, dep = 0.f, wr = 0.f, wg = 0.f, wb = 0.f;
-  for (int i = b; i < e; ++i) {
-    const float4 v = smp[3 * (size_t)i];
-    const float a = v.w;
-    if (use_mask && !(a > thr)) continue;
-    const float w = T * a;
-    if (!use_mask || w > thr) {
-      cr += w * v.x; cg += w * v.y; cb += w * v.z;
-      dep += w * (float)__float_as_int(s_pos[i].w);
-      const float4 c = smp[3 * (size_t)i + 2];
-      wr += w * c.x; wg += w * c.y; wb += w * c.z;
+  float Td = 1.f, dr = 0.f, dg = 0.f, db = 0.f;
+  bool run_a = true, run_d = true;
+  float4 va, vd, vc, vp;
+  if (b < e) {
+    va = smp[3 * (size_t)b]; vd = smp[3 * (size_t)b + 1]; vc = smp[3 * (size_t)b + 2]; vp = s_pos[b];
+  }
+  for (int i = b; i < e && (run_a || run_d); ++i) {
+    const float4 a4 = va, d4 = vd, c4 = vc, p4 = vp;
+    if (i + 1 < e) {   // next sample's records in flight while this one is accumulated
+      va = smp[3 * (size_t)(i + 1)]; vd = smp[3 * (size_t)(i + 1) + 1]; vc = smp[3 * (size_t)(i + 1) + 2];
+      vp = s_pos[i + 1];
     }
-    T = (float)((double)T * (1.0 - (double)a));
-    if ((double)T < 1e-3) break;
+    if (run_a) {
+      const float a = a4.w;
+      if (!use_mask || a > thr) {
+        const float w = T * a;
+        if (!use_mask || w > thr) {
+          cr += w * a4.x; cg += w * a4.y; cb += w * a4.z;
+          dep += w * (float)__float_as_int(p4.w);
+          wr += w * c4.x; wg += w * c4.y; wb += w * c4.z;
+        }
+        T = (float)((double)T * (1.0 - (double)a));
+        if ((double)T < 1e-3) run_a = false;
+      }
+    }
+    if (run_d) {
+      const float a = d4.w;
+      if (!use_mask || a > thr) {
+        const float w = Td * a;
+        if (!use_mask || w > thr) { dr += w * d4.x; dg += w * d4.y; db += w * d4.z; }
+        Td = (float)((double)Td * (1.0 - (double)a));
+        if ((double)Td < 1e-3) run_d = false;
+      }
+    }
   }
   rgb_out[3 * r] = cr + T * bg; rgb_out[3 * r + 1] = cg + T * bg; rgb_out[3 * r + 2] = cb + T * bg;
   depth_out[r] = dep;
   wvis_out[3 * r] = wr + T * bg; wvis_out[3 * r + 1] = wg + T * bg; wvis_out[3 * r + 2] = wb + T * bg;
   last_out[r] = T;
-  // direct path
-  float Td = 1.f, dr = 0.f, dg = 0.f, db = 0.f;
-  for (int i = b; i < e; ++i) {
-    const float4 v = smp[3 * (size_t)i + 1];
-    const float a = v.w;
-    if (use_mask && !(a > thr)) continue;
-    const float w = Td * a;
-    if (!use_mask || w > thr) { dr += w * v.x; dg += w * v.y; db += w * v.z; }
-    Td = (float)((double)Td * (1.0 - (double)a));
-    if ((double)Td < 1e-3) break;
-  }
   rgb_d_out[3 * r] = dr + Td * bg; rgb_d_out[3 * r + 1] = dg + Td * bg; rgb_d_out[3 * r + 2] = db + Td * bg;
   last_d_out[r] = Td;
 }

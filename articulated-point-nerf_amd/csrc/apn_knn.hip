@@ -110,6 +110,21 @@ __global__ void k_coarse_counts(const GridParams* __restrict__ gp, const int* __
   ccount[c] = n;
 }
 
+// Points in the 3x3x3 coarse block around each coarse cell (clamped at the grid's faces): the
+// classify test of k_knn_classify as one load per query instead of 27.
+__global__ void k_coarse_sum27(const GridParams* __restrict__ gp, const int* __restrict__ ccount,
+                               int* __restrict__ csum27) {
+  const GridParams g = *gp;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= g.nc) return;
+  const int cx = c % g.cdx, cy = (c / g.cdx) % g.cdy, cz = c / (g.cdx * g.cdy);
+  int cnt = 0;
+  for (int z = max(cz - 1, 0); z <= min(cz + 1, g.cdz - 1); ++z)
+    for (int y = max(cy - 1, 0); y <= min(cy + 1, g.cdy - 1); ++y)
+      for (int x = max(cx - 1, 0); x <= min(cx + 1, g.cdx - 1); ++x) cnt += ccount[(z * g.cdy + y) * g.cdx + x];
+  csum27[c] = cnt;
+}
+
 __global__ void k_grid_scatter(const float* __restrict__ xyz, int64_t N, const int* __restrict__ pcell,
                                const int* __restrict__ cell_start, int* __restrict__ cursor,
                                float4* __restrict__ sorted) {
@@ -565,6 +580,7 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_classify(const float4* __re
                                                               const int* __restrict__ n_q_dev,
                                                               const GridParams* __restrict__ gp,
                                                               const int* __restrict__ ccount,
+                                                              const int* __restrict__ csum27,
                                                               int* __restrict__ cand, int* __restrict__ blk_cnt) {
   __shared__ int wave_cnt[KNN_THREADS / 64];
   const int nq = *n_q_dev;
@@ -577,9 +593,13 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_classify(const float4* __re
     const int cy = floor_div((int)floorf((q.y - g.oy) * g.inv_h), g.cf);
     const int cz = floor_div((int)floorf((q.z - g.oz) * g.inv_h), g.cf);
     int cnt = 0;
-    for (int z = max(cz - 1, 0); z <= min(cz + 1, g.cdz - 1); ++z)
-      for (int y = max(cy - 1, 0); y <= min(cy + 1, g.cdy - 1); ++y)
-        for (int x = max(cx - 1, 0); x <= min(cx + 1, g.cdx - 1); ++x) cnt += ccount[(z * g.cdy + y) * g.cdx + x];
+    if (cx >= 0 && cx < g.cdx && cy >= 0 && cy < g.cdy && cz >= 0 && cz < g.cdz) {
+      cnt = csum27[(cz * g.cdy + cy) * g.cdx + cx];
+    } else {   // a query outside the grid (the sampling bbox is padded by r): the clamped block
+      for (int z = max(cz - 1, 0); z <= min(cz + 1, g.cdz - 1); ++z)
+        for (int y = max(cy - 1, 0); y <= min(cy + 1, g.cdy - 1); ++y)
+          for (int x = max(cx - 1, 0); x <= min(cx + 1, g.cdx - 1); ++x) cnt += ccount[(z * g.cdy + y) * g.cdx + x];
+    }
     keep = cnt >= KNN_K;
   }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1652,13 +1672,14 @@ extern "C" size_t apn_grid_workspace_bytes(int64_t n_points, int32_t cell_cap) {
          al256((size_t)cell_cap * 4) + al256((size_t)n_points * 4) + al256((size_t)cell_cap * 4) +
          al256(scan_workspace_bytes(cell_cap)) + al256((size_t)cell_cap * 4) * 3 +
          al256((size_t)(cell_cap + 1) * 4) + al256(4) + al256(sizeof(AGrid)) + al256((size_t)cell_cap * 4) * 2 +
-         al256((size_t)(cell_cap + 1) * 4) + al256((size_t)n_points * 4) + al256((size_t)n_points * 16);
+         al256((size_t)(cell_cap + 1) * 4) + al256((size_t)n_points * 4) + al256((size_t)n_points * 16) +
+         al256((size_t)cell_cap * 4);
 }
 
 struct GridWs {
   GridParams* gp; int* counts; int* cell_start; int* cursor; int* pcell; int* ccount; void* scan;
   int* tile_cnt; int* tile_start; int* tile_cursor; int* tile_list; int* n_tile_list;
-  AGrid* ag; int* counts2; int* cursor2; int* cell_start2; int* pcell2; float4* sorted2;
+  AGrid* ag; int* counts2; int* cursor2; int* cell_start2; int* pcell2; float4* sorted2; int* csum27;
 };
 static GridWs grid_ws(void* ws, int64_t N, int cap) {
   char* p = (char*)ws;
@@ -1680,7 +1701,8 @@ static GridWs grid_ws(void* ws, int64_t N, int cap) {
   w.cursor2 = (int*)p; p += al256((size_t)cap * 4);
   w.cell_start2 = (int*)p; p += al256((size_t)(cap + 1) * 4);
   w.pcell2 = (int*)p; p += al256((size_t)N * 4);
-  w.sorted2 = (float4*)p;
+  w.sorted2 = (float4*)p; p += al256((size_t)N * 16);
+  w.csum27 = (int*)p;
   return w;
 }
 
@@ -1702,6 +1724,7 @@ extern "C" int apn_grid_build(const float* xyz, int64_t n_points, const int32_t*
   if (st) return st;
   // coarse cells never outnumber fine cells (cap)
   hipLaunchKernelGGL(k_coarse_counts, dim3(ceil_div(cell_cap, 256)), dim3(256), 0, s, w.gp, w.cell_start, w.ccount);
+  hipLaunchKernelGGL(k_coarse_sum27, dim3(ceil_div(cell_cap, 256)), dim3(256), 0, s, w.gp, w.ccount, w.csum27);
   hipLaunchKernelGGL(k_grid_scatter, dim3(ceil_div(n_points, 256)), dim3(256), 0, s, xyz, n_points, w.pcell,
                      w.cell_start, w.cursor, (float4*)sorted_pts4);
   return launch_status();
@@ -1745,7 +1768,7 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
   int* blk_off = (int*)p; p += al256((size_t)(nb + 1) * 4);
   void* sws = p;
   hipLaunchKernelGGL(k_knn_classify, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, n_queries_dev, g.gp,
-                     g.ccount, cand_blk, cblk_cnt);
+                     g.ccount, g.csum27, cand_blk, cblk_cnt);
   int st = scan_exclusive_i32(cblk_cnt, cblk_off, nb, sws, s);
   if (st) return st;
   hipLaunchKernelGGL(k_compact_i32, dim3(nb), dim3(KNN_THREADS), 0, s, cand_blk, cblk_cnt, cblk_off, cand);

@@ -232,6 +232,70 @@ __global__ void k_inbbox_fill(const float* __restrict__ ro, const float* __restr
   }
 }
 
+// The same samples, written block-cooperatively (k_inbbox_fill walks one ray per thread, so a
+// wave's stores scatter over 64 rays' output ranges: 1.6 TB/s). The block's 256 rays own the
+// contiguous output range [off[r0], off[r0 + 256]); thread t puts ray r0 + t's geometry and first
+// in-bbox step into LDS, then the block walks the output range with coalesced stores, each slot
+// finding its ray by binary search over the block's offsets. A ray's in-bbox steps are contiguous
+// (every coordinate of start + dir * (stepdist * k) is monotone in k under rounding), so slot o of
+// ray r is step k0[r] + (o - off[r]); positions come from the same ray_geom / sample_at arithmetic.
+constexpr int FILL_RAYS = 256;
+__global__ __launch_bounds__(FILL_RAYS) void k_inbbox_fill_blk(const float* __restrict__ ro,
+                                                             const float* __restrict__ rd,
+                                                             const float* __restrict__ bbox6, float near,
+                                                             float far, float stepdist, int64_t n_rays,
+                                                             const int* __restrict__ off, float4* __restrict__ q_pos,
+                                                             int* __restrict__ q_ray, int cap) {
+  __shared__ int sOff[FILL_RAYS + 1];
+  __shared__ int sK0[FILL_RAYS];
+  __shared__ float sG[6][FILL_RAYS];
+  const int64_t r0 = (int64_t)blockIdx.x * FILL_RAYS;
+  const int nr = (int)min((int64_t)FILL_RAYS, n_rays - r0);
+  const int t = threadIdx.x;
+  const float lo[3] = {bbox6[0], bbox6[1], bbox6[2]}, hi[3] = {bbox6[3], bbox6[4], bbox6[5]};
+  if (t < nr) sOff[t] = off[r0 + t];
+  if (t == 0 && nr > 0) sOff[nr] = off[r0 + nr];
+  if (t < nr) {
+    const int64_t r = r0 + t;
+    const RayGeom g = ray_geom(ro + 3 * r, rd + 3 * r, lo, hi, near, far, stepdist);
+    int k0 = 0;
+    if (off[r + 1] > off[r]) {   // first in-bbox step (0 or 1 in practice: step 0 is on the entry face)
+      float px, py, pz;
+      while (k0 < g.n && !sample_at(g, k0, stepdist, lo, hi, px, py, pz)) ++k0;
+    }
+    sK0[t] = k0;
+    sG[0][t] = g.sx; sG[1][t] = g.sy; sG[2][t] = g.sz;
+    sG[3][t] = g.dx; sG[4][t] = g.dy; sG[5][t] = g.dz;
+  }
+  __syncthreads();
+  if (nr <= 0) return;
+  const int ob = sOff[0], oe = min(sOff[nr], cap);
+  for (int o = ob + t; o < oe; o += FILL_RAYS) {
+    int a = 0, b = nr - 1;   // the largest j with sOff[j] <= o (rays without samples share offsets)
+    while (a < b) {
+      const int m = (a + b + 1) >> 1;
+      if (sOff[m] <= o) a = m; else b = m - 1;
+    }
+    RayGeom g;
+    g.sx = sG[0][a]; g.sy = sG[1][a]; g.sz = sG[2][a];
+    g.dx = sG[3][a]; g.dy = sG[4][a]; g.dz = sG[5][a];
+    g.n = 0;
+    const int k = sK0[a] + (o - sOff[a]);
+    float px, py, pz;
+    sample_at(g, k, stepdist, lo, hi, px, py, pz);
+    q_pos[o] = make_float4(px, py, pz, __int_as_float(k));
+    q_ray[o] = (int)(r0 + a);
+  }
+}
+
+static bool inbbox_fill_per_ray() {   // A/B: APN_INBBOX_FILL=ray selects the one-ray-per-thread fill
+  static const bool v = [] {
+    const char* e = getenv("APN_INBBOX_FILL");
+    return e && e[0] == 'r';
+  }();
+  return v;
+}
+
 // frame_info = {min(total, cap), total, total > cap} from the exclusive scan's last entry.
 __global__ void k_frame_info(const int* __restrict__ total, int cap, int* __restrict__ info) {
   if (threadIdx.x != 0) return;
@@ -364,8 +428,9 @@ extern "C" int apn_inbbox_fill(const float* rays_o, const float* rays_d, const f
                                float stepdist, int64_t n_rays, const int32_t* offsets, float* q_pos4, int32_t* q_ray,
                                void* stream) {
   if (n_rays <= 0) return APN_ERR_ARG;
-  hipLaunchKernelGGL(k_inbbox_fill, dim3(ceil_div(n_rays, 256)), dim3(256), 0, (hipStream_t)stream, rays_o, rays_d,
-                     bbox6, near, far, stepdist, n_rays, offsets, (float4*)q_pos4, q_ray, INT_MAX);
+  hipLaunchKernelGGL(inbbox_fill_per_ray() ? k_inbbox_fill : k_inbbox_fill_blk, dim3(ceil_div(n_rays, 256)), dim3(256),
+                     0, (hipStream_t)stream, rays_o, rays_d, bbox6, near, far, stepdist, n_rays, offsets,
+                     (float4*)q_pos4, q_ray, INT_MAX);
   return launch_status();
 }
 
@@ -376,8 +441,9 @@ extern "C" int apn_inbbox_fill_capped(const float* rays_o, const float* rays_d, 
   if (n_rays <= 0 || capacity < 0 || capacity > INT_MAX || !frame_info) return APN_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(k_frame_info, dim3(1), dim3(64), 0, s, offsets + n_rays, (int)capacity, frame_info);
-  hipLaunchKernelGGL(k_inbbox_fill, dim3(ceil_div(n_rays, 256)), dim3(256), 0, s, rays_o, rays_d, bbox6, near, far,
-                     stepdist, n_rays, offsets, (float4*)q_pos4, q_ray, (int)capacity);
+  hipLaunchKernelGGL(inbbox_fill_per_ray() ? k_inbbox_fill : k_inbbox_fill_blk, dim3(ceil_div(n_rays, 256)), dim3(256),
+                     0, s, rays_o, rays_d, bbox6, near, far, stepdist, n_rays, offsets, (float4*)q_pos4, q_ray,
+                     (int)capacity);
   return launch_status();
 }
 

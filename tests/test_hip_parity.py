@@ -73,6 +73,49 @@ def test_sample_pts_on_golden_rays_bit_exact(dev):
         assert int((~got[1]).sum()) == len(g.z["trace_kmin_d2"])
 
 
+@pytest.mark.parametrize("seed", [0, 1])
+def test_inbbox_fill_bit_exact(dev, seed):
+    """apn_inbbox_count / apn_inbbox_fill (block-cooperative: a ray's in-bbox steps are contiguous)
+    and apn_inbbox_fill_capped vs the oracle's sample_pts_on_rays + mask: positions, step ids and
+    ray ids bit-exact, on random rays incl. zero direction components, rays starting inside the box
+    and rays that miss it; the capped fill writes exactly the first `cap` samples."""
+    from apn_amd import _lib as L
+    from apn_amd._lib import call, ptr
+    lib = L.load()
+    o, d = _rand_rays(70001, seed)   # > 256 blocks, a ragged last block
+    o[::5] *= 0.1                    # some origins inside the box
+    lo = np.array([-1.0, -0.7, -1.2], F32); hi = np.array([0.9, 1.1, 0.8], F32)
+    near, far, sd = 0.0, 6.0, 0.013
+    pts, mo, rid, sid, *_ = O.sample_pts_on_rays(o, d, lo, hi, near, far, sd)
+    q_ref = pts[~mo]; r_ref = rid[~mo]; s_ref = sid[~mo]
+    R = len(o)
+    ro, rd = torch.from_numpy(o).to(dev), torch.from_numpy(d).to(dev)
+    bbox6 = torch.from_numpy(np.concatenate([lo, hi])).to(dev)
+    offs = torch.empty(R + 1, dtype=torch.int32, device=dev)
+    ws = torch.empty(lib.apn_sample_pts_on_rays_workspace_bytes(R), dtype=torch.uint8, device=dev)
+    s = L.stream_ptr(dev)
+    call("apn_inbbox_count", ptr(ro), ptr(rd), ptr(bbox6), near, far, sd, R, ptr(offs), ptr(ws), s)
+    n = int(offs[R])
+    assert n == len(q_ref)
+    q = torch.full((n + 8, 4), -7.0, device=dev)
+    qr = torch.full((n + 8,), -7, dtype=torch.int32, device=dev)
+    call("apn_inbbox_fill", ptr(ro), ptr(rd), ptr(bbox6), near, far, sd, R, ptr(offs), ptr(q), ptr(qr), s)
+    qc = q.cpu().numpy()
+    assert np.array_equal(qc[:n, :3], q_ref)
+    assert np.array_equal(qc[:n, 3].view(np.int32), s_ref.astype(np.int32))
+    assert np.array_equal(qr.cpu().numpy()[:n], r_ref.astype(np.int32))
+    assert (qc[n:] == -7.0).all()                                  # nothing past the last sample
+    cap = n // 3
+    q2 = torch.full((n, 4), -7.0, device=dev)
+    qr2 = torch.full((n,), -7, dtype=torch.int32, device=dev)
+    info = torch.empty(4, dtype=torch.int32, device=dev)
+    call("apn_inbbox_fill_capped", ptr(ro), ptr(rd), ptr(bbox6), near, far, sd, R, ptr(offs), cap, ptr(q2),
+         ptr(qr2), ptr(info), s)
+    assert info.cpu().tolist()[:3] == [cap, n, 1]
+    assert torch.equal(q2[:cap], q[:cap]) and torch.equal(qr2[:cap], qr[:cap])
+    assert (q2[cap:] == -7.0).all() and (qr2[cap:] == -7).all()
+
+
 def test_raw2alpha(dev):
     from apn_amd import render_utils as ru
     d = np.concatenate([np.linspace(-30, 30, 10001), [1e4, -1e4]]).astype(F32)
