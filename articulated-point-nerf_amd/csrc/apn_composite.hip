@@ -8,6 +8,8 @@
 // Sequential per-ray accumulation in sample order reproduces segment_coo's sum order.
 #include "apn_common.h"
 
+#include <climits>
+
 namespace apn {
 
 __global__ void k_ray_bounds(const int* __restrict__ s_ray, const int* __restrict__ n_dev, int* __restrict__ beg,
@@ -76,6 +78,83 @@ __global__ void k_composite(const float4* __restrict__ smp, const float4* __rest
   last_d_out[r] = Td;
 }
 
+// The same per-ray walks with each wave's samples staged through LDS: a wave's 64 rays own one
+// contiguous sample range (survivors are sorted by ray), which it loads in chunks of CMP_CH
+// samples with coalesced stores into LDS; each lane then walks its ray from LDS. The walks are
+// the sequential T products above (bit-identical); only the loads move, from a chain of
+// dependent global reads per ray (long rays set the wave's time) to one coalesced stage per chunk.
+constexpr int CMP_CH = 256;
+__global__ __launch_bounds__(64) void k_composite_lds(const float4* __restrict__ smp, const float4* __restrict__ s_pos,
+                                                      const int* __restrict__ beg, const int* __restrict__ end,
+                                                      int64_t n_rays, float thr, int use_mask, float bg,
+                                                      float* __restrict__ rgb_out, float* __restrict__ rgb_d_out,
+                                                      float* __restrict__ depth_out, float* __restrict__ wvis_out,
+                                                      float* __restrict__ last_out, float* __restrict__ last_d_out) {
+  __shared__ float4 sA[CMP_CH], sD[CMP_CH], sC[CMP_CH];
+  __shared__ float sStep[CMP_CH];
+  const int lane = threadIdx.x;
+  const int64_t r = (int64_t)blockIdx.x * 64 + lane;
+  const bool valid = r < n_rays;
+  const int b = valid ? beg[r] : 0, e = valid ? end[r] : 0;
+  int lo = e > b ? b : INT_MAX, hi = e > b ? e : 0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = min(lo, __shfl_xor(lo, o, 64));
+    hi = max(hi, __shfl_xor(hi, o, 64));
+  }
+  float T = 1.f, cr = 0.f, cg = 0.f, cb = 0.f, dep = 0.f, wr = 0.f, wg = 0.f, wb = 0.f;
+  float Td = 1.f, dr = 0.f, dg = 0.f, db = 0.f;
+  bool run_a = true, run_d = true;
+  int i = b;
+  for (int cs = lo; cs < hi; cs += CMP_CH) {
+    const int ce = min(cs + CMP_CH, hi);
+    __syncthreads();   // the previous chunk is consumed
+    for (int j = lane; j < ce - cs; j += 64) {
+      const size_t k = (size_t)(cs + j);
+      sA[j] = smp[3 * k];
+      sD[j] = smp[3 * k + 1];
+      sC[j] = smp[3 * k + 2];
+      sStep[j] = (float)__float_as_int(s_pos[k].w);
+    }
+    __syncthreads();
+    for (; i < e && i < ce && (run_a || run_d); ++i) {
+      const int j = i - cs;
+      if (run_a) {
+        const float4 a4 = sA[j];
+        const float a = a4.w;
+        if (!use_mask || a > thr) {
+          const float w = T * a;
+          if (!use_mask || w > thr) {
+            cr += w * a4.x; cg += w * a4.y; cb += w * a4.z;
+            dep += w * sStep[j];
+            const float4 c4 = sC[j];
+            wr += w * c4.x; wg += w * c4.y; wb += w * c4.z;
+          }
+          T = (float)((double)T * (1.0 - (double)a));
+          if ((double)T < 1e-3) run_a = false;
+        }
+      }
+      if (run_d) {
+        const float4 d4 = sD[j];
+        const float a = d4.w;
+        if (!use_mask || a > thr) {
+          const float w = Td * a;
+          if (!use_mask || w > thr) { dr += w * d4.x; dg += w * d4.y; db += w * d4.z; }
+          Td = (float)((double)Td * (1.0 - (double)a));
+          if ((double)Td < 1e-3) run_d = false;
+        }
+      }
+    }
+  }
+  if (!valid) return;
+  rgb_out[3 * r] = cr + T * bg; rgb_out[3 * r + 1] = cg + T * bg; rgb_out[3 * r + 2] = cb + T * bg;
+  depth_out[r] = dep;
+  wvis_out[3 * r] = wr + T * bg; wvis_out[3 * r + 1] = wg + T * bg; wvis_out[3 * r + 2] = wb + T * bg;
+  last_out[r] = T;
+  rgb_d_out[3 * r] = dr + Td * bg; rgb_d_out[3 * r + 1] = dg + Td * bg; rgb_d_out[3 * r + 2] = db + Td * bg;
+  last_d_out[r] = Td;
+}
+
 }  // namespace apn
 
 using namespace apn;
@@ -95,8 +174,17 @@ extern "C" int apn_composite(const float* smp12, const float* s_pos4, const int3
   if (max_samples > 0)
     hipLaunchKernelGGL(k_ray_bounds, dim3(ceil_div(max_samples, 256)), dim3(256), 0, s, s_ray, n_samples_dev, beg,
                        end);
-  hipLaunchKernelGGL(k_composite, dim3(ceil_div(n_rays, 256)), dim3(256), 0, s, (const float4*)smp12,
-                     (const float4*)s_pos4, beg, end, n_rays, fast_color_thres, fast_color_thres > 0.f ? 1 : 0, bg,
-                     rgb_marched, rgb_marched_direct, depth, weights_vis, alphainv_last, alphainv_last_direct);
+  static const bool per_ray = [] {   // A/B: APN_COMPOSITE=seq runs the one-ray-per-thread walk from global
+    const char* e = getenv("APN_COMPOSITE");
+    return e && e[0] == 's';
+  }();
+  if (per_ray)
+    hipLaunchKernelGGL(k_composite, dim3(ceil_div(n_rays, 256)), dim3(256), 0, s, (const float4*)smp12,
+                       (const float4*)s_pos4, beg, end, n_rays, fast_color_thres, fast_color_thres > 0.f ? 1 : 0, bg,
+                       rgb_marched, rgb_marched_direct, depth, weights_vis, alphainv_last, alphainv_last_direct);
+  else
+    hipLaunchKernelGGL(k_composite_lds, dim3(ceil_div(n_rays, 64)), dim3(64), 0, s, (const float4*)smp12,
+                       (const float4*)s_pos4, beg, end, n_rays, fast_color_thres, fast_color_thres > 0.f ? 1 : 0, bg,
+                       rgb_marched, rgb_marched_direct, depth, weights_vis, alphainv_last, alphainv_last_direct);
   return launch_status();
 }
