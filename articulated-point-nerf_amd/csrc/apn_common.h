@@ -36,6 +36,28 @@ inline int fill_i32(int* p, int v, int64_t n, hipStream_t s) {
   hipLaunchKernelGGL(k_fill_i32, dim3((unsigned)(nb < 2048 ? nb : 2048)), dim3(256), 0, s, p, v, n);
   return hipPeekAtLastError() == hipSuccess ? APN_OK : APN_ERR_HIP;
 }
+// Up to four int32 fills in one launch (per-frame counters and count arrays: each separate
+// fill is a launch of its own inside the frame).
+struct Fill4 {
+  int* p[4];
+  int64_t n[4];
+  int v[4];
+};
+__global__ static void __launch_bounds__(256) k_fill4_i32(Fill4 f) {
+  const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x, st = (int64_t)gridDim.x * 256;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    for (int64_t i = i0; i < f.n[k]; i += st) f.p[k][i] = f.v[k];
+}
+inline int fill4_i32(int* p0, int64_t n0, int* p1, int64_t n1, int* p2 = nullptr, int64_t n2 = 0, int* p3 = nullptr,
+                     int64_t n3 = 0, hipStream_t s = nullptr) {
+  Fill4 f{{p0, p1, p2, p3}, {p0 ? n0 : 0, p1 ? n1 : 0, p2 ? n2 : 0, p3 ? n3 : 0}, {0, 0, 0, 0}};
+  int64_t m = 1;
+  for (int k = 0; k < 4; ++k) m = f.n[k] > m ? f.n[k] : m;
+  const int64_t nb = (m + 255) / 256;
+  hipLaunchKernelGGL(k_fill4_i32, dim3((unsigned)(nb < 2048 ? nb : 2048)), dim3(256), 0, s, f);
+  return hipPeekAtLastError() == hipSuccess ? APN_OK : APN_ERR_HIP;
+}
 inline int copy_i32(const int* src, int* dst, int n, hipStream_t s) {
   hipLaunchKernelGGL(k_copy_i32, dim3(1), dim3(64), 0, s, src, dst, n);
   return hipPeekAtLastError() == hipSuccess ? APN_OK : APN_ERR_HIP;

@@ -1711,8 +1711,7 @@ extern "C" int apn_grid_build(const float* xyz, int64_t n_points, const int32_t*
   if (n_points <= 0 || cell_cap <= 0 || !xyz || !bbox_ord || !sorted_pts4 || !workspace) return APN_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   GridWs w = grid_ws(workspace, n_points, cell_cap);
-  APN_TRY(fill_i32(w.counts, 0, cell_cap, s));
-  APN_TRY(fill_i32(w.cursor, 0, cell_cap, s));
+  APN_TRY(fill4_i32(w.counts, cell_cap, w.cursor, cell_cap, nullptr, 0, nullptr, 0, s));
   static const int subdiv = [] {
     const char* e = getenv("APN_KNN_SUBDIV");
     return e ? atoi(e) : KNN_SUBDIV;
@@ -1790,8 +1789,7 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
         const int v = e ? atoi(e) : 2;
         return (v == 1 || v == 2 || v == 4) ? v : 2;
       }();
-      APN_TRY(fill_i32(g.counts2, 0, cell_cap, s));
-      APN_TRY(fill_i32(g.cursor2, 0, cell_cap, s));
+      APN_TRY(fill4_i32(g.counts2, cell_cap, g.cursor2, cell_cap, nullptr, 0, nullptr, 0, s));
       hipLaunchKernelGGL(k_agrid_params, dim3(1), dim3(64), 0, s, g.gp, f, g.ag);
       hipLaunchKernelGGL(k_agrid_count, dim3(ceil_div(n_points, 256)), dim3(256), 0, s, (const float4*)sorted_pts4,
                          n_points, g.gp, f, g.counts2, g.pcell2);
@@ -1808,9 +1806,8 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
     int* u1 = g.counts;          // free after the grid build
     int* u2 = g.tile_cnt;
     int* u4 = g.tile_cursor;
-    APN_TRY(fill_i32(mark, 0, cell_cap, s));
-    APN_TRY(fill_i32(g.n_tile_list, 0, 1, s));
-    APN_TRY(fill_i32(n_hard, 0, 1, s));
+    int* n_hard_r = cblk_off + nb + 1;    // cblk_off has nb + 2 entries
+    APN_TRY(fill4_i32(mark, cell_cap, g.n_tile_list, 1, n_hard, 1, n_hard_r, 1, s));
     hipLaunchKernelGGL(k_mark_cells, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, cblk_off + nb,
                        g.gp, ccell, mark);
     hipLaunchKernelGGL(k_tile_list, dim3(ceil_div(cell_cap, LIST_THREADS)), dim3(LIST_THREADS), 0, s, mark, cell_cap,
@@ -1818,8 +1815,6 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
     hipLaunchKernelGGL(k_cell_bound3, dim3(ceil_div(std::min<int64_t>(cell_cap, slots), KNN_THREADS)),
                        dim3(KNN_THREADS), 0, s, g.gp, g.cell_start, g.tile_list, g.n_tile_list, u1, u2, u4);
     int* hard_r = ccell + slots;          // second quarter of the t_pos region
-    int* n_hard_r = cblk_off + nb + 1;    // cblk_off has nb + 2 entries
-    APN_TRY(fill_i32(n_hard_r, 0, 1, s));
     static const bool a_aniso = getenv("APN_KNN_A_ANISO") != nullptr;   // A/B: pass A's r/4 ball on the second grid
     hipLaunchKernelGGL((aniso && a_aniso) ? k_knn_pass_a8<true> : k_knn_pass_a8<false>, dim3(nb), dim3(KNN_THREADS), 0,
                        s, (const float4*)q_pos4, cand, cblk_off + nb, g.gp, g.cell_start, (const float4*)sorted_pts4,
