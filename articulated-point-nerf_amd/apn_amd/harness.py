@@ -89,3 +89,264 @@ def psnr(a: torch.Tensor, b: torch.Tensor) -> float:
     """run.py:186: -10 log10(mean((a-b)^2))."""
     mse = float(((a.float() - b.float()) ** 2).mean())
     return float("inf") if mse == 0 else -10.0 * math.log10(mse)
+
+
+# ---------------------------------------------------------------------------------------------
+# run.py --render_pcd / --render_test harness (f-2): render_viewpoints and render_repose with
+# the reference's signatures and returns (run.py:80-239, 241-356), PNG output, PSNR / SSIM.
+# A TemporalPoints frame runs as ONE forward over all H*W rays (the fused path is chunk-invariant,
+# tests/test_hip_parity.py), so ``batch_size`` only chunks the stage-1 TiNeuVox model, as the
+# reference does for it.
+
+def to8b(x):
+    """utils.to8b: uint8(255 * clip(x, 0, 1))."""
+    import numpy as np
+    return (255 * np.clip(x, 0, 1)).astype(np.uint8)
+
+
+def write_png(path, img8):
+    """8-bit greyscale / RGB / RGBA PNG writer (zlib, filter 0 per row) standing in for
+    imageio.imwrite, which this image does not ship."""
+    import struct
+    import zlib
+    import numpy as np
+    a = np.ascontiguousarray(img8, dtype=np.uint8)
+    if a.ndim == 2:
+        a = a[:, :, None]
+    h, w, c = a.shape
+    ctype = {1: 0, 3: 2, 4: 6}[c]
+    raw = np.concatenate([np.zeros((h, 1), np.uint8), a.reshape(h, w * c)], axis=1).tobytes()
+
+    def chunk(tag, data):
+        return struct.pack(">I", len(data)) + tag + data + struct.pack(">I", zlib.crc32(tag + data) & 0xFFFFFFFF)
+    png = b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, 8, ctype, 0, 0, 0)) + \
+        chunk(b"IDAT", zlib.compress(raw, 6)) + chunk(b"IEND", b"")
+    with open(path, "wb") as f:
+        f.write(png)
+
+
+def read_png(path):
+    """The inverse of write_png (filter-0 images only): -> uint8 [H, W, C]."""
+    import struct
+    import zlib
+    import numpy as np
+    data = open(path, "rb").read()
+    assert data[:8] == b"\x89PNG\r\n\x1a\n"
+    pos, idat, hdr = 8, b"", None
+    while pos < len(data):
+        n = struct.unpack(">I", data[pos:pos + 4])[0]
+        tag, body = data[pos + 4:pos + 8], data[pos + 8:pos + 8 + n]
+        if tag == b"IHDR":
+            hdr = struct.unpack(">IIBBBBB", body)
+        elif tag == b"IDAT":
+            idat += body
+        pos += 12 + n
+    w, h, _, ctype = hdr[:4]
+    c = {0: 1, 2: 3, 6: 4}[ctype]
+    rows = np.frombuffer(zlib.decompress(idat), np.uint8).reshape(h, 1 + w * c)
+    assert (rows[:, 0] == 0).all(), "filter-0 rows only"
+    return rows[:, 1:].reshape(h, w, c)
+
+
+def _draw_line(img, p0, p1, color):
+    """8-connected line (cv2.LINE_8 style) from p0 to p1 = (x, y), clipped to the image."""
+    x0, y0 = int(p0[0]), int(p0[1])
+    x1, y1 = int(p1[0]), int(p1[1])
+    dx, dy = abs(x1 - x0), -abs(y1 - y0)
+    sx, sy = (1 if x0 < x1 else -1), (1 if y0 < y1 else -1)
+    err = dx + dy
+    H, W = img.shape[:2]
+    while True:
+        if 0 <= x0 < W and 0 <= y0 < H:
+            img[y0, x0] = color
+        if x0 == x1 and y0 == y1:
+            break
+        e2 = 2 * err
+        if e2 >= dy:
+            err += dy
+            x0 += sx
+        if e2 <= dx:
+            err += dx
+            y0 += sy
+
+
+def _draw_disc(img, c, radius, color):
+    import numpy as np
+    H, W = img.shape[:2]
+    cx, cy = int(c[0]), int(c[1])
+    y0, y1, x0, x1 = max(cy - radius, 0), min(cy + radius + 1, H), max(cx - radius, 0), min(cx + radius + 1, W)
+    if y0 >= y1 or x0 >= x1:
+        return
+    ys, xs = np.mgrid[y0:y1, x0:x1]
+    m = (xs - cx) ** 2 + (ys - cy) ** 2 <= radius * radius
+    img[ys[m], xs[m]] = color
+
+
+def draw_skeleton(img, joints, bones):
+    """The skeleton overlay of run.py:225-233 (cv2.line thickness 1 per bone, cv2.circle radius 3
+    filled per joint, black) on a float [H, W, 3] image, in place. joints: int32 [J, 2] (x, y).
+    Pixel parity with OpenCV's rasteriser is unpinned (cv2 is absent here)."""
+    for b in bones:
+        _draw_line(img, joints[int(b[0])], joints[int(b[1])], 0.0)
+    for j in range(len(joints)):
+        _draw_disc(img, joints[j], 3, 0.0)
+    return img
+
+
+def rgb_ssim(img0, img1, max_val, filter_size=11, filter_sigma=1.5, k1=0.01, k2=0.03, return_map=False):
+    """utils.rgb_ssim (the mip-NeRF SSIM): separable Gaussian blur ('valid' 2D convolutions),
+    per-channel statistics, mean of the SSIM map."""
+    import numpy as np
+    from scipy.signal import convolve2d
+    assert img0.ndim == 3 and img0.shape[-1] == 3 and img0.shape == img1.shape
+    half = filter_size // 2
+    offs = (np.arange(filter_size) - half + (2 * half - filter_size + 1) / 2) / filter_sigma
+    g = np.exp(-0.5 * offs ** 2)
+    g /= g.sum()
+
+    def blur(z):
+        return np.stack([convolve2d(convolve2d(z[..., c], g[:, None], mode="valid"), g[None, :], mode="valid")
+                         for c in range(z.shape[-1])], -1)
+    m0, m1 = blur(img0), blur(img1)
+    s00 = np.maximum(0.0, blur(img0 ** 2) - m0 * m0)
+    s11 = np.maximum(0.0, blur(img1 ** 2) - m1 * m1)
+    s01 = blur(img0 * img1) - m0 * m1
+    s01 = np.sign(s01) * np.minimum(np.sqrt(s00 * s11), np.abs(s01))
+    c1, c2 = (k1 * max_val) ** 2, (k2 * max_val) ** 2
+    smap = ((2 * m0 * m1 + c1) * (2 * s01 + c2)) / ((m0 * m0 + m1 * m1 + c1) * (s00 + s11 + c2))
+    return smap if return_map else float(np.mean(smap))
+
+
+def _scaled_views(HW, Ks, render_factor):
+    import numpy as np
+    if render_factor:
+        HW = np.copy(HW) // render_factor
+        Ks = torch.as_tensor(Ks).clone()
+        Ks[:, :2, :3] = Ks[:, :2, :3] // render_factor
+    return HW, torch.as_tensor(Ks)
+
+
+def _finish(rgbs, depths, weights, joints, bones, savedir, psnrs, ssims, eval_psnr, eval_ssim):
+    import os
+    import numpy as np
+    if psnrs or ssims:
+        if savedir is not None:
+            with open(os.path.join(savedir, "results.txt"), "w") as f:
+                if eval_psnr:
+                    f.write(f"psnr: {np.mean(psnrs)}\n")
+                if eval_ssim:
+                    f.write(f"ssim: {np.mean(ssims)}\n")
+    if savedir is not None:
+        for i, rgb in enumerate(rgbs):
+            write_png(os.path.join(savedir, f"img_{i:03d}.png"), to8b(rgb))
+        for i, w in enumerate(weights):
+            write_png(os.path.join(savedir, f"weights_{i:03d}.png"), to8b(w))
+    rgbs, depths, weights = np.array(rgbs), np.array(depths), np.array(weights)
+    J = np.array([joints[i] for i in range(len(joints))]).astype(np.int32)
+    if len(J) > 0 and bones is not None:
+        for i in range(len(weights)):
+            draw_skeleton(weights[i], J[i], bones)
+    return rgbs, depths, weights
+
+
+def _joint_record(out, joints, i, HW, render_kwargs):
+    j = out.get("joints")
+    if j is None:
+        return None
+    if not render_kwargs.get("inverse_y", False):   # run.py:151-152 (mirrors x by the first view's height)
+        j[:, :, 0] = (int(HW[0][0]) - 1) - j[:, :, 0]
+    if i not in joints:
+        joints[i] = j[0].cpu().numpy()
+    return out.get("bones")
+
+
+@torch.no_grad()
+def render_viewpoints(model, render_poses, HW, Ks, ndc, render_kwargs, gt_imgs=None, savedir=None, test_times=None,
+                      render_factor=0, eval_psnr=False, eval_ssim=False, eval_lpips_alex=False,
+                      eval_lpips_vgg=False, inverse_y=False, flip_x=False, flip_y=False, batch_size=4096 * 2,
+                      verbose=True, render_pcd_direct=False, render_flow=False, fixed_viewdirs=None):
+    """run.py:80-239: every view's rays (tineuvox.get_rays_of_a_view), the model at that view's
+    time, rgb / depth / weight-visualisation images, optional PSNR / SSIM against gt_imgs, PNGs
+    in savedir, the skeleton drawn on the weight images. Returns (rgbs, depths, weights, flows)."""
+    import numpy as np
+    from .tineuvox import get_rays_of_a_view
+    if eval_lpips_alex or eval_lpips_vgg:
+        raise NotImplementedError("LPIPS needs the torchvision / lpips network weights, absent here")
+    if render_flow:
+        raise NotImplementedError("render_flow: the scene-flow output is not on the fused render path")
+    assert len(render_poses) == len(HW) and len(HW) == len(Ks)
+    HW, Ks = _scaled_views(HW, Ks, render_factor)
+    is_tp = isinstance(model, TemporalPoints)
+    rgbs, depths, weights, psnrs, ssims, joints, bones = [], [], [], [], [], {}, None
+    for i, c2w in enumerate(render_poses):
+        H, W = int(HW[i][0]), int(HW[i][1])
+        K = Ks[i].to(torch.float32)
+        ro, rd, vd = get_rays_of_a_view(H, W, K, c2w, ndc, inverse_y=inverse_y, flip_x=flip_x, flip_y=flip_y)
+        if fixed_viewdirs is not None:
+            vd = fixed_viewdirs
+        ro, rd, vd = ro.reshape(-1, 3), rd.reshape(-1, 3), vd.reshape(-1, 3)
+        if is_tp:
+            dev = model.canonical_feat.device
+            rk = dict(render_kwargs, rays_o=ro.to(dev), rays_d=rd.to(dev), viewdirs=vd.to(dev))
+            px = torch.stack(torch.meshgrid(torch.arange(0, W), torch.arange(0, H), indexing="ij"), -1)
+            rk["pixel_coords"] = px.reshape(-1, 2).float().to(dev)
+            t = torch.as_tensor(test_times[i], dtype=torch.float32, device=dev).reshape(1)
+            out = model(t, render_depth=True, render_kwargs=rk, render_weights=True,
+                        render_pcd_direct=render_pcd_direct, poses=torch.as_tensor(c2w)[None].to(dev),
+                        Ks=Ks[i][None].to(dev), cam_per_ray=torch.zeros(len(ro))[:, None], get_skeleton=True)
+            b = _joint_record(out, joints, i, HW, render_kwargs)
+            bones = b if b is not None else bones
+            rgb = (out["rgb_marched_direct"] if render_pcd_direct else out["rgb_marched"]).reshape(H, W, -1)
+            res = {"rgb_marched": rgb, "depth": out["depth"].reshape(H, W, -1),
+                   "weights": out["weights"].reshape(H, W, -1)}
+        else:   # stage-1 TiNeuVox: the reference's chunked calls
+            chunks = []
+            ts = float(test_times[i]) * torch.ones_like(ro[:, :1])
+            for a, b_, c, d in zip(ro.split(batch_size), rd.split(batch_size), vd.split(batch_size), ts.split(batch_size)):
+                o = model(a, b_, c, d, **render_kwargs)
+                chunks.append({k: o[k] for k in ("rgb_marched", "depth")})
+            res = {k: torch.cat([c[k] for c in chunks]).reshape(H, W, -1) for k in ("rgb_marched", "depth")}
+        rgb = res["rgb_marched"].cpu().numpy()
+        rgbs.append(rgb)
+        depths.append(res["depth"].cpu().numpy())
+        if "weights" in res:
+            weights.append(res["weights"].cpu().numpy())
+        if gt_imgs is not None and render_factor == 0:
+            if eval_psnr:
+                psnrs.append(float(-10.0 * np.log10(np.mean(np.square(rgb - gt_imgs[i])))))
+            if eval_ssim:
+                ssims.append(rgb_ssim(rgb, gt_imgs[i], max_val=1))
+    if verbose and psnrs:
+        print("Testing psnr", np.mean(psnrs), "(avg)")
+    if verbose and ssims:
+        print("Testing ssim", np.mean(ssims), "(avg)")
+    rgbs, depths, weights = _finish(rgbs, depths, weights, joints, bones, savedir, psnrs, ssims, eval_psnr, eval_ssim)
+    return rgbs, depths, weights, np.array([])
+
+
+@torch.no_grad()
+def render_repose(rot_params, render_poses, HW, Ks, ndc, model, render_kwargs, gt_imgs=None, savedir=None,
+                  render_factor=0, eval_psnr=False, eval_ssim=False, eval_lpips_alex=False, eval_lpips_vgg=False,
+                  inverse_y=False, flip_x=False, flip_y=False):
+    """run.py:241-356: view i rendered with the skeleton posed by rot_params[i] (the
+    TemporalPoints rot_params path). Returns (rgbs, depths, weights)."""
+    from .tineuvox import get_rays_of_a_view
+    assert isinstance(model, TemporalPoints)
+    assert len(render_poses) == len(HW) and len(HW) == len(Ks)
+    HW, Ks = _scaled_views(HW, Ks, render_factor)
+    dev = model.canonical_feat.device
+    rgbs, depths, weights, joints, bones = [], [], [], {}, None
+    for i, c2w in enumerate(render_poses):
+        H, W = int(HW[i][0]), int(HW[i][1])
+        ro, rd, vd = get_rays_of_a_view(H, W, Ks[i], c2w, ndc, inverse_y=inverse_y, flip_x=flip_x, flip_y=flip_y)
+        rk = dict(render_kwargs, rays_o=ro.reshape(-1, 3).to(dev), rays_d=rd.reshape(-1, 3).to(dev),
+                  viewdirs=vd.reshape(-1, 3).to(dev))
+        out = model(None, render_depth=True, render_kwargs=rk, render_weights=True,
+                    rot_params=torch.as_tensor(rot_params[i]).to(dev), calc_min_max=True, get_skeleton=True,
+                    poses=torch.as_tensor(c2w)[None].to(dev), Ks=Ks[i][None].to(dev))
+        b = _joint_record(out, joints, i, HW, render_kwargs)
+        bones = b if b is not None else bones
+        rgbs.append(out["rgb_marched"].reshape(H, W, -1).cpu().numpy())
+        depths.append(out["depth"].reshape(H, W, -1).cpu().numpy())
+        weights.append(out["weights"].reshape(H, W, -1).cpu().numpy())
+    return _finish(rgbs, depths, weights, joints, bones, savedir, [], [], False, False)
