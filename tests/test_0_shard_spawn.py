@@ -81,6 +81,12 @@ def test_render_sharded_two_processes_bit_identical():
         assert torch.equal(res[1][f"bounds{i}"], res[0][f"bounds{i}"]), i   # every rank on the same split
         for r in range(WORLD):
             assert tuple(res[r][f"range{i}"].tolist()) == (bounds[r], bounds[r + 1])
-            assert torch.equal(res[r][f"assembled{i}"], single), (i, r)
+            a = res[r][f"assembled{i}"]
+            if not torch.equal(a, single):
+                bad = (a != single).any(1).nonzero().flatten()
+                cols = (a != single).any(0).nonzero().flatten().tolist()
+                raise AssertionError(f"frame {i} rank {r}: {len(bad)} rays differ (first {bad[:8].tolist()}), "
+                                     f"columns {cols}, max |d| {float((a - single).abs().max()):.3e}, "
+                                     f"bounds {bounds}")
         # both ranks did real work (the object is hit by rays of both halves of the split)
         assert 0 < bounds[1] < single.shape[0]
