@@ -130,8 +130,8 @@ __device__ __forceinline__ void layer_mfma(const char* __restrict__ X, rsrc_t rs
   const int lane = threadIdx.x & 63;
   const int li = lane & 15, g = lane >> 4;
   if constexpr (!BPF) {
-    // no B double-buffering of whole chunks (fewer VGPRs): the activation fragments are read one
-    // M-tile ahead of their MFMAs
+    // no B double-buffering (fewer VGPRs): the chunk's activation fragments are read per M-tile
+    // right before its MFMAs
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       h8 an[2][2];
@@ -146,20 +146,12 @@ __device__ __forceinline__ void layer_mfma(const char* __restrict__ X, rsrc_t rs
 #pragma unroll
           for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, vb, FBN + j * NQN * 2 + pt);
       }
-      // (same-box A/B: MLP 6.98-7.02 vs 7.05-7.06 ms when each M-tile read its own right before)
-      h8 bh = *(const h8*)(X + act_off(li, 4 * q + g)), bl = *(const h8*)(X + act_off(li, 4 * q + g) + 256);
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
-        h8 nh = bh, nl = bl;
-        if (mt + 1 < 4) {
-          const char* pn = X + act_off(16 * (mt + 1) + li, 4 * q + g);
-          nh = *(const h8*)pn;
-          nl = *(const h8*)(pn + 256);
-        }
+        const char* p = X + act_off(16 * mt + li, 4 * q + g);
+        const h8 bh = *(const h8*)p, bl = *(const h8*)(p + 256);
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[mt][j] = mfma3(a[j][0], a[j][1], bh, bl, acc[mt][j]);
-        bh = nh;
-        bl = nl;
       }
       if (q + 1 < NQ) {
 #pragma unroll
