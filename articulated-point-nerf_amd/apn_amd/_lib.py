@@ -34,7 +34,7 @@ SIGNATURES = {
     "apn_lbs_skin": (C.c_int, [P, P, I64, I32, P, F32, P, P, P, P, P, P, P, F32, I32, P, P, P, P, P, P, P, P]),
     "apn_skeleton_pose": (C.c_int, [P, I32, P, I32, I32, P, I32, I32, P, P, I32, P, P, P, P, P, P, P, P, P, P, P]),
     "apn_skeleton_frame": (C.c_int, [P, P, I32, P, I32, I32, P, I32, I32, P, P, I32, P, P, P, P, P, P, P, P, P, P,
-                                     P, P, I32, P, P]),
+                                     P, P, I32, P, P, I32, P]),
     "apn_bbox_unpack": (C.c_int, [P, F32, P, P]),
     "apn_inbbox_count": (C.c_int, [P, P, P, F32, F32, F32, I64, P, P, P]),
     "apn_inbbox_fill": (C.c_int, [P, P, P, F32, F32, F32, I64, P, P, P, P]),

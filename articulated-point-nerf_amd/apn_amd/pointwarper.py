@@ -160,7 +160,7 @@ class PointWarper(torch.nn.Module):
             self._tree_key = key
         return self._tree
 
-    def pose(self, joints, t=None, rot_params=None, global_t=None, time_poc=None, proj=None):
+    def pose(self, joints, t=None, rot_params=None, global_t=None, time_poc=None, proj=None, sweep_index=None):
         """Skeleton stage of forward (pointwarper.py:216-239) as one HIP launch
         (apn_skeleton_frame): returns bone_Ts [J,4,4], global_t [3] and joints_rel [J,3]; the
         bone rows [J,12] for apn_lbs_skin are kept in ``last_T34``. Sets prev_params /
@@ -170,7 +170,9 @@ class PointWarper(torch.nn.Module):
         (tineuvox.py:872-878) is computed in the same launch. ``proj=(c2w [P,4,4], K [P,3,3])``:
         the skeleton projection project_point_to_image_plane(joints_rel + global_t, c2w, K)
         (temporalpoints.py:578-583) runs in the launch too, left in ``last_joints2d`` [P,J,2]
-        (None when not requested or beyond the kernel's limits: the caller projects in torch)."""
+        (None when not requested or beyond the kernel's limits: the caller projects in torch).
+        ``sweep_index`` (device int32 [1]): rot_params is a pose sweep [P, J, rot_dim]; the launch
+        takes pose sweep_index % P and advances the index (TemporalPoints.capture_repose)."""
         assert (t is None) ^ (rot_params is None)
         dev = joints.device
         L.require_cuda(joints, what="PointWarper.pose")
@@ -208,7 +210,7 @@ class PointWarper(torch.nn.Module):
                 call("apn_skeleton_frame", ptr(tr), ptr(poc), poc.numel(), None, 4, J, ptr(tn), hidden, n_layers,
                      ptr(jts), ptr(pi), pi.shape[1], ptr(pjx), ptr(sib), ptr(rmask), ptr(params), ptr(thetas),
                      ptr(bone_Ts), ptr(T34), ptr(gt), ptr(joints_rel), ptr(prog), ptr(c2w), ptr(Km), n_views, ptr(j2d),
-                     s)
+                     None, 0, s)
             else:
                 te = t.detach().float().reshape(-1).contiguous()   # t is already the time embedding
                 call("apn_skeleton_pose", ptr(te), te.numel(), None, 4, J, ptr(tn), hidden, n_layers, ptr(jts),
@@ -219,9 +221,12 @@ class PointWarper(torch.nn.Module):
             self.prev_global_t = gt
         else:
             rp = rot_params.detach().float().contiguous()
+            n_sweep = rp.shape[0] if sweep_index is not None else 0
+            if sweep_index is not None and (rp.dim() != 3 or rp.shape[1] != J):
+                raise ValueError("PointWarper.pose: a sweep is [P, J, rot_dim]")
             call("apn_skeleton_frame", None, None, 0, ptr(rp), rp.shape[-1], J, None, 0, 0, ptr(jts), ptr(pi),
                  pi.shape[1], ptr(pjx), ptr(sib), ptr(rmask), None, ptr(thetas), ptr(bone_Ts), ptr(T34), ptr(gt),
-                 ptr(joints_rel), ptr(prog), ptr(c2w), ptr(Km), n_views, ptr(j2d), s)
+                 ptr(joints_rel), ptr(prog), ptr(c2w), ptr(Km), n_views, ptr(j2d), ptr(sweep_index), n_sweep, s)
             if global_t is not None:
                 gt = global_t
                 j2d = None   # projected with the kernel's zero global_t: the caller projects in torch

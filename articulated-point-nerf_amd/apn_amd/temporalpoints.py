@@ -473,23 +473,37 @@ class TemporalPoints(torch.nn.Module):
         out.index_add_(1, rules.to(sm.device), sm)
         return out
 
-    def repose(self, rot_params):
-        """temporalpoints.py:370-371 -> [xyz (N,3), joints_rel (J,3)] via the fused LBS kernel."""
-        bone_Ts, global_t, joints_rel = self.forward_warp.pose(self.joints, rot_params=rot_params)
+    def repose(self, rot_params, sweep_index=None):
+        """temporalpoints.py:370-371 -> [xyz (N,3), joints_rel (J,3)] via the fused LBS kernel.
+        (``sweep_index``: rot_params is a pose sweep, see capture_repose.)"""
+        bone_Ts, global_t, joints_rel = self.forward_warp.pose(self.joints, rot_params=rot_params,
+                                                               sweep_index=sweep_index)
         self._mark("frame")
         xyz, _, _ = self._lbs(bone_Ts, global_t, records=False, T34=self.forward_warp.last_T34)
         self._mark("lbs")
         return [xyz, joints_rel]
 
-    def capture_repose(self, rot_dim=4):
+    def capture_repose(self, rot_dim=4, sweep=None):
         """The repose step (skeleton launch + fused LBS launch, run.py:1355-1396 sweeps it per pose)
         captured once in a HIP graph: returns ``step(rot_params) -> (xyz, joints_rel)``, which
         copies rot_params [J, rot_dim] into the graph's input and replays it -- no per-pose host
         work besides one copy and one graph launch. The outputs are the graph's static buffers
-        (overwritten by the next step). Capture again after changing the model."""
+        (overwritten by the next step). Capture again after changing the model.
+
+        ``sweep`` = the poses of the sweep [P, J, rot_dim] (device): the graph reads pose
+        ``index % P`` from the sweep itself and advances a device index, so a step that is given
+        the next row of the sweep (the sweep's order, as run.py walks it) is one graph launch with
+        no input copy; another row sets the index first (one small fill), and rot_params that are
+        not a row of the sweep take the eager path."""
         dev = self.canonical_pcd.device
         J = self.weights.shape[1]
+        if sweep is not None:
+            sweep = sweep.detach().to(dev, torch.float32).contiguous()
+            if sweep.dim() != 3 or sweep.shape[1] != J:
+                raise ValueError("capture_repose: sweep must be [P, J, rot_dim]")
+            rot_dim = sweep.shape[2]
         rp = torch.zeros(J, rot_dim, device=dev)
+        idx = torch.zeros(1, dtype=torch.int32, device=dev)
         with torch.no_grad():
             side = torch.cuda.Stream(dev)
             side.wait_stream(torch.cuda.current_stream(dev))
@@ -498,14 +512,35 @@ class TemporalPoints(torch.nn.Module):
             torch.cuda.current_stream(dev).wait_stream(side)
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
-                xyz, joints_rel = self.repose(rp)
+                if sweep is None:
+                    xyz, joints_rel = self.repose(rp)
+                else:
+                    xyz, joints_rel = self.repose(sweep, sweep_index=idx)
+        if sweep is None:
+            def step(rot_params):
+                rp.copy_(rot_params.reshape(J, rot_dim))
+                graph.replay()
+                return xyz, joints_rel
+        else:
+            P, row = sweep.shape[0], J * rot_dim * 4
+            base = sweep.data_ptr()
+            state = {"next": 0}
+            idx.zero_()
 
-        def step(rot_params):
-            rp.copy_(rot_params.reshape(J, rot_dim))
-            graph.replay()
-            return xyz, joints_rel
+            def step(rot_params):
+                off = rot_params.data_ptr() - base
+                if (rot_params.device != sweep.device or not rot_params.is_contiguous() or off < 0 or off % row
+                        or off // row >= P or rot_params.numel() != J * rot_dim):
+                    with torch.no_grad():
+                        return self.repose(rot_params)
+                i = off // row
+                if i != state["next"]:
+                    idx.fill_(i)
+                state["next"] = (i + 1) % P
+                graph.replay()
+                return xyz, joints_rel
 
-        step.graph, step.inputs = graph, rp
+        step.graph, step.inputs = graph, (rp if sweep is None else (sweep, idx))
         return step
 
     def capture_frame(self, t, render_kwargs, render_depth=True, render_weights=True, query_radius=0.01, poses=None,

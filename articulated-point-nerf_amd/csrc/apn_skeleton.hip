@@ -62,7 +62,7 @@ __global__ __launch_bounds__(SK_THREADS) void k_skeleton_pose(
     float* __restrict__ thetas_out, float* __restrict__ bone_T16, float* __restrict__ bone_T34,
     float* __restrict__ global_t_out, float* __restrict__ joints_rel_out, const int* __restrict__ chain_prog,
     const float* __restrict__ time_poc, int n_freq, const float* __restrict__ c2w, const float* __restrict__ Kmat,
-    int n_views, float* __restrict__ joints2d_out) {
+    int n_views, float* __restrict__ joints2d_out, int* __restrict__ sweep_idx, int sweep_len) {
   __shared__ float h[2][SK_OUT];
   __shared__ float sPart[SK_SLICES][SK_OUT];
   __shared__ float sInv[SK_MAX_VIEWS][12];
@@ -76,6 +76,10 @@ __global__ __launch_bounds__(SK_THREADS) void k_skeleton_pose(
   __shared__ float sStk[SK_MAX_J][SK_STACK][16];
   const int tid = threadIdx.x;
   const bool tpath = rot_params == nullptr;
+  // sweep mode (rot path): rot_params holds sweep_len poses; this launch takes pose *sweep_idx and
+  // advances the index (a captured repose step then needs no per-pose input copy)
+  const int sweep_i = sweep_idx ? *sweep_idx : 0;
+  if (sweep_idx) rot_params += (size_t)(sweep_i % sweep_len) * J * rot_dim;
   if (chain_prog) {   // the host's program for this depth (2 depth - 1 ops)
     if (tid < 2 * depth - 1) sProg[tid] = chain_prog[tid];
     if (tid == 0) sNProg = 2 * depth - 1;
@@ -260,6 +264,7 @@ __global__ __launch_bounds__(SK_THREADS) void k_skeleton_pose(
       joints2d_out[2 * tid + 1] = q[1] / q[2];
     }
   }
+  if (sweep_idx && tid == 0) *sweep_idx = (sweep_i + 1) % sweep_len;   // every thread read it before the barriers above
 }
 
 }  // namespace apn
@@ -273,7 +278,7 @@ extern "C" int apn_skeleton_frame(const float* t, const float* time_poc, int32_t
                                   float* params_out, float* thetas_out, float* bone_T16, float* bone_T34,
                                   float* global_t_out, float* joints_rel_out, const int32_t* chain_prog,
                                   const float* c2w, const float* K, int32_t n_views, float* joints2d_out,
-                                  void* stream) {
+                                  int32_t* sweep_index, int32_t sweep_len, void* stream) {
   const bool tpath = rot_params == nullptr;
   const int t_dim = 1 + 2 * n_freq;
   if (n_joints <= 0 || n_joints > SK_MAX_J || depth <= 0 || depth > SK_MAX_DEPTH || !joints || !parent_indices ||
@@ -286,10 +291,12 @@ extern "C" int apn_skeleton_frame(const float* t, const float* time_poc, int32_t
   if (n_views < 0 || n_views > SK_MAX_VIEWS || n_joints * n_views > SK_THREADS ||
       (n_views > 0 && (!c2w || !K || !joints2d_out)))
     return APN_ERR_ARG;
+  if (sweep_index && (tpath || sweep_len <= 0)) return APN_ERR_ARG;
   hipLaunchKernelGGL(k_skeleton_pose, dim3(1), dim3(SK_THREADS), 0, (hipStream_t)stream, t, t_dim, rot_params,
                      rot_dim, n_joints, tn_weights, hidden, n_layers, joints, parent_indices, depth, parent_joint_ex,
                      sibling_mask, rot_mask, params_out, thetas_out, bone_T16, bone_T34, global_t_out,
-                     joints_rel_out, chain_prog, time_poc, n_freq, c2w, K, n_views, joints2d_out);
+                     joints_rel_out, chain_prog, time_poc, n_freq, c2w, K, n_views, joints2d_out, sweep_index,
+                     sweep_len);
   return launch_status();
 }
 
@@ -312,6 +319,6 @@ extern "C" int apn_skeleton_pose(const float* t_embed, int32_t t_dim, const floa
   hipLaunchKernelGGL(k_skeleton_pose, dim3(1), dim3(SK_THREADS), 0, (hipStream_t)stream, t_embed, t_dim, rot_params,
                      rot_dim, n_joints, tn_weights, hidden, n_layers, joints, parent_indices, depth, parent_joint_ex,
                      sibling_mask, rot_mask, params_out, thetas_out, bone_T16, bone_T34, global_t_out,
-                     joints_rel_out, chain_prog, nullptr, 0, nullptr, nullptr, 0, nullptr);
+                     joints_rel_out, chain_prog, nullptr, 0, nullptr, nullptr, 0, nullptr, nullptr, 0);
   return launch_status();
 }

@@ -199,7 +199,9 @@ def lbs_sweep(args, rank, world, dev):
         del g_lbs
     # throughput: every pose of the sweep through the captured repose step (skeleton + LBS in one
     # HIP graph; per pose one device copy of rot_params + one graph launch)
-    step = model.capture_repose(rot_dim=poses.shape[-1])
+    # the sweep's poses in their order: the graph reads pose i from the sweep through a device
+    # index it advances itself (no per-pose input copy; TemporalPoints.capture_repose)
+    step = model.capture_repose(sweep=poses)
     for i in range(args.warmup):
         step(poses[i % len(poses)])
     if world > 1:
@@ -248,7 +250,7 @@ def lbs_sweep(args, rank, world, dev):
         "vs_baseline": None, "dtype": "fp32", "data": "synthetic (procedural 48-joint capsule cloud, repose sweep)",
         "config": {"workload": S.CONFIGS[args.config].name + f" ({args.config})", "points": N_total, "bones": J,
                    "points_per_rank": N, "poses_per_s": args.steps / elapsed,
-                   "step": "skeleton + LBS captured in one HIP graph (TemporalPoints.capture_repose)",
+                   "step": "skeleton + LBS captured in one HIP graph reading the sweep's next pose (TemporalPoints.capture_repose(sweep=...))",
                    "lbs_kernel_ms": lbs_ms,
                    "parallelism": f"points x{world} (no collective)" if world > 1 else "single"},
         "roofline": {"bound": "hbm", "kernel": "k_lbs_skin_quad",

@@ -191,14 +191,18 @@ int apn_skeleton_pose(const float* t_embed, int32_t t_dim, const float* rot_para
  * utils.py:435-450)). As apn_skeleton_pose, except: t path = t [1] (device) with the time
  * embedding [t, sin(t f), cos(t f)] of the n_freq frequencies time_poc computed in the kernel
  * (t_dim = 1 + 2 n_freq); c2w [n_views,4,4], K [n_views,3,3] -> joints2d_out [n_views,J,2]
- * (n_views <= 16, n_views * J <= 1024; 0 = no projection). */
+ * (n_views <= 16, n_views * J <= 1024; 0 = no projection). sweep_index (rot path, optional, device
+ * int32): rot_params holds sweep_len poses [sweep_len, J, rot_dim]; the launch takes pose
+ * *sweep_index % sweep_len and advances *sweep_index (the repose sweep of run.py:1355-1396 as a
+ * captured graph without a per-pose input copy); NULL = rot_params is one pose. */
 int apn_skeleton_frame(const float* t, const float* time_poc, int32_t n_freq, const float* rot_params,
                        int32_t rot_dim, int32_t n_joints, const float* tn_weights, int32_t hidden, int32_t n_layers,
                        const float* joints, const int32_t* parent_indices, int32_t depth,
                        const int32_t* parent_joint_ex, const int32_t* sibling_mask, const int32_t* rot_mask,
                        float* params_out, float* thetas_out, float* bone_T16, float* bone_T34,
                        float* global_t_out, float* joints_rel_out, const int32_t* chain_prog,
-                       const float* c2w, const float* K, int32_t n_views, float* joints2d_out, void* stream);
+                       const float* c2w, const float* K, int32_t n_views, float* joints2d_out,
+                       int32_t* sweep_index, int32_t sweep_len, void* stream);
 
 /* Padded sampling bbox = bbox_ord -/+ query_radius (temporalpoints.py:424) as 6 floats. */
 int apn_bbox_unpack(const int32_t* bbox_ord, float query_radius, float* out6, void* stream);
