@@ -1,0 +1,6 @@
+source tools/gpu_steps.sh
+step tests 900 python -u -m pytest tests -m gpu -q -x -rf --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_au.log 2>&1
+tail -1 gpurun_out/gpu_tests_au.log
+step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+step bench 300 python -u bench.py -o gpurun_out/bench_au.json
+step rocprof 400 bash tools/bench_rocprof.sh gpurun_out/prof_au
