@@ -1196,6 +1196,67 @@ __global__ __launch_bounds__(KNN_THREADS) void k_cell_bound3(const GridParams* _
   u4[cell] = a4;
 }
 
+// k_cell_bound3 with 16 lanes per cell, for short cell lists (ray shards): one thread per cell
+// walks its ~650 row loads in sequence, and with few cells that walk sets the launch time (a
+// shard of 1/8 of a C2 frame took 117 us against 190 for the whole frame). Lane l takes every
+// 16th (z, y) row of the window; the integer sums are combined with shuffles (exact, any order).
+// On a full frame the list is long and the plain kernel is load-throughput bound (the 16-lane
+// form measured 2x slower there), so apn_knn_radius picks by query count.
+constexpr int CB_LANES = 16;
+__global__ __launch_bounds__(KNN_THREADS) void k_cell_bound3w(const GridParams* __restrict__ gp,
+                                                             const int* __restrict__ cell_start,
+                                                             const int* __restrict__ list,
+                                                             const int* __restrict__ n_list, int* __restrict__ u1,
+                                                             int* __restrict__ u2, int* __restrict__ u4) {
+  const int nl = *n_list;
+  const GridParams g = *gp;
+  const int sub = threadIdx.x % CB_LANES;
+  const float lim = g.r2 * 1.0002f * g.inv_h * g.inv_h;   // (r/h)^2 with slack, as k_cell_bound3
+  const int K = (int)ceilf(sqrtf(lim)) + 1;
+  const int W = 2 * K + 1;
+  for (int base = blockIdx.x * (KNN_THREADS / CB_LANES); base < nl; base += gridDim.x * (KNN_THREADS / CB_LANES)) {
+    const int i = base + threadIdx.x / CB_LANES;
+    const bool ok = i < nl;
+    const int cell = ok ? list[i] : 0;
+    const int cx = cell % g.dx, cy = (cell / g.dx) % g.dy, cz = cell / (g.dx * g.dy);
+    int a1 = 0, a2 = 0, a4 = 0;
+    if (ok) {
+      for (int p = sub; p < W * W; p += CB_LANES) {
+        const int dz = p / W - K, dy = p % W - K;
+        const int z = cz + dz, y = cy + dy;
+        if (z < 0 || z >= g.dz || y < 0 || y >= g.dy) continue;
+        const float gz = (float)max(abs(dz) - 1, 0), gy = (float)max(abs(dy) - 1, 0);
+        const float rem = lim - gz * gz - gy * gy;
+        if (rem < 0.f) continue;
+        const int row = (z * g.dy + y) * g.dx;
+        const int kx = (int)floorf(sqrtf(rem)) + 1;
+        a1 += cell_start[row + min(cx + kx, g.dx - 1) + 1] - cell_start[row + max(cx - kx, 0)];
+        const float rem2 = 0.25f * lim - gz * gz - gy * gy;
+        if (rem2 >= 0.f) {
+          const int k2 = (int)floorf(sqrtf(rem2)) + 1;
+          a2 += cell_start[row + min(cx + k2, g.dx - 1) + 1] - cell_start[row + max(cx - k2, 0)];
+          const float rem4 = 0.0625f * lim - gz * gz - gy * gy;
+          if (rem4 >= 0.f) {
+            const int k4 = (int)floorf(sqrtf(rem4)) + 1;
+            a4 += cell_start[row + min(cx + k4, g.dx - 1) + 1] - cell_start[row + max(cx - k4, 0)];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int o = CB_LANES / 2; o > 0; o >>= 1) {
+      a1 += __shfl_xor(a1, o, 64);
+      a2 += __shfl_xor(a2, o, 64);
+      a4 += __shfl_xor(a4, o, 64);
+    }
+    if (ok && sub == 0) {
+      u1[cell] = a1;
+      u2[cell] = a2;
+      u4[cell] = a4;
+    }
+  }
+}
+
 // Pass A of mode 8: reject on u1 < 8; the r/4 ball (flat scan) only where u4 >= 8; the rest go to
 // the hard list tagged with their first useful level (r/2 if u2 >= 8, else r).
 template <bool ANISO>
@@ -1821,8 +1882,17 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
                        g.gp, ccell, mark);
     hipLaunchKernelGGL(k_tile_list, dim3(ceil_div(cell_cap, LIST_THREADS)), dim3(LIST_THREADS), 0, s, mark, cell_cap,
                        g.tile_list, g.n_tile_list);
-    hipLaunchKernelGGL(k_cell_bound3, dim3(ceil_div(std::min<int64_t>(cell_cap, slots), KNN_THREADS)),
-                       dim3(KNN_THREADS), 0, s, g.gp, g.cell_start, g.tile_list, g.n_tile_list, u1, u2, u4);
+    static const int64_t cb16_max = [] {   // query count up to which the cell bounds run 16 lanes per cell
+      const char* e = getenv("APN_CELL_BOUND16_MAX");
+      return e ? (int64_t)atoll(e) : (int64_t)3 << 20;
+    }();
+    if (n_queries <= cb16_max)
+      hipLaunchKernelGGL(k_cell_bound3w,
+                         dim3(std::max<int64_t>(1, std::min<int64_t>(256 * 16, ceil_div(std::min<int64_t>(cell_cap, slots) * CB_LANES, KNN_THREADS)))),
+                         dim3(KNN_THREADS), 0, s, g.gp, g.cell_start, g.tile_list, g.n_tile_list, u1, u2, u4);
+    else
+      hipLaunchKernelGGL(k_cell_bound3, dim3(ceil_div(std::min<int64_t>(cell_cap, slots), KNN_THREADS)),
+                         dim3(KNN_THREADS), 0, s, g.gp, g.cell_start, g.tile_list, g.n_tile_list, u1, u2, u4);
     int* hard_r = ccell + slots;          // second quarter of the t_pos region
     static const bool a_aniso = getenv("APN_KNN_A_ANISO") != nullptr;   // A/B: pass A's r/4 ball on the second grid
     hipLaunchKernelGGL((aniso && a_aniso) ? k_knn_pass_a8<true> : k_knn_pass_a8<false>, dim3(nb), dim3(KNN_THREADS), 0,
