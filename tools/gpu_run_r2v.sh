@@ -1,4 +1,4 @@
+#!/bin/bash
+# Interleaved-block ray shards vs the cost split, one-GPU emulation.
 source tools/gpu_steps.sh
-step tests 600 python -u -m pytest tests/test_frame_graph.py tests/test_hip_parity.py tests/test_0_shard_spawn.py -m gpu -q -x -rf --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_v.log 2>&1
-tail -3 gpurun_out/gpu_tests_v.log
-AB_STEPS=20 step ab 600 bash tools/ab.sh "APN_AB=conc" "APN_CONCURRENT_GRID=0" "APN_AB=conc2" "APN_CONCURRENT_GRID=0"
+step ilv 400 python -u tools/shard_balance.py --split cost,ilv64,ilv800,ilv4096 --worlds 4,8 --reps 5 > gpurun_out/ilv.log 2>&1

@@ -7,6 +7,8 @@ what a strong-scaling step waits for. Diagnostic tool (not a test).
 
 --split cost: the split render_sharded uses from the second frame on (shard.cost_offsets of the
 previous frame's survivors and in-bbox samples), preset in the model's SplitTracker.
+--split ilv<B>: interleaved blocks of B rays (rank k takes blocks k, k + W, ...), each rank's rays
+gathered and rendered as a frame of their own (equal ray counts: an unpadded all-gather).
 """
 from __future__ import annotations
 
@@ -74,6 +76,27 @@ def main():
     if args.kept_weights:
         splits = [s for s in splits if s != "cost"] + [f"cost{w}" for w in args.kept_weights.split(",")]
     for split, world in [(sp, int(w)) for sp in splits for w in args.worlds.split(",")]:
+        if split.startswith("ilv"):
+            B = int(split[3:])
+            blk = torch.arange(R, device=dev) // B
+            rows = []
+            for k in range(world):
+                idx = torch.nonzero(blk % world == k).squeeze(1)
+                rkk = dict(rk, rays_o=rk["rays_o"][idx].contiguous(), rays_d=rk["rays_d"][idx].contiguous(),
+                           viewdirs=rk["viewdirs"][idx].contiguous())
+                kwk = dict(kw, render_kwargs=rkk)
+                ms, o = timed(lambda: model(t, **kwk), args.reps)
+                s = model.last_stats.resolved()
+                rows.append((ms, s.get("inbbox_samples", -1), s.get("kept_samples", -1), idx.numel()))
+                print(f"   shard {k}: {ms:.3f} ms, stages " + " ".join(f"{n} {v:.3f}" for n, v in stages.items()))
+            mx = max(r[0] for r in rows)
+            mean = sum(r[0] for r in rows) / world
+            print(f"[{split}] world {world}: shard ms " + " ".join(f"{r[0]:.3f}" for r in rows)
+                  + f" | max {mx:.3f} mean {mean:.3f} (max/mean {mx / mean:.3f}); ideal full/world {full_ms / world:.3f}; "
+                  f"speedup bound {full_ms / mx:.2f}x")
+            print("   kept per shard: " + " ".join(str(r[2]) for r in rows)
+                  + " | inbbox per shard: " + " ".join(str(r[1]) for r in rows))
+            continue
         model._splits.clear()
         model._capacity = {k: v for k, v in model._capacity.items() if not isinstance(k, tuple)}
         if split.startswith("cost"):
