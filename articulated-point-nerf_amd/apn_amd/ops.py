@@ -18,14 +18,22 @@ def _f32c(t):
 
 
 class Workspace:
-    """Grow-only device scratch buffers keyed by name (reused across forward calls)."""
+    """Grow-only device scratch buffers keyed by name (reused across forward calls). Once a HIP
+    graph has captured them (``pinned``, set by capture_frame / capture_repose) a replaced buffer is
+    kept alive, not freed: the graph holds its address, and a later larger frame (an overflow
+    rendered again exactly, another ray shard's capture, a bigger ray set) must not hand that
+    memory to anything else."""
 
     def __init__(self):
         self.bufs = {}
+        self.retired = []
+        self.pinned = False
 
     def get(self, name, numel, dtype, device):
         b = self.bufs.get(name)
         if b is None or b.numel() < numel or b.dtype != dtype or b.device != torch.device(device):
+            if b is not None and self.pinned:
+                self.retired.append(b)
             b = torch.empty(max(int(numel), 1), dtype=dtype, device=device)
             self.bufs[name] = b
         return b[:max(int(numel), 1)]

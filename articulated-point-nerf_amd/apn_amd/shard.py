@@ -10,13 +10,23 @@ Tile layout: [rays, 12] float32 = rgb_marched (3), rgb_marched_direct (3), depth
 weights (3), alphainv_last (1), alphainv_last_direct (1); render_sharded appends one column, the
 ray's kNN survivor count, for the next frame's split.
 
-Load balance: a shard's time follows its kNN survivors (the MLP's rows) far more than its in-bbox
-samples -- at C2 with 8 ranks, equal in-bbox shards held 0.13M to 0.60M survivors and took 1.5 to
-3.5 ms (tools/shard_balance.py). The first frame splits the in-bbox samples; every later frame
-splits the previous frame's per-ray cost KEPT_WEIGHT * survivors + in-bbox samples (the survivor
-counts ride in the tile all-gather, so every rank computes the same split).
+Two splits (``render_sharded(split=...)``, default ``DEFAULT_SPLIT``, env APN_SHARD_SPLIT):
+
+* ``"blocks"`` (default): fixed blocks of RAY_BLOCK consecutive rays dealt round-robin, rank k
+  taking blocks k, k + world, ... Every rank holds the same number of rays (to one block), so the
+  all-gather is unpadded, and the image-space interleave balances the work statistically from
+  the first frame: at C2 with 8 ranks the slowest shard is 1.02x the mean (2.14 ms, bound 5.12x
+  of the 10.98 ms frame) against 1.12x (2.27 ms) for the cost-balanced ranges below, whose
+  unequal ray counts also pad the gather to the longest range (tools/shard_balance.py --split).
+* ``"ranges"``: one contiguous ray range per rank. A shard's time follows its kNN survivors (the
+  MLP's rows) far more than its in-bbox samples -- at C2 with 8 ranks, equal in-bbox shards held
+  0.13M to 0.60M survivors and took 1.5 to 3.5 ms. The first frame splits the in-bbox samples;
+  every later frame splits the previous frame's per-ray cost KEPT_WEIGHT * survivors + in-bbox
+  samples (the survivor counts ride in the tile all-gather, so every rank computes the same split).
 """
 from __future__ import annotations
+
+import os
 
 import torch
 
@@ -24,6 +34,56 @@ TILE_KEYS = (("rgb_marched", 3), ("rgb_marched_direct", 3), ("depth", 1), ("weig
              ("alphainv_last", 1), ("alphainv_last_direct", 1))
 TILE_WIDTH = sum(w for _, w in TILE_KEYS)
 KEPT_WEIGHT = 10   # cost of a survivor (neighbour MLP + its kNN) in in-bbox-sample units: ~4.5 vs ~0.45 ns at C2
+RAY_BLOCK = 4096   # rays per block of the "blocks" split (~5 image rows at 800 wide; 64 and 800 measured slower)
+DEFAULT_SPLIT = os.environ.get("APN_SHARD_SPLIT", "blocks")
+
+
+def block_rays(R: int, rank: int, world: int, block: int = RAY_BLOCK) -> torch.Tensor:
+    """Ray indices (int64, ascending, CPU) of rank's blocks k, k + world, ... of ``block`` rays
+    (the last block of the frame may be short)."""
+    if rank * block >= R:
+        return torch.zeros(0, dtype=torch.int64)
+    starts = torch.arange(rank * block, R, world * block, dtype=torch.int64)
+    idx = (starts[:, None] + torch.arange(block, dtype=torch.int64)[None]).reshape(-1)
+    return idx[idx < R]
+
+
+def block_slots(R: int, world: int, block: int = RAY_BLOCK) -> int:
+    """Block slots per rank: ceil(ceil(R / block) / world)."""
+    return -(-(-(-R // block)) // world)
+
+
+def assemble_blocks(parts: torch.Tensor, R: int, world: int, block: int = RAY_BLOCK) -> torch.Tensor:
+    """[world, slots * block, w] per-rank tiles (rank k's blocks in order, zero-padded) -> the
+    frame's [R, w] in ray order: block j is slot j // world of rank j % world."""
+    per = block_slots(R, world, block)
+    w = parts.shape[-1]
+    return parts[:, :per * block].reshape(world, per, block, w).transpose(0, 1).reshape(per * world * block, w)[:R]
+
+
+def gather_blocks(tile: torch.Tensor, R: int, world: int, block: int = RAY_BLOCK, group=None,
+                  info: torch.Tensor | None = None):
+    """All-gather of the "blocks" split: every rank's tile is padded to the same slots * block rows
+    (at most one block of padding), plus one row carrying its frame_info [4] when given ->
+    ([R, w] in ray order, infos [world, 4] int32 or None)."""
+    import torch.distributed as dist
+    m = block_slots(R, world, block) * block
+    rows = m + (1 if info is not None else 0)
+    assert tile.shape[0] <= m, (tile.shape, m)
+    padded = torch.zeros(rows, tile.shape[1], device=tile.device, dtype=tile.dtype)
+    padded[:tile.shape[0]] = tile
+    if info is not None:
+        padded[m, :4] = info.to(torch.int32).view(torch.float32)
+    full = torch.empty(world * rows, tile.shape[1], device=tile.device, dtype=tile.dtype)
+    if dist.get_backend(group) == "gloo":
+        dist.all_gather(list(full.view(world, rows, -1).unbind(0)), padded, group=group)
+    else:
+        dist.all_gather_into_tensor(full, padded, group=group)
+    parts = full.view(world, rows, -1)
+    tiles = assemble_blocks(parts[:, :m], R, world, block)
+    if info is None:
+        return tiles, None
+    return tiles, parts[:, m, :4].contiguous().view(torch.int32)
 
 
 def cost_offsets(offsets: torch.Tensor, kept: torch.Tensor) -> torch.Tensor:
@@ -205,21 +265,51 @@ class ShardedFrame(dict):
 
 
 @torch.no_grad()
-def render_sharded(model, t, render_kwargs, rank: int, world: int, group=None, **forward_kwargs) -> dict:
-    """One frame rendered by ``world`` ranks: this rank's ray range through
-    TemporalPoints.forward(ray_shard=(rank, world)), then the tile all-gather. Returns the
-    reference output keys for all rays on every rank (a ShardedFrame, validated on first read)."""
-    out = model(t, render_kwargs=render_kwargs, ray_shard=(rank, world), render_depth=True,
+def render_sharded(model, t, render_kwargs, rank: int, world: int, group=None, split: str | None = None,
+                   block: int = RAY_BLOCK, **forward_kwargs) -> dict:
+    """One frame rendered by ``world`` ranks: this rank's rays through
+    TemporalPoints.forward(ray_shard=(rank, world, block)) ("blocks" split) or
+    forward(ray_shard=(rank, world)) ("ranges"), then the tile all-gather. Returns the reference
+    output keys for all rays on every rank (a ShardedFrame, validated on first read)."""
+    split = split or DEFAULT_SPLIT
+    if split not in ("blocks", "ranges"):
+        raise ValueError(f"split must be 'blocks' or 'ranges', got {split!r}")
+    blocks = split == "blocks"
+    shard = (rank, world, block) if blocks else (rank, world)
+    out = model(t, render_kwargs=render_kwargs, ray_shard=shard, render_depth=True,
                 render_weights=True, **forward_kwargs)
-    r0, r1 = model.last_ray_range
+    return _assemble(model, t, out, render_kwargs, rank, world, group, blocks, block, forward_kwargs)
+
+
+def capture_sharded(model, t, render_kwargs, rank: int, world: int, group=None, block: int = RAY_BLOCK,
+                    **forward_kwargs):
+    """The "blocks" split with this rank's frame captured as one HIP graph
+    (TemporalPoints.capture_frame(ray_shard=(rank, world, block))): returns ``step(t)``, which
+    replays the graph and all-gathers the tiles (the collective stays outside the graph, so the
+    same step runs over RCCL or gloo) -> a ShardedFrame like render_sharded's. Capture again after
+    changing the model or the rays."""
+    local = model.capture_frame(t, render_kwargs, ray_shard=(rank, world, block), **forward_kwargs)
+
+    def step(t):
+        out = local(t)
+        return _assemble(model, t, out, render_kwargs, rank, world, group, True, block, forward_kwargs)
+    step.graph = local.graph
+    return step
+
+
+def _assemble(model, t, out, render_kwargs, rank, world, group, blocks, block, forward_kwargs):
     dev = render_kwargs["rays_o"].device
-    tile = pack_tile(out, r1 - r0, dev)
-    kept = model.last_kept_per_ray(r1 - r0)
-    tile = torch.cat([tile, kept.float().reshape(-1, 1)], dim=1)   # survivors per ray (exact in f32)
+    R = render_kwargs["rays_o"].shape[0]
+    n = model.last_ray_count
+    tile = pack_tile(out, n, dev)
     info = getattr(out, "_info", None)
-    if world > 1:
-        if info is None:   # exact path: nothing was dropped
-            info = torch.zeros(4, dtype=torch.int32, device=dev)
+    if world > 1 and info is None:   # exact path: nothing was dropped
+        info = torch.zeros(4, dtype=torch.int32, device=dev)
+    if world > 1 and blocks:
+        full, infos = gather_blocks(tile, R, world, block, group, info=info)
+    elif world > 1:
+        kept = model.last_kept_per_ray(n)
+        tile = torch.cat([tile, kept.float().reshape(-1, 1)], dim=1)   # survivors per ray (exact in f32)
         full, infos = gather_tiles(tile, model.last_ray_bounds, group, info=info)
         tracker = model.last_split_tracker
         if tracker is not None and not model._force_exact:
@@ -233,7 +323,7 @@ def render_sharded(model, t, render_kwargs, rank: int, world: int, group=None, *
     def rerender(infos):
         # grow this rank's capacity from its in-bbox total (frame_info[1]) for the frames to come
         from .temporalpoints import _grow_capacity
-        key = (render_kwargs["rays_o"].shape[0], rank, world)
+        key = (R, rank, world, block) if blocks else (R, rank, world)
         model._capacity[key] = max(model._capacity.get(key, 0), _grow_capacity(int(infos[rank, 1])))
         model._force_exact = True
         try:

@@ -312,6 +312,7 @@ class TemporalPoints(torch.nn.Module):
         self._side_streams = {}
         self._splits = {}           # (ray count, world) -> SplitTracker of the ray-sharded frames
         self.last_split_tracker = self.last_full_offsets = self._last_ray_ws = None
+        self._block_index = {}      # (ray count, rank, world, block) -> ray indices of the "blocks" split
         self._force_exact = False
         self._last_info = None
 
@@ -510,6 +511,7 @@ class TemporalPoints(torch.nn.Module):
             with torch.cuda.stream(side):   # warm-up: caches, workspaces, packed buffers
                 self.repose(rp)
             torch.cuda.current_stream(dev).wait_stream(side)
+            self._ws.pinned = True   # the graph holds workspace addresses from here on
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
                 if sweep is None:
@@ -544,7 +546,7 @@ class TemporalPoints(torch.nn.Module):
         return step
 
     def capture_frame(self, t, render_kwargs, render_depth=True, render_weights=True, query_radius=0.01, poses=None,
-                      Ks=None, get_skeleton=False):
+                      Ks=None, get_skeleton=False, ray_shard=None):
         """The render frame for a fixed ray set (skeleton, LBS, grid, sampling, kNN, MLP,
         compositing: the whole no-grad forward) captured once in a HIP graph: returns
         ``step(t) -> RenderOutput``, which copies the time into the graph's input and replays it.
@@ -553,14 +555,19 @@ class TemporalPoints(torch.nn.Module):
         whose samples overflowed the capacity is rendered again eagerly. Needs no host sync inside
         the frame: the capacity is set by the warm-up frames. Capture again after changing the
         model or the rays. ``get_skeleton`` (with fixed ``poses`` / ``Ks``) captures the joint
-        projection too, as the eager forward runs it."""
+        projection too, as the eager forward runs it. ``ray_shard=(rank, world, block)`` captures
+        this rank's frame of the "blocks" ray split (apn_amd.shard.capture_sharded); the
+        contiguous-range split is not capturable (its split moves from frame to frame)."""
+        if ray_shard is not None and len(ray_shard) != 3:
+            raise ValueError("capture_frame: ray_shard must be (rank, world, block) (the blocks split)")
         dev = self.canonical_feat.device
         t_in = torch.as_tensor(t, dtype=torch.float32, device=dev).reshape(-1).clone()
         rk = dict(render_kwargs)
         R = len(rk['rays_o'])
         if get_skeleton:
             poses, Ks = poses.to(dev), Ks.to(dev, torch.float32)   # device-resident before the capture
-        args = (render_depth, rk, query_radius, render_weights, None, poses, Ks, True, get_skeleton, None)
+        args = (render_depth, rk, query_radius, render_weights, None, poses, Ks, True, get_skeleton, ray_shard)
+        cap_key = R if ray_shard is None else (R, *ray_shard)
         with torch.no_grad():
             side = torch.cuda.Stream(dev)
             side.wait_stream(torch.cuda.current_stream(dev))
@@ -569,8 +576,9 @@ class TemporalPoints(torch.nn.Module):
                 warm = self._forward_render(t_in, *args)
             torch.cuda.current_stream(dev).wait_stream(side)
             warm.keys()   # validate: an overflow renders again and grows the capacity
-            if self._capacity.get(R) is None:
+            if self._capacity.get(cap_key) is None:
                 raise RuntimeError("capture_frame: no sample capacity for this ray set (empty frame?)")
+            self._ws.pinned = True   # the graph holds workspace addresses from here on
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
                 out = self._forward_render(t_in, *args)
@@ -698,7 +706,10 @@ class TemporalPoints(torch.nn.Module):
 
         ``ray_shard=(rank, world)`` (not in the reference signature) renders only this rank's
         contiguous ray range with ~1/world of the frame's in-bbox samples; the range is left in
-        ``self.last_ray_range`` (see apn_amd.shard for the tile all-gather)."""
+        ``self.last_ray_range``. ``ray_shard=(rank, world, block)`` renders the rank's blocks
+        k, k + world, ... of ``block`` consecutive rays (their indices in
+        ``self.last_ray_index``). Either way ``self.last_ray_count`` is the rank's ray count (see
+        apn_amd.shard for the tile all-gather)."""
         assert (t is None) ^ (rot_params is None)
         if torch.is_grad_enabled():
             if ray_shard is not None:
@@ -751,7 +762,7 @@ class TemporalPoints(torch.nn.Module):
         except NoPointsException:
             bg = render_kwargs['bg']
             if ray_shard is not None:
-                R = self.last_ray_range[1] - self.last_ray_range[0]
+                R = self.last_ray_count
             return {'rgb_marched': torch.ones(R, 3, device=dev) * bg,
                     'rgb_marched_direct': torch.ones(R, 3, device=dev) * bg,
                     'depth': torch.zeros(R, device=dev), 'weights': torch.ones(R, 3, device=dev) * bg,
@@ -808,6 +819,20 @@ class TemporalPoints(torch.nn.Module):
         vd = rk['viewdirs'].detach().float().contiguous()
         L.require_cuda(ro, rd, vd, what="render_kwargs")
         R = ro.shape[0]
+        block_key = None
+        if shard is not None and len(shard) == 3:
+            # interleaved ray blocks (shard.py "blocks" split): this rank's rays, gathered
+            rank, world, block = shard
+            block_key = (R, rank, world, block)
+            idx = self._block_index.get(block_key)
+            if idx is None or idx.device != dev:
+                from .shard import block_rays
+                idx = self._block_index[block_key] = block_rays(R, rank, world, block).to(dev)
+            ro, rd, vd = ro.index_select(0, idx), rd.index_select(0, idx), vd.index_select(0, idx)
+            self.last_ray_index, self.last_ray_range, self.last_ray_count = idx, None, idx.numel()
+            R = idx.numel()
+            if R == 0:
+                raise NoPointsException("No rays in this shard.")
         qr = float(query_radius)
         stepdist = float(rk['stepsize']) * float(self.voxel_size)
         interval = float(rk['stepsize']) * float(self.tineuvox.voxel_size_ratio)
@@ -843,8 +868,8 @@ class TemporalPoints(torch.nn.Module):
         offs = ws.get("offs", R + 1, torch.int32, dev)
         sws = ws.bytes("samp_ws", lib.apn_sample_pts_on_rays_workspace_bytes(R), dev)
         call("apn_inbbox_count", ptr(ro), ptr(rd), ptr(bbox6), near, far, stepdist, R, ptr(offs), ptr(sws), s)
-        cap_key = R
-        if shard is not None:
+        cap_key = R if block_key is None else block_key
+        if shard is not None and block_key is None:
             # contiguous ray range holding ~1/world of the in-bbox samples; after
             # the first frame, the split of the previous frame's counts (no host sync, shard.py)
             rank, world = shard
@@ -855,6 +880,7 @@ class TemporalPoints(torch.nn.Module):
             r0, r1 = bounds[rank], bounds[rank + 1]
             self.last_ray_range = (r0, r1)
             self.last_ray_bounds = bounds
+            self.last_ray_count = r1 - r0
             ro, rd, vd = ro[r0:r1], rd[r0:r1], vd[r0:r1]
             offs = (offs[r0:r1 + 1] - offs[r0]).contiguous()
             R = r1 - r0

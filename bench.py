@@ -289,8 +289,9 @@ def main():
                          "over RCCL (strong scaling, SURVEY.md 8(e)); 'frames' = every rank renders its own "
                          "frame (weak scaling, no data-path collective)")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
-                    help="replay the frame as one HIP graph (TemporalPoints.capture_frame); auto = on unless "
-                         "the ranks split one frame's rays (the split is read on the host)")
+                    help="replay the frame as one HIP graph (TemporalPoints.capture_frame; with --shard rays "
+                         "each rank's blocks, shard.capture_sharded); auto = on unless the ranks use the "
+                         "'ranges' ray split (APN_SHARD_SPLIT=ranges: its split moves per frame)")
     args = ap.parse_args()
     torch.set_grad_enabled(False)   # a render benchmark: the reference renders under no_grad (run.py:80, 241)
 
@@ -326,7 +327,9 @@ def main():
     log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.2f}s, rays/frame {R}")
 
     poses, Ks = scene.c2w[None].to(dev), scene.K[None].to(dev)
-    use_graph = args.graph == "on" or (args.graph == "auto" and not shard_rays)
+    from apn_amd import shard as SH
+    # the blocks ray split captures each rank's frame as a graph; the ranges split moves per frame
+    use_graph = args.graph == "on" or (args.graph == "auto" and not (shard_rays and SH.DEFAULT_SPLIT == "ranges"))
 
     def eager_step():
         if shard_rays:
@@ -342,7 +345,10 @@ def main():
     stats = model.last_stats.resolved()
     log(f"[rank {rank}] scene: {stats}")
     if use_graph:   # the whole frame as one HIP graph replay (no per-kernel host launches, no host sync)
-        graph_step = model.capture_frame(t_arg, rk, poses=poses, Ks=Ks, get_skeleton=True)
+        if shard_rays:   # this rank's blocks as one graph replay, then the tile all-gather
+            graph_step = SH.capture_sharded(model, t_arg, rk, rank, world, poses=poses, Ks=Ks, get_skeleton=True)
+        else:
+            graph_step = model.capture_frame(t_arg, rk, poses=poses, Ks=Ks, get_skeleton=True)
         step = lambda: graph_step(t_arg)   # noqa: E731
         for _ in range(2):
             step()
@@ -462,10 +468,14 @@ def main():
         "config": {"workload": S.CONFIGS[args.config].name + f" ({args.config})", "rays_per_frame": R,
                    "points": scene.cfg.N, "bones": scene.cfg.J, "inbbox_samples": stats.get("inbbox_samples"),
                    "kept_samples": S_kept,
-                   "parallelism": (f"rays x{world} + {backend} all_gather_into_tensor of the per-ray tiles"
+                   "parallelism": (f"rays x{world} ({SH.DEFAULT_SPLIT} split"
+                                   + (f" of {SH.RAY_BLOCK}-ray blocks" if SH.DEFAULT_SPLIT == "blocks" else "")
+                                   + f") + {backend} all_gather_into_tensor of the per-ray tiles"
                                    if shard_rays else f"frames x{world} (no data-path collective)")
                    if world > 1 else "single",
-                   "step": ("whole frame replayed as one HIP graph (TemporalPoints.capture_frame)" if use_graph
+                   "step": (("each rank's blocks replayed as one HIP graph (shard.capture_sharded), then the "
+                             "all-gather" if shard_rays else
+                             "whole frame replayed as one HIP graph (TemporalPoints.capture_frame)") if use_graph
                             else "eager launches")},
         "roofline": {"bound": "mfma", "kernel": kernel, "achieved": achieved, "peak": peak,
                      "unit": "TFLOP/s", "frac": achieved / peak,

@@ -1,7 +1,7 @@
 """Ray-sharded rendering across real processes (apn_amd/shard.py).
 
-Two fresh child processes (torch.multiprocessing ``spawn``) each render their ray range of one
-frame through ``render_sharded`` and assemble the frame with the tile all-gather over ``gloo``
+Two fresh child processes (torch.multiprocessing ``spawn``) each render their rays of one
+frame through ``render_sharded`` (both splits: interleaved ray blocks, contiguous ranges) and assemble the frame with the tile all-gather over ``gloo``
 (RCCL needs one GPU per rank; this box has one). Rank 0 also renders the frame in one process.
 The assembled frames of both ranks must equal the single-process frame bit for bit.
 
@@ -31,11 +31,11 @@ def _assembled(out, R, dev):
     return torch.cat([out[k].reshape(R, w).float() for k, w in TILE_KEYS], dim=1).cpu()   # validated reads
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, split):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     import torch.distributed as dist
     from apn_amd import harness, synthetic as S
-    from apn_amd.shard import pack_tile, render_sharded
+    from apn_amd.shard import RAY_BLOCK, capture_sharded, pack_tile, render_sharded
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         dev = torch.device("cuda", 0)
@@ -52,13 +52,20 @@ def _worker(rank, world, port, outdir):
             # frame 0: exact path (split and sample count read on the host); frames 1-2: the
             # sync-free path (previous frame's split, per-rank capacity); frame 3: rank 1 overflows
             # its capacity, which every rank must detect through the gathered frame_info rows
+            # ("graph": the blocks split with each rank's frame replayed from a HIP graph, bench's step)
+            step = capture_sharded(model, t0, rk, rank, world, **kw) if split == "graph" else None
             for i, t in enumerate((t0, t1, t0, t1)):
-                if i == 3 and rank == 1:
-                    model._capacity[(R, rank, world)] = 64
-                out = render_sharded(model, t, rk, rank, world, **kw)
+                if i == 3 and rank == 1 and step is None:
+                    model._capacity[(R, rank, world, RAY_BLOCK) if split == "blocks" else (R, rank, world)] = 64
+                if step is not None:
+                    out = step(t)
+                else:
+                    out = render_sharded(model, t, rk, rank, world, split=split, **kw)
                 tiles[f"assembled{i}"] = _assembled(out, R, dev)
-                tiles[f"range{i}"] = torch.tensor(model.last_ray_range)
-                tiles[f"bounds{i}"] = torch.tensor(model.last_ray_bounds)
+                tiles[f"count{i}"] = torch.tensor(model.last_ray_count)
+                if split == "ranges":
+                    tiles[f"range{i}"] = torch.tensor(model.last_ray_range)
+                    tiles[f"bounds{i}"] = torch.tensor(model.last_ray_bounds)
             if rank == 0:
                 for i, t in enumerate((t0, t1)):
                     single = model(t, render_depth=True, render_kwargs=rk, render_weights=True, **kw)
@@ -69,24 +76,31 @@ def _worker(rank, world, port, outdir):
         dist.destroy_process_group()
 
 
-def test_render_sharded_two_processes_bit_identical():
+@pytest.mark.parametrize("split", ["blocks", "ranges", "graph"])
+def test_render_sharded_two_processes_bit_identical(split):
     import torch.multiprocessing as mp
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(WORLD, _free_port(), d), nprocs=WORLD, join=True)
+        mp.spawn(_worker, args=(WORLD, _free_port(), d, split), nprocs=WORLD, join=True)
         res = [torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=True) for r in range(WORLD)]
     for i in range(4):
         single = res[0][f"single{i % 2}"]
-        bounds = res[0][f"bounds{i}"].tolist()
-        assert bounds[0] == 0 and bounds[-1] == single.shape[0]
-        assert torch.equal(res[1][f"bounds{i}"], res[0][f"bounds{i}"]), i   # every rank on the same split
+        R = single.shape[0]
+        if split == "ranges":
+            bounds = res[0][f"bounds{i}"].tolist()
+            assert bounds[0] == 0 and bounds[-1] == R
+            assert torch.equal(res[1][f"bounds{i}"], res[0][f"bounds{i}"]), i   # every rank on the same split
+            # both ranks did real work (the object is hit by rays of both halves of the split)
+            assert 0 < bounds[1] < R
+        else:
+            bounds = None
+            assert int(res[0][f"count{i}"]) + int(res[1][f"count{i}"]) == R
         for r in range(WORLD):
-            assert tuple(res[r][f"range{i}"].tolist()) == (bounds[r], bounds[r + 1])
+            if split == "ranges":
+                assert tuple(res[r][f"range{i}"].tolist()) == (bounds[r], bounds[r + 1])
             a = res[r][f"assembled{i}"]
             if not torch.equal(a, single):
                 bad = (a != single).any(1).nonzero().flatten()
                 cols = (a != single).any(0).nonzero().flatten().tolist()
-                raise AssertionError(f"frame {i} rank {r}: {len(bad)} rays differ (first {bad[:8].tolist()}), "
+                raise AssertionError(f"{split} frame {i} rank {r}: {len(bad)} rays differ (first {bad[:8].tolist()}), "
                                      f"columns {cols}, max |d| {float((a - single).abs().max()):.3e}, "
                                      f"bounds {bounds}")
-        # both ranks did real work (the object is hit by rays of both halves of the split)
-        assert 0 < bounds[1] < single.shape[0]

@@ -101,3 +101,30 @@ def test_captured_frame_back_to_back(dev):
                         Ks=Ks, get_skeleton=True)
         for k in KEYS + ("joints",):
             assert torch.equal(got[k], ref[k]), (i, k)
+
+
+def test_captured_ray_block_shards_equal_eager_and_assemble(dev):
+    """capture_frame(ray_shard=(rank, world, block)) -- the per-rank graph of shard.capture_sharded
+    (bench --gpus N) -- replays back to back equal to the eager shard frame, and the ranks' replays
+    assemble into the single-GPU frame."""
+    from apn_amd.shard import assemble_blocks, block_slots, pack_tile
+    scene, model = _scene_model(dev)
+    rk = scene.render_kwargs(dev)
+    R = len(rk["rays_o"])
+    ts = [torch.tensor([scene.cfg.t + 0.07 * i], device=dev) for i in range(3)]
+    world, block = 2, 512
+    steps = [model.capture_frame(ts[0], rk, ray_shard=(r, world, block)) for r in range(world)]
+    counts = [model._block_index[(R, r, world, block)].numel() for r in range(world)]
+    for i in range(6):
+        t = ts[i % 3]
+        parts = torch.zeros(world, block_slots(R, world, block) * block, 12, device=dev)
+        for r in range(world):
+            g = steps[r](t)
+            parts[r, :counts[r]] = pack_tile(g, counts[r], dev)
+        with torch.no_grad():
+            for r in range(world):
+                e = model(t, render_depth=True, render_kwargs=rk, render_weights=True, ray_shard=(r, world, block))
+                assert torch.equal(parts[r, :counts[r]], pack_tile(e, counts[r], dev)), (i, r)
+        with torch.no_grad():
+            full = pack_tile(model(t, render_depth=True, render_kwargs=rk, render_weights=True), R, dev)
+        assert torch.equal(assemble_blocks(parts, R, world, block), full), i

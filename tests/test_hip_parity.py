@@ -630,6 +630,28 @@ def test_ray_shards_assemble_bit_identical(golden_model, dev, world):
     assert torch.equal(torch.cat(tiles), pack_tile(full, R, dev))
 
 
+@pytest.mark.parametrize("world,block", [(2, 37), (3, 64), (8, 4096)])
+def test_ray_blocks_assemble_bit_identical(golden_model, dev, world, block):
+    """The "blocks" split (apn_amd/shard.py): each rank's interleaved ray blocks rendered on one
+    GPU and put back in ray order equal the single-GPU frame bit for bit (a short last block and,
+    at 8 x 4096, ranks without rays included)."""
+    from apn_amd.shard import assemble_blocks, block_rays, block_slots, pack_tile
+    g, m = golden_model
+    full = _forward(g, m, dev)
+    R = g.render_kwargs(dev)["rays_o"].shape[0]
+    slots = block_slots(R, world, block) * block
+    parts = torch.zeros(world, slots, 12, device=dev)
+    for rank in range(world):
+        o = m(g.t("in_t").to(dev), render_depth=True, render_kwargs=g.render_kwargs(dev), render_weights=True,
+              ray_shard=(rank, world, block))
+        n = m.last_ray_count
+        assert n == block_rays(R, rank, world, block).numel()
+        if n:
+            assert torch.equal(m.last_ray_index.cpu(), block_rays(R, rank, world, block))
+            parts[rank, :n] = pack_tile(o, n, dev)
+    assert torch.equal(assemble_blocks(parts, R, world, block), pack_tile(full, R, dev))
+
+
 def test_repeatable(golden_model, dev):
     g, m = golden_model
     a = _forward(g, m, dev)

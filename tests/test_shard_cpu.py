@@ -169,3 +169,54 @@ def test_cost_offsets_weights_survivors():
     assert b[0] == 0 and b[-1] == len(inb) and b[1] < 4
     costs = [int(c[b[i + 1]] - c[b[i]]) for i in range(2)]
     assert abs(costs[0] - costs[1]) <= 2 * int(per.max())   # a boundary lands within one ray of the target
+
+
+@pytest.mark.parametrize("R,world,block", [(10, 2, 3), (11, 3, 2), (64, 8, 4), (5, 4, 4), (4096 * 3 + 7, 2, 4096)])
+def test_block_split_partitions_and_assembles(R, world, block):
+    """The "blocks" split: the ranks' rays partition the frame, each rank holds at most
+    block_slots * block rays, and the zero-padded per-rank tiles assemble into ray order."""
+    from apn_amd.shard import assemble_blocks, block_rays, block_slots
+    idx = [block_rays(R, r, world, block) for r in range(world)]
+    allr = torch.cat(idx)
+    assert torch.equal(allr.sort().values, torch.arange(R))
+    assert all(bool((i[1:] > i[:-1]).all()) for i in idx if i.numel() > 1)
+    m = block_slots(R, world, block) * block
+    assert max(i.numel() for i in idx) <= m
+    assert max(i.numel() for i in idx) - min(i.numel() for i in idx) <= block
+    full = torch.arange(R * 5, dtype=torch.float32).reshape(R, 5)
+    parts = torch.zeros(world, m, 5)
+    for r in range(world):
+        parts[r, :idx[r].numel()] = full[idx[r]]
+    assert torch.equal(assemble_blocks(parts, R, world, block), full)
+
+
+def _worker_blocks(rank, world, port, R, block, result_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from apn_amd.shard import block_rays, gather_blocks
+        full = torch.arange(R * TILE_WIDTH, dtype=torch.float32).reshape(R, TILE_WIDTH)
+        idx = block_rays(R, rank, world, block)
+        info = torch.tensor([10 + rank, 20 + rank, rank, 30 + rank], dtype=torch.int32)
+        got, infos = gather_blocks(full[idx].clone(), R, world, block, info=info)
+        want = torch.tensor([[10 + r, 20 + r, r, 30 + r] for r in range(world)], dtype=torch.int32)
+        result_q.put((rank, bool(torch.equal(got, full)), bool(torch.equal(infos, want))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("R,block", [(23, 4), (24, 4), (3, 8)])
+def test_gather_blocks_gloo_world2(R, block):
+    """The unpadded block all-gather (plus the frame_info row) over two gloo processes, with a
+    short last block on either rank and a rank without rays."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_blocks, args=(r, 2, port, R, block, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert res == [(0, True, True), (1, True, True)]

@@ -1,4 +1,4 @@
+#!/bin/bash
+# Blocks split shards: eager vs per-rank graph replay, one-GPU emulation.
 source tools/gpu_steps.sh
-step bench_c2_off 400 python -u bench.py --no-cpu-baseline --steps 20 --warmup 3 -o gpurun_out/r2y_c2_off.json
-step bench_c2_on 400 python -u bench.py --no-cpu-baseline --steps 20 --warmup 3 --graph on -o gpurun_out/r2y_c2_on.json
-step g3_full_repack 150 python -u tools/graph_diag.py --scene G3 --mode replay_only --full-repack
+step ilv 400 python -u tools/shard_balance.py --split ilv4096,gilv4096 --worlds 2,4,8 --reps 10 > gpurun_out/y_ilv.log 2>&1

@@ -7,8 +7,8 @@ what a strong-scaling step waits for. Diagnostic tool (not a test).
 
 --split cost: the split render_sharded uses from the second frame on (shard.cost_offsets of the
 previous frame's survivors and in-bbox samples), preset in the model's SplitTracker.
---split ilv<B>: interleaved blocks of B rays (rank k takes blocks k, k + W, ...), each rank's rays
-gathered and rendered as a frame of their own (equal ray counts: an unpadded all-gather).
+--split ilv<B> / gilv<B> (graph replays): the "blocks" split of render_sharded with blocks of B rays (rank k takes blocks
+k, k + W, ...; ray_shard=(k, W, B)): equal ray counts, an unpadded all-gather.
 """
 from __future__ import annotations
 
@@ -76,18 +76,20 @@ def main():
     if args.kept_weights:
         splits = [s for s in splits if s != "cost"] + [f"cost{w}" for w in args.kept_weights.split(",")]
     for split, world in [(sp, int(w)) for sp in splits for w in args.worlds.split(",")]:
-        if split.startswith("ilv"):
-            B = int(split[3:])
-            blk = torch.arange(R, device=dev) // B
+        if split.startswith("ilv") or split.startswith("gilv"):
+            graph = split.startswith("g")
+            B = int(split[4:] if graph else split[3:])
             rows = []
             for k in range(world):
-                idx = torch.nonzero(blk % world == k).squeeze(1)
-                rkk = dict(rk, rays_o=rk["rays_o"][idx].contiguous(), rays_d=rk["rays_d"][idx].contiguous(),
-                           viewdirs=rk["viewdirs"][idx].contiguous())
-                kwk = dict(kw, render_kwargs=rkk)
-                ms, o = timed(lambda: model(t, **kwk), args.reps)
+                if graph:   # the rank's frame as one graph replay (shard.capture_sharded, bench's step)
+                    fk = {n: v for n, v in kw.items() if n not in ("render_kwargs", "render_depth", "render_weights")}
+                    gstep = model.capture_frame(t, rk, ray_shard=(k, world, B), **fk)
+                    fn = lambda: gstep(t)   # noqa: E731
+                else:
+                    fn = lambda: model(t, ray_shard=(k, world, B), **kw)   # noqa: E731
+                ms, o = timed(fn, args.reps)
                 s = model.last_stats.resolved()
-                rows.append((ms, s.get("inbbox_samples", -1), s.get("kept_samples", -1), idx.numel()))
+                rows.append((ms, s.get("inbbox_samples", -1), s.get("kept_samples", -1), model.last_ray_count))
                 print(f"   shard {k}: {ms:.3f} ms, stages " + " ".join(f"{n} {v:.3f}" for n, v in stages.items()))
             mx = max(r[0] for r in rows)
             mean = sum(r[0] for r in rows) / world
