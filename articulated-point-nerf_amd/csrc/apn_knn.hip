@@ -1257,6 +1257,73 @@ __global__ __launch_bounds__(KNN_THREADS) void k_cell_bound3w(const GridParams* 
   }
 }
 
+// Heavy-first block order for the kNN passes of short launches (ray shards). A launch of ~1M
+// queries fills the chip for only a few rounds of waves, so it waits on its slowest workgroups:
+// the ones whose queries sit in dense cells. k_block_cost sums a per-query work estimate over
+// each workgroup's 256 queries (pass A: the point count of the ball it scans, u4 or u1 of its
+// cell; pass B: u2 + u1 or u1 by its first level); k_order_blocks (one workgroup) deals the block
+// ids into 33 buckets by the bit length of their cost, heaviest bucket first, and the pass reads
+// its block id through that permutation. Query results do not depend on the order.
+template <bool PASS_B>
+__global__ __launch_bounds__(KNN_THREADS) void k_block_cost(
+    const int* __restrict__ n_a, const int* __restrict__ list1, const int* __restrict__ n1_dev,
+    const int* __restrict__ list2, const int* __restrict__ n2_dev, const GridParams* __restrict__ gp,
+    const int* __restrict__ ccell, const int* __restrict__ u1, const int* __restrict__ u2,
+    const int* __restrict__ u4, int* __restrict__ cost) {
+  __shared__ int sw[KNN_THREADS / 64];
+  const int i = blockIdx.x * KNN_THREADS + threadIdx.x;
+  int w = 0;
+  if (!PASS_B) {
+    if (i < *n_a) {
+      const int cell = ccell[i];
+      const int a1 = u1[cell];
+      w = a1 < KNN_K ? 1 : (gp->h > 0.25f * gp->r ? a1 : u4[cell] + 1);
+    }
+  } else {
+    const int n1 = *n1_dev, n2 = *n2_dev;
+    if (i < n1 + n2) {
+      const int hc = i < n1 ? list1[i] : list2[i - n1];
+      const int cell = ccell[hc >> 1];
+      w = (hc & 1) ? u1[cell] : u2[cell] + u1[cell];
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) w += __shfl_xor(w, o, 64);
+  if ((threadIdx.x & 63) == 0) sw[threadIdx.x >> 6] = w;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+#pragma unroll
+    for (int k = 0; k < KNN_THREADS / 64; ++k) t += sw[k];
+    cost[blockIdx.x] = t;
+  }
+}
+
+constexpr int ORDER_THREADS = 1024;
+
+__global__ __launch_bounds__(ORDER_THREADS) void k_order_blocks(const int* __restrict__ cost, int nb,
+                                                                int* __restrict__ perm) {
+  __shared__ int hist[33];
+  __shared__ int off[33];
+  const int t = threadIdx.x;
+  if (t < 33) hist[t] = 0;
+  __syncthreads();
+  for (int b = t; b < nb; b += ORDER_THREADS) {
+    const unsigned c = (unsigned)max(cost[b], 0);
+    atomicAdd(&hist[c ? 32 - __clz(c) : 0], 1);
+  }
+  __syncthreads();
+  if (t == 0) {   // heaviest bucket first
+    int run = 0;
+    for (int k = 32; k >= 0; --k) { off[k] = run; run += hist[k]; }
+  }
+  __syncthreads();
+  for (int b = t; b < nb; b += ORDER_THREADS) {
+    const unsigned c = (unsigned)max(cost[b], 0);
+    perm[atomicAdd(&off[c ? 32 - __clz(c) : 0], 1)] = b;
+  }
+}
+
 // Pass A of mode 8: reject on u1 < 8; the r/4 ball (flat scan) only where u4 >= 8; the rest go to
 // the hard list tagged with their first useful level (r/2 if u2 >= 8, else r).
 template <bool ANISO>
@@ -1266,9 +1333,9 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_a8(
     const int* __restrict__ ccell, const int* __restrict__ u1, const int* __restrict__ u2,
     const int* __restrict__ u4, int* __restrict__ flag, int* __restrict__ t_nbr, int* __restrict__ hard,
     int* __restrict__ n_hard, int* __restrict__ hard_r, int* __restrict__ n_hard_r, const AGrid* __restrict__ agp,
-    const int* __restrict__ cell_start2, const float4* __restrict__ sorted2) {
+    const int* __restrict__ cell_start2, const float4* __restrict__ sorted2, const int* __restrict__ perm) {
   const int nc = *n_cand_dev;
-  const int c = blockIdx.x * KNN_THREADS + threadIdx.x;
+  const int c = (perm ? perm[blockIdx.x] : (int)blockIdx.x) * KNN_THREADS + threadIdx.x;
   const GridParams g = *gp;
   bool push = false;
   int tag = 0;
@@ -1635,8 +1702,8 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_b9(
     const float4* __restrict__ q_pos, const int* __restrict__ cand, const int* __restrict__ hard,
     const int* __restrict__ n_hard, const int* __restrict__ hard2, const int* __restrict__ n_hard2,
     const AGrid* __restrict__ agp, const int* __restrict__ cell_start2, const float4* __restrict__ sorted2,
-    int* __restrict__ flag, int* __restrict__ t_nbr) {
-  const int i = blockIdx.x * KNN_THREADS + threadIdx.x;
+    int* __restrict__ flag, int* __restrict__ t_nbr, const int* __restrict__ perm) {
+  const int i = (perm ? perm[blockIdx.x] : (int)blockIdx.x) * KNN_THREADS + threadIdx.x;
   const int n1 = *n_hard, n2 = hard2 ? *n_hard2 : 0;
   if (i >= n1 + n2) return;
   const AGrid g = *agp;
@@ -1894,10 +1961,22 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
       hipLaunchKernelGGL(k_cell_bound3, dim3(ceil_div(std::min<int64_t>(cell_cap, slots), KNN_THREADS)),
                          dim3(KNN_THREADS), 0, s, g.gp, g.cell_start, g.tile_list, g.n_tile_list, u1, u2, u4);
     int* hard_r = ccell + slots;          // second quarter of the t_pos region
+    static const int64_t lpt_max = [] {   // query count up to which the passes run heavy blocks first
+      const char* e = getenv("APN_KNN_LPT_MAX");   // 8 shards 2.17 -> 2.05 ms, 2 shards (forced) 6.05 -> 5.86
+      return e ? (int64_t)atoll(e) : (int64_t)6 << 20;
+    }();
+    // blk_cnt / blk_off are free until the survivor count below: block costs and the permutation
+    int* perm = (aniso && n_queries <= lpt_max && nb <= (1 << 24)) ? blk_off : nullptr;
+    if (perm) {
+      hipLaunchKernelGGL(k_block_cost<false>, dim3(nb), dim3(KNN_THREADS), 0, s, cblk_off + nb, nullptr, nullptr,
+                         nullptr, nullptr, g.gp, ccell, u1, u2, u4, blk_cnt);
+      hipLaunchKernelGGL(k_order_blocks, dim3(1), dim3(ORDER_THREADS), 0, s, blk_cnt, nb, perm);
+    }
     static const bool a_aniso = getenv("APN_KNN_A_ANISO") != nullptr;   // A/B: pass A's r/4 ball on the second grid
     hipLaunchKernelGGL((aniso && a_aniso) ? k_knn_pass_a8<true> : k_knn_pass_a8<false>, dim3(nb), dim3(KNN_THREADS), 0,
                        s, (const float4*)q_pos4, cand, cblk_off + nb, g.gp, g.cell_start, (const float4*)sorted_pts4,
-                       ccell, u1, u2, u4, flag, t_nbr, hard, n_hard, hard_r, n_hard_r, g.ag, g.cell_start2, g.sorted2);
+                       ccell, u1, u2, u4, flag, t_nbr, hard, n_hard, hard_r, n_hard_r, g.ag, g.cell_start2, g.sorted2,
+                       perm);
     if (small) {
       const dim3 nb4(ceil_div(n_queries * 8, KNN_THREADS));
       hipLaunchKernelGGL(k_knn_pass_b8s<8>, nb4, dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard, n_hard,
@@ -1917,12 +1996,17 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
       }();
       if (split) {
         hipLaunchKernelGGL(pass_b, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard, n_hard,
-                           nullptr, nullptr, g.ag, g.cell_start2, g.sorted2, flag, t_nbr);
+                           nullptr, nullptr, g.ag, g.cell_start2, g.sorted2, flag, t_nbr, nullptr);
         hipLaunchKernelGGL(pass_b, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard_r,
-                           n_hard_r, nullptr, nullptr, g.ag, g.cell_start2, g.sorted2, flag, t_nbr);
+                           n_hard_r, nullptr, nullptr, g.ag, g.cell_start2, g.sorted2, flag, t_nbr, nullptr);
       } else {   // n_hard + n_hard_r <= candidates <= nb * KNN_THREADS
+        if (perm) {
+          hipLaunchKernelGGL(k_block_cost<true>, dim3(nb), dim3(KNN_THREADS), 0, s, nullptr, hard_r, n_hard_r, hard,
+                             n_hard, g.gp, ccell, u1, u2, u4, blk_cnt);
+          hipLaunchKernelGGL(k_order_blocks, dim3(1), dim3(ORDER_THREADS), 0, s, blk_cnt, nb, perm);
+        }
         hipLaunchKernelGGL(pass_b, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard_r,
-                           n_hard_r, hard, n_hard, g.ag, g.cell_start2, g.sorted2, flag, t_nbr);
+                           n_hard_r, hard, n_hard, g.ag, g.cell_start2, g.sorted2, flag, t_nbr, perm);
       }
     } else {
       auto pass_b = stats ? k_knn_pass_b8<true> : k_knn_pass_b8<false>;

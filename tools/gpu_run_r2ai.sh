@@ -1,6 +1,6 @@
 source tools/gpu_steps.sh
-t() { python -u -m pytest tests/test_0_shard_spawn.py -q -x --timeout 200 --timeout-method thread 2>&1 | grep -E "passed|failed|AssertionError: frame" | head -3; }
-echo "== current"; t
-echo "== composite seq"; APN_COMPOSITE=seq t
-echo "== no bpf1"; APN_HIP_LIB=ab/nobpf/libapn_hip.so t
-echo "== no bpf1 + seq"; APN_COMPOSITE=seq APN_HIP_LIB=ab/nobpf/libapn_hip.so t
+step tests 900 python -u -m pytest tests -m gpu -q -x -rf --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_ai.log 2>&1
+tail -2 gpurun_out/gpu_tests_ai.log
+step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+step bench 300 python -u bench.py --no-cpu-baseline -o gpurun_out/bench_ai.json
+step ilv 200 python -u tools/shard_balance.py --split ilv4096 --worlds 2,4,8 --reps 10 > gpurun_out/ai_ilv.log 2>&1
