@@ -288,7 +288,8 @@ def capture_sharded(model, t, render_kwargs, rank: int, world: int, group=None, 
     replays the graph and all-gathers the tiles (the collective stays outside the graph, so the
     same step runs over RCCL or gloo) -> a ShardedFrame like render_sharded's. Capture again after
     changing the model or the rays."""
-    local = model.capture_frame(t, render_kwargs, ray_shard=(rank, world, block), **forward_kwargs)
+    local = model.capture_frame(t, render_kwargs, ray_shard=(rank, world, block), capture_error_mode="thread_local",
+                                **forward_kwargs)
 
     def step(t):
         out = local(t)

@@ -546,7 +546,7 @@ class TemporalPoints(torch.nn.Module):
         return step
 
     def capture_frame(self, t, render_kwargs, render_depth=True, render_weights=True, query_radius=0.01, poses=None,
-                      Ks=None, get_skeleton=False, ray_shard=None):
+                      Ks=None, get_skeleton=False, ray_shard=None, capture_error_mode="global"):
         """The render frame for a fixed ray set (skeleton, LBS, grid, sampling, kNN, MLP,
         compositing: the whole no-grad forward) captured once in a HIP graph: returns
         ``step(t) -> RenderOutput``, which copies the time into the graph's input and replays it.
@@ -557,7 +557,9 @@ class TemporalPoints(torch.nn.Module):
         model or the rays. ``get_skeleton`` (with fixed ``poses`` / ``Ks``) captures the joint
         projection too, as the eager forward runs it. ``ray_shard=(rank, world, block)`` captures
         this rank's frame of the "blocks" ray split (apn_amd.shard.capture_sharded); the
-        contiguous-range split is not capturable (its split moves from frame to frame)."""
+        contiguous-range split is not capturable (its split moves from frame to frame).
+        ``capture_error_mode`` goes to torch.cuda.graph ("thread_local" where other threads of the
+        process -- a process group's watchdog -- may make HIP calls during the capture)."""
         if ray_shard is not None and len(ray_shard) != 3:
             raise ValueError("capture_frame: ray_shard must be (rank, world, block) (the blocks split)")
         dev = self.canonical_feat.device
@@ -580,7 +582,7 @@ class TemporalPoints(torch.nn.Module):
                 raise RuntimeError("capture_frame: no sample capacity for this ray set (empty frame?)")
             self._ws.pinned = True   # the graph holds workspace addresses from here on
             graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
+            with torch.cuda.graph(graph, capture_error_mode=capture_error_mode):
                 out = self._forward_render(t_in, *args)
         static = {k: dict.__getitem__(out, k) for k in dict.keys(out)}
         info, n_rays, bg = out._info, out._n_rays, out._bg

@@ -344,10 +344,20 @@ def main():
     torch.cuda.synchronize(dev)
     stats = model.last_stats.resolved()
     log(f"[rank {rank}] scene: {stats}")
-    if use_graph:   # the whole frame as one HIP graph replay (no per-kernel host launches, no host sync)
-        if shard_rays:   # this rank's blocks as one graph replay, then the tile all-gather
+    if use_graph and shard_rays:   # this rank's blocks as one graph replay, then the tile all-gather
+        try:
             graph_step = SH.capture_sharded(model, t_arg, rk, rank, world, poses=poses, Ks=Ks, get_skeleton=True)
-        else:
+        except Exception as e:   # the eager shard frame runs the same kernels and the same collectives
+            log(f"[rank {rank}] shard graph capture failed ({e!r}); timing eager shard frames")
+            use_graph = False
+            torch.cuda.synchronize(dev)
+        # every rank must run the same step (same collectives): graphs only if all ranks captured
+        ok = torch.tensor([1 if use_graph else 0], dtype=torch.int32,
+                          device=dev if torch.distributed.get_backend() == "nccl" else "cpu")
+        torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN)
+        use_graph = bool(ok.item())
+    if use_graph:   # the whole frame as one HIP graph replay (no per-kernel host launches, no host sync)
+        if not shard_rays:
             graph_step = model.capture_frame(t_arg, rk, poses=poses, Ks=Ks, get_skeleton=True)
         step = lambda: graph_step(t_arg)   # noqa: E731
         for _ in range(2):
