@@ -1,5 +1,5 @@
 source tools/gpu_steps.sh
-t() { python -u -m pytest tests/test_0_shard_spawn.py -q -x --timeout 200 --timeout-method thread 2>&1 | grep -E "passed|failed|AssertionError: frame" | head -2; }
-for k in 1 2 3; do echo "== default $k"; t; done
-for k in 1 2 3; do echo "== serial grid $k"; APN_CONCURRENT_GRID=0 t; done
-for k in 1 2 3; do echo "== nobpf $k"; APN_HIP_LIB=ab/nobpf/libapn_hip.so t; done
+step tests 900 python -u -m pytest tests -m gpu -q -x -rf --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_ah.log 2>&1
+tail -2 gpurun_out/gpu_tests_ah.log
+step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+step bench 300 python -u bench.py --no-cpu-baseline -o gpurun_out/bench_ah.json
