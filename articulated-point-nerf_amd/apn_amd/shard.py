@@ -1,9 +1,9 @@
 """Ray-sharded rendering of one frame over the GPUs of a node.
 
-Every rank replicates the cheap per-frame work (skeleton, LBS, kNN grid, the per-ray in-bbox
-sample counts) and renders one contiguous ray range holding ~1/world of the frame's in-bbox
-samples; the per-ray outputs are then exchanged with one all-gather (RCCL over xGMI on the GPU
-box, gloo in the CPU tests). Rays are independent given the warped cloud, so the assembled
+Every rank replicates the cheap per-frame work (skeleton, LBS, kNN grid) and renders its share
+of the rays -- by default the interleaved 4096-ray blocks k, k + world, ... (the "blocks" split
+below) -- and the per-ray outputs are then exchanged with one all-gather (RCCL over xGMI on the
+GPU box, gloo in the CPU tests). Rays are independent given the warped cloud, so the assembled
 frame is bit-identical to a single-GPU render (chunk invariance, tests/test_hip_parity.py).
 
 Tile layout: [rays, 12] float32 = rgb_marched (3), rgb_marched_direct (3), depth (1),
@@ -260,6 +260,28 @@ class ShardedFrame(dict):
         self._resolve()
         return super().__contains__(k)
 
+    # every other read of the dict validates too (dict(frame) / {**frame} take the slow path
+    # through keys() + __getitem__ because __iter__ is overridden)
+    def values(self):
+        self._resolve()
+        return super().values()
+
+    def __iter__(self):
+        self._resolve()
+        return super().__iter__()
+
+    def __len__(self):
+        self._resolve()
+        return super().__len__()
+
+    def pop(self, k, *default):
+        self._resolve()
+        return super().pop(k, *default)
+
+    def copy(self):
+        self._resolve()
+        return dict(super().items())
+
     def raw(self, k, default=None):
         return super().get(k, default)
 
@@ -294,7 +316,7 @@ def capture_sharded(model, t, render_kwargs, rank: int, world: int, group=None, 
     def step(t):
         out = local(t)
         return _assemble(model, t, out, render_kwargs, rank, world, group, True, block, forward_kwargs)
-    step.graph = local.graph
+    step.graph, step.overflowed = local.graph, local.overflowed
     return step
 
 
@@ -328,7 +350,11 @@ def _assemble(model, t, out, render_kwargs, rank, world, group, blocks, block, f
         model._capacity[key] = max(model._capacity.get(key, 0), _grow_capacity(int(infos[rank, 1])))
         model._force_exact = True
         try:
-            whole = model(t, render_kwargs=render_kwargs, render_depth=True, render_weights=True, **forward_kwargs)
+            # the frame may be read after render_sharded's no_grad scope has exited: the re-render
+            # must stay on the fused render path, not the differentiable one
+            with torch.no_grad():
+                whole = model(t, render_kwargs=render_kwargs, render_depth=True, render_weights=True,
+                              **forward_kwargs)
             return {k: whole.get(k) for k, _ in TILE_KEYS} | {k: whole.get(k) for k in ("t_hat_pcd", "joints", "bones")}
         finally:
             model._force_exact = False

@@ -570,38 +570,65 @@ class TemporalPoints(torch.nn.Module):
             poses, Ks = poses.to(dev), Ks.to(dev, torch.float32)   # device-resident before the capture
         args = (render_depth, rk, query_radius, render_weights, None, poses, Ks, True, get_skeleton, ray_shard)
         cap_key = R if ray_shard is None else (R, *ray_shard)
-        with torch.no_grad():
-            side = torch.cuda.Stream(dev)
-            side.wait_stream(torch.cuda.current_stream(dev))
-            with torch.cuda.stream(side):   # warm-up: capacity (first frame), caches, workspaces
-                self._forward_render(t_in, *args)
-                warm = self._forward_render(t_in, *args)
-            torch.cuda.current_stream(dev).wait_stream(side)
-            warm.keys()   # validate: an overflow renders again and grows the capacity
-            if self._capacity.get(cap_key) is None:
-                raise RuntimeError("capture_frame: no sample capacity for this ray set (empty frame?)")
-            self._ws.pinned = True   # the graph holds workspace addresses from here on
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph, capture_error_mode=capture_error_mode):
-                out = self._forward_render(t_in, *args)
-        static = {k: dict.__getitem__(out, k) for k in dict.keys(out)}
-        info, n_rays, bg = out._info, out._n_rays, out._bg
+        # sticky overflow flag of every replay since the last step.overflowed() (the OR of the
+        # frames' frame_info[2], accumulated inside the graph): a caller that never reads its
+        # frames (bench's timed loop) still learns whether any of them dropped samples
+        ovf = torch.zeros(1, dtype=torch.int32, device=dev)
+        st = {}
+
+        def capture():
+            with torch.no_grad():
+                side = torch.cuda.Stream(dev)
+                side.wait_stream(torch.cuda.current_stream(dev))
+                with torch.cuda.stream(side):   # warm-up: capacity (first frame), caches, workspaces
+                    self._forward_render(t_in, *args)
+                    warm = self._forward_render(t_in, *args)
+                torch.cuda.current_stream(dev).wait_stream(side)
+                warm.keys()   # validate: an overflow renders again and grows the capacity
+                if self._capacity.get(cap_key) is None:
+                    raise RuntimeError("capture_frame: no sample capacity for this ray set (empty frame?)")
+                self._ws.pinned = True   # the graph holds workspace addresses from here on
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph, capture_error_mode=capture_error_mode):
+                    out = self._forward_render(t_in, *args)
+                    if out._info is not None:
+                        torch.bitwise_or(ovf, out._info[2:3], out=ovf)
+            st.update(graph=graph, static={k: dict.__getitem__(out, k) for k in dict.keys(out)}, info=out._info,
+                      n_rays=out._n_rays, bg=out._bg, cap=self._capacity.get(cap_key), stale=False)
+            step.graph = graph
 
         def step(t):
+            if st["stale"]:
+                # a replay overflowed the captured capacity; its re-render grew the capacity, so
+                # capture again (the old graph would overflow -- and re-render -- on every frame)
+                t0 = t_in.clone()
+                capture()
+                t_in.copy_(t0)
             t_in.copy_(torch.as_tensor(t, dtype=torch.float32, device=dev).reshape(-1))
-            graph.replay()
+            st["graph"].replay()
             tt = t_in.clone()
 
             def rerender():
+                st["stale"] = True
                 self._force_exact = True
                 try:
                     with torch.no_grad():
                         return self._forward_render(tt, *args)
                 finally:
                     self._force_exact = False
-            return RenderOutput(dict(static), n_rays=n_rays, bg=bg, info=info, rerender=rerender)
+            return RenderOutput(dict(st["static"]), n_rays=st["n_rays"], bg=st["bg"], info=st["info"],
+                                rerender=rerender)
 
-        step.graph, step.inputs = graph, t_in
+        def overflowed():
+            """True if any replay since the last call dropped samples past the captured capacity
+            (one device read; clears the flag)."""
+            v = bool(ovf.item())
+            ovf.zero_()
+            return v
+
+        capture()
+        step.inputs, step.overflowed = t_in, overflowed
+        step.capacity = lambda: st["cap"]
         return step
 
     def sample_ray(self, rays_o, rays_d, near, far, stepsize, xyz_min=None, xyz_max=None, **render_kwargs):

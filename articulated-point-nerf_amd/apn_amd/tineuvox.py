@@ -1,11 +1,14 @@
-"""The pieces of the reference's ``lib/tineuvox.py`` that the point render path uses
-(SURVEY.md §2 row 4): RGBNet, the density head holder, poc_fre, Raw2Alpha /
-Alphas2Weights (re-exported from ``ops``: HIP forward and backward) and ray generation.
+"""The reference's ``lib/tineuvox.py`` as the point render path and its stage-1 source use it
+(SURVEY.md §2 row 4, §8 f-3): RGBNet, the density head holder, poc_fre, Raw2Alpha /
+Alphas2Weights (re-exported from ``ops``: HIP forward and backward), ray generation, and the
+stage-1 TiNeuVox voxel model (``TiNeuVox`` below: constructor, state dict, forward,
+get_grid_as_point_cloud, mult_dist_interp over the HIP field ``apn_tnv_field``; default
+configuration only).
 
-The TiNeuVox voxel model itself (stage 1) is out of scope; ``TiNeuVoxHeads`` is the
-lightweight holder TemporalPoints takes as its ``tineuvox`` argument
-(temporalpoints.py:133-152): rgbnet, densitynet, timenet, the positional-encoding
-frequency buffers, ``no_view_dir``, ``voxel_size_ratio``, ``act_shift``, ``activate_density``.
+``TiNeuVoxHeads`` is the lightweight holder TemporalPoints takes as its ``tineuvox`` argument
+when no stage-1 model is at hand (temporalpoints.py:133-152): rgbnet, densitynet, timenet, the
+positional-encoding frequency buffers, ``no_view_dir``, ``voxel_size_ratio``, ``act_shift``,
+``activate_density``.
 """
 from __future__ import annotations
 

@@ -379,21 +379,33 @@ def main():
     host_s = 0.0
     if not use_graph:
         model.timing = timing
+    eager_infos = []
     for _ in range(args.steps):
         h0 = time.perf_counter()
         out = step()
         host_s += time.perf_counter() - h0
+        if not use_graph and model._last_info is not None:
+            eager_infos.append(model._last_info)
     torch.cuda.synchronize(dev)
     if not use_graph:
         timing, model.timing = model.timing, None
+    # the timed frames are never read: a replay that dropped samples past the captured capacity
+    # would be timed short. The graph ORs every replay's overflow flag on the device; read it once.
+    # (eager frames: the device frame_info of each timed frame, kept by the loop below)
+    if use_graph:
+        overflowed = bool(graph_step.overflowed())
+    else:
+        overflowed = any(bool(i[2]) for i in torch.stack(eager_infos).cpu()) if eager_infos else False
     n_timed = min(args.steps, 10) if use_graph else args.steps
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed, float(overflowed)], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t)
+        elapsed, overflowed = float(t[0]), bool(t[1] > 0)
+    if overflowed:
+        log(f"[rank {rank}] WARNING: a timed frame overflowed its sample capacity (dropped samples)")
     if os.environ.get("APN_MLP_VARIANT") in ("2", "3"):   # timed MLP variants: per-phase cycle split
         import ctypes
         from apn_amd import _lib
@@ -486,7 +498,8 @@ def main():
                    "step": (("each rank's blocks replayed as one HIP graph (shard.capture_sharded), then the "
                              "all-gather" if shard_rays else
                              "whole frame replayed as one HIP graph (TemporalPoints.capture_frame)") if use_graph
-                            else "eager launches")},
+                            else "eager launches"),
+                   "timed_frames_overflowed": overflowed},
         "roofline": {"bound": "mfma", "kernel": kernel, "achieved": achieved, "peak": peak,
                      "unit": "TFLOP/s", "frac": achieved / peak,
                      "traffic": traffic.get("bytes_per_launch") if traffic else None,

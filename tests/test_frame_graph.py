@@ -103,6 +103,46 @@ def test_captured_frame_back_to_back(dev):
             assert torch.equal(got[k], ref[k]), (i, k)
 
 
+def test_captured_frame_overflow_recaptures(dev, monkeypatch):
+    """A replay whose samples overflow the captured capacity is flagged (step.overflowed(), the OR
+    of every replay's frame_info[2] accumulated inside the graph), its read re-renders it exactly,
+    and the next step captures again with the grown capacity instead of overflowing every frame."""
+    import apn_amd.temporalpoints as TP
+    scene, model = _scene_model(dev)
+    rk = scene.render_kwargs(dev)
+    R = len(rk["rays_o"])
+    # two times whose in-bbox sample counts differ: capture at the smaller one with no headroom
+    ts = [torch.tensor([scene.cfg.t + 0.1 * i], device=dev) for i in range(6)]
+    counts = []
+    for t in ts:
+        model._force_exact = True
+        _frame(model, t, rk)
+        model._force_exact = False
+        counts.append(model.last_stats["inbbox_samples"])
+    lo, hi = min(range(6), key=lambda i: counts[i]), max(range(6), key=lambda i: counts[i])
+    assert counts[hi] > counts[lo], counts
+    model._capacity.pop(R, None)
+    monkeypatch.setattr(TP, "_grow_capacity", lambda n: int(n))
+    step = model.capture_frame(ts[lo], rk)
+    monkeypatch.undo()
+    assert step.capacity() == counts[lo]
+    g = step(ts[lo])
+    torch.cuda.synchronize()
+    assert not step.overflowed()
+    g = step(ts[hi])                                   # more samples than the graph holds
+    assert step.overflowed()
+    got = {k: g[k].clone() for k in KEYS}              # first read: rendered again exactly
+    ref = _frame(model, ts[hi], rk)
+    for k in KEYS:
+        assert torch.equal(got[k], ref[k]), k
+    g = step(ts[hi])                                   # captured again with the grown capacity
+    assert step.capacity() >= counts[hi]
+    got = {k: g[k].clone() for k in KEYS}
+    assert not step.overflowed()
+    for k in KEYS:
+        assert torch.equal(got[k], ref[k]), k
+
+
 def test_captured_ray_block_shards_equal_eager_and_assemble(dev):
     """capture_frame(ray_shard=(rank, world, block)) -- the per-rank graph of shard.capture_sharded
     (bench --gpus N) -- replays back to back equal to the eager shard frame, and the ranks' replays

@@ -220,3 +220,25 @@ def test_gather_blocks_gloo_world2(R, block):
     for p in ps:
         p.join(timeout=60)
     assert res == [(0, True, True), (1, True, True)]
+
+
+@pytest.mark.parametrize("read", ["getitem", "dict", "splat", "values", "iter", "len", "copy", "pop", "items"])
+def test_sharded_frame_every_read_validates(read):
+    """An overflowed ShardedFrame re-renders on its first read through ANY dict access path
+    (dict(frame), {**frame}, values(), iteration, len, copy, pop skipped the check)."""
+    from apn_amd.shard import ShardedFrame
+    calls = []
+
+    def rerender(infos):
+        calls.append(infos[:, 2].tolist())
+        return {"rgb_marched": torch.ones(4, 3), "depth": torch.full((4,), 2.0)}
+    f = ShardedFrame({"rgb_marched": torch.zeros(4, 3), "depth": torch.zeros(4)},
+                     infos=torch.tensor([[10, 10, 0, 5], [10, 20, 1, 5]], dtype=torch.int32), rerender=rerender)
+    with torch.enable_grad():   # read after render_sharded's no_grad scope
+        got = {"getitem": lambda: {"rgb_marched": f["rgb_marched"]}, "dict": lambda: dict(f),
+               "splat": lambda: {**f}, "values": lambda: dict(zip(("rgb_marched", "depth"), list(f.values()))),
+               "iter": lambda: {k: dict.__getitem__(f, k) for k in iter(f)},
+               "len": lambda: (len(f), dict(dict.items(f)))[1], "copy": lambda: f.copy(),
+               "pop": lambda: {"rgb_marched": f.pop("rgb_marched")}, "items": lambda: dict(f.items())}[read]()
+    assert calls == [[0, 1]]   # exactly one re-render, on the first read
+    assert torch.equal(got["rgb_marched"], torch.ones(4, 3))

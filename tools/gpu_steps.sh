@@ -1,5 +1,5 @@
 #!/bin/bash
-# Sourced by the tools/gpu_run_*.sh scripts on the GPU box.
+# Sourced by tools/gpu_recipes.sh on the GPU box.
 #   step <name> <seconds> <command...>
 # runs one GPU step under its own time limit and ends the script on any failure
 # (fault, abort, time limit): no further GPU step runs in that call.
