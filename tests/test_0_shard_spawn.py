@@ -104,3 +104,41 @@ def test_render_sharded_two_processes_bit_identical(split):
                 raise AssertionError(f"{split} frame {i} rank {r}: {len(bad)} rays differ (first {bad[:8].tolist()}), "
                                      f"columns {cols}, max |d| {float((a - single).abs().max()):.3e}, "
                                      f"bounds {bounds}")
+
+
+def _concurrent_worker(rank, frames, outdir):
+    """One of several processes sharing the GPU: the full render frame of the spawn scene, again and
+    again; every frame's skinned cloud, survivor list and tile must equal the process's first."""
+    from apn_amd import harness, synthetic as S
+    from apn_amd.shard import pack_tile
+    dev = torch.device("cuda", 0)
+    scene = S.make_scene(S.SceneConfig("spawn shard 200x200 50k pts 24 bones", 50_000, 24, 200, 200))
+    model = harness.build_model(scene, dev)
+    rk = scene.render_kwargs(dev)
+    R = rk["rays_o"].shape[0]
+    t0 = torch.tensor([scene.cfg.t], device=dev)
+    ref, bad = None, {"xyz": 0, "s_nbr": 0, "tile": 0}
+    with torch.no_grad():
+        for f in range(frames):
+            out = model(t0, render_depth=True, render_kwargs=rk, render_weights=True)
+            ns = int(model.last_stats["kept_samples"])
+            cur = {"xyz": out["t_hat_pcd"].clone(), "s_nbr": model._ws.bufs["s_nbr"][:8 * ns].clone(),
+                   "tile": pack_tile(out, R, dev)}
+            if ref is None:
+                ref = cur
+                continue
+            for k in bad:
+                bad[k] += int(not torch.equal(cur[k], ref[k]))
+    torch.save(bad, os.path.join(outdir, f"conc{rank}.pt"))
+
+
+def test_concurrent_processes_render_deterministically():
+    """Three processes render the same frame 150 times each on one GPU. Round 3's root cause of the
+    two-process mismatch: packed-FP32 VALU in k_lbs_skin gave a wrong y coordinate
+    for one 16-lane pass in ~8 % of such frames (tools/determinism_probe3.py); the library is now
+    built without packed-FP32 instructions (tests/test_build_isa.py) and every frame must repeat."""
+    import torch.multiprocessing as mp
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_concurrent_worker, args=(150, d), nprocs=3, join=True)
+        res = [torch.load(os.path.join(d, f"conc{r}.pt"), weights_only=True) for r in range(3)]
+    assert all(sum(r.values()) == 0 for r in res), res

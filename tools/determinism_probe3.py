@@ -29,7 +29,7 @@ def snapshot(model, out, R):
     ws = model._ws.bufs
     xyz = out.raw("t_hat_pcd").detach().clone()
     N = xyz.shape[0]
-    snap = {"xyz": xyz, "bbox": ws["bbox_ord"][:6].clone()}
+    snap = {"xyz": xyz, "bbox": ws["bbox_ord"][:6].clone(), "recA_xyz": ws["recA"][:N * 16].view(N, 16)[:, :3].clone()}
     s4 = ws["sorted4"][:N * 4].view(N, 4)
     idx = s4[:, 3].contiguous().view(torch.int32).long()
     canon = torch.empty_like(s4)
@@ -101,8 +101,14 @@ def worker(wid, nproc, frames, mode, outdir):
         if st is not None:
             bad[st] = bad.get(st, 0) + 1
             if len(log) < 20:
-                log.append(f"frame {f}: first differing stage {st}: {msg}")
-            if len(log) <= 2:
+                detail = ""
+                if st == "xyz":
+                    rows = (snap["xyz"] != ref["xyz"]).any(1).nonzero().flatten()[:3].tolist()
+                    detail = "; ".join(f"pt {r}: now {snap['xyz'][r].tolist()} ref {ref['xyz'][r].tolist()} "
+                                       f"recA now {snap['recA_xyz'][r].tolist()} ref {ref['recA_xyz'][r].tolist()}"
+                                       for r in rows)
+                log.append(f"frame {f}: first differing stage {st}: {msg} {detail}")
+            if os.environ.get("PROBE_DUMP") and len(log) <= 1:
                 torch.save({k: v.cpu() for k, v in snap.items()} | {f"ref_{k}": v.cpu() for k, v in ref.items()},
                            os.path.join(outdir, f"probe3_w{wid}_f{f}.pt"))
         if f % 200 == 0:
