@@ -421,6 +421,34 @@ def main():
         if name != "frame":
             stage_ms[name] = stage_ms.get(name, 0.0) + a.elapsed_time(b) / n_timed
     log(f"[rank {rank}] stage ms/frame (HIP events, eager frames): " + ", ".join(f"{k} {v:.3f}" for k, v in stage_ms.items()))
+    shard_diag = None
+    if shard_rays:
+        # N>1 diagnostics: every rank's stage times, the tile all-gather alone (HIP events around
+        # the collective on the current stream, this frame's tile shape) and the per-frame work every
+        # rank replicates (skinning, bbox, kNN grid build)
+        from apn_amd.shard import RAY_BLOCK, TILE_WIDTH, gather_blocks
+        n_local = model.last_ray_count
+        tile = torch.zeros(n_local, TILE_WIDTH, device=dev)
+        info = torch.zeros(4, dtype=torch.int32, device=dev)
+        gather_blocks(tile, R, world, RAY_BLOCK, info=info)
+        torch.distributed.barrier()
+        g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        g0.record()
+        for _ in range(10):
+            gather_blocks(tile, R, world, RAY_BLOCK, info=info)
+        g1.record()
+        torch.cuda.synchronize(dev)
+        ag_ms = g0.elapsed_time(g1) / 10
+        mine = {"rank": rank, "rays": n_local, "allgather_ms": round(ag_ms, 4),
+                "replicated_ms": round(sum(stage_ms.get(k, 0.0) for k in ("lbs", "bbox", "grid")), 4),
+                "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()}}
+        per_rank = [None] * world
+        torch.distributed.all_gather_object(per_rank, mine)
+        shard_diag = {"per_rank": per_rank, "allgather_ms_max": max(p["allgather_ms"] for p in per_rank),
+                      "note": "stage_ms from HIP events on eager shard frames; allgather_ms = one gather_blocks "
+                              "(the frame's tile all-gather) alone, mean of 10; replicated_ms = lbs + bbox + grid, "
+                              "the per-frame stages every rank runs on the whole cloud"}
+        log(f"[rank {rank}] all-gather {ag_ms:.3f} ms/frame, replicated stages {mine['replicated_ms']:.3f} ms/frame")
     log(f"[rank {rank}] host time inside step() {1e3 * host_s / args.steps:.3f} ms/step "
         f"({'graph replay' if use_graph else 'eager launches'}; device {1e3 * elapsed / args.steps:.3f} ms/step)")
     if os.environ.get("APN_KNN_MODE") == "3":   # kNN query-class counters
@@ -511,6 +539,7 @@ def main():
                      "executed_tflops": executed,
                      "mfma_util": executed / mfma_peak},
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
+        **({"shards": shard_diag} if shard_diag is not None else {}),
         "cpu_baseline": cpu,
         "psnr_vs_oracle": psnr,
         "same_cloud_vs_oracle": same,
