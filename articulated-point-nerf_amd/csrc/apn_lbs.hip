@@ -22,6 +22,9 @@ constexpr int LBS_MAX_J = 64;
 #ifndef QUAD_WAVES_PER_EU
 #define QUAD_WAVES_PER_EU 4
 #endif
+#ifndef LBS_PF
+#define LBS_PF 1   // rows in flight ahead of the one being skinned (k_lbs_skin_quad)
+#endif
 
 // Per-point tail shared by the LBS kernels: x' = G [x;1] + global_t, optional G (get_frames),
 // records (adjugate inverse of the blended 3x3, direct-render sigma, clipped colours); bbox seed.
@@ -284,9 +287,10 @@ void k_lbs_skin_quad(
   const float rth = 1.f / th;   // IEEE reciprocal, once per thread
   const int64_t stride = (int64_t)gridDim.x * PPB;
   int64_t n = (int64_t)blockIdx.x * PPB + (tid >> 2);
-  // the next row is in flight while the current one is processed (grid-stride, one step ahead)
-  float nrow[JL];
-  quad_load_row<JL>(W + min(n, N - 1) * J + sub * JL, nrow);
+  // the next LBS_PF rows are in flight while the current one is processed (grid-stride)
+  float nrow[LBS_PF][JL];
+#pragma unroll
+  for (int d = 0; d < LBS_PF; ++d) quad_load_row<JL>(W + min(n + d * stride, N - 1) * J + sub * JL, nrow[d]);
   __syncthreads();
   float bmin[3] = {INFINITY, INFINITY, INFINITY}, bmax[3] = {-INFINITY, -INFINITY, -INFINITY};
   const int64_t n_end = (N + PPB - 1) / PPB * PPB;   // every lane of a quad runs the same trips
@@ -294,8 +298,12 @@ void k_lbs_skin_quad(
     const bool valid = n < N;
     float row[JL];
 #pragma unroll
-    for (int j = 0; j < JL; ++j) row[j] = nrow[j];
-    quad_load_row<JL>(W + min(n + stride, N - 1) * J + sub * JL, nrow);
+    for (int j = 0; j < JL; ++j) row[j] = nrow[0][j];
+#pragma unroll
+    for (int d = 0; d + 1 < LBS_PF; ++d)
+#pragma unroll
+      for (int j = 0; j < JL; ++j) nrow[d][j] = nrow[d + 1][j];
+    quad_load_row<JL>(W + min(n + LBS_PF * stride, N - 1) * J + sub * JL, nrow[LBS_PF - 1]);
     if (!weights_final) {   // softmax(W / th) over J (temporalpoints.py:403)
       // W / th as the reciprocal product plus one fma residual correction (3 VALU instead of the
       // ~10 of an IEEE division; the corrected quotient is the correctly rounded one)
@@ -402,10 +410,13 @@ extern "C" int apn_lbs_skin(const float* canonical_pcd, const float* raw_weights
   // hence every sample position -- follows that cloud (bbox sensitivity).
   static const bool quad_ok = getenv("APN_LBS_LDS") == nullptr;
   if (quad_ok && !recA16 && !merge_rules && J % 4 == 0 && ((uintptr_t)raw_weights % 16) == 0) {
-    // persistent grid (each block strides over point groups, one row ahead); <= 1 partial per block
+    // grid-stride blocks (one row ahead); <= 1 partial per block. 32 blocks per CU: the launch
+    // then carries more rows in flight per CU than the 4-per-CU persistent grid (C5, 1M points,
+    // J = 48: 0.0511 -> 0.0429 ms; 6: 0.048, 12: 0.044, 64: 0.044 -- tools/c5_lbs_ab.sh); a
+    // second row in flight per lane (LBS_PF = 2, 3) measured slower
     static const int per_cu = [] {
       const char* e = getenv("APN_LBS_BLOCKS_PER_CU");
-      return e ? atoi(e) : 4;
+      return e ? atoi(e) : 32;
     }();
     const int qblocks = (int)std::min<int64_t>(ceil_div(n_points, LBS_THREADS / 4), 256 * per_cu);
     auto quad = [&](auto kern) {

@@ -76,6 +76,15 @@ def emit(line, args):
             f.write(text + "\n")
 
 
+def threads_note(threads):
+    """Why the CPU baseline runs on this many threads: the GPU box gives one GPU's job a 16-core
+    share of its host (OMP_NUM_THREADS / MAX_JOBS are set to 16 there; os.cpu_count() reports the
+    whole machine), and torch's intra-op pool follows OMP_NUM_THREADS."""
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return (f"{threads} threads = torch.get_num_threads() (OMP_NUM_THREADS={omp}: the box's CPU share for one GPU; "
+            f"the host reports {os.cpu_count()} logical CPUs in total)")
+
+
 def cpu_model_name():
     try:
         with open("/proc/cpuinfo") as f:
@@ -117,7 +126,8 @@ def cpu_baseline(model, scene, rows, threads):
             break
     dt = (time.perf_counter() - t0) / n_rep
     nrays = rows * W
-    return {"value": nrays / dt, "unit": "rays/s", "cores": threads, "cpu_model": cpu_model_name(), "kind": "port",
+    return {"value": nrays / dt, "unit": "rays/s", "cores": threads, "cores_note": threads_note(threads),
+            "cpu_model": cpu_model_name(), "kind": "port",
             "sample": f"{rows} evenly spaced rows x {W} = {nrays} rays of the same frame, {n_rep} timed repeats "
                       f"(oracle: torch-CPU MLP, scipy cKDTree kNN), {dt:.2f} s/band"}, ref, sel, (orc, sub, t)
 
@@ -236,6 +246,7 @@ def lbs_sweep(args, rank, world, dev):
                 n_rep += 1
             dt = (time.perf_counter() - c0) / n_rep
             cpu = {"value": N / dt, "unit": "points/s", "cores": torch.get_num_threads(),
+                   "cores_note": threads_note(torch.get_num_threads()),
                    "cpu_model": cpu_model_name(), "kind": "port",
                    "sample": f"{n_rep} poses of the same sweep, full 1M-point cloud (oracle: torch-CPU get_weights + "
                              f"LBS), {dt:.2f} s/pose"}
