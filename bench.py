@@ -7,9 +7,9 @@ sampling, radius kNN, neighbour MLP, compositing), inputs resident in HBM.
 
 Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process per GPU. By
 default (``--shard rays``) the N ranks render ONE frame together (BASELINE
-configs C3/C4): every rank replicates the cheap per-frame stages, renders the contiguous ray
-range holding ~1/N of the in-bbox samples, and the per-ray tiles are assembled with one RCCL
-all-gather over xGMI -- strong scaling, ``value`` = frame rays / step time. ``--shard frames``
+configs C3/C4): every rank replicates the cheap per-frame stages, renders its interleaved
+4096-ray blocks (apn_amd/shard.py "blocks" split), and the per-ray tiles are assembled with one
+RCCL all-gather over xGMI -- strong scaling, ``value`` = frame rays / step time. ``--shard frames``
 has every rank render its own frame instead (weak scaling, no data-path collective). C5
 (LBS-only) shards the points N/W per rank with no collective (strong scaling). The timing is
 barrier + synchronize bracketed and the max over ranks (all-reduce MAX of the elapsed time).
