@@ -39,6 +39,17 @@ constexpr int XBUF = TR * XB;      // one activation buffer (32 KB)
 constexpr int HB = 800;            // bytes per head-input row: hi 160 | lo 160 | pad (800/4 = 8 mod 64)
 constexpr int HLO = 320;           // lo offset inside a head-input row
 
+#ifndef APN_H3_ROWSTRIDE
+#define APN_H3_ROWSTRIDE 9
+#endif
+// floats per MLP row of sRow (direct-blend terms: 8 used); 9 = odd stride, conflict-free columns
+constexpr int RS = APN_H3_ROWSTRIDE;
+#ifdef APN_H3_BPF   // A/B: B-operand activation fragments read one M-tile ahead in the OCC = 3 build
+constexpr bool kBPF3 = true;
+#else
+constexpr bool kBPF3 = false;
+#endif
+
 constexpr int SW_B1 = 0, SW_B2 = 128, SW_B3 = 256, SW_B4 = 384, SW_WD = 512, SW_BD = 640, SW_BH = 644,
               SW_WV2 = 708, SW_BV2 = 900, SW_SC = 904, SW_DS = 912, SW_HSC = 921,
               SW_TOTAL = 924;
@@ -129,6 +140,55 @@ __device__ __forceinline__ void layer_mfma(const char* __restrict__ X, rsrc_t rs
                                            h8 (&a)[2][2]) {
   const int lane = threadIdx.x & 63;
   const int li = lane & 15, g = lane >> 4;
+#ifdef APN_H3_MT1
+  if constexpr (!BPF) {
+    // A/B: the activation fragments of the next M-tile (or of the next chunk's first M-tile) are
+    // read before this M-tile's six MFMAs, so their LDS latency overlaps them (+8 VGPRs)
+    h8 bh = *(const h8*)(X + act_off(li, g)), bl = *(const h8*)(X + act_off(li, g) + 256);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      h8 an[2][2];
+      if (q + 1 < NQ) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, vb, FB + (j * NQ + q + 1) * 2 + pt);
+      } else {
+#pragma unroll
+        for (int j = 0; j < NTN; ++j)
+#pragma unroll
+          for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, vb, FBN + j * NQN * 2 + pt);
+      }
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        h8 nbh = bh, nbl = bl;
+        if (mt + 1 < 4 || q + 1 < NQ) {
+          const char* p = X + act_off(16 * ((mt + 1) & 3) + li, 4 * (mt + 1 < 4 ? q : q + 1) + g);
+          nbh = *(const h8*)p;
+          nbl = *(const h8*)(p + 256);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[mt][j] = mfma3(a[j][0], a[j][1], bh, bl, acc[mt][j]);
+        bh = nbh;
+        bl = nbl;
+      }
+      if (q + 1 < NQ) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          a[j][0] = an[j][0];
+          a[j][1] = an[j][1];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < NTN; ++j) {
+          a[j][0] = an[j][0];
+          a[j][1] = an[j][1];
+        }
+      }
+    }
+    return;
+  }
+#endif
   if constexpr (!BPF) {
     // no B double-buffering (fewer VGPRs): the chunk's activation fragments are read per M-tile
     // right before its MFMAs
@@ -385,7 +445,7 @@ __device__ __forceinline__ void ws_gather_q(int nb, float4 q, const GatherRegs& 
       sTo[r] = (dx * dx + dy * dy) + dz * dz;
     } else if constexpr (P == 1) {
       const float tn = (dx * dx + dy * dy) + dz * dz;
-      float* rw = sRow + 8 * r;
+      float* rw = sRow + RS * r;
       rw[0] = expf(-(tn * tn) / a0.w);   // temporalpoints.py:461 (to_nn is already squared)
       rw[1] = a3.y;
       rw[2] = G.b0.x; rw[3] = G.b0.y; rw[4] = G.b0.z;
@@ -434,7 +494,7 @@ __device__ __forceinline__ void ws_gather_q(int nb, float4 q, const GatherRegs& 
     if constexpr (P == 0) {
       sTo[r] = 1.f;
     } else if constexpr (P == 1) {
-      for (int c = 0; c < 8; ++c) sRow[8 * r + c] = 0.f;
+      for (int c = 0; c < 8; ++c) sRow[RS * r + c] = 0.f;
     }
   }
 }
@@ -624,26 +684,26 @@ __device__ __forceinline__ void mlp_tiles(
           if (!pok[mt]) acc[mt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
     // ------------------------------------------------ feat_net: 4 x (Linear + LeakyReLU)
-    if constexpr (PP || !kD2) layer_mfma<2, 4, 2, FR_W1E, FR_W2, PP>(X0, rs, vb, acc, a);
+    if constexpr (PP || !kD2) layer_mfma<2, 4, 2, FR_W1E, FR_W2, PP || kBPF3>(X0, rs, vb, acc, a);
     else layer_mfma_d2<2, 4, 2, FR_W1E, FR_W2, false, true>(X0, rs, vb, acc, a, a1);
     if (!PP) __syncthreads();
     store_act(X1, ot0, sW + SW_B1, acc, SCALED, SCALED ? sW[SW_DS + 0] : 1.f);
     __syncthreads();
     APN_PHASE(1)
     init_bias(acc, ot0, sW + SW_B2);
-    if constexpr (PP || !kD2) layer_mfma<4, 4, 2, FR_W2, FR_W3, PP>(X1, rs, vb, acc, a);
+    if constexpr (PP || !kD2) layer_mfma<4, 4, 2, FR_W2, FR_W3, PP || kBPF3>(X1, rs, vb, acc, a);
     else layer_mfma_d2<4, 4, 2, FR_W2, FR_W3, true, true>(X1, rs, vb, acc, a, a1);
     if (!PP) __syncthreads();
     store_act(X0, ot0, nullptr, acc, SCALED, SCALED ? sW[SW_DS + 1] : 1.f);
     __syncthreads();
     init_bias(acc, ot0, sW + SW_B3);
-    if constexpr (PP || !kD2) layer_mfma<4, 4, 2, FR_W3, FR_W4, PP>(X0, rs, vb, acc, a);
+    if constexpr (PP || !kD2) layer_mfma<4, 4, 2, FR_W3, FR_W4, PP || kBPF3>(X0, rs, vb, acc, a);
     else layer_mfma_d2<4, 4, 2, FR_W3, FR_W4, true, true>(X0, rs, vb, acc, a, a1);
     if (!PP) __syncthreads();
     store_act(X1, ot0, nullptr, acc, SCALED, SCALED ? sW[SW_DS + 2] : 1.f);
     __syncthreads();
     init_bias(acc, ot0, sW + SW_B4);
-    if constexpr (PP || !kD2) layer_mfma<4, 5, 1, FR_W4, FR_WH, PP>(X1, rs, vb, acc, a);
+    if constexpr (PP || !kD2) layer_mfma<4, 5, 1, FR_W4, FR_WH, PP || kBPF3>(X1, rs, vb, acc, a);
     else layer_mfma_d2<4, 5, 1, FR_W4, FR_WH, true, true>(X1, rs, vb, acc, a, a1);
     if (!PP) __syncthreads();
     // layer-4 output lrelu(acc) (bias in the accumulator) as fp32 rows (for the IDW sum)
@@ -706,21 +766,21 @@ __device__ __forceinline__ void mlp_tiles(
     // (sample, quantity); sums over the 8 neighbours in order
     if (wid == 1) {
       const int s = lane >> 3, qn = lane & 7;
-      const float* rw = sRow + 64 * s;
+      const float* rw = sRow + 8 * RS * s;
       float sumd = 0.f;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) sumd += rw[8 * k];
+      for (int k = 0; k < 8; ++k) sumd += rw[RS * k];
       const float idn = __builtin_amdgcn_rcpf(sumd + 1e-12f);
       float acc1 = 0.f;
       if (qn == 0) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc1 += (0.125f * rw[8 * k]) * rw[8 * k + 1];
+        for (int k = 0; k < 8; ++k) acc1 += (0.125f * rw[RS * k]) * rw[RS * k + 1];
       } else if (qn < 4) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc1 += (rw[8 * k] * idn) * rw[8 * k + 1 + qn];
+        for (int k = 0; k < 8; ++k) acc1 += (rw[RS * k] * idn) * rw[RS * k + 1 + qn];
       } else if (qn < 7) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc1 += sIdw[8 * s + k] * rw[8 * k + 1 + qn];
+        for (int k = 0; k < 8; ++k) acc1 += sIdw[8 * s + k] * rw[RS * k + 1 + qn];
       }
       // sOut[s] = {r, g, b, alpha, r_d, g_d, b_d, alpha_d, wr, wg, wb, 0}
       const int slot = qn == 0 ? 7 : (qn < 4 ? 3 + qn : (qn < 7 ? 4 + qn : 11));
@@ -850,7 +910,7 @@ __global__ __launch_bounds__(MLP_THREADS, OCC) void k_point_mlp_h3(
   __shared__ __attribute__((aligned(16))) char Hs[PP ? 16 : TS * HB];
   __shared__ float sTo[TR];
   __shared__ float sIdw[TR];
-  __shared__ float sRow[TR * 8];     // direct blend per row: wdir, alpha_c, rgb_c(3), pcol(3)
+  __shared__ float sRow[TR * RS];    // direct blend per row: wdir, alpha_c, rgb_c(3), pcol(3)
   __shared__ __attribute__((aligned(16))) float sOut[TS * 12];
   __shared__ float sV[TS * 32];      // view embedding per sample (27 + zero pad)
   __shared__ __attribute__((aligned(16))) float sW[SW_TOTAL];

@@ -675,8 +675,8 @@ def test_no_points_fallback(dev):
 @pytest.mark.parametrize("mode", [1, 2, 4, 5, 6, 7, 8, 9])
 def test_knn_modes_identical_full_scene(dev, mode):
     """Full C2 frame (300k points, 640k rays, ~8M in-bbox samples): every kNN search strategy
-    gives bit-identical renders and survivor counts to the default one (size-independent
-    exactness property at the benchmark size)."""
+    gives bit-identical survivor lists (ray, neighbour indices), renders and survivor counts to
+    the single-pass search (size-independent exactness property at the benchmark size)."""
     from apn_amd import _lib as L, harness, synthetic as S
     scene = S.make_scene("C2")
     model = harness.build_model(scene, dev)
@@ -690,10 +690,13 @@ def test_knn_modes_identical_full_scene(dev, mode):
             torch.cuda.synchronize()
         finally:
             L.load().apn_set_knn_mode(prev)
-        outs.append(({k: v.clone() for k, v in o.items() if torch.is_tensor(v)}, model.last_stats.resolved()))
+        st = model.last_stats.resolved()
+        ns = st["kept_samples"]
+        lists = {k: model._ws.bufs[k][:n * ns].clone() for k, n in (("s_ray", 1), ("s_nbr", 8), ("s_pos", 4))}
+        outs.append(({k: v.clone() for k, v in o.items() if torch.is_tensor(v)} | lists, st))
     (a, sa), (b, sb) = outs
     assert sa == sb
-    for k in ("rgb_marched", "rgb_marched_direct", "depth", "weights"):
+    for k in ("s_ray", "s_nbr", "s_pos", "rgb_marched", "rgb_marched_direct", "depth", "weights"):
         assert torch.equal(a[k], b[k]), k
 
 

@@ -132,7 +132,7 @@ def main():
               + "; ".join(f"r/{f}: {n} queries in {c} cells, {p / 1e6:.0f} M pairs" for f, n, c, p in per_level))
 
 
-if __name__ == "__main__" and not (len(sys.argv) > 2 and sys.argv[2] == "tiles"):
+if __name__ == "__main__" and len(sys.argv) <= 2:
     main()
 
 
@@ -223,3 +223,55 @@ def tile_model(T=2, cfg="C2", levels=(8, 4, 2, 1), lanes_per_query_max=1):
 if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[2] == "tiles":
     for T in (1, 2, 4):
         tile_model(T, sys.argv[1])
+
+
+def seed_model(cfg="C2"):
+    """How tight is the 8-NN bound a query inherits from its ray neighbours (the samples one step
+    before / after it on the same ray, stepdist = 0.17 r at C2)? For every candidate query whose
+    neighbour survived: tau = max distance from the query to the neighbour's 8 nearest points
+    (an upper bound on its own 8th-NN distance d8), reported as tau / d8 and tau / r."""
+    from apn_amd import harness, synthetic as S
+    from oracle.apn_oracle import OracleModel, sample_pts_on_rays
+    from scipy.spatial import cKDTree
+    scene = S.make_scene(cfg)
+    model = harness.build_model(scene, "cpu")
+    st = {k: v.detach() for k, v in model.state_dict().items()}
+    orc = OracleModel(st, model.canonical_pcd, model.bones, mean_min_distance_value=0.0)
+    with torch.no_grad():
+        _, (xyz, *_r) = orc.warp(torch.tensor([scene.cfg.t]))
+    xyz = xyz.numpy().astype(np.float32)
+    r2 = np.float32(0.01)
+    r = float(np.sqrt(r2))
+    lo, hi = xyz.min(0), xyz.max(0)
+    rk = scene.render_kwargs("cpu")
+    pts, mask_out, ray_id, step_id, *_ = sample_pts_on_rays(
+        rk["rays_o"].numpy(), rk["rays_d"].numpy(), lo - r2, hi + r2, rk["near"], rk["far"],
+        rk["stepsize"] * S.VOXEL_SIZE)
+    m = ~mask_out
+    q, ray_id, step_id = pts[m], ray_id[m], step_id[m]
+    tree = cKDTree(xyz.astype(np.float64))
+    d, nn = tree.query(q.astype(np.float64), k=8)
+    d8 = d[:, -1]
+    surv = d8 <= r
+    hard = (d8 > r / 4) & (d8 <= 1.5 * r)    # pass-B-like queries (not finished inside r/4)
+    for name, off in (("prev", -1), ("next", 1), ("both", 0)):
+        taus = []
+        idx = np.nonzero(hard)[0]
+        tau = np.full(len(idx), np.inf)
+        for o in ((-1,) if off == -1 else (1,) if off == 1 else (-1, 1)):
+            j = idx + o
+            ok = (j >= 0) & (j < len(q))
+            jj = np.clip(j, 0, len(q) - 1)
+            ok &= (ray_id[jj] == ray_id[idx]) & (step_id[jj] == step_id[idx] + o) & surv[jj]
+            pn = xyz[nn[jj]]                                   # [n, 8, 3]
+            t = np.sqrt(((q[idx][:, None, :] - pn) ** 2).sum(-1)).max(1)
+            tau = np.where(ok, np.minimum(tau, t), tau)
+        have = np.isfinite(tau)
+        ratio = tau[have] / d8[idx][have]
+        print(f"{name}: {have.mean():.3f} of {len(idx)} hard queries have a surviving ray neighbour; "
+              f"tau/d8 p50 {np.median(ratio):.3f} p90 {np.percentile(ratio, 90):.3f}; "
+              f"(tau/r)^2 mean {np.mean((tau[have] / r) ** 2):.3f} vs (d8/r)^2 {np.mean((d8[idx][have] / r) ** 2):.3f}")
+
+
+if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[2] == "seeds":
+    seed_model(sys.argv[1])
