@@ -9,7 +9,7 @@ src=$root/articulated-point-nerf_amd/csrc
 objs=""
 for f in $src/*.hip $src/apn_version.cpp; do
   b=$(basename $f); o=$out/build/${b%.*}.o
-  extra=""; [ "$b" = "apn_mlp_h3.hip" ] && extra="-fno-slp-vectorize"
+  extra="-fno-slp-vectorize -Xclang -target-feature -Xclang -packed-fp32-ops"
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off $extra $flags -c $f -o $o &
   objs="$objs $o"
 done
