@@ -44,6 +44,11 @@ constexpr int HLO = 320;           // lo offset inside a head-input row
 #endif
 // floats per MLP row of sRow (direct-blend terms: 8 used); 9 = odd stride, conflict-free columns
 constexpr int RS = APN_H3_ROWSTRIDE;
+#ifdef APN_H3_NO_HEADPF   // A/B: the head's fragments one chunk ahead inside the head loop
+constexpr bool kHeadPF = false;
+#else
+constexpr bool kHeadPF = true;
+#endif
 #ifdef APN_H3_BPF   // A/B: B-operand activation fragments read one M-tile ahead in the OCC = 3 build
 constexpr bool kBPF3 = true;
 #else
@@ -719,6 +724,17 @@ __device__ __forceinline__ void mlp_tiles(
         *(f32x4*)(X0 + out32_off(16 * mt + li, o0 >> 2)) =
             lrelu4(SCALED ? acc[mt][j] * sW[SW_DS + 3] : acc[mt][j]);
     }
+    // the head's remaining fragment chunks (1..4; chunk 0 came with layer 4) are issued here, a
+    // whole IDW phase ahead of their MFMAs: in the head loop each chunk has only 3 MFMAs, so a
+    // one-deep prefetch there waits out one L2 latency per chunk (the accumulators are dead now)
+    constexpr bool kHeadEarly = !PP && !kD2 && kHeadPF;
+    h8 hfr[KV / 32 - 1][2];
+    if constexpr (kHeadEarly) {
+#pragma unroll
+      for (int q = 1; q < KV / 32; ++q)
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt) hfr[q - 1][pt] = frag(rs, vb, FR_WH + q * 2 + pt);
+    }
 
     __syncthreads();
     APN_PHASE(2)
@@ -798,7 +814,26 @@ __device__ __forceinline__ void mlp_tiles(
       // B columns 8..15 of the 16-wide MFMA tile repeat rows 0..7: their outputs are never read
       // (each output column depends on its own B column only), so no zero fill or select
       const char* hr = HX + (li & (TS - 1)) * HB;
-      if constexpr (PP || !kD2) {
+      if constexpr (kHeadEarly) {
+        // the next tile's W1E chunk 0 first (it is carried across the gather), then 5 chunks of
+        // MFMAs on fragments already in registers
+        h8 an[2][2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, vb, FR_W1E + j * 4 + pt);
+#pragma unroll
+        for (int q = 0; q < KV / 32; ++q) {
+          const h8 bh = *(const h8*)(hr + 16 * (4 * q + g));
+          const h8 bl = *(const h8*)(hr + HLO + 16 * (4 * q + g));
+          ah = q == 0 ? mfma3(a[0][0], a[0][1], bh, bl, ah) : mfma3(hfr[q - 1][0], hfr[q - 1][1], bh, bl, ah);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          a[j][0] = an[j][0];
+          a[j][1] = an[j][1];
+        }
+      } else if constexpr (PP || !kD2) {
 #pragma unroll
         for (int q = 0; q < KV / 32; ++q) {
           h8 an[2][2];

@@ -18,6 +18,7 @@ from apn_amd.temporalpoints import CELL_CAP  # noqa: E402
 
 
 def main():
+    torch.set_grad_enabled(False)   # the render path (with grad, forward() takes the training path)
     dev = torch.device("cuda", 0)
     scene = S.make_scene("C2")
     model = harness.build_model(scene, dev)
