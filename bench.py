@@ -275,7 +275,73 @@ def lbs_sweep(args, rank, world, dev):
                              "launches on the launch stream); the step also runs the skeleton kernel"},
         "cpu_baseline": cpu,
     }
-    emit(line, args)
+    return line
+
+
+def frame_rate(config, dev, steps=10, warmup=2):
+    """One GPU, one config (C3 / C4): whole frames replayed as one HIP graph, as the headline line,
+    plus the MLP kernel's time from HIP events on eager frames and its F_alg roofline fraction.
+    Rides along in the default line (`other_configs`), so every config has a driver-run number."""
+    scene = S.make_scene(config)
+    model = harness.build_model(scene, dev)
+    rk = scene.render_kwargs(dev)
+    R = rk["rays_o"].shape[0]
+    t_arg = torch.tensor([scene.cfg.t], device=dev)
+    poses, Ks = scene.c2w[None].to(dev), scene.K[None].to(dev)
+    kw = dict(render_depth=True, render_kwargs=rk, render_weights=True, poses=poses, Ks=Ks, get_skeleton=True)
+    for _ in range(warmup):
+        model(t_arg, **kw)
+    torch.cuda.synchronize(dev)
+    stats = model.last_stats.resolved()
+    model.timing = {}
+    for _ in range(5):
+        model(t_arg, **kw)
+    torch.cuda.synchronize(dev)
+    timing, model.timing = model.timing, None
+    ev = timing.get("mlp_events", [])
+    mlp_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / max(len(ev), 1)
+    kept = int(ev[-1][2].item()) if ev else stats.get("kept_samples", 0)
+    step = model.capture_frame(t_arg, rk, poses=poses, Ks=Ks, get_skeleton=True)
+    for _ in range(2):
+        step(t_arg)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(t_arg)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    d_in = 191 + model.pose_embedding_dim
+    achieved = kept * flop_per_kept_sample(d_in) / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else 0.0
+    return {"workload": S.CONFIGS[config].name + f" ({config})", "value": steps * R / elapsed, "unit": "rays/s",
+            "ms_per_step": elapsed / steps * 1e3, "steps": steps, "rays_per_frame": R, "points": scene.cfg.N,
+            "bones": scene.cfg.J, "inbbox_samples": stats.get("inbbox_samples"), "kept_samples": kept,
+            "timed_frames_overflowed": bool(step.overflowed()),
+            "mlp_kernel_ms": mlp_ms, "mlp_roofline_frac": achieved / SPLIT3_PEAK_TFLOPS}
+
+
+def other_configs(dev):
+    """C3, C4 (frames) and C5 (repose sweep) on this GPU, compact; a failure is reported, never fatal."""
+    out = {}
+    for cfg in ("C3", "C4"):
+        try:
+            out[cfg] = frame_rate(cfg, dev)
+            log(f"[other configs] {cfg}: {out[cfg]['value'] / 1e6:.1f} M rays/s, {out[cfg]['ms_per_step']:.2f} ms/frame")
+        except Exception as e:
+            out[cfg] = {"error": repr(e)}
+        torch.cuda.empty_cache()
+    try:
+        a = argparse.Namespace(config="C5", steps=300, warmup=3, no_cpu_baseline=True)
+        c5 = lbs_sweep(a, 0, 1, dev)
+        out["C5"] = {"workload": c5["config"]["workload"], "value": c5["value"], "unit": c5["unit"],
+                     "ms_per_step": c5["ms_per_step"], "steps": a.steps, "lbs_kernel_ms": c5["config"]["lbs_kernel_ms"],
+                     "lbs_roofline_frac": c5["roofline"]["frac"], "lbs_bytes_per_launch": c5["roofline"]["bytes_per_launch"]}
+        log(f"[other configs] C5: {c5['value'] / 1e9:.2f} G points/s, LBS {c5['config']['lbs_kernel_ms']:.4f} ms")
+    except Exception as e:
+        out["C5"] = {"error": repr(e)}
+    out["note"] = ("one GPU each, after the headline run: C3/C4 = whole frames replayed as one HIP graph (10 timed), "
+                   "MLP kernel ms from HIP events on 5 eager frames; C5 = 300 poses of the repose sweep graph, LBS "
+                   "kernel from a graph of 20 launches (bench.py --config C5 gives the full line)")
+    return out
 
 
 def read_traffic(path):
@@ -294,6 +360,8 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--cpu-rows", type=int, default=16, help="image rows in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-other-configs", action="store_true",
+                    help="skip the compact C3 / C4 / C5 measurements the default one-GPU C2 line carries")
     ap.add_argument("-o", "--out", default=None, help="also write the JSON line to this file")
     ap.add_argument("--shard", choices=["frames", "rays"], default="rays",
                     help="N>1: 'rays' (default) = the ranks split one frame's rays and all-gather the tiles "
@@ -320,7 +388,9 @@ def main():
     dev = torch.device("cuda", local)
 
     if args.config == "C5":
-        lbs_sweep(args, rank, world, dev)
+        line = lbs_sweep(args, rank, world, dev)
+        if line is not None:
+            emit(line, args)
         if world > 1:
             torch.distributed.destroy_process_group()
         return
@@ -518,6 +588,9 @@ def main():
             same = same_cloud_error(out, rk, model.last_palette_perm, orc, sub, t_cpu, sel)
         except Exception as e:  # never lose the GPU line over the baseline leg
             log(f"cpu baseline failed: {e!r}")
+    others = None
+    if world == 1 and args.config == "C2" and not args.no_other_configs:
+        others = other_configs(dev)
     line = {
         "metric": f"rendered rays/sec at {scene.cfg.W}x{scene.cfg.H}, {scene.cfg.N // 1000}k pts, {scene.cfg.J} bones",
         "value": value, "unit": "rays/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -554,6 +627,7 @@ def main():
         "cpu_baseline": cpu,
         "psnr_vs_oracle": psnr,
         "same_cloud_vs_oracle": same,
+        **({"other_configs": others} if others is not None else {}),
     }
     emit(line, args)
     if world > 1:

@@ -5,6 +5,6 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 i=0
 for r in $(seq 1 ${ROUNDS:-2}); do for e in $ENVS; do
   i=$((i+1))
-  env ${e//,/ } timeout -k 10 150 python bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline -o gpurun_out/envab_$i.json "$@" 2>/dev/null >/dev/null || exit 1
+  env ${e//,/ } timeout -k 10 150 python bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline --no-other-configs -o gpurun_out/envab_$i.json "$@" 2>/dev/null >/dev/null || exit 1
   python -c "import json; d=json.load(open('gpurun_out/envab_$i.json')); s=d['stage_ms']; print('$e', 'mlp %.3f knn %.3f frame %.3f' % (s['mlp'], s['knn'], d['ms_per_step']))"
 done; done
