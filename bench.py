@@ -577,7 +577,7 @@ def main():
     else:
         kernel, peak, mfma_peak = "k_point_mlp_h3 (3-term fp16-split MFMA)", SPLIT3_PEAK_TFLOPS, FP16_MFMA_PEAK_TFLOPS
         peak_note = "peak = fp16 dense MFMA peak / 3 (three fp16 MFMA terms per fp32-accurate product)"
-    traffic = read_traffic(os.path.join(ROOT, "profiles", "r02_point_mlp_traffic.json"))
+    traffic = read_traffic(os.path.join(ROOT, "profiles", "r03_point_mlp_traffic.json"))
     ms_per_step = elapsed / args.steps * 1e3
     value = (1 if shard_rays else world) * args.steps * R / elapsed
     cpu = psnr = same = None
