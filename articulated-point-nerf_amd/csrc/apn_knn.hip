@@ -160,6 +160,12 @@ __device__ __forceinline__ void knn_insert(float d, int id, float (&bd)[K], int 
   }
 }
 
+#ifdef APN_KNN_DUPCHECK_ALL   // A/B: the duplicate check on every insert (the round-2 kernels)
+constexpr bool kFirstScanNoDup = false;
+#else
+constexpr bool kFirstScanNoDup = true;
+#endif
+
 template <int K, bool EXCL>
 __device__ __forceinline__ void consider(const float4& P, float qx, float qy, float qz, float dmax2, int excl,
                                          float (&bd)[K], int (&bi)[K]) {
@@ -891,7 +897,9 @@ __device__ __forceinline__ void scan_ball_flat(const GridParams& g, const int* _
 // alone, so the lanes partition each slab's rows whatever bound sizes the slab). Pruning with
 // the lane-local K-th distance stays exact: K points of this lane already beat every point of a
 // pruned row.
-template <int K, bool STATS = false, int S = 1>
+// DUP = false: the caller's list holds no point this scan can reach (a first scan): plain inserts,
+// no duplicate check (every point of the ball is visited at most once within one scan).
+template <int K, bool STATS = false, int S = 1, bool DUP = true>
 __device__ __forceinline__ void scan_ball_flat2(const GridParams& g, const int* __restrict__ cell_start,
                                                 const float4* __restrict__ sorted, float qx, float qy, float qz,
                                                 float R2, float (&bd)[K], int (&bi)[K], unsigned* ctr = nullptr,
@@ -926,8 +934,13 @@ __device__ __forceinline__ void scan_ball_flat2(const GridParams& g, const int* 
       const float d0 = (d0x * d0x + d0y * d0y) + d0z * d0z;
       const float d1x = qx - P1.x, d1y = qy - P1.y, d1z = qz - P1.z;
       const float d1 = (d1x * d1x + d1y * d1y) + d1z * d1z;
-      if (d0 <= g.r2) knn_insert_unique<K>(d0, i0, bd, bi);
-      if (p1 != b && d1 <= g.r2) knn_insert_unique<K>(d1, i1, bd, bi);
+      if constexpr (DUP) {
+        if (d0 <= g.r2) knn_insert_unique<K>(d0, i0, bd, bi);
+        if (p1 != b && d1 <= g.r2) knn_insert_unique<K>(d1, i1, bd, bi);
+      } else {
+        if (d0 <= g.r2) knn_insert<K>(d0, i0, bd, bi);
+        if (p1 != b && d1 <= g.r2) knn_insert<K>(d1, i1, bd, bi);
+      }
       b += 2;
       if (b > e) b = e;
     } else {
@@ -1024,7 +1037,7 @@ __global__ void k_agrid_scatter(const float4* __restrict__ sorted, int64_t N, co
 // scan_ball_flat2 on the anisotropic grid (cell sides hx, hy, hz): the same lock-step row/point
 // state machine, nearest-first slabs, running K-th-best culling with 1e-4 slack.
 // PTS points per point step (2 or 4).
-template <int K, bool STATS = false, int PTS = 2>
+template <int K, bool STATS = false, int PTS = 2, bool DUP = true>
 __device__ __forceinline__ void scan_ball_aniso(const AGrid& g, const int* __restrict__ cell_start,
                                                 const float4* __restrict__ sorted, float qx, float qy, float qz,
                                                 float R2, float (&bd)[K], int (&bi)[K], unsigned* ctr = nullptr) {
@@ -1059,7 +1072,10 @@ __device__ __forceinline__ void scan_ball_aniso(const AGrid& g, const int* __res
       for (int u = 0; u < PTS; ++u) {
         const float dx = qx - P[u].x, dy = qy - P[u].y, dz = qz - P[u].z;
         const float d = (dx * dx + dy * dy) + dz * dz;
-        if (b + u < e && d <= g.r2) knn_insert_unique<K>(d, id[u], bd, bi);
+        if (b + u < e && d <= g.r2) {
+          if constexpr (DUP) knn_insert_unique<K>(d, id[u], bd, bi);
+          else knn_insert<K>(d, id[u], bd, bi);
+        }
       }
       b += PTS;
       if (b > e) b = e;
@@ -1351,8 +1367,8 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_a8(
 #pragma unroll
         for (int k = 0; k < KNN_K; ++k) { bd[k] = INFINITY; bi[k] = 0x7fffffff; }
         const float R2 = coarse ? g.r2 : 0.0625f * g.r2;
-        if (ANISO) scan_ball_aniso<KNN_K>(*agp, cell_start2, sorted2, q.x, q.y, q.z, R2, bd, bi);
-        else scan_ball_flat2<KNN_K>(g, cell_start, sorted, q.x, q.y, q.z, R2, bd, bi);
+        if (ANISO) scan_ball_aniso<KNN_K, false, 2, kFirstScanNoDup ? false : true>(*agp, cell_start2, sorted2, q.x, q.y, q.z, R2, bd, bi);
+        else scan_ball_flat2<KNN_K, false, 1, kFirstScanNoDup ? false : true>(g, cell_start, sorted, q.x, q.y, q.z, R2, bd, bi);
         if (R2 == g.r2 || bd[KNN_K - 1] < R2 * (1.f - 2e-4f)) {
           surv = bd[KNN_K - 1] <= g.r2;
           if (surv) {
@@ -1716,11 +1732,22 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_b9(
 #pragma unroll
   for (int k = 0; k < KNN_K; ++k) { bd[k] = INFINITY; bi[k] = 0x7fffffff; }
   bool done = false;
-  if ((hc & 1) == 0) {
-    scan_ball_aniso<KNN_K, STATS, PTS>(g, cell_start2, sorted2, q.x, q.y, q.z, 0.25f * g.r2, bd, bi, c2);
-    done = bd[KNN_K - 1] < 0.25f * g.r2 * (1.f - 2e-4f);
+  if constexpr (kFirstScanNoDup) {
+    // only the r scan after an r/2 scan revisits points already in the list
+    if ((hc & 1) == 0) {
+      scan_ball_aniso<KNN_K, STATS, PTS, false>(g, cell_start2, sorted2, q.x, q.y, q.z, 0.25f * g.r2, bd, bi, c2);
+      done = bd[KNN_K - 1] < 0.25f * g.r2 * (1.f - 2e-4f);
+      if (!done) scan_ball_aniso<KNN_K, STATS, PTS, true>(g, cell_start2, sorted2, q.x, q.y, q.z, g.r2, bd, bi, cr);
+    } else {
+      scan_ball_aniso<KNN_K, STATS, PTS, false>(g, cell_start2, sorted2, q.x, q.y, q.z, g.r2, bd, bi, cr);
+    }
+  } else {
+    if ((hc & 1) == 0) {
+      scan_ball_aniso<KNN_K, STATS, PTS>(g, cell_start2, sorted2, q.x, q.y, q.z, 0.25f * g.r2, bd, bi, c2);
+      done = bd[KNN_K - 1] < 0.25f * g.r2 * (1.f - 2e-4f);
+    }
+    if (!done) scan_ball_aniso<KNN_K, STATS, PTS>(g, cell_start2, sorted2, q.x, q.y, q.z, g.r2, bd, bi, cr);
   }
-  if (!done) scan_ball_aniso<KNN_K, STATS, PTS>(g, cell_start2, sorted2, q.x, q.y, q.z, g.r2, bd, bi, cr);
   const bool surv = bd[KNN_K - 1] <= g.r2;
   if (STATS) {
     unsigned long long* st = g_knn_stats + 10 * (hc & 1);
