@@ -279,6 +279,78 @@ __device__ __forceinline__ void knn_insert_unique(float d, int id, float (&bd)[K
   }
 }
 
+// Top-K lists for the ball scans. ArrList: the (distance, index) arrays, pairwise compares.
+// KeyList: one 64-bit key per entry, bits(d) << 32 | index -- for d >= 0 the unsigned key order is
+// exactly knn_less (distance, then index), so each compare is one 64-bit integer compare; an insert
+// computes every position flag from the old list (independent compares) and shifts with selects.
+template <int K>
+struct ArrList {
+  float (&bd)[K];
+  int (&bi)[K];
+  __device__ __forceinline__ float worst() const { return bd[K - 1]; }
+  __device__ __forceinline__ int index(int k) const { return bi[k]; }
+  template <bool DUP>
+  __device__ __forceinline__ void insert(float d, int id) {
+    if constexpr (DUP) knn_insert_unique<K>(d, id, bd, bi);
+    else knn_insert<K>(d, id, bd, bi);
+  }
+};
+
+typedef unsigned long long knn_key_t;
+__device__ __forceinline__ knn_key_t knn_key(float d, int i) {
+  return ((knn_key_t)__float_as_uint(d) << 32) | (unsigned)i;
+}
+
+template <int K>
+struct KeyList {
+  knn_key_t kk[K];
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int k = 0; k < K; ++k) kk[k] = knn_key(INFINITY, 0x7fffffff);
+  }
+  __device__ __forceinline__ float worst() const { return __uint_as_float((unsigned)(kk[K - 1] >> 32)); }
+  __device__ __forceinline__ int index(int k) const { return (int)(unsigned)kk[k]; }
+  template <bool DUP>
+  __device__ __forceinline__ void insert(float d, int id) {
+    const knn_key_t x = knn_key(d, id);
+    if (!(x < kk[K - 1])) return;
+    if constexpr (DUP) {
+#pragma unroll
+      for (int k = 0; k < K - 1; ++k)
+        if (kk[k] == x) return;
+    }
+    bool m[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) m[k] = x < kk[k];   // monotone: false..false true..true
+#pragma unroll
+    for (int k = K - 1; k > 0; --k) kk[k] = m[k] ? (m[k - 1] ? kk[k - 1] : x) : kk[k];
+    kk[0] = m[0] ? x : kk[0];
+  }
+};
+
+// pass A / pass B lists (mode 9): 64-bit keys, or (APN_KNN_PAIRLIST, A/B) the (distance, index) pairs
+template <int K>
+struct PairList {
+  float bd[K];
+  int bi[K];
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int k = 0; k < K; ++k) { bd[k] = INFINITY; bi[k] = 0x7fffffff; }
+  }
+  __device__ __forceinline__ float worst() const { return bd[K - 1]; }
+  __device__ __forceinline__ int index(int k) const { return bi[k]; }
+  template <bool DUP>
+  __device__ __forceinline__ void insert(float d, int id) {
+    if constexpr (DUP) knn_insert_unique<K>(d, id, bd, bi);
+    else knn_insert<K>(d, id, bd, bi);
+  }
+};
+#ifdef APN_KNN_PAIRLIST
+typedef PairList<KNN_K> KnnList;
+#else
+typedef KeyList<KNN_K> KnnList;
+#endif
+
 template <int K>
 __device__ __forceinline__ void scan_range_u(const float4* __restrict__ sorted, int b, int e, float qx, float qy,
                                              float qz, float dmax2, float (&bd)[K], int (&bi)[K]) {
@@ -899,11 +971,10 @@ __device__ __forceinline__ void scan_ball_flat(const GridParams& g, const int* _
 // pruned row.
 // DUP = false: the caller's list holds no point this scan can reach (a first scan): plain inserts,
 // no duplicate check (every point of the ball is visited at most once within one scan).
-template <int K, bool STATS = false, int S = 1, bool DUP = true>
-__device__ __forceinline__ void scan_ball_flat2(const GridParams& g, const int* __restrict__ cell_start,
-                                                const float4* __restrict__ sorted, float qx, float qy, float qz,
-                                                float R2, float (&bd)[K], int (&bi)[K], unsigned* ctr = nullptr,
-                                                int slice = 0) {
+template <int K, bool STATS, int S, bool DUP, class L>
+__device__ __forceinline__ void scan_ball_flat2_l(const GridParams& g, const int* __restrict__ cell_start,
+                                                  const float4* __restrict__ sorted, float qx, float qy, float qz,
+                                                  float R2, L& lst, unsigned* ctr = nullptr, int slice = 0) {
   const float R = sqrtf(R2) * 1.0001f;
   const int z0 = max((int)floorf((qz - R - g.oz) * g.inv_h), 0), z1 = min((int)floorf((qz + R - g.oz) * g.inv_h), g.dz - 1);
   const int y0 = max((int)floorf((qy - R - g.oy) * g.inv_h), 0), y1 = min((int)floorf((qy + R - g.oy) * g.inv_h), g.dy - 1);
@@ -934,18 +1005,13 @@ __device__ __forceinline__ void scan_ball_flat2(const GridParams& g, const int* 
       const float d0 = (d0x * d0x + d0y * d0y) + d0z * d0z;
       const float d1x = qx - P1.x, d1y = qy - P1.y, d1z = qz - P1.z;
       const float d1 = (d1x * d1x + d1y * d1y) + d1z * d1z;
-      if constexpr (DUP) {
-        if (d0 <= g.r2) knn_insert_unique<K>(d0, i0, bd, bi);
-        if (p1 != b && d1 <= g.r2) knn_insert_unique<K>(d1, i1, bd, bi);
-      } else {
-        if (d0 <= g.r2) knn_insert<K>(d0, i0, bd, bi);
-        if (p1 != b && d1 <= g.r2) knn_insert<K>(d1, i1, bd, bi);
-      }
+      if (d0 <= g.r2) lst.template insert<DUP>(d0, i0);
+      if (p1 != b && d1 <= g.r2) lst.template insert<DUP>(d1, i1);
       b += 2;
       if (b > e) b = e;
     } else {
       if (pend) { b = pb; e = pe; pend = false; }
-      const float tau = fminf(bd[K - 1], R2) * 1.0001f;
+      const float tau = fminf(lst.worst(), R2) * 1.0001f;
       if (iy >= nyz) {               // next slab
         ++iz;
         iy = S == 1 ? 0 : slice;
@@ -980,6 +1046,15 @@ __device__ __forceinline__ void scan_ball_flat2(const GridParams& g, const int* 
       }
     }
   }
+}
+
+template <int K, bool STATS = false, int S = 1, bool DUP = true>
+__device__ __forceinline__ void scan_ball_flat2(const GridParams& g, const int* __restrict__ cell_start,
+                                                const float4* __restrict__ sorted, float qx, float qy, float qz,
+                                                float R2, float (&bd)[K], int (&bi)[K], unsigned* ctr = nullptr,
+                                                int slice = 0) {
+  ArrList<K> lst{bd, bi};
+  scan_ball_flat2_l<K, STATS, S, DUP>(g, cell_start, sorted, qx, qy, qz, R2, lst, ctr, slice);
 }
 
 // ---- mode 9: pass B on a second, anisotropic grid. A hard query's r-ball scan on the fine grid
@@ -1037,10 +1112,10 @@ __global__ void k_agrid_scatter(const float4* __restrict__ sorted, int64_t N, co
 // scan_ball_flat2 on the anisotropic grid (cell sides hx, hy, hz): the same lock-step row/point
 // state machine, nearest-first slabs, running K-th-best culling with 1e-4 slack.
 // PTS points per point step (2 or 4).
-template <int K, bool STATS = false, int PTS = 2, bool DUP = true>
-__device__ __forceinline__ void scan_ball_aniso(const AGrid& g, const int* __restrict__ cell_start,
-                                                const float4* __restrict__ sorted, float qx, float qy, float qz,
-                                                float R2, float (&bd)[K], int (&bi)[K], unsigned* ctr = nullptr) {
+template <int K, bool STATS, int PTS, bool DUP, class L>
+__device__ __forceinline__ void scan_ball_aniso_l(const AGrid& g, const int* __restrict__ cell_start,
+                                                  const float4* __restrict__ sorted, float qx, float qy, float qz,
+                                                  float R2, L& lst, unsigned* ctr = nullptr) {
   const float R = sqrtf(R2) * 1.0001f;
   const int z0 = max((int)floorf((qz - R - g.oz) * g.ihz), 0), z1 = min((int)floorf((qz + R - g.oz) * g.ihz), g.dz - 1);
   const int y0 = max((int)floorf((qy - R - g.oy) * g.ihy), 0), y1 = min((int)floorf((qy + R - g.oy) * g.ihy), g.dy - 1);
@@ -1072,16 +1147,13 @@ __device__ __forceinline__ void scan_ball_aniso(const AGrid& g, const int* __res
       for (int u = 0; u < PTS; ++u) {
         const float dx = qx - P[u].x, dy = qy - P[u].y, dz = qz - P[u].z;
         const float d = (dx * dx + dy * dy) + dz * dz;
-        if (b + u < e && d <= g.r2) {
-          if constexpr (DUP) knn_insert_unique<K>(d, id[u], bd, bi);
-          else knn_insert<K>(d, id[u], bd, bi);
-        }
+        if (b + u < e && d <= g.r2) lst.template insert<DUP>(d, id[u]);
       }
       b += PTS;
       if (b > e) b = e;
     } else {
       if (pend) { b = pb; e = pe; pend = false; }
-      const float tau = fminf(bd[K - 1], R2) * 1.0001f;
+      const float tau = fminf(lst.worst(), R2) * 1.0001f;
       if (iy >= nyz) {
         ++iz;
         iy = 0;
@@ -1116,6 +1188,14 @@ __device__ __forceinline__ void scan_ball_aniso(const AGrid& g, const int* __res
       }
     }
   }
+}
+
+template <int K, bool STATS = false, int PTS = 2, bool DUP = true>
+__device__ __forceinline__ void scan_ball_aniso(const AGrid& g, const int* __restrict__ cell_start,
+                                                const float4* __restrict__ sorted, float qx, float qy, float qz,
+                                                float R2, float (&bd)[K], int (&bi)[K], unsigned* ctr = nullptr) {
+  ArrList<K> lst{bd, bi};
+  scan_ball_aniso_l<K, STATS, PTS, DUP>(g, cell_start, sorted, qx, qy, qz, R2, lst, ctr);
 }
 
 // ---- mode 6: per-cell rejection bound. For every fine cell C holding a candidate, U(C) = number
@@ -1362,19 +1442,17 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_a8(
       const bool coarse = g.h > 0.25f * g.r;
       if (coarse || u4[cell] >= KNN_K) {
         const float4 q = q_pos[cand[c]];
-        float bd[KNN_K];
-        int bi[KNN_K];
-#pragma unroll
-        for (int k = 0; k < KNN_K; ++k) { bd[k] = INFINITY; bi[k] = 0x7fffffff; }
+        KnnList lst;
+        lst.init();
         const float R2 = coarse ? g.r2 : 0.0625f * g.r2;
-        if (ANISO) scan_ball_aniso<KNN_K, false, 2, kFirstScanNoDup ? false : true>(*agp, cell_start2, sorted2, q.x, q.y, q.z, R2, bd, bi);
-        else scan_ball_flat2<KNN_K, false, 1, kFirstScanNoDup ? false : true>(g, cell_start, sorted, q.x, q.y, q.z, R2, bd, bi);
-        if (R2 == g.r2 || bd[KNN_K - 1] < R2 * (1.f - 2e-4f)) {
-          surv = bd[KNN_K - 1] <= g.r2;
+        if (ANISO) scan_ball_aniso_l<KNN_K, false, 2, !kFirstScanNoDup>(*agp, cell_start2, sorted2, q.x, q.y, q.z, R2, lst);
+        else scan_ball_flat2_l<KNN_K, false, 1, !kFirstScanNoDup>(g, cell_start, sorted, q.x, q.y, q.z, R2, lst);
+        if (R2 == g.r2 || lst.worst() < R2 * (1.f - 2e-4f)) {
+          surv = lst.worst() <= g.r2;
           if (surv) {
             int4* nb = (int4*)(t_nbr + (int64_t)c * KNN_K);
-            nb[0] = make_int4(bi[0], bi[1], bi[2], bi[3]);
-            nb[1] = make_int4(bi[4], bi[5], bi[6], bi[7]);
+            nb[0] = make_int4(lst.index(0), lst.index(1), lst.index(2), lst.index(3));
+            nb[1] = make_int4(lst.index(4), lst.index(5), lst.index(6), lst.index(7));
           }
         } else {
           push = true;
@@ -1727,28 +1805,26 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_b9(
   const int hc = i < n1 ? hard[i] : hard2[i - n1];
   const int c = hc >> 1;
   const float4 q = q_pos[cand[c]];
-  float bd[KNN_K];
-  int bi[KNN_K];
-#pragma unroll
-  for (int k = 0; k < KNN_K; ++k) { bd[k] = INFINITY; bi[k] = 0x7fffffff; }
+  KnnList lst;
+  lst.init();
   bool done = false;
   if constexpr (kFirstScanNoDup) {
     // only the r scan after an r/2 scan revisits points already in the list
     if ((hc & 1) == 0) {
-      scan_ball_aniso<KNN_K, STATS, PTS, false>(g, cell_start2, sorted2, q.x, q.y, q.z, 0.25f * g.r2, bd, bi, c2);
-      done = bd[KNN_K - 1] < 0.25f * g.r2 * (1.f - 2e-4f);
-      if (!done) scan_ball_aniso<KNN_K, STATS, PTS, true>(g, cell_start2, sorted2, q.x, q.y, q.z, g.r2, bd, bi, cr);
+      scan_ball_aniso_l<KNN_K, STATS, PTS, false>(g, cell_start2, sorted2, q.x, q.y, q.z, 0.25f * g.r2, lst, c2);
+      done = lst.worst() < 0.25f * g.r2 * (1.f - 2e-4f);
+      if (!done) scan_ball_aniso_l<KNN_K, STATS, PTS, true>(g, cell_start2, sorted2, q.x, q.y, q.z, g.r2, lst, cr);
     } else {
-      scan_ball_aniso<KNN_K, STATS, PTS, false>(g, cell_start2, sorted2, q.x, q.y, q.z, g.r2, bd, bi, cr);
+      scan_ball_aniso_l<KNN_K, STATS, PTS, false>(g, cell_start2, sorted2, q.x, q.y, q.z, g.r2, lst, cr);
     }
   } else {
     if ((hc & 1) == 0) {
-      scan_ball_aniso<KNN_K, STATS, PTS>(g, cell_start2, sorted2, q.x, q.y, q.z, 0.25f * g.r2, bd, bi, c2);
-      done = bd[KNN_K - 1] < 0.25f * g.r2 * (1.f - 2e-4f);
+      scan_ball_aniso_l<KNN_K, STATS, PTS, true>(g, cell_start2, sorted2, q.x, q.y, q.z, 0.25f * g.r2, lst, c2);
+      done = lst.worst() < 0.25f * g.r2 * (1.f - 2e-4f);
     }
-    if (!done) scan_ball_aniso<KNN_K, STATS, PTS>(g, cell_start2, sorted2, q.x, q.y, q.z, g.r2, bd, bi, cr);
+    if (!done) scan_ball_aniso_l<KNN_K, STATS, PTS, true>(g, cell_start2, sorted2, q.x, q.y, q.z, g.r2, lst, cr);
   }
-  const bool surv = bd[KNN_K - 1] <= g.r2;
+  const bool surv = lst.worst() <= g.r2;
   if (STATS) {
     unsigned long long* st = g_knn_stats + 10 * (hc & 1);
     atomicAdd(&st[0], 1ull);
@@ -1763,8 +1839,8 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_b9(
   flag[c] = surv;
   if (surv) {
     int4* nb = (int4*)(t_nbr + (int64_t)c * KNN_K);
-    nb[0] = make_int4(bi[0], bi[1], bi[2], bi[3]);
-    nb[1] = make_int4(bi[4], bi[5], bi[6], bi[7]);
+    nb[0] = make_int4(lst.index(0), lst.index(1), lst.index(2), lst.index(3));
+    nb[1] = make_int4(lst.index(4), lst.index(5), lst.index(6), lst.index(7));
   }
 }
 
