@@ -1791,14 +1791,52 @@ __global__ void k_knn_points(const float* __restrict__ q, int64_t M, const GridP
 // Pass B of mode 9: k_knn_pass_b8 with the r/2 and r balls on the anisotropic grid. One launch
 // over both hard lists (first list first: the host passes the heavier r list there, so the
 // longest waves start first and the two lists share one tail); hard2 == nullptr: one list.
+#ifdef APN_KNN_NO_BSORT   // A/B: pass B lanes in list order
+constexpr bool kSortB = false;
+#else
+constexpr bool kSortB = true;
+#endif
+// kSortB: a workgroup's queries are ranked by their cost estimate (k_block_cost's: u1, plus u2 for the
+// r/2 list) with a bitonic sort in LDS before the scans, so each wave holds queries of similar cost
+// and fewer lanes idle while the wave's longest scan runs (the lanes still cover the same 256
+// consecutive list entries: the workgroup's spatial locality is kept).
 template <bool STATS, int PTS>
 __global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_b9(
     const float4* __restrict__ q_pos, const int* __restrict__ cand, const int* __restrict__ hard,
     const int* __restrict__ n_hard, const int* __restrict__ hard2, const int* __restrict__ n_hard2,
     const AGrid* __restrict__ agp, const int* __restrict__ cell_start2, const float4* __restrict__ sorted2,
-    int* __restrict__ flag, int* __restrict__ t_nbr, const int* __restrict__ perm) {
-  const int i = (perm ? perm[blockIdx.x] : (int)blockIdx.x) * KNN_THREADS + threadIdx.x;
+    int* __restrict__ flag, int* __restrict__ t_nbr, const int* __restrict__ perm, const int* __restrict__ ccell,
+    const int* __restrict__ u1, const int* __restrict__ u2) {
+  const int base = (perm ? perm[blockIdx.x] : (int)blockIdx.x) * KNN_THREADS;
   const int n1 = *n_hard, n2 = hard2 ? *n_hard2 : 0;
+  int i = base + threadIdx.x;
+  if (kSortB && ccell) {
+    if (base >= n1 + n2) return;   // workgroup-uniform
+    __shared__ unsigned skey[KNN_THREADS];
+    const int tid = threadIdx.x;
+    unsigned w = 0;
+    if (i < n1 + n2) {
+      const int hc = i < n1 ? hard[i] : hard2[i - n1];
+      const int cell = ccell[hc >> 1];
+      w = (hc & 1) ? (unsigned)u1[cell] : (unsigned)(u2[cell] + u1[cell]);
+    }
+    // ascending keys = descending cost (heaviest wave first), entries past the list last
+    skey[tid] = ((0xffffffu - min(w, 0xffffffu)) << 8) | (unsigned)tid;
+    __syncthreads();
+#pragma unroll
+    for (int k = 2; k <= KNN_THREADS; k <<= 1) {
+#pragma unroll
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        const int p = tid ^ j;
+        if (p > tid) {
+          const unsigned a = skey[tid], b = skey[p];
+          if ((a > b) == ((tid & k) == 0)) { skey[tid] = b; skey[p] = a; }
+        }
+        __syncthreads();
+      }
+    }
+    i = base + (int)(skey[tid] & (KNN_THREADS - 1));
+  }
   if (i >= n1 + n2) return;
   const AGrid g = *agp;
   unsigned c2[2] = {0, 0}, cr[2] = {0, 0};
@@ -2099,9 +2137,10 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
       }();
       if (split) {
         hipLaunchKernelGGL(pass_b, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard, n_hard,
-                           nullptr, nullptr, g.ag, g.cell_start2, g.sorted2, flag, t_nbr, nullptr);
+                           nullptr, nullptr, g.ag, g.cell_start2, g.sorted2, flag, t_nbr, nullptr, ccell, u1, u2);
         hipLaunchKernelGGL(pass_b, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard_r,
-                           n_hard_r, nullptr, nullptr, g.ag, g.cell_start2, g.sorted2, flag, t_nbr, nullptr);
+                           n_hard_r, nullptr, nullptr, g.ag, g.cell_start2, g.sorted2, flag, t_nbr, nullptr, ccell, u1,
+                           u2);
       } else {   // n_hard + n_hard_r <= candidates <= nb * KNN_THREADS
         if (perm) {
           hipLaunchKernelGGL(k_block_cost<true>, dim3(nb), dim3(KNN_THREADS), 0, s, nullptr, hard_r, n_hard_r, hard,
@@ -2109,7 +2148,7 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
           hipLaunchKernelGGL(k_order_blocks, dim3(1), dim3(ORDER_THREADS), 0, s, blk_cnt, nb, perm);
         }
         hipLaunchKernelGGL(pass_b, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard_r,
-                           n_hard_r, hard, n_hard, g.ag, g.cell_start2, g.sorted2, flag, t_nbr, perm);
+                           n_hard_r, hard, n_hard, g.ag, g.cell_start2, g.sorted2, flag, t_nbr, perm, ccell, u1, u2);
       }
     } else {
       auto pass_b = stats ? k_knn_pass_b8<true> : k_knn_pass_b8<false>;
