@@ -1420,6 +1420,11 @@ __global__ __launch_bounds__(ORDER_THREADS) void k_order_blocks(const int* __res
   }
 }
 
+#ifdef APN_KNN_NO_ASORT   // A/B: pass A lanes in candidate order
+constexpr bool kSortA = false;
+#else
+constexpr bool kSortA = true;
+#endif
 // Pass A of mode 8: reject on u1 < 8; the r/4 ball (flat scan) only where u4 >= 8; the rest go to
 // the hard list tagged with their first useful level (r/2 if u2 >= 8, else r).
 template <bool ANISO>
@@ -1431,8 +1436,41 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_a8(
     int* __restrict__ n_hard, int* __restrict__ hard_r, int* __restrict__ n_hard_r, const AGrid* __restrict__ agp,
     const int* __restrict__ cell_start2, const float4* __restrict__ sorted2, const int* __restrict__ perm) {
   const int nc = *n_cand_dev;
-  const int c = (perm ? perm[blockIdx.x] : (int)blockIdx.x) * KNN_THREADS + threadIdx.x;
+  const int base = (perm ? perm[blockIdx.x] : (int)blockIdx.x) * KNN_THREADS;
+  int c = base + threadIdx.x;
   const GridParams g = *gp;
+  if (kSortA) {
+    // rank the workgroup's candidates by their scan cost (0 for the ones rejected or passed on without
+    // a search, u4 for an r/4 ball) so the scanning lanes share waves (see kSortB)
+    if (base >= nc) return;   // workgroup-uniform
+    __shared__ unsigned skey[KNN_THREADS];
+    const int tid = threadIdx.x;
+    unsigned w = 0;
+    if (c < nc) {
+      const int cell = ccell[c];
+      const int a1 = u1[cell];
+      if (a1 >= KNN_K) {
+        const bool coarse = g.h > 0.25f * g.r;
+        const int a4 = coarse ? a1 : u4[cell];
+        w = a4 >= KNN_K ? (unsigned)a4 : 0u;
+      }
+    }
+    skey[tid] = ((0xffffffu - min(w, 0xffffffu)) << 8) | (unsigned)tid;
+    __syncthreads();
+#pragma unroll
+    for (int k = 2; k <= KNN_THREADS; k <<= 1) {
+#pragma unroll
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        const int p = tid ^ j;
+        if (p > tid) {
+          const unsigned a = skey[tid], b = skey[p];
+          if ((a > b) == ((tid & k) == 0)) { skey[tid] = b; skey[p] = a; }
+        }
+        __syncthreads();
+      }
+    }
+    c = base + (int)(skey[tid] & (KNN_THREADS - 1));
+  }
   bool push = false;
   int tag = 0;
   if (c < nc) {
