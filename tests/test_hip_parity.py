@@ -277,6 +277,71 @@ def _knn_on_reference_cloud(dev, name, cap):
     assert np.array_equal(s_pos[:S].cpu().numpy(), q4[keep])
 
 
+def _lattice_scene():
+    """Three cubic point lattices with dyadic spacings 2^-6, 2^-5, 2^-4 (so every coordinate and
+    every squared distance below is exact in float32) and queries on their lattice points, cell
+    centres and face centres: many neighbours tie at exactly the same distance, and the top-8
+    boundary falls inside such ties (a lattice point: itself, 6 faces, then 1 of 12 tied edges).
+    The sparser lattices put queries on pass B's r/2 and r lists; 300k queries take the mode-9
+    path (more than the 2^18 of the small-launch kernel)."""
+    pts, qs = [], []
+    for h, n, off in ((2.0 ** -6, 40, 0.0), (2.0 ** -5, 30, 1.0), (2.0 ** -4, 20, 2.25)):
+        g = np.arange(n, dtype=np.float64) * h
+        P = np.stack(np.meshgrid(g, g, g, indexing="ij"), -1).reshape(-1, 3)
+        P[:, 0] += off
+        pts.append(P)
+        qs += [P, P + 0.5 * h, P + np.array([0.5 * h, 0.0, 0.0])]
+    return np.concatenate(pts).astype(F32), np.concatenate(qs).astype(F32)
+
+
+def _exact_top8(pts, q, r2=F32(0.01)):
+    """Reference top-8 by (float32 squared distance (dx^2 + dy^2) + dz^2, index) among the 64
+    float64-nearest points (exact here: the lattice distances are exact in both precisions)."""
+    from scipy.spatial import cKDTree
+    _, nn = cKDTree(pts.astype(np.float64)).query(q.astype(np.float64), k=64)
+    d = q[:, None, :] - pts[nn]                                   # float32
+    d2 = (d[..., 0] * d[..., 0] + d[..., 1] * d[..., 1]) + d[..., 2] * d[..., 2]
+    order = np.lexsort((nn, d2), axis=-1)[:, :8]                  # distance, then index
+    idx = np.take_along_axis(nn, order, -1).astype(np.int32)
+    d8 = np.take_along_axis(d2, order, -1)[:, -1]
+    return idx, d8 <= r2
+
+
+def test_knn_exact_ties_on_lattices(dev):
+    """apn_knn_radius (mode 9: pass A and pass B with 64-bit (distance, index) keys, cost-ranked
+    lanes) on a cloud full of exact distance ties returns the reference's top-8 order: ties broken
+    by point index (temporalpoints.py:433-447 through pykeops' argKmin; oracle: knn_exact)."""
+    from apn_amd import _lib as L
+    pts, q = _lattice_scene()
+    N, nq = len(pts), len(q)
+    assert nq > (1 << 18)
+    ref_idx, keep = _exact_top8(pts, q)
+    cap = 1 << 20
+    bbox = np.concatenate([_ord(pts.min(0)), _ord(pts.max(0)), [0, 0]]).astype(np.int32)
+    xyz = torch.from_numpy(pts).to(dev)
+    bbox_t = torch.from_numpy(bbox).to(dev)
+    sorted4 = torch.empty(N, 4, device=dev)
+    gws = torch.empty(L.load().apn_grid_workspace_bytes(N, cap), dtype=torch.uint8, device=dev)
+    s = L.stream_ptr(dev)
+    L.call("apn_grid_build", L.ptr(xyz), N, L.ptr(bbox_t), 0.01, cap, L.ptr(sorted4), L.ptr(gws), s)
+    q4 = np.concatenate([q, np.zeros((nq, 1), np.int32).view(F32)], 1).astype(F32)
+    rid = np.arange(nq, dtype=np.int32)
+    q_pos = torch.from_numpy(q4).to(dev)
+    q_ray = torch.from_numpy(rid).to(dev)
+    nq_dev = torch.tensor([nq], dtype=torch.int32, device=dev)
+    s_pos = torch.empty(nq, 4, device=dev); s_ray = torch.empty(nq, dtype=torch.int32, device=dev)
+    s_nbr = torch.empty(nq, 8, dtype=torch.int32, device=dev); ns = torch.empty(1, dtype=torch.int32, device=dev)
+    kws = torch.empty(L.load().apn_knn_workspace_bytes(nq), dtype=torch.uint8, device=dev)
+    L.call("apn_knn_radius", L.ptr(q_pos), L.ptr(q_ray), nq, L.ptr(nq_dev), L.ptr(gws), N, cap, L.ptr(sorted4), 0.01,
+           L.ptr(s_pos), L.ptr(s_ray), L.ptr(s_nbr), L.ptr(ns), L.ptr(kws), s)
+    S = int(ns.item())
+    assert S == int(keep.sum())
+    assert np.array_equal(s_ray[:S].cpu().numpy(), rid[keep])
+    got = s_nbr[:S].cpu().numpy()
+    bad = np.nonzero((got != ref_idx[keep]).any(1))[0]
+    assert len(bad) == 0, f"{len(bad)} queries differ, first {rid[keep][bad[:3]]}: {got[bad[:3]]} vs {ref_idx[keep][bad[:3]]}"
+
+
 def _oracle_on_cloud(g, t_hat, perm=None):
     orc = g.oracle(mean_min_distance_value=g.t("in_mean_min_distance"))
     out = orc.forward(g.t("in_t"), render_depth=True, render_kwargs=g.render_kwargs(), render_weights=True,
