@@ -740,9 +740,14 @@ class TemporalPoints(torch.nn.Module):
         ``self.last_ray_index``). Either way ``self.last_ray_count`` is the rank's ray count (see
         apn_amd.shard for the tile all-gather)."""
         assert (t is None) ^ (rot_params is None)
-        if torch.is_grad_enabled():
+        # feat_depth != 4 (temporalpoints.py:53, 117-130): the fused MLP kernel is built for the
+        # reference default; other depths render through the generic GPU path (HIP skinning / kNN /
+        # loss kernels, the layers as GEMMs), the same code as the differentiable step
+        generic = len(self.feat_net) != 6
+        if torch.is_grad_enabled() or generic:
             if ray_shard is not None:
-                raise NotImplementedError("ray_shard is a render-path option (use torch.no_grad())")
+                raise NotImplementedError("ray_shard is a render-path option of the fused pipeline "
+                                          "(torch.no_grad(), feat_depth=4)")
             from .train import forward_train
             return forward_train(self, t, render_depth, render_kwargs, query_radius, render_weights, rot_params,
                                  poses, Ks, calc_min_max, get_skeleton)

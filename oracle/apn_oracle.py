@@ -20,6 +20,8 @@ from __future__ import annotations
 import colorsys
 import math
 
+import re
+
 import numpy as np
 import torch
 
@@ -464,9 +466,21 @@ def _lin(x, st, name):
     return torch.nn.functional.linear(x, st[name + ".weight"], st.get(name + ".bias"))
 
 
+def feat_net_names(st):
+    """The Linear layers of feat_net in order (temporalpoints.py:123-130): feat_net.0, then
+    feat_net.{2..depth-1}.0 (the hidden Sequentials), then feat_net.{depth} -- for the default
+    feat_depth=4: feat_net.0, .2.0, .3.0, .4."""
+    idx = []
+    for k in st:
+        m = re.fullmatch(r"feat_net\.(\d+)(\.0)?\.weight", k)
+        if m:
+            idx.append((int(m.group(1)), k[:-len(".weight")]))
+    return [nm for _, nm in sorted(idx)]
+
+
 def feat_net(x, st):
-    """temporalpoints.py:123-130 (feat_depth=4): 4 x [Linear + LeakyReLU(0.01)]."""
-    for nm in ["feat_net.0", "feat_net.2.0", "feat_net.3.0", "feat_net.4"]:
+    """temporalpoints.py:123-130: feat_depth x [Linear + LeakyReLU(0.01)]."""
+    for nm in feat_net_names(st):
         x = torch.nn.functional.leaky_relu(_lin(x, st, nm), 0.01)
     return x
 
