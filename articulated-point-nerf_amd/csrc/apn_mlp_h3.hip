@@ -934,444 +934,6 @@ __device__ __forceinline__ void mlp_tiles(
   if (range_bad) __builtin_amdgcn_raw_buffer_store_b32(1, rs, 0, H_TOTAL * 2, 0);   // the range flag (OFF_FLAG)
 }
 
-// ======================================================================= software-pipelined build
-// (APN_MLP_OCC=4): the posenc gather of tile i+1 is computed inside tile i's layer 2-4 MFMA
-// phases, so its VALU work fills the MFMA shadows of the same wave instead of forming a phase of
-// its own. Needs a PE buffer beside the activations (the next tile's layer-1 input) and double-
-// buffered row records, 67 KB of LDS: 2 workgroups per CU, 256 VGPRs per lane. Same arithmetic as
-// mlp_tiles (bit-identical outputs); the posenc quarter is a runtime wave-uniform index here (one
-// copy of the tile loop), and every wave writes three of the nine per-row record entries.
-constexpr int PEB = 256;   // bytes per PE row: 16 chunks of 16 B -- hi columns 0..63 = chunks 0..7, lo = 8..15
-__device__ __forceinline__ int pe_off(int m, int c) { return m * PEB + ((c ^ (m & 15)) << 4); }
-
-struct PipeG {   // the next tile's gather inputs: this lane's row (sample lane >> 3, neighbour lane & 7)
-  float4 a0, a1, a2, a3, b0, b1, q;
-  float vv;
-  int nb;        // < 0: no row
-};
-struct PipeS {   // gather values carried between the pieces
-  float rc0, rc1, rc2, tn;
-  f32x4 sv0, sv1, cv0, cv1;
-};
-
-template <int J0, int J1>
-__device__ __forceinline__ void pipe_pe_args(int p, PipeS& S) {
-#pragma unroll
-  for (int j = J0; j < J1; ++j) {
-    float sv, cv;
-    if (j < 7) {   // argument a = p + 4 j = 10 i + f < 30 (apn_mlp_layout.h pe_col_to_ref)
-      const int aa = p + 4 * j, ci = aa / 10, f = aa - 10 * ci;
-      const float x = ci == 0 ? S.rc0 : (ci == 1 ? S.rc1 : S.rc2);
-      sincos_pe(x * __int_as_float((127 + f) << 23), sv, cv);   // rc * 2^f, exact scale
-    } else {       // a = p + 28: sin/cos of rc[2] 2^(8 + p) for p < 2, the raw rel_c slots for p >= 2
-      float s1, c1;
-      sincos_pe(S.rc2 * __int_as_float((127 + 8 + (p & 1)) << 23), s1, c1);
-      sv = p < 2 ? s1 : (p == 2 ? S.rc0 : S.rc2);
-      cv = p < 2 ? c1 : (p == 2 ? S.rc1 : 0.f);
-    }
-    if (j < 4) { S.sv0[j] = sv; S.cv0[j] = cv; } else { S.sv1[j - 4] = sv; S.cv1[j - 4] = cv; }
-  }
-}
-
-__device__ __forceinline__ void pipe_load(int nb, int ray, float4 q, PipeG& G, const float4* __restrict__ recA,
-                                          const float4* __restrict__ recB, const float* __restrict__ viewdirs,
-                                          const float* __restrict__ vemb_const, int p) {
-  const int k = threadIdx.x & 7;
-  const size_t n = (size_t)max(nb, 0);
-  G.nb = nb;
-  G.q = q;
-  G.a0 = recA[4 * n + 0];
-  G.a1 = recA[4 * n + 1];
-  G.a2 = recA[4 * n + 2];
-  G.a3 = recA[4 * n + 3];
-  G.b0 = recB[2 * n];
-  G.b1 = recB[2 * n + 1];
-  const int e = min(4 * k + p, 26);
-  const int ee = e < 3 ? 0 : (e < 15 ? e - 3 : e - 15);
-  // frozen view direction (vemb_const): the embedding element itself; else the direction component
-  G.vv = vemb_const ? vemb_const[e] : viewdirs[3 * (size_t)ray + (e < 3 ? e : ee >> 2)];
-}
-
-__device__ __forceinline__ void pipe_piece_a(int p, const PipeG& G, PipeS& S) {
-  const float dx = G.q.x - G.a0.x, dy = G.q.y - G.a0.y, dz = G.q.z - G.a0.z;
-  S.rc0 = (G.a1.x * dx + G.a1.y * dy) + G.a1.z * dz;
-  S.rc1 = (G.a1.w * dx + G.a2.x * dy) + G.a2.y * dz;
-  S.rc2 = (G.a2.z * dx + G.a2.w * dy) + G.a3.x * dz;
-  S.tn = (dx * dx + dy * dy) + dz * dz;
-  pipe_pe_args<0, 3>(p, S);
-}
-
-// the last piece: the remaining arguments, the hi/lo split and the LDS writes of the next tile's
-// PE row, its row records (sRow: 0 wdir, 1 alpha_c, 2-4 rgb_c, 5-7 pcol, 8 to_nn; wave p writes
-// entries 3 min(p, 2) .. + 2) and its view-embedding element 4 (lane & 7) + p
-__device__ __forceinline__ void pipe_piece_c(int p, const PipeG& G, PipeS& S, char* __restrict__ PE,
-                                             float* __restrict__ sRowN, float* __restrict__ sVN,
-                                             const float* __restrict__ vemb_const) {
-  pipe_pe_args<6, 8>(p, S);
-  int r_ = threadIdx.x & 63;
-  asm volatile("" : "+v"(r_));
-  const int r = r_, s = r >> 3, k = r & 7;
-  const bool ok = G.nb >= 0;
-  h4 hs0, ls0, hs1, ls1, hc0, lc0, hc1, lc1;
-  split4(S.sv0, hs0, ls0); split4(S.sv1, hs1, ls1);
-  split4(S.cv0, hc0, lc0); split4(S.cv1, hc1, lc1);
-  const h8 z = {0, 0, 0, 0, 0, 0, 0, 0};
-  const h8 hs = __builtin_shufflevector(hs0, hs1, 0, 1, 2, 3, 4, 5, 6, 7);
-  const h8 ls = __builtin_shufflevector(ls0, ls1, 0, 1, 2, 3, 4, 5, 6, 7);
-  const h8 hc = __builtin_shufflevector(hc0, hc1, 0, 1, 2, 3, 4, 5, 6, 7);
-  const h8 lc = __builtin_shufflevector(lc0, lc1, 0, 1, 2, 3, 4, 5, 6, 7);
-  *(h8*)(PE + pe_off(r, 2 * p)) = ok ? hs : z;
-  *(h8*)(PE + pe_off(r, 8 + 2 * p)) = ok ? ls : z;
-  *(h8*)(PE + pe_off(r, 2 * p + 1)) = ok ? hc : z;
-  *(h8*)(PE + pe_off(r, 9 + 2 * p)) = ok ? lc : z;
-  // row records (temporalpoints.py:459-470): the entries this wave owns. Every candidate value is
-  // computed and the wave-uniform choice is a select (no branch: the piece must stay inside the
-  // layer's basic block for the scheduler to interleave it with the MFMAs)
-  const float ex = expf(-(S.tn * S.tn) / G.a0.w);   // temporalpoints.py:461 (to_nn is already squared)
-  const float ev0 = p == 0 ? ex : (p == 1 ? G.b0.y : G.b1.y);
-  const float ev1 = p == 0 ? G.a3.y : (p == 1 ? G.b0.z : G.b1.z);
-  const float ev2 = p == 0 ? G.b0.x : (p == 1 ? G.b1.x : S.tn);
-  float* rw = sRowN + RS * r + 3 * min(p, 2);
-  rw[0] = ok ? ev0 : 0.f;
-  rw[1] = ok ? ev1 : 0.f;
-  rw[2] = ok ? ev2 : (p >= 2 ? 1.f : 0.f);
-  // view embedding element e of this sample (tineuvox.py:872-878 of the ray's view direction; with a
-  // frozen direction G.vv is already the element)
-  const int e = 4 * k + p;
-  const int ee = e < 3 ? 0 : (e < 15 ? e - 3 : e - 15);
-  float sn_, cs_;
-  sincos_pe(G.vv * (float)(1 << (ee & 3)), sn_, cs_);
-  const float v = vemb_const ? G.vv : (e < 3 ? G.vv : (e < 15 ? sn_ : cs_));
-  sVN[s * 32 + e] = (ok && e < 27) ? v : 0.f;
-}
-
-// layer 1 with the activations (posenc) from the PE buffer: K = 64, two chunks of 32
-__device__ __forceinline__ void layer1_pe(const char* __restrict__ PE, rsrc_t rs, int vb, f32x4 (&acc)[4][2],
-                                          h8 (&a)[2][2]) {
-  const int lane = threadIdx.x & 63;
-  const int li = lane & 15, g = lane >> 4;
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    h8 an[2][2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int pt = 0; pt < 2; ++pt)
-        an[j][pt] = q == 0 ? frag(rs, vb, FR_W1E + (j * 2 + 1) * 2 + pt) : frag(rs, vb, FR_W2 + j * 4 * 2 + pt);
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      const int m = 16 * mt + li, c = 4 * q + g;
-      const h8 bh = *(const h8*)(PE + pe_off(m, c)), bl = *(const h8*)(PE + pe_off(m, 8 + c));
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[mt][j] = mfma3(a[j][0], a[j][1], bh, bl, acc[mt][j]);
-    }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      a[j][0] = an[j][0];
-      a[j][1] = an[j][1];
-    }
-  }
-}
-
-template <bool SCALED>
-__device__ __forceinline__ void mlp_tiles_pipe(
-    const float4* __restrict__ s_pos, const int* __restrict__ s_ray, const int* __restrict__ s_nbr,
-    const int* __restrict__ n_samples_dev, const float4* __restrict__ recA, const float4* __restrict__ recB,
-    const float4* __restrict__ pproj, const float* __restrict__ viewdirs, const float* __restrict__ vemb_const,
-    const float* __restrict__ wbuf, float eps, float shift, float interval, float4* __restrict__ out,
-    char* const X0, char* const PE, char* const HX, float* const sIdw, float* const sRowB, float* const sOut,
-    float* const sVB, float* const sW, float* const sPart) {
-  const int nS = *n_samples_dev;
-  const int ntiles = (nS + TS - 1) / TS;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int li = lane & 15, g = lane >> 4;
-  const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(wbuf + OFF_H16), 0, H_TOTAL * 2 + 4, 0x00020000);
-  const int ot0 = 2 * wid;
-  const int vb = (wid * FR_WAVE * FRAG_HALVES + lane * 8) * 2;
-  const float* const scp = wbuf + OFF_SCALE;
-  for (int i = tid; i < 128; i += MLP_THREADS) {
-    sW[SW_B1 + i] = wbuf[OFF_B1 + i];
-    sW[SW_B2 + i] = SCALED ? wbuf[OFF_B2 + i] * scp[1] : wbuf[OFF_B2 + i];
-    sW[SW_B3 + i] = SCALED ? wbuf[OFF_B3 + i] * scp[2] : wbuf[OFF_B3 + i];
-    sW[SW_B4 + i] = SCALED ? wbuf[OFF_B4 + i] * scp[3] : wbuf[OFF_B4 + i];
-    sW[SW_WD + i] = wbuf[OFF_WD + i];
-  }
-  if (SCALED && tid < 6) {
-    sW[SW_SC + tid] = scp[tid];
-    sW[SW_DS + tid] = 1.f / scp[tid];
-  }
-  if (SCALED && tid == 7) sW[SW_HSC] = scp[5] / scp[4];
-  if (tid < 64) sW[SW_BH + tid] = SCALED ? wbuf[OFF_BH + tid] * scp[5] : wbuf[OFF_BH + tid];
-  if (tid < 192) sW[SW_WV2 + tid] = wbuf[OFF_WV2 + tid];
-  if (tid < 3) sW[SW_BV2 + tid] = wbuf[OFF_BV2 + tid];
-  if (tid == 0) sW[SW_BD] = wbuf[OFF_BD];
-  const int nx = (gridDim.x % 8 == 0) ? 8 : 1;
-  const int xcd = blockIdx.x % nx, per_xcd = gridDim.x / nx;
-  const int chunk = (ntiles + nx - 1) / nx;
-  const int t_beg = xcd * chunk, t_end = min(ntiles, t_beg + chunk);
-
-  // index prefetch of tile tl: this lane's gather row (neighbour, sample position, ray) and the 4
-  // rows whose P it loads; validity is recomputed from the tile number where it is needed
-  int pf_nb = 0, pf_ray = 0, pf_pn[4];
-  float4 pf_q = make_float4(0.f, 0.f, 0.f, 0.f);
-  auto fetch = [&](int tl) {
-    const int tc = min(tl, t_end - 1);
-    const int gc = min(tc * TS + (lane >> 3), nS - 1);
-    pf_nb = s_nbr[(size_t)gc * 8 + (lane & 7)];
-    pf_q = s_pos[gc];
-    pf_ray = s_ray[gc];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) pf_pn[mt] = s_nbr[min((size_t)tc * TR + 16 * mt + li, (size_t)nS * 8 - 1)];
-  };
-  auto row_ok = [&](int tl) { return tl < t_end && tl * TS + (lane >> 3) < nS; };
-  int tile = t_beg + blockIdx.x / nx;
-  if (tile >= t_end) return;   // block-uniform
-  h8 a[2][2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int pt = 0; pt < 2; ++pt) a[j][pt] = frag(rs, vb, FR_W1E + j * 4 + pt);
-  f32x4 acc[4][2];
-  PipeG G;
-  PipeS S;
-  // prologue: the first tile's gather, straight through
-  fetch(tile);
-  pipe_load(row_ok(tile) ? pf_nb : -1, pf_ray, pf_q, G, recA, recB, viewdirs, vemb_const, wid);
-  int pn_cur[4];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) pn_cur[mt] = pf_pn[mt];
-  fetch(tile + per_xcd);
-  pipe_piece_a(wid, G, S);
-  pipe_pe_args<3, 6>(wid, S);
-  pipe_piece_c(wid, G, S, PE, sRowB, sVB, vemb_const);
-  int par = 0, prev_s0 = -1;
-  bool range_bad = false;
-  for (; tile < t_end; tile += per_xcd) {
-    const int s0 = tile * TS;
-    float* const sRowC = sRowB + par * (TR * RS);   // this tile's row records / view embedding
-    float* const sVC = sVB + par * (TS * 32);
-    float* const sRowN = sRowB + (par ^ 1) * (TR * RS);   // the next tile's
-    float* const sVN = sVB + (par ^ 1) * (TS * 32);
-    // loads in consumption order: the next tile's indices are older than this tile's P rows (layer 1
-    // waits on those anyway), the next tile's records come last (piece A in layer 2 waits on them)
-    int pn_next[4];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) pn_next[mt] = pf_pn[mt];
-    const int nb_n = row_ok(tile + per_xcd) ? pf_nb : -1, ray_n = pf_ray;
-    const float4 q_n = pf_q;
-    fetch(tile + 2 * per_xcd);
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const float4 v = pproj[(size_t)max(pn_cur[mt], 0) * (FEAT / 4) + 4 * (ot0 + j) + g];
-        acc[mt][j] = f32x4{v.x, v.y, v.z, v.w};
-      }
-    }
-    pipe_load(nb_n, ray_n, q_n, G, recA, recB, viewdirs, vemb_const, wid);
-    if (SCALED) {
-      const float sc1 = sW[SW_SC];
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[mt][j] = acc[mt][j] * sc1;
-    }
-    __syncthreads();
-    if (prev_s0 >= 0 && tid < TS * 3 && prev_s0 + tid / 3 < nS)
-      out[(size_t)prev_s0 * 3 + tid] = *(const float4*)(sOut + 4 * tid);
-    if (tid < TS) {  // IDW weights (temporalpoints.py:473-475) from the rows' to_nn (record entry 8)
-      float w[8], sum = 0.f;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        w[k] = __builtin_amdgcn_rcpf(sRowC[RS * (tid * 8 + k) + 8] + eps);
-        sum += w[k];
-      }
-      const float inv = __builtin_amdgcn_rcpf(sum);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) sIdw[tid * 8 + k] = w[k] * inv;
-    }
-    if (s0 + TS > nS) {   // the last tile only: rows past the last sample loaded P rows of point 0
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          if (s0 + ((16 * mt + li) >> 3) >= nS) acc[mt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    // layer 1 from the PE buffer; afterwards PE is free for the next tile's rows (piece C)
-    layer1_pe(PE, rs, vb, acc, a);
-    __syncthreads();
-    store_act(X0, ot0, sW + SW_B1, acc, SCALED, SCALED ? sW[SW_DS + 0] : 1.f);
-    __syncthreads();
-    init_bias(acc, ot0, sW + SW_B2);
-    pipe_piece_a(wid, G, S);                // the next tile's gather, piece by piece, beside the MFMAs
-    layer_mfma<4, 4, 2, FR_W2, FR_W3, false>(X0, rs, vb, acc, a);
-    __syncthreads();
-    store_act(X0, ot0, nullptr, acc, SCALED, SCALED ? sW[SW_DS + 1] : 1.f);
-    __syncthreads();
-    init_bias(acc, ot0, sW + SW_B3);
-    pipe_pe_args<3, 6>(wid, S);
-    layer_mfma<4, 4, 2, FR_W3, FR_W4, false>(X0, rs, vb, acc, a);
-    __syncthreads();
-    store_act(X0, ot0, nullptr, acc, SCALED, SCALED ? sW[SW_DS + 2] : 1.f);
-    __syncthreads();
-    init_bias(acc, ot0, sW + SW_B4);
-    pipe_piece_c(wid, G, S, PE, sRowN, sVN, vemb_const);
-    layer_mfma<4, 5, 1, FR_W4, FR_WH, false>(X0, rs, vb, acc, a);
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int o0 = 16 * (ot0 + j) + 4 * g;
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-        *(f32x4*)(X0 + out32_off(16 * mt + li, o0 >> 2)) =
-            lrelu4(SCALED ? acc[mt][j] * sW[SW_DS + 3] : acc[mt][j]);
-    }
-    __syncthreads();
-    {   // IDW sum, density head, head input rows (as mlp_tiles)
-      const int s = tid >> 5, oq = tid & 31;
-      f32x4 h = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const f32x4 v = *(const f32x4*)(X0 + out32_off(8 * s + k, oq));
-        const float w = sIdw[8 * s + k];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) h[r] = fmaf(w, v[r], h[r]);
-      }
-      const f32x4 wd = *(const f32x4*)(sW + SW_WD + 4 * oq);
-      float d = ((h[0] * wd[0] + h[1] * wd[1]) + h[2] * wd[2]) + h[3] * wd[3];
-      if (SCALED) h = h * sW[SW_HSC];
-      range_bad |= !(fmaxf(fmaxf(fabsf(h[0]), fabsf(h[1])), fmaxf(fabsf(h[2]), fabsf(h[3]))) <= H3_RANGE);
-      d += __shfl_xor(d, 16, 64);
-      d += __shfl_xor(d, 8, 64);
-      d += __shfl_xor(d, 4, 64);
-      d += __shfl_xor(d, 2, 64);
-      d += __shfl_xor(d, 1, 64);
-      if (oq == 0) {
-        const float e = expf((d + sW[SW_BD]) + shift);
-        sOut[12 * s + 3] = 1.f - __builtin_amdgcn_exp2f(-interval * __builtin_amdgcn_logf(1.f + e));
-      }
-      char* hr = HX + s * HB;
-      h4 hi, lo;
-      split4(h, hi, lo);
-      *(h4*)(hr + 8 * oq) = hi;
-      *(h4*)(hr + HLO + 8 * oq) = lo;
-      const float ve = sVC[s * 32 + oq];
-      const _Float16 vh = (_Float16)ve;
-      *(_Float16*)(hr + 2 * (128 + oq)) = vh;
-      *(_Float16*)(hr + HLO + 2 * (128 + oq)) = (_Float16)(ve - (float)vh);
-    }
-    if (wid == 1) {   // direct blend + weight-vis colour (as mlp_tiles)
-      const int s = lane >> 3, qn = lane & 7;
-      const float* rw = sRowC + 8 * RS * s;
-      float sumd = 0.f;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) sumd += rw[RS * k];
-      const float idn = __builtin_amdgcn_rcpf(sumd + 1e-12f);
-      float acc1 = 0.f;
-      if (qn == 0) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) acc1 += (0.125f * rw[RS * k]) * rw[RS * k + 1];
-      } else if (qn < 4) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) acc1 += (rw[RS * k] * idn) * rw[RS * k + 1 + qn];
-      } else if (qn < 7) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) acc1 += sIdw[8 * s + k] * rw[RS * k + 1 + qn];
-      }
-      const int slot = qn == 0 ? 7 : (qn < 4 ? 3 + qn : (qn < 7 ? 4 + qn : 11));
-      sOut[12 * s + slot] = acc1;
-    }
-    __syncthreads();
-    {   // rgb head (one-deep fragment prefetch, as mlp_tiles)
-      const int o0 = 16 * wid + 4 * g;
-      f32x4 ah = *(const f32x4*)(sW + SW_BH + o0);
-      const char* hr = HX + (li & (TS - 1)) * HB;
-#pragma unroll
-      for (int q = 0; q < KV / 32; ++q) {
-        h8 an[2][2];
-        if (q + 1 < KV / 32) {
-#pragma unroll
-          for (int pt = 0; pt < 2; ++pt) an[0][pt] = frag(rs, vb, FR_WH + (q + 1) * 2 + pt);
-        } else {
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, vb, FR_W1E + j * 4 + pt);
-        }
-        const h8 bh = *(const h8*)(hr + 16 * (4 * q + g));
-        const h8 bl = *(const h8*)(hr + HLO + 16 * (4 * q + g));
-        ah = mfma3(a[0][0], a[0][1], bh, bl, ah);
-        if (q + 1 < KV / 32) {
-          a[0][0] = an[0][0];
-          a[0][1] = an[0][1];
-        } else {
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            a[j][0] = an[j][0];
-            a[j][1] = an[j][1];
-          }
-        }
-      }
-      float pc[3] = {0.f, 0.f, 0.f};
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float v = fmaxf(SCALED ? ah[r] * sW[SW_DS + 5] : ah[r], 0.f);
-#pragma unroll
-        for (int c = 0; c < 3; ++c) pc[c] += v * sW[SW_WV2 + 64 * c + o0 + r];
-      }
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        pc[c] += __shfl_xor(pc[c], 16, 64);
-        pc[c] += __shfl_xor(pc[c], 32, 64);
-      }
-      if (g == 0 && li < TS) {
-#pragma unroll
-        for (int c = 0; c < 3; ++c) sPart[(wid * TS + li) * 4 + c] = pc[c];
-      }
-    }
-    __syncthreads();
-    if (tid < TS * 3) {
-      const int s = tid / 3, c = tid % 3;
-      const float v = ((sPart[(0 * TS + s) * 4 + c] + sPart[(1 * TS + s) * 4 + c]) + sPart[(2 * TS + s) * 4 + c]) +
-                      sPart[(3 * TS + s) * 4 + c];
-      sOut[12 * s + c] = 1.f / (1.f + expf(-(v + sW[SW_BV2 + c])));
-    }
-    prev_s0 = s0;
-    par ^= 1;
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) pn_cur[mt] = pn_next[mt];
-  }
-  __syncthreads();
-  if (prev_s0 >= 0 && tid < TS * 3 && prev_s0 + tid / 3 < nS)
-    out[(size_t)prev_s0 * 3 + tid] = *(const float4*)(sOut + 4 * tid);
-  if (range_bad) __builtin_amdgcn_raw_buffer_store_b32(1, rs, 0, H_TOTAL * 2, 0);
-}
-
-template <bool SCALED>
-__global__ __launch_bounds__(MLP_THREADS, 2) void k_point_mlp_h3p(
-    const float4* __restrict__ s_pos, const int* __restrict__ s_ray, const int* __restrict__ s_nbr,
-    const int* __restrict__ n_samples_dev, const float4* __restrict__ recA, const float4* __restrict__ recB,
-    const float4* __restrict__ pproj, const float* __restrict__ viewdirs, const float* __restrict__ vemb_const,
-    const float* __restrict__ wbuf, float eps, float shift, float interval, float4* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) char Xs[XBUF];
-  __shared__ __attribute__((aligned(16))) char PEs[TR * PEB];
-  __shared__ __attribute__((aligned(16))) char Hs[TS * HB];
-  __shared__ float sIdw[TR];
-  __shared__ float sRowB[2 * TR * RS];
-  __shared__ __attribute__((aligned(16))) float sOut[TS * 12];
-  __shared__ float sVB[2 * TS * 32];
-  __shared__ __attribute__((aligned(16))) float sW[SW_TOTAL];
-  __shared__ float sPart[4 * TS * 4];
-  __shared__ int s_skip;
-  if (threadIdx.x == 0)
-    s_skip = __builtin_nontemporal_load((const int*)(wbuf + OFF_FLAG)) != 0 || (wbuf[OFF_SCALE + 6] != 0.f) != SCALED;
-  __syncthreads();
-  if (s_skip) return;
-  mlp_tiles_pipe<SCALED>(s_pos, s_ray, s_nbr, n_samples_dev, recA, recB, pproj, viewdirs, vemb_const, wbuf, eps,
-                         shift, interval, out, Xs, PEs, Hs, sIdw, sRowB, sOut, sVB, sW, sPart);
-}
-
 // One instantiation per weight-scale mode (separate register allocation); apn_point_mlp launches
 // both and the one that does not match wbuf's mode exits at once (a launch with the range flag
 // already set -- these weights overflowed before -- leaves every sample to the FP32 kernel).
@@ -1518,10 +1080,7 @@ void launch_point_mlp_h3(int blocks, bool timed, hipStream_t stream, const float
   // the scaled-weights instantiation runs on a smaller grid (a rare mode: weight magnitudes outside
   // [2^-5, 2^12]); when it does not match, its 8 workgroups per CU exit at once
   const int nb_scaled = blocks < 256 * 8 ? blocks : 256 * 8;
-  if (occ == 4) {   // software-pipelined build (the gather inside the layers' MFMA phases)
-    go(h3::k_point_mlp_h3p<false>, blocks);
-    go(h3::k_point_mlp_h3p<true>, nb_scaled);
-  } else if (occ == 3) {
+  if (occ == 3) {
     if (timed) { go(h3::k_point_mlp_h3<true, 3, false>, blocks); go(h3::k_point_mlp_h3<true, 3, true>, nb_scaled); }
     else { go(h3::k_point_mlp_h3<false, 3, false>, blocks); go(h3::k_point_mlp_h3<false, 3, true>, nb_scaled); }
   } else {
