@@ -227,15 +227,18 @@ class ShardedFrame(dict):
     of any key checks them (one device read): if a rank overflowed, the frame is rendered again
     on this rank alone, exactly (no collective, so it is safe whichever ranks read the frame)."""
 
-    def __init__(self, *a, infos=None, rerender=None, **kw):
+    def __init__(self, *a, infos=None, rerender=None, on_infos=None, **kw):
         super().__init__(*a, **kw)
         self._infos = infos
         self._rerender = rerender
+        self._on_infos = on_infos
 
     def _resolve(self):
         if self._infos is None:
             return
         infos, self._infos = self._infos, None
+        if self._on_infos is not None:
+            self._on_infos(infos)
         if bool((infos[:, 2] != 0).any()):
             fresh = self._rerender(infos)
             dict.update(self, fresh)
@@ -348,6 +351,7 @@ def _assemble(model, t, out, render_kwargs, rank, world, group, blocks, block, f
         from .temporalpoints import _grow_capacity
         key = (R, rank, world, block) if blocks else (R, rank, world)
         model._capacity[key] = max(model._capacity.get(key, 0), _grow_capacity(int(infos[rank, 1])))
+        model.sharded_rerenders = getattr(model, "sharded_rerenders", 0) + 1
         model._force_exact = True
         try:
             # the frame may be read after render_sharded's no_grad scope has exited: the re-render
@@ -358,4 +362,12 @@ def _assemble(model, t, out, render_kwargs, rank, world, group, blocks, block, f
             return {k: whole.get(k) for k, _ in TILE_KEYS} | {k: whole.get(k) for k in ("t_hat_pcd", "joints", "bones")}
         finally:
             model._force_exact = False
-    return ShardedFrame(res, infos=infos, rerender=rerender)
+    on_infos = None
+    if not blocks and world > 1:
+        def on_infos(infos):
+            # the ranges split follows the survivors once the cost split starts, so a rank's in-bbox
+            # share moves between frames: size every rank for the largest share any rank had
+            from .temporalpoints import _grow_capacity
+            key = (R, rank, world)
+            model._capacity[key] = max(model._capacity.get(key, 0), _grow_capacity(int(infos[:, 1].max())))
+    return ShardedFrame(res, infos=infos, rerender=rerender, on_infos=on_infos)

@@ -526,6 +526,7 @@ def main():
         per_rank = [None] * world
         torch.distributed.all_gather_object(per_rank, mine)
         shard_diag = {"per_rank": per_rank, "allgather_ms_max": max(p["allgather_ms"] for p in per_rank),
+                      "rerenders": getattr(model, "sharded_rerenders", 0),
                       "note": "stage_ms from HIP events on eager shard frames; allgather_ms = one gather_blocks "
                               "(the frame's tile all-gather) alone, mean of 10; replicated_ms = lbs + bbox + grid, "
                               "the per-frame stages every rank runs on the whole cloud"}

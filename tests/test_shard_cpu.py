@@ -242,3 +242,18 @@ def test_sharded_frame_every_read_validates(read):
                "pop": lambda: {"rgb_marched": f.pop("rgb_marched")}, "items": lambda: dict(f.items())}[read]()
     assert calls == [[0, 1]]   # exactly one re-render, on the first read
     assert torch.equal(got["rgb_marched"], torch.ones(4, 3))
+
+
+def test_sharded_frame_reports_every_ranks_info_once():
+    """The ranges split sizes each rank's sample capacity from the largest in-bbox share any rank
+    had (the cost split moves shares between frames): ShardedFrame hands the gathered
+    frame_infos to on_infos exactly once, on the first read, whether or not a rank overflowed."""
+    from apn_amd.shard import ShardedFrame
+    seen = []
+    f = ShardedFrame({"depth": torch.zeros(4)}, infos=torch.tensor([[10, 7, 0, 5], [10, 9, 0, 5]], dtype=torch.int32),
+                     rerender=lambda infos: pytest.fail("no rank overflowed"),
+                     on_infos=lambda infos: seen.append(int(infos[:, 1].max())))
+    assert seen == []
+    _ = f["depth"]
+    _ = dict(f)
+    assert seen == [9]
