@@ -160,6 +160,17 @@ __device__ __forceinline__ void knn_insert(float d, int id, float (&bd)[K], int 
   }
 }
 
+// Culling radii of the ball scans: v_sqrt_f32 (about 1 ulp) instead of the correctly rounded
+// sqrtf sequence (~14 instructions: denormal scaling, two correction fmas). Every use is a bound
+// with 1e-4 relative slack (plus 1e-12 absolute for denormal arguments), so the rows and cells a
+// scan visits still cover the ball exactly as before. (APN_KNN_IEEE_SQRT: the library sqrtf.)
+__device__ __forceinline__ float bound_sqrt(float x) {
+#ifdef APN_KNN_IEEE_SQRT
+  return sqrtf(x) * 1.0001f;
+#else
+  return __builtin_amdgcn_sqrtf(x) * 1.0001f + 1e-12f;
+#endif
+}
 #ifdef APN_KNN_DUPCHECK_ALL   // A/B: the duplicate check on every insert (the round-2 kernels)
 constexpr bool kFirstScanNoDup = false;
 #else
@@ -975,7 +986,7 @@ template <int K, bool STATS, int S, bool DUP, class L>
 __device__ __forceinline__ void scan_ball_flat2_l(const GridParams& g, const int* __restrict__ cell_start,
                                                   const float4* __restrict__ sorted, float qx, float qy, float qz,
                                                   float R2, L& lst, unsigned* ctr = nullptr, int slice = 0) {
-  const float R = sqrtf(R2) * 1.0001f;
+  const float R = bound_sqrt(R2);
   const int z0 = max((int)floorf((qz - R - g.oz) * g.inv_h), 0), z1 = min((int)floorf((qz + R - g.oz) * g.inv_h), g.dz - 1);
   const int y0 = max((int)floorf((qy - R - g.oy) * g.inv_h), 0), y1 = min((int)floorf((qy + R - g.oy) * g.inv_h), g.dy - 1);
   const int fz = min(max((int)floorf((qz - g.oz) * g.inv_h), z0), z1);
@@ -1021,7 +1032,7 @@ __device__ __forceinline__ void scan_ball_flat2_l(const GridParams& g, const int
           if (z >= z0 && z <= z1) {
             dz2 = slab_d2(qz, g.oz, g.h, z, z);
             if (dz2 <= tau) {
-              const int my = (int)floorf(sqrtf(tau - dz2) * g.inv_h * 1.0001f) + 1;
+              const int my = (int)floorf(bound_sqrt(tau - dz2) * g.inv_h) + 1;
               nyz = min(2 * my + 1, ny);
             }
           }
@@ -1032,7 +1043,7 @@ __device__ __forceinline__ void scan_ball_flat2_l(const GridParams& g, const int
         if (y >= y0 && y <= y1) {
           const float dyz2 = dz2 + slab_d2(qy, g.oy, g.h, y, y);
           if (dyz2 <= tau) {
-            const float w = sqrtf(tau - dyz2) * 1.0001f;
+            const float w = bound_sqrt(tau - dyz2);
             const int x0 = max((int)floorf((qx - w - g.ox) * g.inv_h), 0);
             const int x1 = min((int)floorf((qx + w - g.ox) * g.inv_h), g.dx - 1);
             if (x0 <= x1) {
@@ -1116,7 +1127,7 @@ template <int K, bool STATS, int PTS, bool DUP, class L>
 __device__ __forceinline__ void scan_ball_aniso_l(const AGrid& g, const int* __restrict__ cell_start,
                                                   const float4* __restrict__ sorted, float qx, float qy, float qz,
                                                   float R2, L& lst, unsigned* ctr = nullptr) {
-  const float R = sqrtf(R2) * 1.0001f;
+  const float R = bound_sqrt(R2);
   const int z0 = max((int)floorf((qz - R - g.oz) * g.ihz), 0), z1 = min((int)floorf((qz + R - g.oz) * g.ihz), g.dz - 1);
   const int y0 = max((int)floorf((qy - R - g.oy) * g.ihy), 0), y1 = min((int)floorf((qy + R - g.oy) * g.ihy), g.dy - 1);
   const int fz = min(max((int)floorf((qz - g.oz) * g.ihz), z0), z1);
@@ -1163,7 +1174,7 @@ __device__ __forceinline__ void scan_ball_aniso_l(const AGrid& g, const int* __r
           if (z >= z0 && z <= z1) {
             dz2 = slab_d2(qz, g.oz, g.hz, z, z);
             if (dz2 <= tau) {
-              const int my = (int)floorf(sqrtf(tau - dz2) * g.ihy * 1.0001f) + 1;
+              const int my = (int)floorf(bound_sqrt(tau - dz2) * g.ihy) + 1;
               nyz = min(2 * my + 1, ny);
             }
           }
@@ -1174,7 +1185,7 @@ __device__ __forceinline__ void scan_ball_aniso_l(const AGrid& g, const int* __r
         if (y >= y0 && y <= y1) {
           const float dyz2 = dz2 + slab_d2(qy, g.oy, g.hy, y, y);
           if (dyz2 <= tau) {
-            const float w = sqrtf(tau - dyz2) * 1.0001f;
+            const float w = bound_sqrt(tau - dyz2);
             const int x0 = max((int)floorf((qx - w - g.ox) * g.ihx), 0);
             const int x1 = min((int)floorf((qx + w - g.ox) * g.ihx), g.dx - 1);
             if (x0 <= x1) {
