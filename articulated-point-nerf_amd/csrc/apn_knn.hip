@@ -1251,7 +1251,7 @@ __global__ __launch_bounds__(KNN_THREADS) void k_cell_bound(const GridParams* __
       const float gy = (float)max(abs(dy) - 1, 0);
       const float rem = lim - gz * gz - gy * gy;
       if (y < 0 || y >= g.dy || rem < 0.f) continue;
-      const int kx = (int)floorf(sqrtf(rem)) + 1;
+      const int kx = (int)floorf(__builtin_amdgcn_sqrtf(rem)) + 1;
       const int row = (z * g.dy + y) * g.dx;
       u += cell_start[row + min(cx + kx, g.dx - 1) + 1] - cell_start[row + max(cx - kx, 0)];
     }
@@ -1271,7 +1271,10 @@ __global__ __launch_bounds__(KNN_THREADS) void k_cell_bound3(const GridParams* _
   const GridParams g = *gp;
   const int cell = list[i];
   const int cx = cell % g.dx, cy = (cell / g.dx) % g.dy, cz = cell / (g.dx * g.dy);
-  const float lim = g.r2 * 1.0002f * g.inv_h * g.inv_h;   // (r/h)^2 with slack
+  // (r/h)^2 with slack. The row half-widths below take v_sqrt_f32 (~1 ulp): the 2e-4 slack on lim
+  // moves sqrt(rem) by >= 8e-4 cells (rem <= 64), so floor(sqrt(rem)) never drops below the exact
+  // bound's (as in the ball scans' bound_sqrt)
+  const float lim = g.r2 * 1.0002f * g.inv_h * g.inv_h;
   const int K = (int)ceilf(sqrtf(lim)) + 1;
   int a1 = 0, a2 = 0, a4 = 0;
   for (int dz = -K; dz <= K; ++dz) {
@@ -1284,15 +1287,15 @@ __global__ __launch_bounds__(KNN_THREADS) void k_cell_bound3(const GridParams* _
       const float rem = lim - gz * gz - gy * gy;
       if (y < 0 || y >= g.dy || rem < 0.f) continue;
       const int row = (z * g.dy + y) * g.dx;
-      const int kx = (int)floorf(sqrtf(rem)) + 1;
+      const int kx = (int)floorf(__builtin_amdgcn_sqrtf(rem)) + 1;
       a1 += cell_start[row + min(cx + kx, g.dx - 1) + 1] - cell_start[row + max(cx - kx, 0)];
       const float rem2 = 0.25f * lim - gz * gz - gy * gy;
       if (rem2 >= 0.f) {
-        const int k2 = (int)floorf(sqrtf(rem2)) + 1;
+        const int k2 = (int)floorf(__builtin_amdgcn_sqrtf(rem2)) + 1;
         a2 += cell_start[row + min(cx + k2, g.dx - 1) + 1] - cell_start[row + max(cx - k2, 0)];
         const float rem4 = 0.0625f * lim - gz * gz - gy * gy;
         if (rem4 >= 0.f) {
-          const int k4 = (int)floorf(sqrtf(rem4)) + 1;
+          const int k4 = (int)floorf(__builtin_amdgcn_sqrtf(rem4)) + 1;
           a4 += cell_start[row + min(cx + k4, g.dx - 1) + 1] - cell_start[row + max(cx - k4, 0)];
         }
       }
@@ -1336,15 +1339,15 @@ __global__ __launch_bounds__(KNN_THREADS) void k_cell_bound3w(const GridParams* 
         const float rem = lim - gz * gz - gy * gy;
         if (rem < 0.f) continue;
         const int row = (z * g.dy + y) * g.dx;
-        const int kx = (int)floorf(sqrtf(rem)) + 1;
+        const int kx = (int)floorf(__builtin_amdgcn_sqrtf(rem)) + 1;
         a1 += cell_start[row + min(cx + kx, g.dx - 1) + 1] - cell_start[row + max(cx - kx, 0)];
         const float rem2 = 0.25f * lim - gz * gz - gy * gy;
         if (rem2 >= 0.f) {
-          const int k2 = (int)floorf(sqrtf(rem2)) + 1;
+          const int k2 = (int)floorf(__builtin_amdgcn_sqrtf(rem2)) + 1;
           a2 += cell_start[row + min(cx + k2, g.dx - 1) + 1] - cell_start[row + max(cx - k2, 0)];
           const float rem4 = 0.0625f * lim - gz * gz - gy * gy;
           if (rem4 >= 0.f) {
-            const int k4 = (int)floorf(sqrtf(rem4)) + 1;
+            const int k4 = (int)floorf(__builtin_amdgcn_sqrtf(rem4)) + 1;
             a4 += cell_start[row + min(cx + k4, g.dx - 1) + 1] - cell_start[row + max(cx - k4, 0)];
           }
         }
