@@ -333,6 +333,11 @@ struct KeyList {
     bool m[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) m[k] = x < kk[k];   // monotone: false..false true..true
+#ifndef APN_KNN_INTERLEAVED_INSERT
+    // all compares first, each into its own SGPR pair, then the selects: interleaved, every select
+    // pair waited out the VALU-SGPR-write -> mask-read hazard of the compare just before it (s_nop)
+    __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
     for (int k = K - 1; k > 0; --k) kk[k] = m[k] ? (m[k - 1] ? kk[k - 1] : x) : kk[k];
     kk[0] = m[0] ? x : kk[0];
