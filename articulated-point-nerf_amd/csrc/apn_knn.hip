@@ -339,7 +339,7 @@ struct KeyList {
     __builtin_amdgcn_sched_barrier(0);
 #endif
 #pragma unroll
-    for (int k = K - 1; k > 0; --k) kk[k] = m[k] ? (m[k - 1] ? kk[k - 1] : x) : kk[k];
+    for (int k = K - 1; k > 0; --k) kk[k] = m[k - 1] ? kk[k - 1] : (m[k] ? x : kk[k]);   // (m[k-1] implies m[k])
     kk[0] = m[0] ? x : kk[0];
   }
 };
