@@ -171,6 +171,11 @@ __device__ __forceinline__ float bound_sqrt(float x) {
   return __builtin_amdgcn_sqrtf(x) * 1.0001f + 1e-12f;
 #endif
 }
+#ifdef APN_KNN_GLOBAL_POINTS   // A/B: pass B's point loads as clamped 64-bit global loads
+constexpr bool kBufferPoints = false;
+#else
+constexpr bool kBufferPoints = true;
+#endif
 #ifdef APN_KNN_DUPCHECK_ALL   // A/B: the duplicate check on every insert (the round-2 kernels)
 constexpr bool kFirstScanNoDup = false;
 #else
@@ -1084,18 +1089,19 @@ __device__ __forceinline__ void scan_ball_flat2(const GridParams& g, const int* 
 struct AGrid {
   float ox, oy, oz, hx;
   float hy, hz, ihx, ihy;
-  float ihz, r, r2, pad0;
+  float ihz, r, r2;
+  int np;   // points in sorted2 (the buffer bound of the scans' point loads)
   int dx, dy, dz, nf;
 };
 
-__global__ void k_agrid_params(const GridParams* __restrict__ gp, int f, AGrid* __restrict__ ag) {
+__global__ void k_agrid_params(const GridParams* __restrict__ gp, int f, int np, AGrid* __restrict__ ag) {
   if (threadIdx.x != 0) return;
   const GridParams g = *gp;
   AGrid a;
   a.ox = g.ox; a.oy = g.oy; a.oz = g.oz;
   a.hx = g.h; a.hy = a.hz = g.h * (float)f;
   a.ihx = g.inv_h; a.ihy = a.ihz = g.inv_h / (float)f;
-  a.r = g.r; a.r2 = g.r2; a.pad0 = 0.f;
+  a.r = g.r; a.r2 = g.r2; a.np = np;
   a.dx = g.dx; a.dy = (g.dy + f - 1) / f; a.dz = (g.dz + f - 1) / f;
   a.nf = a.dx * a.dy * a.dz;
   *ag = a;
@@ -1133,6 +1139,7 @@ __device__ __forceinline__ void scan_ball_aniso_l(const AGrid& g, const int* __r
                                                   const float4* __restrict__ sorted, float qx, float qy, float qz,
                                                   float R2, L& lst, unsigned* ctr = nullptr) {
   const float R = bound_sqrt(R2);
+  const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc((void*)sorted, 0, g.np * 16, 0x00020000);
   const int z0 = max((int)floorf((qz - R - g.oz) * g.ihz), 0), z1 = min((int)floorf((qz + R - g.oz) * g.ihz), g.dz - 1);
   const int y0 = max((int)floorf((qy - R - g.oy) * g.ihy), 0), y1 = min((int)floorf((qy + R - g.oy) * g.ihy), g.dy - 1);
   const int fz = min(max((int)floorf((qz - g.oz) * g.ihz), z0), z1);
@@ -1154,7 +1161,15 @@ __device__ __forceinline__ void scan_ball_aniso_l(const AGrid& g, const int* __r
       int id[PTS];
 #pragma unroll
       for (int u = 0; u < PTS; ++u) {
-        P[u] = sorted[min(b + u, e - 1)];
+        if constexpr (kBufferPoints) {
+          // 32-bit offsets through a buffer descriptor (no 64-bit address arithmetic); slots past
+          // the row read the next cells' points or, past the array, zeros -- b + u < e masks them
+          typedef float f4v __attribute__((ext_vector_type(4)));
+          const f4v v = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(prs, (b + u) * 16, 0, 0));
+          P[u] = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+          P[u] = sorted[min(b + u, e - 1)];
+        }
         id[u] = __float_as_int(P[u].w);
       }
 #pragma unroll
@@ -2125,7 +2140,7 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
         return (v == 1 || v == 2 || v == 4) ? v : 2;
       }();
       APN_TRY(fill4_i32(g.counts2, cell_cap, g.cursor2, cell_cap, nullptr, 0, nullptr, 0, s));
-      hipLaunchKernelGGL(k_agrid_params, dim3(1), dim3(64), 0, s, g.gp, f, g.ag);
+      hipLaunchKernelGGL(k_agrid_params, dim3(1), dim3(64), 0, s, g.gp, f, (int)n_points, g.ag);
       hipLaunchKernelGGL(k_agrid_count, dim3(ceil_div(n_points, 256)), dim3(256), 0, s, (const float4*)sorted_pts4,
                          n_points, g.gp, f, g.counts2, g.pcell2);
       st = scan_exclusive_i32(g.counts2, g.cell_start2, cell_cap, g.scan, s);
