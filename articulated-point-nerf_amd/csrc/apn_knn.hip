@@ -28,7 +28,7 @@ struct GridParams {
   float inv_h, r, r2, pad0;   // search radius r = sqrt(query_radius), r2 = query_radius
   int dx, dy, dz, nf;         // fine grid dims and cell count
   int cf, cdx, cdy, cdz;      // fine cells per coarse cell (coarse side >= r), coarse dims
-  int nc, kmax, pad1, pad2;   // coarse cell count, search limit (kmax * h >= r)
+  int nc, kmax, np, pad2;     // coarse cell count, search limit (kmax * h >= r), points in sorted
 };
 
 constexpr int KNN_K = 8;
@@ -39,7 +39,7 @@ constexpr int KNN_SUBDIV = 8;   // fine cell side = r / KNN_SUBDIV (before the c
 
 __device__ __forceinline__ int floor_div(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
 
-__global__ void k_grid_params(const int* __restrict__ bbox_ord, float qr, int cap, int subdiv,
+__global__ void k_grid_params(const int* __restrict__ bbox_ord, float qr, int cap, int subdiv, int np,
                               GridParams* __restrict__ gp) {
   if (threadIdx.x != 0) return;
   float lo[3], hi[3];
@@ -68,7 +68,8 @@ __global__ void k_grid_params(const int* __restrict__ bbox_ord, float qr, int ca
   g.cdx = (d[0] + g.cf - 1) / g.cf; g.cdy = (d[1] + g.cf - 1) / g.cf; g.cdz = (d[2] + g.cf - 1) / g.cf;
   g.nc = g.cdx * g.cdy * g.cdz;
   g.kmax = g.cf;
-  g.pad1 = g.pad2 = 0;
+  g.np = np;
+  g.pad2 = 0;
   *gp = g;
 }
 
@@ -176,6 +177,19 @@ constexpr bool kBufferPoints = false;
 #else
 constexpr bool kBufferPoints = true;
 #endif
+// Buffer-descriptor loads for the ball scans: 32-bit byte offsets (no 64-bit address arithmetic per
+// load); reads past num_records return zeros.
+typedef float knn_f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t knn_rsrc(const void* p, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, bytes, 0x00020000);
+}
+__device__ __forceinline__ float4 knn_ld_pt(__amdgpu_buffer_rsrc_t rs, int i) {
+  const knn_f4v v = __builtin_bit_cast(knn_f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, i * 16, 0, 0));
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+__device__ __forceinline__ int knn_ld_i32(__amdgpu_buffer_rsrc_t rs, int i) {
+  return (int)__builtin_amdgcn_raw_buffer_load_b32(rs, i * 4, 0, 0);
+}
 #ifdef APN_KNN_DUPCHECK_ALL   // A/B: the duplicate check on every insert (the round-2 kernels)
 constexpr bool kFirstScanNoDup = false;
 #else
@@ -997,6 +1011,8 @@ __device__ __forceinline__ void scan_ball_flat2_l(const GridParams& g, const int
                                                   const float4* __restrict__ sorted, float qx, float qy, float qz,
                                                   float R2, L& lst, unsigned* ctr = nullptr, int slice = 0) {
   const float R = bound_sqrt(R2);
+  const __amdgpu_buffer_rsrc_t prs = knn_rsrc(sorted, g.np * 16);
+  const __amdgpu_buffer_rsrc_t crs = knn_rsrc(cell_start, (g.nf + 1) * 4);
   const int z0 = max((int)floorf((qz - R - g.oz) * g.inv_h), 0), z1 = min((int)floorf((qz + R - g.oz) * g.inv_h), g.dz - 1);
   const int y0 = max((int)floorf((qy - R - g.oy) * g.inv_h), 0), y1 = min((int)floorf((qy + R - g.oy) * g.inv_h), g.dy - 1);
   const int fz = min(max((int)floorf((qz - g.oz) * g.inv_h), z0), z1);
@@ -1016,7 +1032,8 @@ __device__ __forceinline__ void scan_ball_flat2_l(const GridParams& g, const int
     if (STATS) ctr[has_pts ? 1 : 0]++;
     if (has_pts) {
       const int p1 = b + 1 < e ? b + 1 : b;
-      const float4 P0 = sorted[b], P1 = sorted[p1];
+      const float4 P0 = kBufferPoints ? knn_ld_pt(prs, b) : sorted[b];
+      const float4 P1 = kBufferPoints ? knn_ld_pt(prs, b + 1) : sorted[p1];
       // the indices pass through an empty asm so they are loaded with the coordinates (one
       // 16-B load per point) instead of by a separate load inside the insert branch, whose
       // vmcnt(0) would also drain the row-bound loads in flight
@@ -1058,8 +1075,8 @@ __device__ __forceinline__ void scan_ball_flat2_l(const GridParams& g, const int
             const int x1 = min((int)floorf((qx + w - g.ox) * g.inv_h), g.dx - 1);
             if (x0 <= x1) {
               const int row = (z * g.dy + y) * g.dx;
-              pb = cell_start[row + x0];
-              pe = cell_start[row + x1 + 1];
+              pb = kBufferPoints ? knn_ld_i32(crs, row + x0) : cell_start[row + x0];
+              pe = kBufferPoints ? knn_ld_i32(crs, row + x1 + 1) : cell_start[row + x1 + 1];
               pend = true;
             }
           }
@@ -1139,7 +1156,8 @@ __device__ __forceinline__ void scan_ball_aniso_l(const AGrid& g, const int* __r
                                                   const float4* __restrict__ sorted, float qx, float qy, float qz,
                                                   float R2, L& lst, unsigned* ctr = nullptr) {
   const float R = bound_sqrt(R2);
-  const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc((void*)sorted, 0, g.np * 16, 0x00020000);
+  const __amdgpu_buffer_rsrc_t prs = knn_rsrc(sorted, g.np * 16);
+  const __amdgpu_buffer_rsrc_t crs = knn_rsrc(cell_start, (g.nf + 1) * 4);
   const int z0 = max((int)floorf((qz - R - g.oz) * g.ihz), 0), z1 = min((int)floorf((qz + R - g.oz) * g.ihz), g.dz - 1);
   const int y0 = max((int)floorf((qy - R - g.oy) * g.ihy), 0), y1 = min((int)floorf((qy + R - g.oy) * g.ihy), g.dy - 1);
   const int fz = min(max((int)floorf((qz - g.oz) * g.ihz), z0), z1);
@@ -1162,11 +1180,8 @@ __device__ __forceinline__ void scan_ball_aniso_l(const AGrid& g, const int* __r
 #pragma unroll
       for (int u = 0; u < PTS; ++u) {
         if constexpr (kBufferPoints) {
-          // 32-bit offsets through a buffer descriptor (no 64-bit address arithmetic); slots past
-          // the row read the next cells' points or, past the array, zeros -- b + u < e masks them
-          typedef float f4v __attribute__((ext_vector_type(4)));
-          const f4v v = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(prs, (b + u) * 16, 0, 0));
-          P[u] = make_float4(v[0], v[1], v[2], v[3]);
+          // slots past the row read the next cells' points or, past the array, zeros -- b + u < e masks them
+          P[u] = knn_ld_pt(prs, b + u);
         } else {
           P[u] = sorted[min(b + u, e - 1)];
         }
@@ -1210,8 +1225,8 @@ __device__ __forceinline__ void scan_ball_aniso_l(const AGrid& g, const int* __r
             const int x1 = min((int)floorf((qx + w - g.ox) * g.ihx), g.dx - 1);
             if (x0 <= x1) {
               const int row = (z * g.dy + y) * g.dx;
-              pb = cell_start[row + x0];
-              pe = cell_start[row + x1 + 1];
+              pb = kBufferPoints ? knn_ld_i32(crs, row + x0) : cell_start[row + x0];
+              pe = kBufferPoints ? knn_ld_i32(crs, row + x1 + 1) : cell_start[row + x1 + 1];
               pend = true;
             }
           }
@@ -2065,7 +2080,8 @@ extern "C" int apn_grid_build(const float* xyz, int64_t n_points, const int32_t*
     const char* e = getenv("APN_KNN_SUBDIV");
     return e ? atoi(e) : KNN_SUBDIV;
   }();
-  hipLaunchKernelGGL(k_grid_params, dim3(1), dim3(64), 0, s, bbox_ord, query_radius, cell_cap, subdiv, w.gp);
+  hipLaunchKernelGGL(k_grid_params, dim3(1), dim3(64), 0, s, bbox_ord, query_radius, cell_cap, subdiv,
+                     (int)n_points, w.gp);
   hipLaunchKernelGGL(k_grid_count, dim3(ceil_div(n_points, 256)), dim3(256), 0, s, xyz, n_points, w.gp, w.counts,
                      w.ccount, w.pcell);
   int st = scan_exclusive_i32(w.counts, w.cell_start, cell_cap, w.scan, s);
