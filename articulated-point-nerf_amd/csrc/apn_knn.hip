@@ -1469,6 +1469,21 @@ __global__ __launch_bounds__(ORDER_THREADS) void k_order_blocks(const int* __res
   }
 }
 
+#ifndef APN_KNN_A_PTS
+#define APN_KNN_A_PTS 4
+#endif
+// points per step of pass A's fine-grid r/4 scan: 0 = scan_ball_flat2_l (2 points), 2 / 4 = the
+// fine grid seen as an isotropic AGrid through scan_ball_aniso_l<PTS>
+constexpr int kAPts = APN_KNN_A_PTS;
+__device__ __forceinline__ AGrid agrid_of(const GridParams& g) {
+  AGrid a;
+  a.ox = g.ox; a.oy = g.oy; a.oz = g.oz;
+  a.hx = a.hy = a.hz = g.h;
+  a.ihx = a.ihy = a.ihz = g.inv_h;
+  a.r = g.r; a.r2 = g.r2; a.np = g.np;
+  a.dx = g.dx; a.dy = g.dy; a.dz = g.dz; a.nf = g.nf;
+  return a;
+}
 #ifdef APN_KNN_NO_ASORT   // A/B: pass A lanes in candidate order
 constexpr bool kSortA = false;
 #else
@@ -1533,6 +1548,8 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_a8(
         lst.init();
         const float R2 = coarse ? g.r2 : 0.0625f * g.r2;
         if (ANISO) scan_ball_aniso_l<KNN_K, false, 2, !kFirstScanNoDup>(*agp, cell_start2, sorted2, q.x, q.y, q.z, R2, lst);
+        else if constexpr (kAPts > 0)
+          scan_ball_aniso_l<KNN_K, false, kAPts, !kFirstScanNoDup>(agrid_of(g), cell_start, sorted, q.x, q.y, q.z, R2, lst);
         else scan_ball_flat2_l<KNN_K, false, 1, !kFirstScanNoDup>(g, cell_start, sorted, q.x, q.y, q.z, R2, lst);
         if (R2 == g.r2 || lst.worst() < R2 * (1.f - 2e-4f)) {
           surv = lst.worst() <= g.r2;
