@@ -1311,6 +1311,12 @@ __global__ __launch_bounds__(KNN_THREADS) void k_cell_bound3(const GridParams* _
   // bound's (as in the ball scans' bound_sqrt)
   const float lim = g.r2 * 1.0002f * g.inv_h * g.inv_h;
   const int K = (int)ceilf(sqrtf(lim)) + 1;
+  const __amdgpu_buffer_rsrc_t crs = knn_rsrc(cell_start, (g.nf + 1) * 4);
+#ifdef APN_KNN_CB_GLOBAL   // A/B: the row bounds as global loads
+  auto CS = [&](int x) { return cell_start[x]; };
+#else
+  auto CS = [&](int x) { return kBufferPoints ? knn_ld_i32(crs, x) : cell_start[x]; };
+#endif
   int a1 = 0, a2 = 0, a4 = 0;
   for (int dz = -K; dz <= K; ++dz) {
     const int z = cz + dz;
@@ -1323,15 +1329,15 @@ __global__ __launch_bounds__(KNN_THREADS) void k_cell_bound3(const GridParams* _
       if (y < 0 || y >= g.dy || rem < 0.f) continue;
       const int row = (z * g.dy + y) * g.dx;
       const int kx = (int)floorf(__builtin_amdgcn_sqrtf(rem)) + 1;
-      a1 += cell_start[row + min(cx + kx, g.dx - 1) + 1] - cell_start[row + max(cx - kx, 0)];
+      a1 += CS(row + min(cx + kx, g.dx - 1) + 1) - CS(row + max(cx - kx, 0));
       const float rem2 = 0.25f * lim - gz * gz - gy * gy;
       if (rem2 >= 0.f) {
         const int k2 = (int)floorf(__builtin_amdgcn_sqrtf(rem2)) + 1;
-        a2 += cell_start[row + min(cx + k2, g.dx - 1) + 1] - cell_start[row + max(cx - k2, 0)];
+        a2 += CS(row + min(cx + k2, g.dx - 1) + 1) - CS(row + max(cx - k2, 0));
         const float rem4 = 0.0625f * lim - gz * gz - gy * gy;
         if (rem4 >= 0.f) {
           const int k4 = (int)floorf(__builtin_amdgcn_sqrtf(rem4)) + 1;
-          a4 += cell_start[row + min(cx + k4, g.dx - 1) + 1] - cell_start[row + max(cx - k4, 0)];
+          a4 += CS(row + min(cx + k4, g.dx - 1) + 1) - CS(row + max(cx - k4, 0));
         }
       }
     }
