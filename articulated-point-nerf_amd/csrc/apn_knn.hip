@@ -1475,6 +1475,13 @@ __global__ __launch_bounds__(ORDER_THREADS) void k_order_blocks(const int* __res
   }
 }
 
+// Pass B held to 64 VGPRs, 8 waves per SIMD (68 -> 64, 5 VGPRs spilled outside the point loop):
+// 1365 -> 1345 us at C2. Pass A the same way ran 566 -> 616 us, so it keeps its 70 (7 waves).
+#ifdef APN_KNN_B_W7   // A/B: pass B at the compiler's 68 VGPRs
+#define APN_KNN_PASS_B_ATTR
+#else
+#define APN_KNN_PASS_B_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))
+#endif
 #ifndef APN_KNN_A_PTS
 #define APN_KNN_A_PTS 4
 #endif
@@ -1911,7 +1918,7 @@ constexpr bool kSortB = true;
 // and fewer lanes idle while the wave's longest scan runs (the lanes still cover the same 256
 // consecutive list entries: the workgroup's spatial locality is kept).
 template <bool STATS, int PTS>
-__global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_b9(
+__global__ __launch_bounds__(KNN_THREADS) APN_KNN_PASS_B_ATTR void k_knn_pass_b9(
     const float4* __restrict__ q_pos, const int* __restrict__ cand, const int* __restrict__ hard,
     const int* __restrict__ n_hard, const int* __restrict__ hard2, const int* __restrict__ n_hard2,
     const AGrid* __restrict__ agp, const int* __restrict__ cell_start2, const float4* __restrict__ sorted2,
