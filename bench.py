@@ -15,6 +15,13 @@ has every rank render its own frame instead (weak scaling, no data-path collecti
 barrier + synchronize bracketed and the max over ranks (all-reduce MAX of the elapsed time).
 
 Rank 0 prints ONE JSON line. Diagnostics go to stderr.
+
+Launch: ``python bench.py --gpus N`` with N > 1 and no WORLD_SIZE in the environment starts the N
+ranks itself (``spawn_ranks``: N child processes of this script, one per GPU, RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set) before anything touches the GPU -- the
+replacement for the reference's sequential chunk loop (run.py:136-151) is then N processes, not
+one. Under an outer launcher (torch.distributed.run) ``--gpus`` must equal WORLD_SIZE, or the run
+aborts (``check_world``).
 """
 from __future__ import annotations
 
@@ -22,12 +29,93 @@ import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
-import torch
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
+
+
+# ----------------------------------------------------------------------------- launcher (stdlib only;
+# runs before torch is imported, so the parent never initialises the GPU)
+def gpus_arg(argv):
+    """The value of --gpus in argv (None when absent)."""
+    for i, a in enumerate(argv):
+        if a == "--gpus" and i + 1 < len(argv):
+            return int(argv[i + 1])
+        if a.startswith("--gpus="):
+            return int(a.split("=", 1)[1])
+    return None
+
+
+def check_world(gpus, env):
+    """World size of this process: WORLD_SIZE from an outer launcher, else 1. --gpus, when given,
+    must match it (a mismatch would time fewer processes than the line claims)."""
+    world = int(env.get("WORLD_SIZE", "1"))
+    if gpus is not None and gpus != world:
+        raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}; launch with --gpus {world} "
+                         f"(or without an outer launcher, where bench.py starts the ranks itself)")
+    return world
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_envs(n, port, base_env):
+    """One environment per rank for a single-node launch of n ranks (one process per GPU)."""
+    envs = []
+    for r in range(n):
+        e = dict(base_env)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        envs.append(e)
+    return envs
+
+
+def spawn_ranks(n, cmd, base_env=None, poll_s=0.2):
+    """Start n child processes of ``cmd`` (rank environments from rank_envs), forward their output
+    (only rank 0 prints the JSON line; the children inherit stdout / stderr), wait for all of them.
+    If any child fails, the others are terminated (they would wait forever in a collective) and the
+    first failing exit code is returned; 0 when every rank succeeded."""
+    env = dict(os.environ if base_env is None else base_env)
+    procs = [subprocess.Popen(cmd, env=e) for e in rank_envs(n, free_port(), env)]
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                break
+            if all(c == 0 for c in codes):
+                break
+            time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    if rc:
+        print(f"bench.py: a rank failed with exit code {rc}; the other ranks were stopped", file=sys.stderr, flush=True)
+    return rc
+
+
+if __name__ == "__main__":
+    _g = gpus_arg(sys.argv[1:])
+    if _g is not None and _g > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(_g, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
+
+import torch  # noqa: E402
+
 sys.path.insert(0, os.path.join(ROOT, "articulated-point-nerf_amd"))
 sys.path.insert(0, ROOT)
 
@@ -354,7 +442,9 @@ def read_traffic(path):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); N > 1 without an outer launcher starts the N ranks itself; "
+                         "under one it must equal WORLD_SIZE")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C2")
@@ -374,7 +464,7 @@ def main():
     args = ap.parse_args()
     torch.set_grad_enabled(False)   # a render benchmark: the reference renders under no_grad (run.py:80, 241)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = check_world(args.gpus, os.environ)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one process per GPU; APN_DIST_BACKEND=gloo rehearses N>1 with several ranks on one card
