@@ -6,6 +6,7 @@ returns a non-zero status raises as well.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import os
 
@@ -43,8 +44,6 @@ SIGNATURES = {
     "apn_grid_build": (C.c_int, [P, I64, P, F32, I32, P, P, P]),
     "apn_knn_workspace_bytes": (SZ, [I64]),
     "apn_knn_radius": (C.c_int, [P, P, I64, P, P, I64, I32, P, F32, P, P, P, P, P, P]),
-    "apn_set_knn_mode": (C.c_int, [I32]),
-    "apn_debug_knn_stats": (C.c_int, [P]),
     "apn_nn1_distance": (C.c_int, [P, I64, F32, I32, P, P, P, P, P]),
     "apn_knn_points": (C.c_int, [P, I64, P, I64, I32, I32, P, P, P, P, P, P]),
     "apn_mlp_weight_layout": (C.c_int, [P]),
@@ -53,7 +52,6 @@ SIGNATURES = {
     "apn_point_mlp": (C.c_int, [P, P, P, I64, P, P, P, P, I32, P, P, P, F32, F32, F32, I32, P, P]),
     "apn_composite": (C.c_int, [P, P, P, I64, P, I64, F32, F32, P, P, P, P, P, P, P, P]),
     "apn_set_mlp_variant": (C.c_int, [I32]),
-    "apn_debug_mlp_phase_cycles": (C.c_int, [P]),
     "apn_adam_upd": (C.c_int, [P, P, P, P, I64, I32, F32, F32, F32, F32, P]),
     "apn_masked_adam_upd": (C.c_int, [P, P, P, P, I64, I32, F32, F32, F32, F32, P]),
     "apn_adam_upd_with_perlr": (C.c_int, [P, P, P, P, P, I64, I32, F32, F32, F32, F32, P]),
@@ -79,8 +77,17 @@ SIGNATURES = {
     "apn_version": (C.c_char_p, []),
 }
 
+# debug-build-only exports (include/apn_hip_debug.h; libapn_hip_debug.so)
+DEBUG_SIGNATURES = {
+    "apn_set_knn_mode": (C.c_int, [I32]),
+    "apn_debug_knn_stats": (C.c_int, [P]),
+    "apn_debug_mlp_phase_cycles": (C.c_int, [P]),
+}
+DEBUG_LIB_PATH = os.path.join(_HERE, "libapn_hip_debug.so")
+
 _lib = None
 _load_error = None
+_debug_lib = None
 
 
 def load():
@@ -103,8 +110,44 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    for name, (res, args) in DEBUG_SIGNATURES.items():   # APN_HIP_LIB = the debug build (tools/)
+        if hasattr(lib, name):
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
     _lib = lib
     return lib
+
+
+def load_debug():
+    """The debug build (libapn_hip_debug.so: earlier kNN strategies, environment A/B switches,
+    instrumented kernels; include/apn_hip_debug.h), for tools/ and the cross-check tests only. The
+    product path never loads it."""
+    global _debug_lib
+    if _debug_lib is not None:
+        return _debug_lib
+    if not os.path.exists(DEBUG_LIB_PATH):
+        raise RuntimeError(f"libapn_hip_debug.so not found at {DEBUG_LIB_PATH} (make -C csrc debug)")
+    lib = C.CDLL(DEBUG_LIB_PATH)
+    for name, (res, args) in {**SIGNATURES, **DEBUG_SIGNATURES}.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _debug_lib = lib
+    return lib
+
+
+@contextlib.contextmanager
+def using(lib):
+    """Route every call of this module through ``lib`` (e.g. load_debug()) inside the block: the
+    cross-check tests run the same model code on the debug build's kernels."""
+    global _lib
+    load()
+    prev, _lib = _lib, lib
+    try:
+        yield lib
+    finally:
+        _lib = prev
 
 
 def exported_symbols():

@@ -6,6 +6,7 @@ has a CPU path.
 from __future__ import annotations
 
 import math
+import weakref
 
 import torch
 
@@ -18,22 +19,47 @@ def _f32c(t):
 
 
 class Workspace:
-    """Grow-only device scratch buffers keyed by name (reused across forward calls). Once a HIP
-    graph has captured them (``pinned``, set by capture_frame / capture_repose) a replaced buffer is
-    kept alive, not freed: the graph holds its address, and a later larger frame (an overflow
-    rendered again exactly, another ray shard's capture, a bigger ray set) must not hand that
-    memory to anything else."""
+    """Grow-only device scratch buffers keyed by name (reused across forward calls). While a HIP
+    graph that captured them is alive (``hold(graph)``, called by capture_frame / capture_repose
+    right before each capture), a replaced buffer is kept alive, not freed: the graph holds its
+    address, and a later larger frame (an overflow rendered again exactly, another ray shard's
+    capture, a bigger ray set) must not hand that memory to anything else. A retired buffer is
+    released once every graph alive at its retirement has been destroyed (a re-capture drops the
+    old graph), so repeated capacity growth does not accumulate buffers."""
 
     def __init__(self):
         self.bufs = {}
-        self.retired = []
-        self.pinned = False
+        self.retired = []      # [(buffer, tokens of the graphs that may hold its address)]
+        self._holders = set()  # tokens of the live graphs
+        self._n = 0
+
+    @property
+    def pinned(self):
+        return bool(self._holders)
+
+    def hold(self, graph):
+        """Register a graph about to capture workspace addresses; its token is released when the
+        graph object is garbage-collected."""
+        self._n += 1
+        tok = self._n
+        self._holders.add(tok)
+        weakref.finalize(graph, self._release, tok)
+        return tok
+
+    def _release(self, tok):
+        self._holders.discard(tok)
+        keep = []
+        for b, toks in self.retired:
+            toks.discard(tok)
+            if toks:
+                keep.append((b, toks))
+        self.retired = keep
 
     def get(self, name, numel, dtype, device):
         b = self.bufs.get(name)
         if b is None or b.numel() < numel or b.dtype != dtype or b.device != torch.device(device):
-            if b is not None and self.pinned:
-                self.retired.append(b)
+            if b is not None and self._holders:
+                self.retired.append((b, set(self._holders)))
             b = torch.empty(max(int(numel), 1), dtype=dtype, device=device)
             self.bufs[name] = b
         return b[:max(int(numel), 1)]

@@ -318,12 +318,15 @@ def capture_sharded(model, t, render_kwargs, rank: int, world: int, group=None, 
 
     def step(t):
         out = local(t)
-        return _assemble(model, t, out, render_kwargs, rank, world, group, True, block, forward_kwargs)
-    step.graph, step.overflowed = local.graph, local.overflowed
+        return _assemble(model, t, out, render_kwargs, rank, world, group, True, block, forward_kwargs,
+                         invalidate=local.invalidate)
+    # (no step.graph: a re-capture replaces local.graph, and a reference here would keep the old
+    # graph -- and the buffers only it holds -- alive)
+    step.local, step.overflowed, step.capacity = local, local.overflowed, local.capacity
     return step
 
 
-def _assemble(model, t, out, render_kwargs, rank, world, group, blocks, block, forward_kwargs):
+def _assemble(model, t, out, render_kwargs, rank, world, group, blocks, block, forward_kwargs, invalidate=None):
     dev = render_kwargs["rays_o"].device
     R = render_kwargs["rays_o"].shape[0]
     n = model.last_ray_count
@@ -352,6 +355,10 @@ def _assemble(model, t, out, render_kwargs, rank, world, group, blocks, block, f
         key = (R, rank, world, block) if blocks else (R, rank, world)
         model._capacity[key] = max(model._capacity.get(key, 0), _grow_capacity(int(infos[rank, 1])))
         model.sharded_rerenders = getattr(model, "sharded_rerenders", 0) + 1
+        if invalidate is not None and int(infos[rank, 2]) != 0:
+            # this rank's captured graph (capture_sharded) holds the old capacity: capture again
+            # before its next replay, or every later frame overflows (and re-renders) as well
+            invalidate()
         model._force_exact = True
         try:
             # the frame may be read after render_sharded's no_grad scope has exited: the re-render
@@ -363,6 +370,17 @@ def _assemble(model, t, out, render_kwargs, rank, world, group, blocks, block, f
         finally:
             model._force_exact = False
     on_infos = None
+    if not blocks and world > 1 and infos.is_cuda:
+        # the capacity for the frames to come, sync-free: the largest in-bbox share any rank had,
+        # copied to the host without waiting; the next frame of this shard applies it once the copy
+        # has landed (TemporalPoints._render), whether or not this frame is ever read
+        mx = infos[:, 1].max().to(torch.int64)
+        host = torch.empty(1, dtype=torch.int64, pin_memory=True)
+        host.copy_(mx.reshape(1), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        model._cap_updates[(R, rank, world)] = (host, ev)
+
     if not blocks and world > 1:
         def on_infos(infos):
             # the ranges split follows the survivors once the cost split starts, so a rank's in-bbox

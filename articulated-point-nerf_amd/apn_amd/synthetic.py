@@ -203,6 +203,9 @@ CONFIGS = {
     "G2": SceneConfig("golden zju 40x40 3k pts 8 bones pose-emb 64", 3_000, 8, 40, 40,
                       camera="zju", pose_embedding_dim=64, fp16_exact=True),
     "G3": SceneConfig("golden dnerf 40x40 2.5k pts 24 bones", 2_500, 24, 40, 40, fp16_exact=True),
+    # features and network weights NOT fp16-representable: the reference itself then pins the lo
+    # halves of the fp16-split MLP contraction
+    "G4": SceneConfig("golden dnerf 48x48 4k pts 24 bones non-fp16-exact", 4_000, 24, 48, 48, fp16_exact=False),
 }
 
 # Render settings shared by every config (configs/nerf/default.py:57-66, 117-126)

@@ -19,6 +19,7 @@ import numpy as np
 import torch
 
 from . import _lib as L
+from . import roctx
 from ._lib import call, ptr, stream_ptr
 from .ops import Workspace, pack_mlp_weights
 from .pointwarper import PointWarper
@@ -306,6 +307,7 @@ class TemporalPoints(torch.nn.Module):
         self.palette_perm_device = None   # None: the weights' device (reference behaviour)
         self.timing = None          # set to {} to record HIP-event timings of the MLP launch
         self.last_stats = FrameStats()
+        self._cap_updates = {}      # ranges-split shard -> (pinned max in-bbox share, event) (shard._assemble)
         self._capacity = {}         # ray count (or shard) -> in-bbox sample capacity of the sync-free render path
         # kNN grid build on a side stream, concurrent with the sampling (APN_CONCURRENT_GRID=0: serial)
         self.concurrent_grid = os.environ.get("APN_CONCURRENT_GRID", "1") != "0"
@@ -511,8 +513,8 @@ class TemporalPoints(torch.nn.Module):
             with torch.cuda.stream(side):   # warm-up: caches, workspaces, packed buffers
                 self.repose(rp)
             torch.cuda.current_stream(dev).wait_stream(side)
-            self._ws.pinned = True   # the graph holds workspace addresses from here on
             graph = torch.cuda.CUDAGraph()
+            self._ws.hold(graph)   # the graph holds workspace addresses from here on
             with torch.cuda.graph(graph):
                 if sweep is None:
                     xyz, joints_rel = self.repose(rp)
@@ -587,8 +589,10 @@ class TemporalPoints(torch.nn.Module):
                 warm.keys()   # validate: an overflow renders again and grows the capacity
                 if self._capacity.get(cap_key) is None:
                     raise RuntimeError("capture_frame: no sample capacity for this ray set (empty frame?)")
-                self._ws.pinned = True   # the graph holds workspace addresses from here on
+                st.pop("graph", None)   # a re-capture: drop the old graph first (its retired buffers go with it)
+                step.graph = None
                 graph = torch.cuda.CUDAGraph()
+                self._ws.hold(graph)   # the graph holds workspace addresses from here on
                 with torch.cuda.graph(graph, capture_error_mode=capture_error_mode):
                     out = self._forward_render(t_in, *args)
                     if out._info is not None:
@@ -626,8 +630,13 @@ class TemporalPoints(torch.nn.Module):
             ovf.zero_()
             return v
 
+        def invalidate():
+            """Capture again before the next replay (the capacity grew: a frame read elsewhere,
+            e.g. an assembled ray-shard frame, overflowed and was rendered again)."""
+            st["stale"] = True
+
         capture()
-        step.inputs, step.overflowed = t_in, overflowed
+        step.inputs, step.overflowed, step.invalidate = t_in, overflowed, invalidate
         step.capacity = lambda: st["cap"]
         return step
 
@@ -764,16 +773,18 @@ class TemporalPoints(torch.nn.Module):
         # in one launch (apn_skeleton_frame)
         proj = (poses, Ks) if get_skeleton else None
         tt = None if rot_params is not None else torch.as_tensor(t, dtype=torch.float32, device=dev).reshape(-1)
-        if tt is not None and tt.numel() == 1:
-            bone_Ts, global_t, joints_rel = self.forward_warp.pose(self.joints, tt, None, time_poc=self.time_poc,
-                                                                   proj=proj)
-        else:
-            t_embed = poc_fre(t, self.time_poc) if rot_params is None else None
-            bone_Ts, global_t, joints_rel = self.forward_warp.pose(self.joints, t_embed, rot_params, proj=proj)
+        with roctx.stage("skeleton"):
+            if tt is not None and tt.numel() == 1:
+                bone_Ts, global_t, joints_rel = self.forward_warp.pose(self.joints, tt, None, time_poc=self.time_poc,
+                                                                       proj=proj)
+            else:
+                t_embed = poc_fre(t, self.time_poc) if rot_params is None else None
+                bone_Ts, global_t, joints_rel = self.forward_warp.pose(self.joints, t_embed, rot_params, proj=proj)
         colors = self._joint_colors(dev) if render_weights else None
         self._mark("frame")
-        t_hat_pcd, weights, recs = self._lbs(bone_Ts, global_t, records=True, colors=colors,
-                                             T34=self.forward_warp.last_T34)
+        with roctx.stage("lbs"):
+            t_hat_pcd, weights, recs = self._lbs(bone_Ts, global_t, records=True, colors=colors,
+                                                 T34=self.forward_warp.last_T34)
         self._mark("lbs")
         self._last_weights = weights
         pose_embedding = None
@@ -873,6 +884,7 @@ class TemporalPoints(torch.nn.Module):
         bg = float(rk['bg'])
         near, far = float(rk['near']), float(rk['far'])
         # sampling bbox (temporalpoints.py:423-427)
+        roctx.begin("sampling")
         if calc_min_max:
             bbox6 = ws.get("bbox6", 6, torch.float32, dev)
             call("apn_bbox_unpack", ptr(bbox_ord), qr, ptr(bbox6), s)
@@ -911,6 +923,12 @@ class TemporalPoints(torch.nn.Module):
             bounds = tracker.bounds_for(offs, world, advance=not self._force_exact)
             self.last_split_tracker, self.last_full_offsets = tracker, offs
             cap_key = (R, rank, world)
+            pend = self._cap_updates.pop(cap_key, None)   # the max share of an assembled frame (shard.py)
+            if pend is not None:
+                if pend[1].query():
+                    self._capacity[cap_key] = max(self._capacity.get(cap_key, 0), _grow_capacity(int(pend[0][0])))
+                else:
+                    self._cap_updates[cap_key] = pend
             r0, r1 = bounds[rank], bounds[rank + 1]
             self.last_ray_range = (r0, r1)
             self.last_ray_bounds = bounds
@@ -929,6 +947,7 @@ class TemporalPoints(torch.nn.Module):
             n_bbox = int(offs[R].item())
             self.last_stats = FrameStats({"rays": R, "inbbox_samples": n_bbox})
             if n_bbox == 0:
+                roctx.end("sampling")
                 raise NoPointsException("No points.")
             self._capacity[cap_key] = max(self._capacity.get(cap_key, 0), _grow_capacity(n_bbox))
             Q = n_bbox
@@ -949,8 +968,10 @@ class TemporalPoints(torch.nn.Module):
             nsurv = info[3:]
             self.last_stats = FrameStats({"rays": R}, info=info)
         self._mark("sampling")
+        roctx.end("sampling")
         if side is not None:
             cur.wait_stream(side)
+        roctx.begin("knn")
         # radius kNN + compaction of survivors
         s_pos = ws.get("s_pos", Q * 4, torch.float32, dev)
         s_ray = ws.get("s_ray", Q, torch.int32, dev)
@@ -959,6 +980,8 @@ class TemporalPoints(torch.nn.Module):
         call("apn_knn_radius", ptr(q_pos), ptr(q_ray), Q, nq_dev, ptr(gws), N,
              CELL_CAP, ptr(sorted4), qr, ptr(s_pos), ptr(s_ray), ptr(s_nbr), ptr(nsurv), ptr(kws), s)
         self._mark("knn")
+        roctx.end("knn")
+        roctx.begin("mlp")
         # The survivor count stays on the device: the MLP and compositing kernels read it there and
         # Q bounds it, so no sync here. (If no sample survives, the kernels produce the
         # reference's NoPointsException values -- bg colour, depth 0 -- and RenderOutput gives
@@ -984,6 +1007,8 @@ class TemporalPoints(torch.nn.Module):
             e1.record()
             self.timing.setdefault("mlp_events", []).append((e0, e1, nsurv))
             self.timing["marks"].append(("mlp", e1))
+        roctx.end("mlp")
+        roctx.begin("composite")
         # compositing
         rgb = torch.empty(R, 3, device=dev); rgb_d = torch.empty(R, 3, device=dev)
         depth = torch.empty(R, device=dev); wvis = torch.empty(R, 3, device=dev)
@@ -993,4 +1018,5 @@ class TemporalPoints(torch.nn.Module):
         call("apn_composite", ptr(out12), ptr(s_pos), ptr(s_ray), S, ptr(nsurv), R, float(self.fast_color_thres), bg,
              ptr(rgb), ptr(rgb_d), ptr(depth), ptr(wvis), ptr(last), ptr(last_d), ptr(rws), s)
         self._mark("composite")
+        roctx.end("composite")
         return rgb, rgb_d, depth, wvis, last, last_d

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/apn_hip.h"
 
@@ -20,6 +21,15 @@ inline int launch_status() {
   } while (0)
 
 inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+// Runtime A/B switches (environment variables) exist in the debug build only
+// (libapn_hip_debug.so, -DAPN_DEBUG_BUILD, used by tools/ and the cross-check tests): the shipped
+// libapn_hip.so reads no environment variable and always runs the defaults.
+#ifdef APN_DEBUG_BUILD
+inline const char* apn_env(const char* name) { return ::getenv(name); }
+#else
+inline const char* apn_env(const char*) { return nullptr; }
+#endif
 
 // Stream-ordered int32 fill and copy as plain kernels rather than hipMemsetAsync /
 // hipMemcpyAsync, so a captured render frame holds kernel nodes only (the same node kind as

@@ -22,6 +22,7 @@ __global__ void k_ray_bounds(const int* __restrict__ s_ray, const int* __restric
   if (i == n - 1 || s_ray[i + 1] != r) end[r] = i + 1;
 }
 
+#ifdef APN_DEBUG_BUILD   // the one-ray-per-thread walk from global memory: debug build only (A/B)
 // Both paths walk the ray's samples in one loop (each keeps its own T, mask and break -- the same
 // arithmetic as two separate walks), and sample i + 1's records are loaded before sample i is
 // accumulated: the per-ray chain of dependent loads is what a compositing thread waits on.
@@ -77,6 +78,7 @@ __global__ void k_composite(const float4* __restrict__ smp, const float4* __rest
   rgb_d_out[3 * r] = dr + Td * bg; rgb_d_out[3 * r + 1] = dg + Td * bg; rgb_d_out[3 * r + 2] = db + Td * bg;
   last_d_out[r] = Td;
 }
+#endif  // APN_DEBUG_BUILD
 
 // The same per-ray walks with each wave's samples staged through LDS: a wave's 64 rays own one
 // contiguous sample range (survivors are sorted by ray), which it loads in chunks of CMP_CH
@@ -174,8 +176,9 @@ extern "C" int apn_composite(const float* smp12, const float* s_pos4, const int3
   if (max_samples > 0)
     hipLaunchKernelGGL(k_ray_bounds, dim3(ceil_div(max_samples, 256)), dim3(256), 0, s, s_ray, n_samples_dev, beg,
                        end);
+#ifdef APN_DEBUG_BUILD
   static const bool per_ray = [] {   // A/B: APN_COMPOSITE=seq runs the one-ray-per-thread walk from global
-    const char* e = getenv("APN_COMPOSITE");
+    const char* e = apn_env("APN_COMPOSITE");
     return e && e[0] == 's';
   }();
   if (per_ray)
@@ -183,6 +186,7 @@ extern "C" int apn_composite(const float* smp12, const float* s_pos4, const int3
                        (const float4*)s_pos4, beg, end, n_rays, fast_color_thres, fast_color_thres > 0.f ? 1 : 0, bg,
                        rgb_marched, rgb_marched_direct, depth, weights_vis, alphainv_last, alphainv_last_direct);
   else
+#endif
     hipLaunchKernelGGL(k_composite_lds, dim3(ceil_div(n_rays, 64)), dim3(64), 0, s, (const float4*)smp12,
                        (const float4*)s_pos4, beg, end, n_rays, fast_color_thres, fast_color_thres > 0.f ? 1 : 0, bg,
                        rgb_marched, rgb_marched_direct, depth, weights_vis, alphainv_last, alphainv_last_direct);

@@ -569,6 +569,7 @@ __device__ __forceinline__ int chord_count_cs(const GridParams& g, const CS& cs,
 // workgroup per tile stages the cell_start row segments of the tile's r-dilated region in LDS,
 // so the per-row bound lookups of every query in the tile are LDS reads, and the lanes of a
 // workgroup are spatial neighbours (similar search depth, little divergence).
+#ifdef APN_DEBUG_BUILD   // earlier search strategy: debug build only (cross-checks, A/B tools)
 constexpr int KT = 4;
 constexpr int KT_LDS = 12288;   // ints of staged row bounds per workgroup (48 KB)
 
@@ -601,6 +602,7 @@ __global__ __launch_bounds__(KNN_THREADS) void k_tile_scatter(const int* __restr
   const int t = ctile[c];
   order[tile_start[t] + atomicAdd(tile_cursor + t, 1)] = c;
 }
+#endif  // APN_DEBUG_BUILD
 
 // Non-zero entries -> list of their indices (any order); n_list[0] = count. One atomic per
 // 1024-entry block (per-wave atomics on the single counter serialised at the L2).
@@ -628,6 +630,7 @@ __global__ __launch_bounds__(LIST_THREADS) void k_tile_list(const int* __restric
   if (ne) list[sbase + wcnt[wid] + __popcll(bal & ((1ull << lane) - 1ull))] = t;
 }
 
+#ifdef APN_DEBUG_BUILD   // earlier search strategy: debug build only (cross-checks, A/B tools)
 __global__ __launch_bounds__(KNN_THREADS) void k_knn_tiles(
     const float4* __restrict__ q_pos, const int* __restrict__ cand, const GridParams* __restrict__ gp,
     const int* __restrict__ cell_start, const float4* __restrict__ sorted, const int* __restrict__ tile_list,
@@ -694,6 +697,7 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_tiles(
     __syncthreads();
   }
 }
+#endif  // APN_DEBUG_BUILD
 
 // Pass 1: coarse rejection. Queries with >= 8 points in the 27 coarse cells around them are
 // compacted (in query order) per block into cand[blockIdx*256 ...]; blk_cnt[block] = count.
@@ -747,11 +751,14 @@ __global__ __launch_bounds__(KNN_THREADS) void k_compact_i32(const int* __restri
   if (t < blk_cnt[blockIdx.x]) dst[blk_off[blockIdx.x] + t] = src[blockIdx.x * KNN_THREADS + t];
 }
 
+// kNN counters of the debug build's instrumented kernels (apn_debug_knn_stats)
+__device__ unsigned long long g_knn_stats[5 * 4];
+
+#ifdef APN_DEBUG_BUILD   // earlier search strategy: debug build only (cross-checks, A/B tools)
 // Pass 2: exact search for the compacted candidates. Survivors are compacted per block (order
 // preserved) into slots [blockIdx*256, ...) of t_*; blk_cnt[block] = survivors.
 // Profiling aid (mode 3 = mode 2 + counters): per query class {stop at 2h, rejected by the chord
 // count, stop at 4h, stop at r, rejected at r}: {queries, cycles, rows, points} summed.
-__device__ unsigned long long g_knn_stats[5 * 4];
 
 template <bool STATS>
 __global__ __launch_bounds__(KNN_THREADS) void k_knn_search(
@@ -931,6 +938,7 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_b(
     nb[1] = make_int4(bi[4], bi[5], bi[6], bi[7]);
   }
 }
+#endif  // APN_DEBUG_BUILD
 
 // Ball scan as a per-lane state machine ("flat" loop): every iteration a lane either consumes
 // points of its current row range, or takes over the row range it loaded one step earlier and
@@ -1265,6 +1273,7 @@ __global__ __launch_bounds__(KNN_THREADS) void k_mark_cells(const float4* __rest
   mark[cell] = 1;
 }
 
+#ifdef APN_DEBUG_BUILD   // earlier search strategy: debug build only (cross-checks, A/B tools)
 __global__ __launch_bounds__(KNN_THREADS) void k_cell_bound(const GridParams* __restrict__ gp,
                                                            const int* __restrict__ cell_start,
                                                            const int* __restrict__ list, const int* __restrict__ n_list,
@@ -1293,6 +1302,7 @@ __global__ __launch_bounds__(KNN_THREADS) void k_cell_bound(const GridParams* __
   }
   ubound[cell] = u;
 }
+#endif  // APN_DEBUG_BUILD
 
 // Mode 8: the cell bound at three radii (r/4, r/2, r) in one pass -- u4[cell], u2[cell], u1[cell] --
 // so a query skips every ball level that cannot hold 8 points for any query of its cell.
@@ -1596,6 +1606,7 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_a8(
   }
 }
 
+#ifdef APN_DEBUG_BUILD   // earlier search strategy: debug build only (cross-checks, A/B tools)
 // Pass B of mode 8: flat ball scans from the tagged first level (r/2 or r).
 template <bool STATS>
 __global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_b8(
@@ -1639,6 +1650,7 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_b8(
     nb[1] = make_int4(bi[4], bi[5], bi[6], bi[7]);
   }
 }
+#endif  // APN_DEBUG_BUILD
 
 // top-K lists of the S lanes of a query group merged in every lane (snapshot, then unique
 // inserts in a fixed lane order): all lanes end with the same sorted list
@@ -1700,6 +1712,7 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_b8s(
   }
 }
 
+#ifdef APN_DEBUG_BUILD   // earlier search strategy: debug build only (cross-checks, A/B tools)
 // Pass A of mode 6: candidates whose cell bound is < 8 are rejected; the rest run the r/4 ball
 // and, unless it already holds the 8 nearest, go to the hard list (pass B).
 __global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_a6(
@@ -1769,6 +1782,7 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_b_flat(
     nb[1] = make_int4(bi[4], bi[5], bi[6], bi[7]);
   }
 }
+#endif  // APN_DEBUG_BUILD
 
 // Survivor counts per block of candidate slots (for the order-preserving compaction).
 __global__ __launch_bounds__(KNN_THREADS) void k_knn_flag_count(const int* __restrict__ flag,
@@ -1811,6 +1825,7 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_flag_compact(
   b[1] = a[1];
 }
 
+#ifdef APN_DEBUG_BUILD   // earlier search strategy: debug build only (cross-checks, A/B tools)
 __global__ __launch_bounds__(KNN_THREADS) void k_knn_compact(
     const float4* __restrict__ t_pos, const int* __restrict__ t_ray, const int* __restrict__ t_nbr,
     const int* __restrict__ blk_cnt, const int* __restrict__ blk_off, float4* __restrict__ s_pos,
@@ -1826,6 +1841,7 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_compact(
   b[0] = a[0];
   b[1] = a[1];
 }
+#endif  // APN_DEBUG_BUILD
 
 // Nearest *other* point for every canonical point (temporalpoints.py:104-111: column 1 of the
 // self-inclusive argKmin is the nearest other point, or a duplicate at distance 0). Cube search
@@ -2028,11 +2044,14 @@ using namespace apn;
 
 static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// Search strategy (apn_set_knn_mode / APN_KNN_MODE; default 9, see include/apn_hip.h). All are
-// exact; the others stay for A/B measurements and as cross-checks in the tests.
+// Search strategy. The shipped library runs mode 9 only (fine grid pass A, anisotropic second
+// grid pass B; the 8-lane pass B for small launches). The debug build (libapn_hip_debug.so,
+// -DAPN_DEBUG_BUILD; include/apn_hip_debug.h) keeps the earlier exact strategies 0-8 behind
+// apn_set_knn_mode / APN_KNN_MODE, for the bit-identity cross-checks and the A/B tools.
+#ifdef APN_DEBUG_BUILD
 static int& knn_mode() {
   static int m = [] {
-    const char* e = getenv("APN_KNN_MODE");
+    const char* e = apn_env("APN_KNN_MODE");
     return e ? atoi(e) : 9;
   }();
   return m;
@@ -2054,6 +2073,11 @@ extern "C" int apn_debug_knn_stats(uint64_t* out20) {
   APN_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_knn_stats), zero, sizeof(zero)));
   return APN_OK;
 }
+static const bool kKnnStats = apn_env("APN_KNN_STATS") != nullptr;   // profiling aid: apn_debug_knn_stats
+#else
+static constexpr int knn_mode() { return 9; }
+static constexpr bool kKnnStats = false;
+#endif
 
 // Grid workspace (bytes, each region 256-B aligned):
 //   GridParams | counts[cap] | cell_start[cap+1] | cursor[cap] | pcell[N] | ccount[cap] | scan ws |
@@ -2107,7 +2131,7 @@ extern "C" int apn_grid_build(const float* xyz, int64_t n_points, const int32_t*
   GridWs w = grid_ws(workspace, n_points, cell_cap);
   APN_TRY(fill4_i32(w.counts, cell_cap, w.cursor, cell_cap, nullptr, 0, nullptr, 0, s));
   static const int subdiv = [] {
-    const char* e = getenv("APN_KNN_SUBDIV");
+    const char* e = apn_env("APN_KNN_SUBDIV");
     return e ? atoi(e) : KNN_SUBDIV;
   }();
   hipLaunchKernelGGL(k_grid_params, dim3(1), dim3(64), 0, s, bbox_ord, query_radius, cell_cap, subdiv,
@@ -2169,19 +2193,19 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
   hipLaunchKernelGGL(k_compact_i32, dim3(nb), dim3(KNN_THREADS), 0, s, cand_blk, cblk_cnt, cblk_off, cand);
   // candidates: count at cblk_off[nb]; launch over the upper bound nb blocks
   if (knn_mode() == 8 || knn_mode() == 9) {
-    static const bool stats = getenv("APN_KNN_STATS") != nullptr;   // profiling aid: apn_debug_knn_stats
+    const bool stats = kKnnStats;
     // small batches (the 8192-ray training steps): 8 lanes per hard query. Up to 2^18 queries:
     // a ray shard of a full frame (~0.5-1M in-bbox samples at C2 over 8 GPUs) ran its kNN 2.3x
     // slower on the 8-lane pass than on mode 9's (tools/shard_balance.py); APN_KNN_SMALL_MAX overrides
     static const int64_t small_max = [] {
-      const char* e = getenv("APN_KNN_SMALL_MAX");
+      const char* e = apn_env("APN_KNN_SMALL_MAX");
       return e ? (int64_t)atoll(e) : KNN_SPLIT_MAX_QUERIES;
     }();
     const bool small = !stats && n_queries <= small_max;
     const bool aniso = knn_mode() == 9 && !small;
     if (aniso) {   // the anisotropic second grid for pass B (built from the fine grid's sorted points)
       static const int f = [] {
-        const char* e = getenv("APN_KNN_ANISO");
+        const char* e = apn_env("APN_KNN_ANISO");
         const int v = e ? atoi(e) : 2;
         return (v == 1 || v == 2 || v == 4) ? v : 2;
       }();
@@ -2209,7 +2233,7 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
     hipLaunchKernelGGL(k_tile_list, dim3(ceil_div(cell_cap, LIST_THREADS)), dim3(LIST_THREADS), 0, s, mark, cell_cap,
                        g.tile_list, g.n_tile_list);
     static const int64_t cb16_max = [] {   // query count up to which the cell bounds run 16 lanes per cell
-      const char* e = getenv("APN_CELL_BOUND16_MAX");
+      const char* e = apn_env("APN_CELL_BOUND16_MAX");
       return e ? (int64_t)atoll(e) : (int64_t)3 << 20;
     }();
     if (n_queries <= cb16_max)
@@ -2221,7 +2245,7 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
                          dim3(KNN_THREADS), 0, s, g.gp, g.cell_start, g.tile_list, g.n_tile_list, u1, u2, u4);
     int* hard_r = ccell + slots;          // second quarter of the t_pos region
     static const int64_t lpt_max = [] {   // query count up to which the passes run heavy blocks first
-      const char* e = getenv("APN_KNN_LPT_MAX");   // 8 shards 2.17 -> 2.05 ms, 2 shards (forced) 6.05 -> 5.86
+      const char* e = apn_env("APN_KNN_LPT_MAX");   // 8 shards 2.17 -> 2.05 ms, 2 shards (forced) 6.05 -> 5.86
       return e ? (int64_t)atoll(e) : (int64_t)6 << 20;
     }();
     // blk_cnt / blk_off are free until the survivor count below: block costs and the permutation
@@ -2231,8 +2255,13 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
                          nullptr, nullptr, g.gp, ccell, u1, u2, u4, blk_cnt);
       hipLaunchKernelGGL(k_order_blocks, dim3(1), dim3(ORDER_THREADS), 0, s, blk_cnt, nb, perm);
     }
-    static const bool a_aniso = getenv("APN_KNN_A_ANISO") != nullptr;   // A/B: pass A's r/4 ball on the second grid
-    hipLaunchKernelGGL((aniso && a_aniso) ? k_knn_pass_a8<true> : k_knn_pass_a8<false>, dim3(nb), dim3(KNN_THREADS), 0,
+#ifdef APN_DEBUG_BUILD
+    static const bool a_aniso = apn_env("APN_KNN_A_ANISO") != nullptr;   // A/B: pass A's r/4 ball on the second grid
+    auto pass_a = (aniso && a_aniso) ? k_knn_pass_a8<true> : k_knn_pass_a8<false>;
+#else
+    auto pass_a = k_knn_pass_a8<false>;
+#endif
+    hipLaunchKernelGGL(pass_a, dim3(nb), dim3(KNN_THREADS), 0,
                        s, (const float4*)q_pos4, cand, cblk_off + nb, g.gp, g.cell_start, (const float4*)sorted_pts4,
                        ccell, u1, u2, u4, flag, t_nbr, hard, n_hard, hard_r, n_hard_r, g.ag, g.cell_start2, g.sorted2,
                        perm);
@@ -2243,14 +2272,18 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
       hipLaunchKernelGGL(k_knn_pass_b8s<8>, nb4, dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard_r,
                          n_hard_r, g.gp, g.cell_start, (const float4*)sorted_pts4, flag, t_nbr);
     } else if (aniso) {
+#ifdef APN_DEBUG_BUILD
       static const int pts = [] {   // points per step of the scan (A/B: APN_KNN_PTS=2)
-        const char* e = getenv("APN_KNN_PTS");
+        const char* e = apn_env("APN_KNN_PTS");
         return e && atoi(e) == 2 ? 2 : 4;
       }();
       auto pass_b = stats ? (pts == 4 ? k_knn_pass_b9<true, 4> : k_knn_pass_b9<true, 2>)
                           : (pts == 4 ? k_knn_pass_b9<false, 4> : k_knn_pass_b9<false, 2>);
+#else
+      auto pass_b = k_knn_pass_b9<false, 4>;
+#endif
       static const bool split = [] {   // A/B: APN_KNN_B_SPLIT=1 runs the two lists as two launches
-        const char* e = getenv("APN_KNN_B_SPLIT");
+        const char* e = apn_env("APN_KNN_B_SPLIT");
         return e && atoi(e) == 1;
       }();
       if (split) {
@@ -2269,11 +2302,15 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
                            n_hard_r, hard, n_hard, g.ag, g.cell_start2, g.sorted2, flag, t_nbr, perm, ccell, u1, u2);
       }
     } else {
+#ifdef APN_DEBUG_BUILD
       auto pass_b = stats ? k_knn_pass_b8<true> : k_knn_pass_b8<false>;
       hipLaunchKernelGGL(pass_b, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard, n_hard,
                          g.gp, g.cell_start, (const float4*)sorted_pts4, flag, t_nbr);
       hipLaunchKernelGGL(pass_b, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard_r,
                          n_hard_r, g.gp, g.cell_start, (const float4*)sorted_pts4, flag, t_nbr);
+#else
+      return APN_ERR_ARG;   // unreachable: mode 9 always takes the small or the anisotropic pass B
+#endif
     }
     hipLaunchKernelGGL(k_knn_flag_count, dim3(nb), dim3(KNN_THREADS), 0, s, flag, cblk_off + nb, blk_cnt);
     st = scan_exclusive_i32(blk_cnt, blk_off, nb, sws, s);
@@ -2283,6 +2320,9 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
     APN_TRY(copy_i32(blk_off + nb, n_survivors_dev, 1, s));
     return launch_status();
   }
+#ifndef APN_DEBUG_BUILD
+  return APN_ERR_ARG;   // unreachable (mode 9)
+#else
   if (knn_mode() == 6 || knn_mode() == 7) {
     int* flag = t_ray;
     int* hard = cand_blk;
@@ -2372,6 +2412,7 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
                      (float4*)s_pos4, s_ray, s_nbr);
   APN_TRY(copy_i32(blk_off + nb, n_survivors_dev, 1, s));
   return launch_status();
+#endif  // APN_DEBUG_BUILD
 }
 
 // Construction-time: per-point nearest-other distance sqrt(d2 + eps) over the canonical cloud.

@@ -408,14 +408,14 @@ extern "C" int apn_lbs_skin(const float* canonical_pcd, const float* raw_weights
   // J % 4 == 0 (APN_LBS_LDS selects the LDS-tile kernel). The render path keeps k_lbs_skin: its
   // sequential sums reproduce the oracle's skinned cloud bit for bit, and the sampling bbox --
   // hence every sample position -- follows that cloud (bbox sensitivity).
-  static const bool quad_ok = getenv("APN_LBS_LDS") == nullptr;
+  static const bool quad_ok = apn_env("APN_LBS_LDS") == nullptr;
   if (quad_ok && !recA16 && !merge_rules && J % 4 == 0 && ((uintptr_t)raw_weights % 16) == 0) {
     // grid-stride blocks (one row ahead); <= 1 partial per block. 32 blocks per CU: the launch
     // then carries more rows in flight per CU than the 4-per-CU persistent grid (C5, 1M points,
     // J = 48: 0.0511 -> 0.0429 ms; 6: 0.048, 12: 0.044, 64: 0.044 -- tools/c5_lbs_ab.sh); a
     // second row in flight per lane (LBS_PF = 2, 3) measured slower
     static const int per_cu = [] {
-      const char* e = getenv("APN_LBS_BLOCKS_PER_CU");
+      const char* e = apn_env("APN_LBS_BLOCKS_PER_CU");
       return e ? atoi(e) : 32;
     }();
     const int qblocks = (int)std::min<int64_t>(ceil_div(n_points, LBS_THREADS / 4), 256 * per_cu);

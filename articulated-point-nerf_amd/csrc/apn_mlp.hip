@@ -517,15 +517,22 @@ extern "C" int apn_feat_project(const float* canonical_feat, int64_t n_points, i
 // Kernel selection: initialised from APN_MLP_VARIANT, changed by apn_set_mlp_variant.
 static int& mlp_variant() {
   static int v = [] {
-    const char* e = getenv("APN_MLP_VARIANT");
+    const char* e = apn_env("APN_MLP_VARIANT");
     return e ? atoi(e) : 0;
   }();
   return v;
 }
 
+// 0 = fp16-split kernel (default), 1 = FP32 MFMA kernel; the debug build also has 2 / 3, the
+// phase-timed builds of each (profiling aid).
+#ifdef APN_DEBUG_BUILD
+constexpr int kMaxMlpVariant = 3;
+#else
+constexpr int kMaxMlpVariant = 1;
+#endif
 extern "C" int apn_set_mlp_variant(int32_t variant) {
   const int prev = mlp_variant();
-  if (variant >= 0 && variant <= 3) mlp_variant() = variant;
+  if (variant >= 0 && variant <= kMaxMlpVariant) mlp_variant() = variant;
   return prev;
 }
 
@@ -546,7 +553,7 @@ extern "C" int apn_point_mlp(const float* s_pos4, const int32_t* s_ray, const in
   // 2 / 3 = their phase-timed builds (profiling aid; same results).
   const int variant = mlp_variant();
   static const int env_blocks = [] {
-    const char* e = getenv("APN_MLP_BLOCKS");
+    const char* e = apn_env("APN_MLP_BLOCKS");
     return e ? atoi(e) : 0;
   }();
   if (grid_blocks <= 0) grid_blocks = env_blocks;
@@ -562,8 +569,10 @@ extern "C" int apn_point_mlp(const float* s_pos4, const int32_t* s_ray, const in
   };
   if (variant == 1) {
     launch(k_point_mlp<2, 2>, blocks, nullptr);
+#ifdef APN_DEBUG_BUILD
   } else if (variant == 2) {
     launch(k_point_mlp<2, 2, true>, blocks, nullptr);
+#endif
   } else {
     launch_point_mlp_h3(blocks, variant == 3, (hipStream_t)stream, (const float4*)s_pos4, s_ray, s_nbr,
                         n_samples_dev, (const float4*)recA16, (const float4*)recB8, (const float4*)feat_proj,
@@ -578,6 +587,7 @@ extern "C" int apn_point_mlp(const float* s_pos4, const int32_t* s_ray, const in
   return launch_status();
 }
 
+#ifdef APN_DEBUG_BUILD
 // Profiling aid: copy (and reset) the per-phase cycle sums of the timed MLP variants
 // (APN_MLP_VARIANT=2, 3): {gather, layer 1, layers 2-4, epilogue, tiles, kernel} summed over
 // workgroups. Synchronous.
@@ -589,3 +599,4 @@ extern "C" int apn_debug_mlp_phase_cycles(uint64_t* out6) {
   APN_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_mlp_phase), zero, sizeof(zero)));
   return debug_phase_cycles_h3(out6);
 }
+#endif  // APN_DEBUG_BUILD

@@ -1069,10 +1069,6 @@ void launch_point_mlp_h3(int blocks, bool timed, hipStream_t stream, const float
                          const int* s_nbr, const int* n_samples_dev, const float4* recA, const float4* recB,
                          const float4* pproj, const float* viewdirs, const float* vemb_const, const float* wbuf,
                          float eps, float shift, float interval, float4* out) {
-  static const int occ = [] {
-    const char* e = getenv("APN_MLP_OCC");
-    return e ? atoi(e) : 3;
-  }();
   auto go = [&](auto kern, int nb) {
     hipLaunchKernelGGL(kern, dim3(nb), dim3(MLP_THREADS), 0, stream, s_pos, s_ray, s_nbr, n_samples_dev, recA, recB,
                        pproj, viewdirs, vemb_const, wbuf, eps, shift, interval, out);
@@ -1080,6 +1076,13 @@ void launch_point_mlp_h3(int blocks, bool timed, hipStream_t stream, const float
   // the scaled-weights instantiation runs on a smaller grid (a rare mode: weight magnitudes outside
   // [2^-5, 2^12]); when it does not match, its 8 workgroups per CU exit at once
   const int nb_scaled = blocks < 256 * 8 ? blocks : 256 * 8;
+#ifdef APN_DEBUG_BUILD
+  // debug build: the phase-timed kernels (APN_MLP_VARIANT=3) and the ping-pong build at 2
+  // workgroups per CU (APN_MLP_OCC=2)
+  static const int occ = [] {
+    const char* e = apn_env("APN_MLP_OCC");
+    return e ? atoi(e) : 3;
+  }();
   if (occ == 3) {
     if (timed) { go(h3::k_point_mlp_h3<true, 3, false>, blocks); go(h3::k_point_mlp_h3<true, 3, true>, nb_scaled); }
     else { go(h3::k_point_mlp_h3<false, 3, false>, blocks); go(h3::k_point_mlp_h3<false, 3, true>, nb_scaled); }
@@ -1087,6 +1090,11 @@ void launch_point_mlp_h3(int blocks, bool timed, hipStream_t stream, const float
     if (timed) { go(h3::k_point_mlp_h3<true, 2, false>, blocks); go(h3::k_point_mlp_h3<true, 2, true>, nb_scaled); }
     else { go(h3::k_point_mlp_h3<false, 2, false>, blocks); go(h3::k_point_mlp_h3<false, 2, true>, nb_scaled); }
   }
+#else
+  (void)timed;
+  go(h3::k_point_mlp_h3<false, 3, false>, blocks);
+  go(h3::k_point_mlp_h3<false, 3, true>, nb_scaled);
+#endif
 }
 
 int debug_phase_cycles_h3(uint64_t* out6) {

@@ -209,6 +209,7 @@ __global__ void k_inbbox_count(const float* __restrict__ ro, const float* __rest
   cnt[r] = c;
 }
 
+#ifdef APN_DEBUG_BUILD   // one ray per thread: debug build only (A/B against the block-cooperative fill)
 // q_pos[i] = (x, y, z, bits(step_id)); q_ray[i] = ray id. Sorted by ray, then step.
 // cap: samples at positions >= cap are not written (the capacity-bounded, sync-free render path:
 // apn_inbbox_fill_capped); INT_MAX = every sample.
@@ -231,6 +232,7 @@ __global__ void k_inbbox_fill(const float* __restrict__ ro, const float* __restr
     }
   }
 }
+#endif  // APN_DEBUG_BUILD
 
 // The same samples, written block-cooperatively (k_inbbox_fill walks one ray per thread, so a
 // wave's stores scatter over 64 rays' output ranges: 1.6 TB/s). The block's 256 rays own the
@@ -288,13 +290,18 @@ __global__ __launch_bounds__(FILL_RAYS) void k_inbbox_fill_blk(const float* __re
   }
 }
 
+#ifdef APN_DEBUG_BUILD
 static bool inbbox_fill_per_ray() {   // A/B: APN_INBBOX_FILL=ray selects the one-ray-per-thread fill
   static const bool v = [] {
-    const char* e = getenv("APN_INBBOX_FILL");
+    const char* e = apn_env("APN_INBBOX_FILL");
     return e && e[0] == 'r';
   }();
   return v;
 }
+#define APN_INBBOX_FILL_KERNEL (inbbox_fill_per_ray() ? k_inbbox_fill : k_inbbox_fill_blk)
+#else
+#define APN_INBBOX_FILL_KERNEL k_inbbox_fill_blk
+#endif
 
 // frame_info = {min(total, cap), total, total > cap} from the exclusive scan's last entry.
 __global__ void k_frame_info(const int* __restrict__ total, int cap, int* __restrict__ info) {
@@ -428,7 +435,7 @@ extern "C" int apn_inbbox_fill(const float* rays_o, const float* rays_d, const f
                                float stepdist, int64_t n_rays, const int32_t* offsets, float* q_pos4, int32_t* q_ray,
                                void* stream) {
   if (n_rays <= 0) return APN_ERR_ARG;
-  hipLaunchKernelGGL(inbbox_fill_per_ray() ? k_inbbox_fill : k_inbbox_fill_blk, dim3(ceil_div(n_rays, 256)), dim3(256),
+  hipLaunchKernelGGL(APN_INBBOX_FILL_KERNEL, dim3(ceil_div(n_rays, 256)), dim3(256),
                      0, (hipStream_t)stream, rays_o, rays_d, bbox6, near, far, stepdist, n_rays, offsets,
                      (float4*)q_pos4, q_ray, INT_MAX);
   return launch_status();
@@ -441,7 +448,7 @@ extern "C" int apn_inbbox_fill_capped(const float* rays_o, const float* rays_d, 
   if (n_rays <= 0 || capacity < 0 || capacity > INT_MAX || !frame_info) return APN_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(k_frame_info, dim3(1), dim3(64), 0, s, offsets + n_rays, (int)capacity, frame_info);
-  hipLaunchKernelGGL(inbbox_fill_per_ray() ? k_inbbox_fill : k_inbbox_fill_blk, dim3(ceil_div(n_rays, 256)), dim3(256),
+  hipLaunchKernelGGL(APN_INBBOX_FILL_KERNEL, dim3(ceil_div(n_rays, 256)), dim3(256),
                      0, s, rays_o, rays_d, bbox6, near, far, stepdist, n_rays, offsets, (float4*)q_pos4, q_ray,
                      (int)capacity);
   return launch_status();

@@ -319,6 +319,7 @@ def lbs_sweep(args, rank, world, dev):
     if rank != 0:
         return
     b_alg = N * (24 + 4 * J)
+    lbs_traffic, lbs_src = latest_traffic("lbs_traffic_c5")
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         try:
@@ -356,8 +357,10 @@ def lbs_sweep(args, rank, world, dev):
                      "achieved": b_alg / (lbs_ms * 1e-3) / 1e9 if lbs_ms > 0 else 0.0,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": b_alg / (lbs_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if lbs_ms > 0 else 0.0,
-                     "traffic": (read_traffic(os.path.join(ROOT, "profiles", "r01_lbs_traffic_c5.json")) or {}).get(
-                         "bytes_per_launch"), "bytes_per_launch": b_alg, "avg_launch_ms": lbs_ms,
+                     "traffic": (lbs_traffic or {}).get("bytes_per_launch"),
+                     "traffic_source": (f"{lbs_src}: PMC passes on an earlier build; NOT measured in this run"
+                                        if lbs_traffic else None),
+                     "bytes_per_launch": b_alg, "avg_launch_ms": lbs_ms,
                      "note": "achieved = B_alg = N_r*(24+4J) bytes per pose (SURVEY.md 8(d) C5; N_r = this rank's "
                              "points) / avg LBS kernel time (HIP events around a graph of 20 back-to-back LBS "
                              "launches on the launch stream); the step also runs the skeleton kernel"},
@@ -430,6 +433,36 @@ def other_configs(dev):
                    "MLP kernel ms from HIP events on 5 eager frames; C5 = 300 poses of the repose sweep graph, LBS "
                    "kernel from a graph of 20 launches (bench.py --config C5 gives the full line)")
     return out
+
+
+def frame_roofline(N, J, R, f_alg, ms_per_step, gpus=1):
+    """SURVEY.md 8(d) binding fraction of the whole frame: t_roofline / t with t_roofline =
+    max(B_alg / BW, F_alg / P) over the frame's GPUs. B_alg = N(60 + 4J) (LBS) + N(580 + 4J)
+    (per-point tables once) + 36 R (rays) + 48 R (outputs); F_alg = the neighbour MLP's reference
+    flops over all kept samples; P = the split-MFMA fp32-equivalent peak (fp16 dense / 3). The kNN's
+    VALU work has no F_alg term: its time is part of the lost fraction."""
+    b_alg = N * (60 + 4 * J) + N * (580 + 4 * J) + 36 * R + 48 * R
+    t_hbm = b_alg / (HBM_PEAK_GBS * 1e9 * gpus) * 1e3
+    t_mfma = f_alg / (SPLIT3_PEAK_TFLOPS * 1e12 * gpus) * 1e3
+    t_fp32 = f_alg / (FP32_MFMA_PEAK_TFLOPS * 1e12 * gpus) * 1e3
+    t_roof = max(t_hbm, t_mfma)
+    return {"t_roofline_ms": t_roof, "bound": "mfma" if t_mfma >= t_hbm else "hbm", "frac": t_roof / ms_per_step,
+            "b_alg_bytes": b_alg, "f_alg_flop": f_alg, "t_hbm_ms": t_hbm, "t_mfma_ms": t_mfma, "gpus": gpus,
+            "frac_vs_fp32_matrix_peak": t_fp32 / ms_per_step,
+            "note": "t_roofline = max(B_alg/8 TB/s, F_alg/833 TF) over the frame's GPUs (SURVEY.md 8(d)); "
+                    "frac_vs_fp32_matrix_peak prices F_alg at the 157.3 TF FP32 matrix peak instead (> 1: the "
+                    "kernel does not run on fp32 MFMA)"}
+
+
+def latest_traffic(stem):
+    """The newest committed PMC traffic summary profiles/rNN_<stem>.json -> (dict, relative path)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r[0-9][0-9]_{stem}.json")))
+    for path in reversed(files):
+        t = read_traffic(path)
+        if t:
+            return t, os.path.relpath(path, ROOT)
+    return None, None
 
 
 def read_traffic(path):
@@ -577,9 +610,12 @@ def main():
         elapsed, overflowed = float(t[0]), bool(t[1] > 0)
     if overflowed:
         log(f"[rank {rank}] WARNING: a timed frame overflowed its sample capacity (dropped samples)")
-    if os.environ.get("APN_MLP_VARIANT") in ("2", "3"):   # timed MLP variants: per-phase cycle split
+    from apn_amd import _lib
+    lib = _lib.load()
+    debug_lib = hasattr(lib, "apn_debug_knn_stats")   # APN_HIP_LIB = libapn_hip_debug.so (tools/ A/B runs)
+    variant = int(lib.apn_set_mlp_variant(-1))        # the library's kernel selection (out of range: query)
+    if debug_lib and variant in (2, 3):   # timed MLP variants of the debug build: per-phase cycle split
         import ctypes
-        from apn_amd import _lib
         ph = (ctypes.c_uint64 * 6)()
         _lib.call("apn_debug_mlp_phase_cycles", ph)
         tot = sum(ph[:4]) or 1
@@ -592,6 +628,10 @@ def main():
         if name != "frame":
             stage_ms[name] = stage_ms.get(name, 0.0) + a.elapsed_time(b) / n_timed
     log(f"[rank {rank}] stage ms/frame (HIP events, eager frames): " + ", ".join(f"{k} {v:.3f}" for k, v in stage_ms.items()))
+    ev = timing.get("mlp_events", [])
+    mlp_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / max(len(ev), 1)
+    S_kept = int(ev[-1][2].item()) if ev else stats.get("kept_samples", 0)
+    kept_total = S_kept * (world if not shard_rays else 1)
     shard_diag = None
     if shard_rays:
         # N>1 diagnostics: every rank's stage times, the tile all-gather alone (HIP events around
@@ -610,11 +650,12 @@ def main():
         g1.record()
         torch.cuda.synchronize(dev)
         ag_ms = g0.elapsed_time(g1) / 10
-        mine = {"rank": rank, "rays": n_local, "allgather_ms": round(ag_ms, 4),
+        mine = {"rank": rank, "rays": n_local, "kept_samples": S_kept, "allgather_ms": round(ag_ms, 4),
                 "replicated_ms": round(sum(stage_ms.get(k, 0.0) for k in ("lbs", "bbox", "grid")), 4),
                 "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()}}
         per_rank = [None] * world
         torch.distributed.all_gather_object(per_rank, mine)
+        kept_total = sum(p["kept_samples"] for p in per_rank)
         shard_diag = {"per_rank": per_rank, "allgather_ms_max": max(p["allgather_ms"] for p in per_rank),
                       "rerenders": getattr(model, "sharded_rerenders", 0),
                       "note": "stage_ms from HIP events on eager shard frames; allgather_ms = one gather_blocks "
@@ -623,9 +664,8 @@ def main():
         log(f"[rank {rank}] all-gather {ag_ms:.3f} ms/frame, replicated stages {mine['replicated_ms']:.3f} ms/frame")
     log(f"[rank {rank}] host time inside step() {1e3 * host_s / args.steps:.3f} ms/step "
         f"({'graph replay' if use_graph else 'eager launches'}; device {1e3 * elapsed / args.steps:.3f} ms/step)")
-    if os.environ.get("APN_KNN_MODE") == "3":   # kNN query-class counters
+    if debug_lib and os.environ.get("APN_KNN_MODE") == "3":   # kNN query-class counters (debug build)
         import ctypes
-        from apn_amd import _lib
         st = (ctypes.c_uint64 * 20)()
         _lib.call("apn_debug_knn_stats", st)
         names = ["stop2h", "chord_reject", "stop4h", "stop_r", "reject_r"]
@@ -634,9 +674,8 @@ def main():
             n = st[4 * i] or 1
             log(f"[knn {nm}] queries/frame {st[4 * i] / args.steps:.0f} cycles share {100 * st[4 * i + 1] / tot_cyc:.1f}% "
                 f"cycles/query {st[4 * i + 1] / n:.0f} rows/query {st[4 * i + 2] / n:.1f} pts/query {st[4 * i + 3] / n:.1f}")
-    if os.environ.get("APN_KNN_STATS"):   # mode-8/9 pass-B counters (per hard list)
+    if debug_lib and os.environ.get("APN_KNN_STATS"):   # mode-8/9 pass-B counters (per hard list, debug build)
         import ctypes
-        from apn_amd import _lib
         st = (ctypes.c_uint64 * 20)()
         _lib.call("apn_debug_knn_stats", st)
         n = args.steps + args.warmup
@@ -646,16 +685,11 @@ def main():
             log(f"[knn pass B {nm}] queries/frame {v[0] / n:.0f}, done at r/2 {v[1] / q:.3f}, survive {v[2] / q:.3f}, "
                 f"r/2 scan rows+pts iters/query {v[3] / q:.1f}+{v[4] / q:.1f}, r scan {v[5] / q:.1f}+{v[6] / q:.1f}, "
                 f"rejected after full r scan {v[7] / q:.3f} ({v[8] / max(v[7], 1):.1f} iters each)")
-    ev = timing.get("mlp_events", [])
-    mlp_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / max(len(ev), 1)
-    S_kept = int(ev[-1][2].item()) if ev else stats.get("kept_samples", 0)
-
     if rank != 0:
         if world > 1:
             torch.distributed.destroy_process_group()
         return
 
-    variant = int(os.environ.get("APN_MLP_VARIANT", "0"))
     d_in = 191  # pose embedding folded into the bias for ZJU; F_alg still counts the reference D_in
     if model.pose_embedding_dim > 0:
         d_in = 191 + model.pose_embedding_dim
@@ -668,8 +702,10 @@ def main():
     else:
         kernel, peak, mfma_peak = "k_point_mlp_h3 (3-term fp16-split MFMA)", SPLIT3_PEAK_TFLOPS, FP16_MFMA_PEAK_TFLOPS
         peak_note = "peak = fp16 dense MFMA peak / 3 (three fp16 MFMA terms per fp32-accurate product)"
-    traffic = read_traffic(os.path.join(ROOT, "profiles", "r03_point_mlp_traffic.json"))
+    traffic, traffic_src = latest_traffic("point_mlp_traffic")
     ms_per_step = elapsed / args.steps * 1e3
+    frame_roof = frame_roofline(scene.cfg.N, scene.cfg.J, R, kept_total * flop_per_kept_sample(d_in), ms_per_step,
+                                world if shard_rays else 1)
     value = (1 if shard_rays else world) * args.steps * R / elapsed
     cpu = psnr = same = None
     if world == 1 and not args.no_cpu_baseline:
@@ -688,6 +724,7 @@ def main():
         "ms_per_step": ms_per_step, "higher_is_better": True,
         "scaling": "strong" if shard_rays else "weak", "vs_baseline": None,
         "dtype": "fp32", "data": "synthetic (procedural SMPL-24 capsule cloud, random-init networks)",
+        "library": lib.apn_version().decode(),
         "mlp_arithmetic": ("fp32 as 3 fp16 MFMA terms (hi*hi+hi*lo+lo*hi), fp32 accumulate; parity vs the fp32 "
                            "oracle <= 3e-7 on alpha/rgb" if variant in (0, 3) else "fp32 MFMA (v_mfma_f32_16x16x4_f32)"),
         "config": {"workload": S.CONFIGS[args.config].name + f" ({args.config})", "rays_per_frame": R,
@@ -706,6 +743,10 @@ def main():
         "roofline": {"bound": "mfma", "kernel": kernel, "achieved": achieved, "peak": peak,
                      "unit": "TFLOP/s", "frac": achieved / peak,
                      "traffic": traffic.get("bytes_per_launch") if traffic else None,
+                     "traffic_source": (f"{traffic_src}: PMC passes (FETCH_SIZE / WRITE_SIZE, gfx950 read "
+                                        f"correction) over bench.py on an earlier build (kernel avg "
+                                        f"{traffic.get('avg_ms', float('nan')):.2f} ms then); NOT measured in this run"
+                                        if traffic else None),
                      "flop_per_launch": flop, "avg_launch_ms": mlp_ms,
                      "note": "achieved = reference F_alg (SURVEY.md 8(d), fp32 flops) / avg MLP kernel time (HIP "
                              "events on the launch stream); " + peak_note + "; the kernel issues fewer MFMA flops "
@@ -713,6 +754,8 @@ def main():
                              "tile): executed_tflops / mfma_util",
                      "executed_tflops": executed,
                      "mfma_util": executed / mfma_peak},
+        "frame_roofline_frac": frame_roof["frac"],
+        "frame_roofline": frame_roof,
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
         **({"shards": shard_diag} if shard_diag is not None else {}),
         "cpu_baseline": cpu,

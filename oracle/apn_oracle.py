@@ -312,6 +312,56 @@ def knn_kmin(query, points, K, chunk=2048, use_tree=None):
     return d_out, i_out
 
 
+def knn_radius_certified(query, points, K=8, r2=0.01, kc=16, chunk=1 << 19, workers=None):
+    """The render path's kNN + radius filter (temporalpoints.py:433-447: Kmin_argKmin K=8, keep a
+    sample iff its K-th float32 squared distance <= query_radius) at full-frame sizes, with a
+    certificate instead of a candidate-window assumption.
+
+    A float64 cKDTree gives each query its ``kc`` nearest points within sqrt(r2)(1 + 1e-4) (a point
+    beyond that bound cannot reach float32 d2 <= r2); they are re-ranked by the float32 distance
+    (dx^2 + dy^2) + dz^2, ties by index. A query whose window is full (kc points inside the bound)
+    is certified only if its window's largest float32 distance exceeds its K-th by more than the
+    float32 / float64 rounding gap; every other full-window query is re-ranked over ALL points of
+    its ball (query_ball_point). Returns (keep [Q] bool, idx [Q, K] int64 (valid where keep),
+    stats dict)."""
+    from scipy.spatial import cKDTree
+    q = np.ascontiguousarray(query, F32); p = np.ascontiguousarray(points, F32)
+    Q, N = len(q), len(p)
+    workers = workers or torch.get_num_threads()
+    bound = float(np.sqrt(np.float64(r2))) * (1 + 1e-4)
+    tree = cKDTree(p.astype(np.float64))
+    keep = np.zeros(Q, bool)
+    idx = np.full((Q, K), -1, np.int64)
+    n_redo = 0
+    for s in range(0, Q, chunk):
+        qq = q[s:s + chunk]
+        _, cand = tree.query(qq.astype(np.float64), k=kc, distance_upper_bound=bound, workers=workers)
+        cand = np.asarray(cand, np.int64)
+        valid = cand < N
+        cc = np.where(valid, cand, 0)
+        d2 = np.where(valid, sqdist(qq[:, None, :], p[cc]), np.float32(np.inf))
+        order = np.lexsort((np.where(valid, cand, N), d2), axis=1)
+        d2s = np.take_along_axis(d2, order, 1)
+        cs = np.take_along_axis(cand, order, 1)
+        kth = d2s[:, K - 1]
+        full = valid.all(1)
+        # a full window holds the true top-K if no point outside it can be closer than its K-th:
+        # every outside point is at float64 distance >= the window's largest, whose float32 d2
+        # is within ~2^-22 relative of the float64 value
+        unsure = full & ~(d2s[:, -1] > kth * np.float32(1 + 1e-5))
+        kk = (kth <= np.float32(r2)) & ~unsure
+        keep[s:s + len(qq)] = kk
+        idx[s:s + len(qq)] = cs[:, :K]
+        for i in np.nonzero(unsure)[0]:
+            n_redo += 1
+            ball = np.asarray(tree.query_ball_point(qq[i].astype(np.float64), bound), np.int64)
+            dd = sqdist(qq[i][None, :], p[ball])
+            o = np.lexsort((ball, dd))[:K]
+            keep[s + i] = len(ball) >= K and dd[o[K - 1]] <= np.float32(r2)
+            idx[s + i, :min(K, len(o))] = ball[o]
+    return keep, idx, {"queries": Q, "survivors": int(keep.sum()), "rechecked_on_full_ball": n_redo}
+
+
 def mean_min_distance(canonical_pcd, K=8, eps=1e-6):
     """temporalpoints.py:104-111: argKmin over the cloud itself (self-inclusive);
     nn_distance = sqrt(sum(delta^2) + eps); mean of column 1."""

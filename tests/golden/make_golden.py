@@ -19,7 +19,11 @@ What it does:
 * T1: the stage-1 TiNeuVox model itself (lib/tineuvox.py:91-625) -- forward,
   mult_dist_interp, get_grid_as_point_cloud -- and get_rays_of_a_view (a-22).
 
-Usage: ``python tests/golden/make_golden.py [G1 G2 G3 T1]`` (default: all).
+* G4: a G1-sized D-NeRF scene with 24 bones whose features and network weights are NOT
+  fp16-representable (``fp16_exact=False``), so the reference pins the lo halves of the split-MFMA
+  MLP contraction too.
+
+Usage: ``python tests/golden/make_golden.py [G1 G2 G3 G4 T1]`` (default: all).
 
 The reference never travels: only the .npz data files are committed.
 """
@@ -343,7 +347,7 @@ def main():
     install_stubs()
     sys.path.insert(0, REF)
     torch.set_num_threads(min(8, os.cpu_count() or 1))
-    which = sys.argv[1:] or ["G1", "G2", "G3", "T1"]
+    which = sys.argv[1:] or ["G1", "G2", "G3", "G4", "T1"]
     for name in which:
         if name.startswith("ckpt_"):
             gen_checkpoint_case(name[5:])

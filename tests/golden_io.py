@@ -7,7 +7,7 @@ import numpy as np
 import torch
 
 GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-CASES = ("G1", "G2", "G3")
+CASES = ("G1", "G2", "G3", "G4")
 
 
 class Golden:

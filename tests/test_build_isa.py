@@ -18,7 +18,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "articulated-point-nerf_amd", "apn_amd", "libapn_hip.so")
 LLVM = "/opt/rocm/lib/llvm/bin"
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
-PACKED_F32 = re.compile(r"\bv_pk_(add|mul|fma)_f32\b")
+# every packed VALU form on 32-bit lanes (v_pk_add/mul/fma_f32 and the packed moves beside them):
+# none is emitted today, and any that reappears is a candidate for the same missing wait state
+PACKED_F32 = re.compile(r"\bv_pk_\w+_(f32|b32)\b")
+LIBS = [LIB, os.path.join(os.path.dirname(LIB), "libapn_hip_debug.so")]
 
 
 def _disassemble_device_code(lib):
@@ -46,9 +49,11 @@ def _disassemble_device_code(lib):
     return out
 
 
-@pytest.mark.skipif(not os.path.exists(LIB), reason="libapn_hip.so not built")
-def test_no_packed_fp32_valu_in_device_code():
-    texts = _disassemble_device_code(LIB)
+@pytest.mark.parametrize("lib", LIBS, ids=["product", "debug"])
+def test_no_packed_fp32_valu_in_device_code(lib):
+    if not os.path.exists(lib):
+        pytest.skip(f"{os.path.basename(lib)} not built")
+    texts = _disassemble_device_code(lib)
     assert len(texts) >= 10, len(texts)                       # one code object per .hip source
     allcode = "\n".join(texts)
     assert "v_mfma_f32_16x16x32_f16" in allcode                # really the MLP kernels' ISA

@@ -168,3 +168,64 @@ def test_captured_ray_block_shards_equal_eager_and_assemble(dev):
         with torch.no_grad():
             full = pack_tile(model(t, render_depth=True, render_kwargs=rk, render_weights=True), R, dev)
         assert torch.equal(assemble_blocks(parts, R, world, block), full), i
+
+
+def test_captured_shard_overflow_recaptures_and_releases(dev, monkeypatch):
+    """shard.capture_sharded (bench --gpus N, one graph per rank): a replay that overflows the
+    captured capacity is read through the assembled frame, which renders it again exactly AND makes
+    the rank's graph capture again (before, every later frame overflowed again). The
+    re-capture drops the old graph, and the workspace buffers retired while it was alive are
+    released with it (no growth of Workspace.retired per capacity step). world = 1: the same code
+    path without a process group."""
+    import gc
+    import apn_amd.temporalpoints as TP
+    from apn_amd.shard import RAY_BLOCK, capture_sharded
+    scene, model = _scene_model(dev)
+    rk = scene.render_kwargs(dev)
+    R = len(rk["rays_o"])
+    ts = [torch.tensor([scene.cfg.t + 0.1 * i], device=dev) for i in range(6)]
+    counts = []
+    for t in ts:
+        model._force_exact = True
+        _frame(model, t, rk)
+        model._force_exact = False
+        counts.append(model.last_stats["inbbox_samples"])
+    lo, hi = min(range(6), key=lambda i: counts[i]), max(range(6), key=lambda i: counts[i])
+    assert counts[hi] > counts[lo], counts
+    key = (R, 0, 1, RAY_BLOCK)
+    model._capacity.pop(key, None)
+    monkeypatch.setattr(TP, "_grow_capacity", lambda n: int(n))
+    step = capture_sharded(model, ts[lo], rk, 0, 1)
+    monkeypatch.undo()
+    assert step.capacity() == counts[lo]
+    g = step(ts[lo])
+    torch.cuda.synchronize()
+    assert not step.overflowed()
+    g = step(ts[hi])
+    assert step.overflowed()
+    got = {k: g[k].clone() for k in KEYS}              # first read: rendered again exactly, graph invalidated
+    ref = _frame(model, ts[hi], rk)
+    for k in KEYS:
+        assert torch.equal(got[k], ref[k]), k
+    g = step(ts[hi])                                   # captured again with the grown capacity
+    assert step.capacity() >= counts[hi]
+    got = {k: g[k].clone() for k in KEYS}
+    assert not step.overflowed()
+    for k in KEYS:
+        assert torch.equal(got[k], ref[k]), k
+    gc.collect()
+    # only the live graph may still hold retired buffers
+    live = model._ws._holders
+    assert len(live) == 1, live
+    assert all(toks <= live for _, toks in model._ws.retired)
+    n_retired = len(model._ws.retired)
+    for _ in range(2):                                  # more growth steps: retired stays bounded
+        model._capacity[key] = int(model._capacity[key] * 1.5)
+        step.local.invalidate()
+        g = step(ts[hi])
+        got = {k: g[k].clone() for k in KEYS}
+        for k in KEYS:
+            assert torch.equal(got[k], ref[k]), k
+        gc.collect()
+        assert len(model._ws._holders) == 1
+        assert len(model._ws.retired) <= max(n_retired, 16), len(model._ws.retired)

@@ -231,7 +231,7 @@ def _golden_queries(g):
     return pts[~mo], rid[~mo], sid[~mo]
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("mode", [9, 0, 1, 2, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("cap", [1 << 20, 1 << 12])
 @pytest.mark.parametrize("name", CASES)
 def test_knn_stage_on_reference_cloud_bit_exact(dev, name, cap, mode):
@@ -239,11 +239,16 @@ def test_knn_stage_on_reference_cloud_bit_exact(dev, name, cap, mode):
     reproduce the reference's kNN survivors and neighbour indices exactly (golden trace), for
     every search strategy and for a fine (r/8) and a cell-cap-coarsened grid."""
     from apn_amd import _lib as L
-    prev = L.load().apn_set_knn_mode(mode)
-    try:
+    if mode == 9:   # the shipped library (mode 9 only)
         _knn_on_reference_cloud(dev, name, cap)
+        return
+    dbg = L.load_debug()   # the earlier strategies live in the debug build only
+    prev = dbg.apn_set_knn_mode(mode)
+    try:
+        with L.using(dbg):
+            _knn_on_reference_cloud(dev, name, cap)
     finally:
-        L.load().apn_set_knn_mode(prev)
+        dbg.apn_set_knn_mode(prev)
 
 
 def _knn_on_reference_cloud(dev, name, cap):
@@ -741,20 +746,26 @@ def test_no_points_fallback(dev):
 def test_knn_modes_identical_full_scene(dev, mode):
     """Full C2 frame (300k points, 640k rays, ~8M in-bbox samples): every kNN search strategy
     gives bit-identical survivor lists (ray, neighbour indices), renders and survivor counts to
-    the single-pass search (size-independent exactness property at the benchmark size)."""
+    the single-pass search (size-independent exactness property at the benchmark size). Modes
+    0-8 run on the debug build (libapn_hip_debug.so); mode 9 on the shipped library."""
     from apn_amd import _lib as L, harness, synthetic as S
     scene = S.make_scene("C2")
     model = harness.build_model(scene, dev)
     rk = scene.render_kwargs(dev)
     t = torch.tensor([scene.cfg.t], device=dev)
     outs = []
+    dbg = L.load_debug()   # the earlier strategies live in the debug build only
     for md in (0, mode):   # mode 0 = the single-pass expanding-ball search
-        prev = L.load().apn_set_knn_mode(md)
+        prev = dbg.apn_set_knn_mode(md)
         try:
-            o = model(t, render_depth=True, render_kwargs=rk, render_weights=True)
+            if md == 9:   # the shipped library
+                o = model(t, render_depth=True, render_kwargs=rk, render_weights=True)
+            else:
+                with L.using(dbg):
+                    o = model(t, render_depth=True, render_kwargs=rk, render_weights=True)
             torch.cuda.synchronize()
         finally:
-            L.load().apn_set_knn_mode(prev)
+            dbg.apn_set_knn_mode(prev)
         st = model.last_stats.resolved()
         ns = st["kept_samples"]
         lists = {k: model._ws.bufs[k][:n * ns].clone() for k, n in (("s_ray", 1), ("s_nbr", 8), ("s_pos", 4))}
@@ -953,10 +964,11 @@ def test_batch_chamfer_loss_2d(golden_model, dev):
 
 @pytest.mark.parametrize("config", ["C2", "C3", "C4"])
 def test_full_size_band_vs_oracle(dev, config):
-    """BASELINE configs C3 (500k points, 32 bones) and C4 (ZJU camera, 1024^2, pose embedding):
-    the full frame on the GPU, then the oracle on two image rows against the GPU's warped cloud
-    (identical sample positions): every output within 1e-5 on every ray whose oracle compositing
-    is not within 1e-6 of a discontinuity (tests/flips.py)."""
+    """BASELINE configs C2 (the headline), C3 (500k points, 32 bones) and C4 (ZJU camera, 1024^2,
+    pose embedding): the full frame on the GPU, then the oracle on image rows against the GPU's
+    warped cloud (identical sample positions) -- C2: 16 evenly spaced rows (12 800 rays, the bench's
+    band), C3 / C4: 4 rows -- every output within 1e-5 on every ray whose oracle compositing is not
+    within 1e-6 of a discontinuity (oracle/flips.py)."""
     import os
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
@@ -969,7 +981,9 @@ def test_full_size_band_vs_oracle(dev, config):
     out = model(t, render_depth=True, render_kwargs=rk, render_weights=True)
     torch.cuda.synchronize()
     H, W = scene.cfg.H, scene.cfg.W
-    sel = torch.cat([torch.arange(r * W, (r + 1) * W) for r in (H // 2 - 40, H // 2 + 40)])
+    n_rows = 16 if config == "C2" else 4
+    stride = H // n_rows
+    sel = torch.cat([torch.arange(r * W, (r + 1) * W) for r in range(stride // 2, H, stride)][:n_rows])
     st = {k: v.detach().cpu() for k, v in model.state_dict().items()}
     orc = O.OracleModel(st, model.canonical_pcd.cpu(), model.bones, stepsize=S.STEPSIZE, voxel_size=S.VOXEL_SIZE,
                         fast_color_thres=S.FAST_COLOR_THRES, pose_embedding_dim=model.pose_embedding_dim,

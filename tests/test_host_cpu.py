@@ -163,3 +163,32 @@ def test_get_rays_of_a_view_pinned_to_reference():
     ro, rd, vd = S.get_rays(H, W, K, c2w)
     assert np.array_equal(rd.numpy(), z["rays_0c00_d"].reshape(-1, 3))
     assert np.array_equal(vd.numpy(), z["rays_0c00_v"].reshape(-1, 3))
+
+
+DEBUG_HEADER = os.path.join(ROOT, "include", "apn_hip_debug.h")
+
+
+def test_product_library_has_no_debug_switches():
+    """The shipped library runs one search strategy / kernel per stage: the debug entry points
+    (include/apn_hip_debug.h) and the environment reads are in libapn_hip_debug.so only."""
+    from apn_amd import _lib
+    lib = _lib.load()
+    txt = re.sub(r"/\*.*?\*/", "", open(DEBUG_HEADER).read(), flags=re.S)
+    dbg_fns = sorted(set(re.findall(r"\b(apn_[a-z0-9_]+)\s*\(", txt)))
+    assert set(dbg_fns) == set(_lib.DEBUG_SIGNATURES), set(dbg_fns) ^ set(_lib.DEBUG_SIGNATURES)
+    for name in dbg_fns:
+        assert not hasattr(lib, name), name
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"getenv" not in data                 # no environment-driven A/B switch in the product
+    assert b"APN_KNN_MODE" not in data and b"APN_MLP_OCC" not in data
+
+
+def test_debug_library_exports_product_and_debug_symbols():
+    from apn_amd import _lib
+    if not os.path.exists(_lib.DEBUG_LIB_PATH):
+        pytest.skip("libapn_hip_debug.so not built")
+    dbg = _lib.load_debug()
+    for name in list(_lib.SIGNATURES) + list(_lib.DEBUG_SIGNATURES):
+        assert hasattr(dbg, name), name
+    assert dbg.apn_version() == b"apn_hip 0.1 gfx950 debug"
+    assert _lib.load().apn_version() == b"apn_hip 0.1 gfx950"

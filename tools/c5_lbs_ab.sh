@@ -1,5 +1,6 @@
 #!/bin/bash
 # C5 LBS A/B of library builds (ab/<tag>/libapn_hip.so, tools/ab_build.sh) x blocks per CU.
+# (APN_LBS_BLOCKS_PER_CU is read by debug builds only: build the variants with -DAPN_DEBUG_BUILD)
 # Usage on the GPU box: VARIANTS="base x" BPCS="8 32" bash tools/c5_lbs_ab.sh
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 for v in ${VARIANTS:-base}; do for bpc in ${BPCS:-32}; do

@@ -2,6 +2,8 @@
 # A/B of environment settings on the C2 bench line (stage ms from HIP events), interleaved.
 # Usage on the GPU box: ENVS="APN_KNN_MODE=9 APN_KNN_MODE=10" ROUNDS=2 bash tools/env_ab.sh [bench args]
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+# the environment switches exist in the debug build only (include/apn_hip_debug.h)
+export APN_HIP_LIB=${APN_HIP_LIB:-$PWD/articulated-point-nerf_amd/apn_amd/libapn_hip_debug.so}
 i=0
 for r in $(seq 1 ${ROUNDS:-2}); do for e in $ENVS; do
   i=$((i+1))
