@@ -525,14 +525,15 @@ static int& mlp_variant() {
 
 // 0 = fp16-split kernel (default), 1 = FP32 MFMA kernel; the debug build also has 2 / 3, the
 // phase-timed builds of each (profiling aid).
+// 4 = the 64-row fp16-split kernel (apn_mlp_h3.hip), the default before the 128-row tiles.
 #ifdef APN_DEBUG_BUILD
-constexpr int kMaxMlpVariant = 3;
+static bool mlp_variant_ok(int v) { return v >= 0 && v <= 5; }
 #else
-constexpr int kMaxMlpVariant = 1;
+static bool mlp_variant_ok(int v) { return v == 0 || v == 1 || v == 4; }
 #endif
 extern "C" int apn_set_mlp_variant(int32_t variant) {
   const int prev = mlp_variant();
-  if (variant >= 0 && variant <= kMaxMlpVariant) mlp_variant() = variant;
+  if (mlp_variant_ok(variant)) mlp_variant() = variant;
   return prev;
 }
 
@@ -547,11 +548,12 @@ extern "C" int apn_point_mlp(const float* s_pos4, const int32_t* s_ray, const in
   if (!s_pos4 || !s_ray || !s_nbr || !n_samples_dev || !recA16 || !recB8 || !feat_proj || !wbuf || !out12 ||
       (!viewdirs && !vemb_const))
     return APN_ERR_ARG;
-  const int64_t ntiles = (max_samples + TS - 1) / TS;
-  // APN_MLP_VARIANT: 0 (default) = 3-term fp16-split MFMA kernel
-  // (apn_mlp_h3.hip; wbuf prepared by apn_mlp_split_weights), 1 = FP32 MFMA kernel (this file),
-  // 2 / 3 = their phase-timed builds (profiling aid; same results).
+  // 0 (default) = 3-term fp16-split MFMA kernel on 128-row tiles (apn_mlp_h4.hip; wbuf prepared by
+  // apn_mlp_split_weights), 1 = FP32 MFMA kernel (this file), 4 = the fp16-split kernel on 64-row
+  // tiles (apn_mlp_h3.hip); debug build: 2 / 3 / 5 = phase-timed builds of 1 / 4 / 0.
   const int variant = mlp_variant();
+  const bool t128 = variant == 0 || variant == 5;
+  const int64_t ntiles = (max_samples + (t128 ? 16 : TS) - 1) / (t128 ? 16 : TS);
   static const int env_blocks = [] {
     const char* e = apn_env("APN_MLP_BLOCKS");
     return e ? atoi(e) : 0;
@@ -574,9 +576,14 @@ extern "C" int apn_point_mlp(const float* s_pos4, const int32_t* s_ray, const in
     launch(k_point_mlp<2, 2, true>, blocks, nullptr);
 #endif
   } else {
-    launch_point_mlp_h3(blocks, variant == 3, (hipStream_t)stream, (const float4*)s_pos4, s_ray, s_nbr,
-                        n_samples_dev, (const float4*)recA16, (const float4*)recB8, (const float4*)feat_proj,
-                        viewdirs, vemb_const, wbuf, eps, act_shift, interval, (float4*)out12);
+    if (t128)
+      launch_point_mlp_h4(blocks, variant == 5, (hipStream_t)stream, (const float4*)s_pos4, s_ray, s_nbr, n_samples_dev,
+                          (const float4*)recA16, (const float4*)recB8, (const float4*)feat_proj, viewdirs, vemb_const,
+                          wbuf, eps, act_shift, interval, (float4*)out12);
+    else
+      launch_point_mlp_h3(blocks, variant == 3, (hipStream_t)stream, (const float4*)s_pos4, s_ray, s_nbr,
+                          n_samples_dev, (const float4*)recA16, (const float4*)recB8, (const float4*)feat_proj,
+                          viewdirs, vemb_const, wbuf, eps, act_shift, interval, (float4*)out12);
     // range fallback (apn_mlp_layout.h OFF_FLAG): the FP32 MFMA kernel redoes the launch iff the
     // split kernel flagged an out-of-fp16-range value; otherwise its workgroups exit at once
     // (8 per CU: a few microseconds). Stream order makes the flag visible; no host sync.
@@ -597,6 +604,7 @@ extern "C" int apn_debug_mlp_phase_cycles(uint64_t* out6) {
   APN_HIP_TRY(hipMemcpyFromSymbol(out6, HIP_SYMBOL(g_mlp_phase), sizeof(uint64_t) * 6));
   static const unsigned long long zero[6] = {0, 0, 0, 0, 0, 0};
   APN_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_mlp_phase), zero, sizeof(zero)));
-  return debug_phase_cycles_h3(out6);
+  APN_TRY(debug_phase_cycles_h3(out6));
+  return debug_phase_cycles_h4(out6);
 }
 #endif  // APN_DEBUG_BUILD

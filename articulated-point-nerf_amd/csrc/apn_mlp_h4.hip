@@ -1,0 +1,620 @@
+// Fused Point-NeRF neighbour MLP (temporalpoints.py:452-519) on fp16 MFMA with the 3-term split
+// (hi*hi + hi*lo + lo*hi, fp32 accumulate; apn_mlp_h3.hip's header explains the arithmetic and the
+// range guard), on 128-row tiles: 16 samples x 8 neighbours per 256-thread workgroup, 2 workgroups
+// per CU.
+//
+// Why 128 rows (apn_mlp_h3.hip runs 64): every wave streams its 66 weight fragments (66 KB: o-tiles
+// 2w, 2w+1 of layers 1-4, o-tile w of the head) from L2 once per tile, so the L2 -> L1 weight
+// stream per MLP row halves (~68 GB per C2 frame at 64 rows), and each fragment load now feeds 48
+// MFMAs instead of 24 -- its L2 latency hides behind one chunk of MFMAs. The head's 16-wide MFMA
+// B tile holds 16 real samples (no padding). Cost: 2 workgroups (8 waves) per CU instead of 3.
+//
+// Layout per workgroup (LDS, 77 KB): one activation buffer X of 128 rows x [hi 128 | lo 128] fp16
+// (512 B rows, 16-B chunks XOR-swizzled by row: conflict-free ds_read_b128 operand reads), reused
+// in place by every layer (a barrier between the last read and the first write), then for the
+// layer-4 output as fp32 rows, then -- after the IDW sums are in registers -- for the 16 head-input
+// rows. Activations are written as whole 16-B chunks: a lane holds 4 consecutive features of a
+// row (the transposed product's C layout), v_permlane16_swap pairs it with the lane holding the
+// next 4 (rows g, g ^ 1 of the lane's 16-lane groups), and the even lane writes the chunk's 8 hi
+// halves, the odd lane its 8 lo halves: one conflict-free ds_write_b128 instead of two 2-way
+// conflicting ds_write_b64 (SQ_LDS_BANK_CONFLICT).
+#include "apn_mlp_split.h"
+
+namespace apn {
+namespace t128 {
+
+using namespace mlpx;
+
+constexpr int TS4 = 16;            // samples per tile
+constexpr int TR4 = TS4 * 8;       // MLP rows per tile
+constexpr int MT = TR4 / 16;       // 16-row M-tiles
+constexpr int HB = 800;            // bytes per head-input row: hi 160 | lo 160 | pad (800/4 = 8 mod 64)
+constexpr int HLO = 320;           // lo offset inside a head-input row
+constexpr int RS = 9;              // floats per row of sRow (8 used; odd stride: conflict-free columns)
+static_assert(TS4 * HB <= TR4 * XB, "head rows alias the activation buffer");
+
+constexpr int SW_B1 = 0, SW_B2 = 128, SW_B3 = 256, SW_B4 = 384, SW_WD = 512, SW_BD = 640, SW_BH = 644,
+              SW_WV2 = 708, SW_BV2 = 900, SW_SC = 904, SW_DS = 912, SW_HSC = 921, SW_TOTAL = 924;
+
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Neighbour records of one gather row (loaded a segment ahead of their use).
+struct GatherRegs {
+  float4 a0, a1, a2, a3, b0, b1;
+  float vv;
+};
+
+// Loads are unconditional (clamped indices; invalid rows read row 0 and are discarded later): a
+// load under a divergent branch makes the compiler drain vmcnt(0) at the join.
+__device__ __forceinline__ void gather_load(int p, int k, int nb, int ray, GatherRegs& G,
+                                            const float4* __restrict__ recA, const float4* __restrict__ recB,
+                                            const float* __restrict__ viewdirs, const float* __restrict__ vemb_const) {
+  const size_t n = (size_t)max(nb, 0);
+  G.a0 = recA[4 * n + 0];
+  G.a1 = recA[4 * n + 1];
+  G.a2 = recA[4 * n + 2];
+  G.a3 = recA[4 * n + 3];
+  G.b0 = recB[2 * n];
+  G.b1 = recB[2 * n + 1];
+  const int e = min(4 * k + p, 26);
+  const int ee = e < 3 ? 0 : (e < 15 ? e - 3 : e - 15);
+  G.vv = vemb_const ? 0.f : viewdirs[3 * (size_t)ray + (e < 3 ? e : ee >> 2)];
+}
+
+// Row r = lane + 64 * HALF of the tile (sample r >> 3, neighbour r & 7); wave P computes quarter P
+// of the row's posenc columns (the reference's dim-major order, apn_mlp_layout.h pe_col_to_ref):
+// P is wave-uniform, so argument indices, frequencies and coordinate choices are compile-time
+// constants. Also writes the row's squared distance (sTo), the direct-blend terms (sRow) and the
+// sample's view-embedding element 4k + P (sV).
+template <int P, int HALF>
+__device__ __forceinline__ void gather_q(int nb, float4 q, const GatherRegs& G, char* __restrict__ PE,
+                                         float* __restrict__ sTo, float* __restrict__ sRow, float* __restrict__ sV,
+                                         const float* __restrict__ vemb_const) {
+  int r_ = (threadIdx.x & 63) + 64 * HALF;
+  asm volatile("" : "+v"(r_));   // per-lane LDS addresses recomputed per tile, not hoisted and spilled
+  const int r = r_, s = r >> 3, k = r & 7;
+  char* xr = PE + r * XB;
+  const int c_sin = (2 * P) ^ (r & 15), c_cos = (2 * P + 1) ^ (r & 15);
+  if (nb >= 0) {
+    const float4 a0 = G.a0, a1 = G.a1, a2 = G.a2, a3 = G.a3;
+    const float dx = q.x - a0.x, dy = q.y - a0.y, dz = q.z - a0.z;
+    // rel_c = Rinv (x - p) (temporalpoints.py:454-458)
+    const float rc[3] = {(a1.x * dx + a1.y * dy) + a1.z * dz, (a1.w * dx + a2.x * dy) + a2.y * dz,
+                         (a2.z * dx + a2.w * dy) + a3.x * dz};
+    if constexpr (P == 0) {
+      sTo[r] = (dx * dx + dy * dy) + dz * dz;
+    } else if constexpr (P == 1) {
+      const float tn = (dx * dx + dy * dy) + dz * dz;
+      float* rw = sRow + RS * r;
+      rw[0] = expf(-(tn * tn) / a0.w);   // temporalpoints.py:461 (to_nn is already squared)
+      rw[1] = a3.y;
+      rw[2] = G.b0.x; rw[3] = G.b0.y; rw[4] = G.b0.z;
+      rw[5] = G.b1.x; rw[6] = G.b1.y; rw[7] = G.b1.z;
+    }
+    f32x4 sv0, sv1, cv0, cv1;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int aa = P + 4 * j;   // reference argument index a = 10 i + f
+      float sv, cv;
+      if (aa < 30) {
+        sincos_pe(rc[aa / 10] * (float)(1 << (aa % 10)), sv, cv);
+      } else {
+        sv = P == 2 ? rc[0] : rc[2];
+        cv = P == 2 ? rc[1] : 0.f;
+      }
+      if (j < 4) { sv0[j] = sv; cv0[j] = cv; } else { sv1[j - 4] = sv; cv1[j - 4] = cv; }
+    }
+    h4 hs0, ls0, hs1, ls1, hc0, lc0, hc1, lc1;
+    split4(sv0, hs0, ls0); split4(sv1, hs1, ls1);
+    split4(cv0, hc0, lc0); split4(cv1, hc1, lc1);
+    *(h8*)(xr + (c_sin << 4)) = __builtin_shufflevector(hs0, hs1, 0, 1, 2, 3, 4, 5, 6, 7);
+    *(h8*)(xr + (c_sin << 4) + 256) = __builtin_shufflevector(ls0, ls1, 0, 1, 2, 3, 4, 5, 6, 7);
+    *(h8*)(xr + (c_cos << 4)) = __builtin_shufflevector(hc0, hc1, 0, 1, 2, 3, 4, 5, 6, 7);
+    *(h8*)(xr + (c_cos << 4) + 256) = __builtin_shufflevector(lc0, lc1, 0, 1, 2, 3, 4, 5, 6, 7);
+    const int e = 4 * k + P;   // view embedding element e of this sample (tineuvox.py:872-878)
+    float v = 0.f;
+    if (e < 27) {
+      if (vemb_const) {
+        v = vemb_const[e];
+      } else {
+        const int ee = e < 3 ? 0 : (e < 15 ? e - 3 : e - 15);
+        float sn_, cs_;
+        sincos_pe(G.vv * (float)(1 << (ee & 3)), sn_, cs_);
+        v = e < 3 ? G.vv : (e < 15 ? sn_ : cs_);
+      }
+    }
+    sV[s * 32 + e] = v;
+  } else {
+    const h8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+    *(h8*)(xr + (c_sin << 4)) = z;
+    *(h8*)(xr + (c_sin << 4) + 256) = z;
+    *(h8*)(xr + (c_cos << 4)) = z;
+    *(h8*)(xr + (c_cos << 4) + 256) = z;
+    sV[s * 32 + 4 * k + P] = 0.f;
+    if constexpr (P == 0) {
+      sTo[r] = 1.f;
+    } else if constexpr (P == 1) {
+      for (int c = 0; c < 8; ++c) sRow[RS * r + c] = 0.f;
+    }
+  }
+}
+
+template <int HALF>
+__device__ __forceinline__ void gather(int p, int nb, float4 q, const GatherRegs& G, char* __restrict__ PE,
+                                       float* __restrict__ sTo, float* __restrict__ sRow, float* __restrict__ sV,
+                                       const float* __restrict__ vemb_const) {
+  switch (p) {
+    case 0: gather_q<0, HALF>(nb, q, G, PE, sTo, sRow, sV, vemb_const); break;
+    case 1: gather_q<1, HALF>(nb, q, G, PE, sTo, sRow, sV, vemb_const); break;
+    case 2: gather_q<2, HALF>(nb, q, G, PE, sTo, sRow, sV, vemb_const); break;
+    default: gather_q<3, HALF>(nb, q, G, PE, sTo, sRow, sV, vemb_const); break;
+  }
+}
+
+// acc[mt][j] += W[o-tile 2w+j] X^T over NQ chunks of 32 and the tile's 8 M-tiles. `a` carries chunk
+// 0 of this matrix's fragments (block FB) in and chunk 0 of the next matrix (block FBN, NQN chunks,
+// NTN o-tiles) out: each chunk's fragments are requested a whole chunk (48 MFMAs) before use. The
+// activation (B) fragments roll one M-tile ahead of their 6 MFMAs.
+template <int NQ, int NQN, int NTN, int FB, int FBN>
+__device__ __forceinline__ void layer_mfma(const char* __restrict__ X, rsrc_t rs, int vb, f32x4 (&acc)[MT][2],
+                                           h8 (&a)[2][2]) {
+  const int lane = threadIdx.x & 63;
+  const int li = lane & 15, g = lane >> 4;
+  h8 bh = *(const h8*)(X + act_off(li, g)), bl = *(const h8*)(X + act_off(li, g) + 256);
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    h8 an[2][2];
+    if (q + 1 < NQ) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, vb, FB + (j * NQ + q + 1) * 2 + pt);
+    } else {
+#pragma unroll
+      for (int j = 0; j < NTN; ++j)
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, vb, FBN + j * NQN * 2 + pt);
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      h8 nbh = bh, nbl = bl;
+      if (mt + 1 < MT || q + 1 < NQ) {
+        const char* p = X + act_off(16 * ((mt + 1) % MT) + li, 4 * (mt + 1 < MT ? q : q + 1) + g);
+        nbh = *(const h8*)p;
+        nbl = *(const h8*)(p + 256);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[mt][j] = mfma3(a[j][0], a[j][1], bh, bl, acc[mt][j]);
+      bh = nbh;
+      bl = nbl;
+    }
+    if (q + 1 < NQ) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) { a[j][0] = an[j][0]; a[j][1] = an[j][1]; }
+    } else {
+#pragma unroll
+      for (int j = 0; j < NTN; ++j) { a[j][0] = an[j][0]; a[j][1] = an[j][1]; }
+    }
+  }
+}
+
+// lrelu(acc [+ bias]) -> the next layer's input rows. Lane (li, g) of (mt, j) holds features
+// 16 (2w + j) + 4g + r of row 16 mt + li; lanes g and g ^ 1 swap halves (v_permlane16_swap) so the
+// even one writes the 16-B chunk's hi halves and the odd one its lo halves. `bias` (layer 1: the
+// unscaled b1 added as fma(acc, 2^-s, b)) or nullptr (layers 2-4: bias in the accumulator; scaled:
+// times 2^-s).
+__device__ __forceinline__ void store_act(char* __restrict__ X, int ot0, const float* __restrict__ bias,
+                                          const f32x4 (&acc)[MT][2], bool scaled, float dsc) {
+  const int lane = threadIdx.x & 63;
+  const int li = lane & 15, g = lane >> 4;
+  const int lo_off = (g & 1) * 256;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int o0 = 16 * (ot0 + j) + 4 * g;
+    const f32x4 bb = bias ? *(const f32x4*)(bias + o0) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const int c = 2 * (ot0 + j) + (g >> 1);   // the chunk holding features of lanes g & ~1, g | 1
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const f32x4 a = acc[mt][j];
+      const f32x4 v = lrelu4(bias ? f32x4{fmaf(a[0], dsc, bb[0]), fmaf(a[1], dsc, bb[1]), fmaf(a[2], dsc, bb[2]),
+                                          fmaf(a[3], dsc, bb[3])}
+                                  : (scaled ? f32x4{a[0] * dsc, a[1] * dsc, a[2] * dsc, a[3] * dsc} : a));
+      h4 hi, lo;
+      split4(v, hi, lo);
+      const u32x2 hb = __builtin_bit_cast(u32x2, hi), lb = __builtin_bit_cast(u32x2, lo);
+      // even row of a 16-lane pair: {own hi, partner hi}; odd row: {partner lo, own lo}
+      const auto s0 = __builtin_amdgcn_permlane16_swap(hb[0], lb[0], false, false);
+      const auto s1 = __builtin_amdgcn_permlane16_swap(hb[1], lb[1], false, false);
+      *(u32x4*)(X + act_off(16 * mt + li, c) + lo_off) = u32x4{s0[0], s1[0], s0[1], s1[1]};
+    }
+  }
+}
+
+__device__ __forceinline__ void init_bias(f32x4 (&acc)[MT][2], int ot0, const float* __restrict__ bias) {
+  const int g = (threadIdx.x & 63) >> 4;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const f32x4 bb = *(const f32x4*)(bias + 16 * (ot0 + j) + 4 * g);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[mt][j] = bb;
+  }
+}
+
+// Phase cycle sums of the timed build (debug library, APN_MLP_VARIANT=5): {gather + loads,
+// layer 1, layers 2-4, epilogue, tiles, whole kernel} over workgroups (wave 0's clock).
+__device__ unsigned long long g_phase4[6];
+
+template <bool SCALED, bool TIMED>
+__device__ __forceinline__ void mlp_tiles(
+    const float4* __restrict__ s_pos, const int* __restrict__ s_ray, const int* __restrict__ s_nbr,
+    const int* __restrict__ n_samples_dev, const float4* __restrict__ recA, const float4* __restrict__ recB,
+    const float4* __restrict__ pproj, const float* __restrict__ viewdirs, const float* __restrict__ vemb_const,
+    const float* __restrict__ wbuf, float eps, float shift, float interval, float4* __restrict__ out,
+    char* const X, float* const sTo, float* const sIdw, float* const sRow, float* const sOut, float* const sV,
+    float* const sW, float* const sPart) {
+  const int nS = *n_samples_dev;
+  const int ntiles = (nS + TS4 - 1) / TS4;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, g = lane >> 4;
+  const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(wbuf + OFF_H16), 0, H_TOTAL * 2 + 4, 0x00020000);
+  const int ot0 = 2 * wid;
+  const int vb = (wid * FR_WAVE * FRAG_HALVES + lane * 8) * 2;
+  const float* const scp = wbuf + OFF_SCALE;
+  for (int i = tid; i < 128; i += MLP_THREADS) {
+    sW[SW_B1 + i] = wbuf[OFF_B1 + i];
+    sW[SW_B2 + i] = SCALED ? wbuf[OFF_B2 + i] * scp[1] : wbuf[OFF_B2 + i];
+    sW[SW_B3 + i] = SCALED ? wbuf[OFF_B3 + i] * scp[2] : wbuf[OFF_B3 + i];
+    sW[SW_B4 + i] = SCALED ? wbuf[OFF_B4 + i] * scp[3] : wbuf[OFF_B4 + i];
+    sW[SW_WD + i] = wbuf[OFF_WD + i];
+  }
+  if (SCALED && tid < 6) {
+    sW[SW_SC + tid] = scp[tid];
+    sW[SW_DS + tid] = 1.f / scp[tid];
+  }
+  if (SCALED && tid == 7) sW[SW_HSC] = scp[5] / scp[4];
+  if (tid < 64) sW[SW_BH + tid] = SCALED ? wbuf[OFF_BH + tid] * scp[5] : wbuf[OFF_BH + tid];
+  if (tid < 192) sW[SW_WV2 + tid] = wbuf[OFF_WV2 + tid];
+  if (tid < 3) sW[SW_BV2 + tid] = wbuf[OFF_BV2 + tid];
+  if (tid == 0) sW[SW_BD] = wbuf[OFF_BD];
+  if (SCALED) __syncthreads();
+  // XCD-aware tile order: XCD x = block % 8 walks a contiguous tile range, so neighbouring samples
+  // (which share neighbour points) gather through the same L2
+  const int nx = (gridDim.x % 8 == 0) ? 8 : 1;
+  const int xcd = blockIdx.x % nx, per_xcd = gridDim.x / nx;
+  const int chunk = (ntiles + nx - 1) / nx;
+  const int t_beg = xcd * chunk, t_end = min(ntiles, t_beg + chunk);
+
+  // next-tile prefetch (unconditional clamped loads): this thread's two gather rows (lane and
+  // lane + 64: neighbour lane & 7 of samples lane >> 3 and 8 + (lane >> 3)) and its 8 P rows
+  int pf_nb[2], pf_ray[2], pf_pn[MT];
+  bool pf_ok[2], pf_pok[MT];
+  float4 pf_q[2];
+  auto fetch = [&](int tl) {
+    const int tc = min(tl, t_end - 1);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int gs = tc * TS4 + 8 * h + (lane >> 3);
+      const int gc = min(gs, nS - 1);
+      pf_ok[h] = tl < t_end && gs < nS;
+      pf_nb[h] = s_nbr[(size_t)gc * 8 + (lane & 7)];
+      pf_q[h] = s_pos[gc];
+      pf_ray[h] = s_ray[gc];
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int m = 16 * mt + li;
+      pf_pok[mt] = tl < t_end && tc * TS4 + (m >> 3) < nS;
+      pf_pn[mt] = s_nbr[min((size_t)tc * TR4 + m, (size_t)nS * 8 - 1)];
+    }
+  };
+  int tile = t_beg + blockIdx.x / nx;
+  if (tile < t_end) fetch(tile);
+  h8 a[2][2];   // carried A-fragment prefetch (chunk 0 of the next weight matrix)
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int pt = 0; pt < 2; ++pt) a[j][pt] = frag(rs, vb, FR_W1E + j * 4 + pt);
+  f32x4 acc[MT][2];
+  bool pok[MT];
+  int prev_s0 = -1;
+  bool range_bad = false;
+  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, tk = 0, tk0 = 0;
+  if (TIMED) tk0 = clock64();
+#define APN_PHASE(i)                          \
+  if (TIMED) {                                \
+    const unsigned long long now = clock64(); \
+    ph[i] += now - tk;                        \
+    tk = now;                                 \
+  }
+  for (; tile < t_end; tile += per_xcd) {
+    const int s0 = tile * TS4;
+    if (TIMED) { tk = clock64(); ph[4] += 1; }
+    // ------------------------------------------------ loads: the gather's records, then the next
+    // tile's indices (vmcnt is in order: what is consumed first is issued first)
+    const int nb0 = pf_ok[0] ? pf_nb[0] : -1, nb1 = pf_ok[1] ? pf_nb[1] : -1;
+    const float4 q0 = pf_q[0], q1 = pf_q[1];
+    GatherRegs g0, g1;
+    gather_load(wid, lane & 7, nb0, pf_ray[0], g0, recA, recB, viewdirs, vemb_const);
+    gather_load(wid, lane & 7, nb1, pf_ray[1], g1, recA, recB, viewdirs, vemb_const);
+    int pn_tile[MT];
+    bool pok_tile[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) { pn_tile[mt] = pf_pn[mt]; pok_tile[mt] = pf_pok[mt]; }
+    fetch(tile + per_xcd);
+    // ------------------------------------------------ gather + posenc + direct-blend terms
+    gather<0>(wid, nb0, q0, g0, X, sTo, sRow, sV, vemb_const);
+    gather<1>(wid, nb1, q1, g1, X, sTo, sRow, sV, vemb_const);
+    // layer-1 accumulators = P[nbr] (global -> VGPR), loaded after the gather's register peak
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      pok[mt] = pok_tile[mt];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const float4 v = pproj[(size_t)max(pn_tile[mt], 0) * (FEAT / 4) + 4 * (ot0 + j) + g];
+        acc[mt][j] = f32x4{v.x, v.y, v.z, v.w};
+      }
+    }
+    if (SCALED) {
+      const float sc1 = sW[SW_SC];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[mt][j] = acc[mt][j] * sc1;
+    }
+    __syncthreads();
+    APN_PHASE(0)
+    // ------------------------------------------------ outputs of the previous tile, IDW weights
+    if (prev_s0 >= 0 && tid < TS4 * 3 && prev_s0 + tid / 3 < nS)
+      out[(size_t)prev_s0 * 3 + tid] = *(const float4*)(sOut + 4 * tid);
+    if (tid < TS4) {  // IDW weights (temporalpoints.py:473-475)
+      float w[8], sum = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        w[k] = __builtin_amdgcn_rcpf(sTo[tid * 8 + k] + eps);   // v_rcp_f32 (1 ulp)
+        sum += w[k];
+      }
+      const float inv = __builtin_amdgcn_rcpf(sum);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sIdw[tid * 8 + k] = w[k] * inv;
+    }
+    if (s0 + TS4 > nS) {   // the last tile only: rows past the last sample loaded P rows of point 0
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          if (!pok[mt]) acc[mt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    // ------------------------------------------------ feat_net: 4 x (Linear + LeakyReLU)
+    layer_mfma<2, 4, 2, FR_W1E, FR_W2>(X, rs, vb, acc, a);
+    __syncthreads();
+    store_act(X, ot0, sW + SW_B1, acc, SCALED, SCALED ? sW[SW_DS + 0] : 1.f);
+    __syncthreads();
+    APN_PHASE(1)
+    init_bias(acc, ot0, sW + SW_B2);
+    layer_mfma<4, 4, 2, FR_W2, FR_W3>(X, rs, vb, acc, a);
+    __syncthreads();
+    store_act(X, ot0, nullptr, acc, SCALED, SCALED ? sW[SW_DS + 1] : 1.f);
+    __syncthreads();
+    init_bias(acc, ot0, sW + SW_B3);
+    layer_mfma<4, 4, 2, FR_W3, FR_W4>(X, rs, vb, acc, a);
+    __syncthreads();
+    store_act(X, ot0, nullptr, acc, SCALED, SCALED ? sW[SW_DS + 2] : 1.f);
+    __syncthreads();
+    init_bias(acc, ot0, sW + SW_B4);
+    layer_mfma<4, 5, 1, FR_W4, FR_WH>(X, rs, vb, acc, a);
+    __syncthreads();
+    // layer-4 output lrelu(acc) as fp32 rows (the IDW sum reads them)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int o0 = 16 * (ot0 + j) + 4 * g;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+        *(f32x4*)(X + out32_off(16 * mt + li, o0 >> 2)) = lrelu4(SCALED ? acc[mt][j] * sW[SW_DS + 3] : acc[mt][j]);
+    }
+    // the head's fragment chunks 1..4 (chunk 0 came with layer 4), a whole IDW phase ahead
+    h8 hfr[KV / 32 - 1][2];
+#pragma unroll
+    for (int q = 1; q < KV / 32; ++q)
+#pragma unroll
+      for (int pt = 0; pt < 2; ++pt) hfr[q - 1][pt] = frag(rs, vb, FR_WH + q * 2 + pt);
+    __syncthreads();
+    APN_PHASE(2)
+    // ------------------------------------------------ IDW sum (temporalpoints.py:493-494) into
+    // registers: thread (sample s, oq) sums features 4 oq .. 4 oq + 3 and 64 + 4 oq .. (chunks oq,
+    // oq + 16: conflict-free ds_read_b128), then the density head
+    const int s_ = tid >> 4, oq = tid & 15;
+    f32x4 h0 = {0.f, 0.f, 0.f, 0.f}, h1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int m = 8 * s_ + k;
+      const f32x4 v0 = *(const f32x4*)(X + out32_off(m, oq));
+      const f32x4 v1 = *(const f32x4*)(X + out32_off(m, oq + 16));
+      const float w = sIdw[m];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        h0[r] = fmaf(w, v0[r], h0[r]);
+        h1[r] = fmaf(w, v1[r], h1[r]);
+      }
+    }
+    {
+      // densitynet Linear(128 -> 1) (tineuvox.py:158) over this thread's 8 features, then the 16 lanes
+      const f32x4 wd0 = *(const f32x4*)(sW + SW_WD + 4 * oq), wd1 = *(const f32x4*)(sW + SW_WD + 64 + 4 * oq);
+      float d = (((h0[0] * wd0[0] + h0[1] * wd0[1]) + h0[2] * wd0[2]) + h0[3] * wd0[3]) +
+                (((h1[0] * wd1[0] + h1[1] * wd1[1]) + h1[2] * wd1[2]) + h1[3] * wd1[3]);
+      d += __shfl_xor(d, 8, 64);
+      d += __shfl_xor(d, 4, 64);
+      d += __shfl_xor(d, 2, 64);
+      d += __shfl_xor(d, 1, 64);
+      if (oq == 0) {  // Raw2Alpha (render_utils_kernel.cu:357-369): (1 + e)^-interval on v_log / v_exp
+        const float e = expf((d + sW[SW_BD]) + shift);
+        sOut[12 * s_ + 3] = 1.f - __builtin_amdgcn_exp2f(-interval * __builtin_amdgcn_logf(1.f + e));
+      }
+      if (SCALED) { h0 = h0 * sW[SW_HSC]; h1 = h1 * sW[SW_HSC]; }
+      // range guard on the last values split (false for NaN too); the flag store waits for the end
+      range_bad |= !(fmaxf(fmaxf(fmaxf(fabsf(h0[0]), fabsf(h0[1])), fmaxf(fabsf(h0[2]), fabsf(h0[3]))),
+                           fmaxf(fmaxf(fabsf(h1[0]), fabsf(h1[1])), fmaxf(fabsf(h1[2]), fabsf(h1[3])))) <= H3_RANGE);
+    }
+    // direct blend + weight-vis colour (temporalpoints.py:459-470, 517-519): waves 1-2, lane =
+    // (sample, quantity); sums over the 8 neighbours in order
+    if (wid == 1 || wid == 2) {
+      const int sl = (wid - 1) * 64 + lane;
+      const int s = sl >> 3, qn = sl & 7;
+      const float* rw = sRow + 8 * RS * s;
+      float sumd = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sumd += rw[RS * k];
+      const float idn = __builtin_amdgcn_rcpf(sumd + 1e-12f);
+      float acc1 = 0.f;
+      if (qn == 0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc1 += (0.125f * rw[RS * k]) * rw[RS * k + 1];
+      } else if (qn < 4) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc1 += (rw[RS * k] * idn) * rw[RS * k + 1 + qn];
+      } else if (qn < 7) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc1 += sIdw[8 * s + k] * rw[RS * k + 1 + qn];
+      }
+      // sOut[s] = {r, g, b, alpha, r_d, g_d, b_d, alpha_d, wr, wg, wb, 0}
+      const int slot = qn == 0 ? 7 : (qn < 4 ? 3 + qn : (qn < 7 ? 4 + qn : 11));
+      sOut[12 * s + slot] = acc1;
+    }
+    __syncthreads();   // every IDW read of X is done: the head rows may overwrite it
+    {
+      // head input row s: [h (128) | view embedding (27) | 0] as hi/lo halves (rows alias X)
+      char* hr = X + s_ * HB;
+      h4 hi0, lo0, hi1, lo1;
+      split4(h0, hi0, lo0);
+      split4(h1, hi1, lo1);
+      *(h4*)(hr + 8 * oq) = hi0;
+      *(h4*)(hr + 128 + 8 * oq) = hi1;
+      *(h4*)(hr + HLO + 8 * oq) = lo0;
+      *(h4*)(hr + HLO + 128 + 8 * oq) = lo1;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int e = 2 * oq + u;
+        const float ve = sV[s_ * 32 + e];
+        const _Float16 vh = (_Float16)ve;
+        *(_Float16*)(hr + 2 * (128 + e)) = vh;
+        *(_Float16*)(hr + HLO + 2 * (128 + e)) = (_Float16)(ve - (float)vh);
+      }
+    }
+    __syncthreads();
+    // ------------------------------------------------ rgb head: folded [h; v] -> 64, ReLU, -> 3, sigmoid
+    {
+      const int o0 = 16 * wid + 4 * g;
+      f32x4 ah = *(const f32x4*)(sW + SW_BH + o0);   // views_linears.0 (folded) bias
+      const char* hr = X + li * HB;                   // B column li = sample li (16 real columns)
+      h8 an[2][2];   // the next tile's W1E chunk 0 (carried across the gather)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, vb, FR_W1E + j * 4 + pt);
+#pragma unroll
+      for (int q = 0; q < KV / 32; ++q) {
+        const h8 bh = *(const h8*)(hr + 16 * (4 * q + g));
+        const h8 bl = *(const h8*)(hr + HLO + 16 * (4 * q + g));
+        ah = q == 0 ? mfma3(a[0][0], a[0][1], bh, bl, ah) : mfma3(hfr[q - 1][0], hfr[q - 1][1], bh, bl, ah);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) { a[j][0] = an[j][0]; a[j][1] = an[j][1]; }
+      // lane (li = sample, g): head features o = 16 wid + 4 g + r
+      float pc[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = fmaxf(SCALED ? ah[r] * sW[SW_DS + 5] : ah[r], 0.f);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) pc[c] += v * sW[SW_WV2 + 64 * c + o0 + r];
+      }
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        pc[c] += __shfl_xor(pc[c], 16, 64);
+        pc[c] += __shfl_xor(pc[c], 32, 64);
+      }
+      if (g == 0) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) sPart[(wid * TS4 + li) * 4 + c] = pc[c];
+      }
+    }
+    __syncthreads();
+    if (tid < TS4 * 3) {  // views_linears.2 bias + sigmoid (temporalpoints.py:513-515)
+      const int s = tid / 3, c = tid % 3;
+      const float v = ((sPart[(0 * TS4 + s) * 4 + c] + sPart[(1 * TS4 + s) * 4 + c]) + sPart[(2 * TS4 + s) * 4 + c]) +
+                      sPart[(3 * TS4 + s) * 4 + c];
+      sOut[12 * s + c] = 1.f / (1.f + expf(-(v + sW[SW_BV2 + c])));
+    }
+    APN_PHASE(3)
+    prev_s0 = s0;
+  }
+#undef APN_PHASE
+  if (TIMED && tid == 0) {
+    ph[5] = clock64() - tk0;
+    for (int i = 0; i < 6; ++i) atomicAdd(&g_phase4[i], ph[i]);
+  }
+  __syncthreads();
+  if (prev_s0 >= 0 && tid < TS4 * 3 && prev_s0 + tid / 3 < nS)
+    out[(size_t)prev_s0 * 3 + tid] = *(const float4*)(sOut + 4 * tid);
+  if (range_bad) __builtin_amdgcn_raw_buffer_store_b32(1, rs, 0, H_TOTAL * 2, 0);   // the range flag (OFF_FLAG)
+}
+
+// One instantiation per weight-scale mode; apn_point_mlp launches both and the one that does not
+// match wbuf's mode exits at once (as does every workgroup once the range flag is set).
+template <bool SCALED, bool TIMED>
+__global__ __launch_bounds__(MLP_THREADS, 2) void k_point_mlp_h4(
+    const float4* __restrict__ s_pos, const int* __restrict__ s_ray, const int* __restrict__ s_nbr,
+    const int* __restrict__ n_samples_dev, const float4* __restrict__ recA, const float4* __restrict__ recB,
+    const float4* __restrict__ pproj, const float* __restrict__ viewdirs, const float* __restrict__ vemb_const,
+    const float* __restrict__ wbuf, float eps, float shift, float interval, float4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) char X[TR4 * XB];
+  __shared__ float sTo[TR4];
+  __shared__ float sIdw[TR4];
+  __shared__ float sRow[TR4 * RS];
+  __shared__ __attribute__((aligned(16))) float sOut[TS4 * 12];
+  __shared__ float sV[TS4 * 32];
+  __shared__ __attribute__((aligned(16))) float sW[SW_TOTAL];
+  __shared__ float sPart[4 * TS4 * 4];
+  __shared__ int s_skip;
+  if (threadIdx.x == 0)
+    s_skip = __builtin_nontemporal_load((const int*)(wbuf + OFF_FLAG)) != 0 || (wbuf[OFF_SCALE + 6] != 0.f) != SCALED;
+  __syncthreads();
+  if (s_skip) return;
+  mlp_tiles<SCALED, TIMED>(s_pos, s_ray, s_nbr, n_samples_dev, recA, recB, pproj, viewdirs, vemb_const, wbuf, eps, shift,
+                    interval, out, X, sTo, sIdw, sRow, sOut, sV, sW, sPart);
+}
+
+}  // namespace t128
+
+void launch_point_mlp_h4(int blocks, bool timed, hipStream_t stream, const float4* s_pos, const int* s_ray, const int* s_nbr,
+                         const int* n_samples_dev, const float4* recA, const float4* recB, const float4* pproj,
+                         const float* viewdirs, const float* vemb_const, const float* wbuf, float eps, float shift,
+                         float interval, float4* out) {
+  auto go = [&](auto kern, int nb) {
+    hipLaunchKernelGGL(kern, dim3(nb), dim3(MLP_THREADS), 0, stream, s_pos, s_ray, s_nbr, n_samples_dev, recA, recB,
+                       pproj, viewdirs, vemb_const, wbuf, eps, shift, interval, out);
+  };
+  const int nb_scaled = blocks < 256 * 8 ? blocks : 256 * 8;
+#ifdef APN_DEBUG_BUILD
+  if (timed) {
+    go(t128::k_point_mlp_h4<false, true>, blocks);
+    go(t128::k_point_mlp_h4<true, true>, nb_scaled);
+    return;
+  }
+#else
+  (void)timed;
+#endif
+  go(t128::k_point_mlp_h4<false, false>, blocks);
+  go(t128::k_point_mlp_h4<true, false>, nb_scaled);
+}
+
+int debug_phase_cycles_h4(uint64_t* out6) {
+  uint64_t v[6];
+  APN_HIP_TRY(hipMemcpyFromSymbol(v, HIP_SYMBOL(t128::g_phase4), sizeof(v)));
+  static const unsigned long long zero[6] = {0, 0, 0, 0, 0, 0};
+  APN_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(t128::g_phase4), zero, sizeof(zero)));
+  for (int i = 0; i < 6; ++i) out6[i] += v[i];
+  return APN_OK;
+}
+
+}  // namespace apn

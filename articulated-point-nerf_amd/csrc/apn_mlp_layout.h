@@ -91,9 +91,15 @@ void launch_point_mlp_h3(int blocks, bool timed, hipStream_t stream, const float
                          const int* s_nbr, const int* n_samples_dev, const float4* recA, const float4* recB,
                          const float4* pproj, const float* viewdirs, const float* vemb_const, const float* wbuf,
                          float eps, float shift, float interval, float4* out);
+// Launcher of the fp16-split kernel on 128-row tiles (apn_mlp_h4.hip).
+void launch_point_mlp_h4(int blocks, bool timed, hipStream_t stream, const float4* s_pos, const int* s_ray, const int* s_nbr,
+                         const int* n_samples_dev, const float4* recA, const float4* recB, const float4* pproj,
+                         const float* viewdirs, const float* vemb_const, const float* wbuf, float eps, float shift,
+                         float interval, float4* out);
 // Largest magnitude the fp16-split kernel carries through its hi/lo halves (fp16 max finite).
 constexpr float H3_RANGE = 65504.f;
 // Adds (and resets) the phase-timed fp16-split kernel's cycle sums into out6.
 int debug_phase_cycles_h3(uint64_t* out6);
+int debug_phase_cycles_h4(uint64_t* out6);
 
 }  // namespace apn

@@ -135,11 +135,16 @@ def flop_per_kept_sample(d_in=191, width=128):
 
 
 def mfma_executed_flop(n_samples, variant=0):
-    """MFMA flops the MLP kernel issues per launch, 4 waves per 8-sample tile.
-    variant 1 (FP32 MFMA): 16x16x4 f32 MFMAs for layer 1 (K=64), layers 2-4 (K=128) and the folded
-    head (16 padded rows, K=160). variant 0 (split): 16x16x32 f16 MFMAs, 3 per 32-wide k chunk
-    and 16x16 output block: layer 1 (2 chunks), layers 2-4 (4 chunks), 8 blocks per wave; head
-    (5 chunks, 1 block)."""
+    """MFMA flops the MLP kernel issues per launch, 4 waves per tile.
+    variant 1 (FP32 MFMA, 8-sample tiles): 16x16x4 f32 MFMAs for layer 1 (K=64), layers 2-4 (K=128)
+    and the folded head (16 padded rows, K=160). Variants 0 / 4 (split, 16- / 8-sample tiles):
+    16x16x32 f16 MFMAs, 3 per 32-wide k chunk and 16x16 output block: layer 1 (2 chunks), layers
+    2-4 (4 chunks), 16 / 8 blocks per wave; head (5 chunks, 1 block)."""
+    if variant in (0, 5):
+        tiles = (n_samples + 15) // 16
+        mfma_per_wave = 3 * (2 * 16 + 3 * 4 * 16 + 5 * 1)
+        assert mfma_per_wave == 687
+        return tiles * 4 * mfma_per_wave * (16 * 16 * 32 * 2)
     tiles = (n_samples + 7) // 8
     if variant in (1, 2):
         steps = lambda k: (k // 16) * 4          # 4 MFMA k-steps per 16-wide chunk
@@ -614,7 +619,7 @@ def main():
     lib = _lib.load()
     debug_lib = hasattr(lib, "apn_debug_knn_stats")   # APN_HIP_LIB = libapn_hip_debug.so (tools/ A/B runs)
     variant = int(lib.apn_set_mlp_variant(-1))        # the library's kernel selection (out of range: query)
-    if debug_lib and variant in (2, 3):   # timed MLP variants of the debug build: per-phase cycle split
+    if debug_lib and variant in (2, 3, 5):   # timed MLP variants of the debug build: per-phase cycle split
         import ctypes
         ph = (ctypes.c_uint64 * 6)()
         _lib.call("apn_debug_mlp_phase_cycles", ph)
@@ -700,7 +705,9 @@ def main():
         kernel, peak, mfma_peak = "k_point_mlp (fp32 MFMA)", FP32_MFMA_PEAK_TFLOPS, FP32_MFMA_PEAK_TFLOPS
         peak_note = "peak = FP32 matrix peak"
     else:
-        kernel, peak, mfma_peak = "k_point_mlp_h3 (3-term fp16-split MFMA)", SPLIT3_PEAK_TFLOPS, FP16_MFMA_PEAK_TFLOPS
+        kernel = ("k_point_mlp_h4 (3-term fp16-split MFMA, 128-row tiles)" if variant in (0, 5)
+                  else "k_point_mlp_h3 (3-term fp16-split MFMA, 64-row tiles)")
+        peak, mfma_peak = SPLIT3_PEAK_TFLOPS, FP16_MFMA_PEAK_TFLOPS
         peak_note = "peak = fp16 dense MFMA peak / 3 (three fp16 MFMA terms per fp32-accurate product)"
     traffic, traffic_src = latest_traffic("point_mlp_traffic")
     ms_per_step = elapsed / args.steps * 1e3
@@ -726,7 +733,7 @@ def main():
         "dtype": "fp32", "data": "synthetic (procedural SMPL-24 capsule cloud, random-init networks)",
         "library": lib.apn_version().decode(),
         "mlp_arithmetic": ("fp32 as 3 fp16 MFMA terms (hi*hi+hi*lo+lo*hi), fp32 accumulate; parity vs the fp32 "
-                           "oracle <= 3e-7 on alpha/rgb" if variant in (0, 3) else "fp32 MFMA (v_mfma_f32_16x16x4_f32)"),
+                           "oracle <= 3e-7 on alpha/rgb" if variant in (0, 3, 4, 5) else "fp32 MFMA (v_mfma_f32_16x16x4_f32)"),
         "config": {"workload": S.CONFIGS[args.config].name + f" ({args.config})", "rays_per_frame": R,
                    "points": scene.cfg.N, "bones": scene.cfg.J, "inbbox_samples": stats.get("inbbox_samples"),
                    "kept_samples": S_kept,

@@ -370,7 +370,7 @@ def _records(orc, t_hat, colors):
     return recA, recB
 
 
-@pytest.mark.parametrize("variant", [0, 1], ids=["split3xfp16", "fp32"])
+@pytest.mark.parametrize("variant", [0, 1, 4], ids=["split3xfp16", "fp32", "split3xfp16_64rows"])
 @pytest.mark.parametrize("name", CASES)
 def test_mlp_stage_vs_oracle(dev, name, variant):
     """apn_point_mlp on the oracle's kept samples: alpha / rgb within 1e-5, the direct blend

@@ -157,7 +157,7 @@ def dev():
     return torch.device("cuda")
 
 
-@pytest.mark.parametrize("variant", [0, 1], ids=["split3xfp16", "fp32"])
+@pytest.mark.parametrize("variant", [0, 1, 4], ids=["split3xfp16", "fp32", "split3xfp16_64rows"])
 @pytest.mark.parametrize("mode", list(MODES))
 @pytest.mark.parametrize("camera", ["dnerf", "zju"])
 def test_mlp_stage_non_fp16_exact(dev, camera, mode, variant):
@@ -180,7 +180,7 @@ def test_mlp_stage_non_fp16_exact(dev, camera, mode, variant):
         o, tr, fallback = run_mlp_stage(dev, m, orc, variant, rk, t)
         f64 = mlp_stage_f64(orc, tr, rk["viewdirs"])
     check_stage(o, tr, f"{camera}/{mode}/v{variant} fallback={fallback}", f64)
-    if variant == 0:
+    if variant in (0, 4):
         # the guard fires exactly when a split value leaves the fp16 range
         assert fallback == (mode == "overflow"), fallback
 
