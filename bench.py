@@ -709,6 +709,9 @@ def main():
                   else "k_point_mlp_h3 (3-term fp16-split MFMA, 64-row tiles)")
         peak, mfma_peak = SPLIT3_PEAK_TFLOPS, FP16_MFMA_PEAK_TFLOPS
         peak_note = "peak = fp16 dense MFMA peak / 3 (three fp16 MFMA terms per fp32-accurate product)"
+    from apn_amd.ops import mlp_range_fallback
+    # the split kernel's range guard hands a launch to the FP32 MFMA kernel; the line says if it fired
+    mlp_fallback = bool(mlp_range_fallback(model._ws.bufs["mlp_w"])) if "mlp_w" in model._ws.bufs else None
     traffic, traffic_src = latest_traffic("point_mlp_traffic")
     ms_per_step = elapsed / args.steps * 1e3
     frame_roof = frame_roofline(scene.cfg.N, scene.cfg.J, R, kept_total * flop_per_kept_sample(d_in), ms_per_step,
@@ -746,7 +749,8 @@ def main():
                              "all-gather" if shard_rays else
                              "whole frame replayed as one HIP graph (TemporalPoints.capture_frame)") if use_graph
                             else "eager launches"),
-                   "timed_frames_overflowed": overflowed},
+                   "timed_frames_overflowed": overflowed,
+                   "mlp_fp32_fallback_fired": mlp_fallback},
         "roofline": {"bound": "mfma", "kernel": kernel, "achieved": achieved, "peak": peak,
                      "unit": "TFLOP/s", "frac": achieved / peak,
                      "traffic": traffic.get("bytes_per_launch") if traffic else None,

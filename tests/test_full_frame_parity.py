@@ -38,6 +38,8 @@ def c2_frame():
     finally:
         model._force_exact = False
     st = model.last_stats.resolved()
+    from apn_amd.ops import mlp_range_fallback
+    assert not mlp_range_fallback(model._ws.bufs["mlp_w"])   # no FP32 re-run: the split kernel's own frame
     nq, ns = st["inbbox_samples"], st["kept_samples"]
     ws = model._ws.bufs
     fr = {

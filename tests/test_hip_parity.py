@@ -980,6 +980,10 @@ def test_full_size_band_vs_oracle(dev, config):
     t = torch.tensor([scene.cfg.t], device=dev)
     out = model(t, render_depth=True, render_kwargs=rk, render_weights=True)
     torch.cuda.synchronize()
+    from apn_amd.ops import mlp_range_fallback
+    # the split-MFMA kernel itself produced the frame: its range guard did not hand it to the FP32
+    # re-run (which would also hide a wrong split-kernel result behind a correct frame)
+    assert not mlp_range_fallback(model._ws.bufs["mlp_w"])
     H, W = scene.cfg.H, scene.cfg.W
     n_rows = 16 if config == "C2" else 4
     stride = H // n_rows
