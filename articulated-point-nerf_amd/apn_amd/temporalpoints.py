@@ -213,6 +213,14 @@ def weights_from_bones(joints, bones, pcd, eps):
     return torch.cat([torch.zeros((len(w), 1)), w], dim=-1)
 
 
+def _collect_graphs():
+    """Destroy unreachable HIP graphs now, before a capture starts: a graph freed by the cyclic
+    garbage collector in the middle of another capture (an earlier step's closure cycle) would call
+    hipGraphExecDestroy while the stream is capturing, which HIP refuses (the process aborts)."""
+    import gc
+    gc.collect()
+
+
 def _grow_capacity(n):
     """In-bbox sample capacity for a frame of n samples: 25 % headroom, 64k granules."""
     return max(65536, (int(n * 1.25) + 65535) // 65536 * 65536)
@@ -513,6 +521,7 @@ class TemporalPoints(torch.nn.Module):
             with torch.cuda.stream(side):   # warm-up: caches, workspaces, packed buffers
                 self.repose(rp)
             torch.cuda.current_stream(dev).wait_stream(side)
+            _collect_graphs()
             graph = torch.cuda.CUDAGraph()
             self._ws.hold(graph)   # the graph holds workspace addresses from here on
             with torch.cuda.graph(graph):
@@ -591,6 +600,7 @@ class TemporalPoints(torch.nn.Module):
                     raise RuntimeError("capture_frame: no sample capacity for this ray set (empty frame?)")
                 st.pop("graph", None)   # a re-capture: drop the old graph first (its retired buffers go with it)
                 step.graph = None
+                _collect_graphs()
                 graph = torch.cuda.CUDAGraph()
                 self._ws.hold(graph)   # the graph holds workspace addresses from here on
                 with torch.cuda.graph(graph, capture_error_mode=capture_error_mode):

@@ -229,3 +229,32 @@ def test_captured_shard_overflow_recaptures_and_releases(dev, monkeypatch):
         gc.collect()
         assert len(model._ws._holders) == 1
         assert len(model._ws.retired) <= max(n_retired, 16), len(model._ws.retired)
+
+
+def test_successive_captures_with_aggressive_gc(dev):
+    """tools/shard_balance.py captured one graph per ray shard in a loop and aborted at world 8:
+    the previous shard's step (a closure cycle holding its graph) was freed by the cyclic garbage
+    collector in the middle of the next capture, and hipGraphExecDestroy is refused while a stream
+    captures. capture_frame now collects unreachable graphs before it captures. With the collector
+    set to run at almost every allocation, successive captures (each dropping the previous step)
+    must all succeed and replay the eager shard frames."""
+    import gc
+    from apn_amd.shard import RAY_BLOCK
+    scene, model = _scene_model(dev)
+    rk = scene.render_kwargs(dev)
+    t = torch.tensor([scene.cfg.t], device=dev)
+    world = 4
+    old = gc.get_threshold()
+    gc.set_threshold(1, 1, 1)
+    try:
+        step = None
+        for k in range(world):
+            step = model.capture_frame(t, rk, ray_shard=(k, world, RAY_BLOCK))   # drops the previous step
+            got = {key: step(t)[key].clone() for key in KEYS}
+            with torch.no_grad():
+                ref = model(t, render_depth=True, render_kwargs=rk, render_weights=True,
+                            ray_shard=(k, world, RAY_BLOCK))
+            for key in KEYS:
+                assert torch.equal(got[key], ref[key]), (k, key)
+    finally:
+        gc.set_threshold(*old)
