@@ -1,5 +1,8 @@
 // Device-wide exclusive prefix sum of int32 counts (rays, grid cells, kNN blocks).
-// Three launches: per-block totals -> one-workgroup scan of the totals -> per-block scan.
+// Per-block totals, then per-block scans that add the sum of the preceding blocks' totals -- each
+// block sums them itself (nb <= SCAN_DIRECT_MAX blocks: every scan of the render frame, up to 8M
+// elements), so two launches instead of three (the one-workgroup scan of the totals was a
+// launch of its own, ~5 us of latency per scan). Larger inputs keep the three-launch form.
 // Deterministic (no atomics), so every consumer sees the same offsets run to run.
 #include "apn_common.h"
 
@@ -98,6 +101,48 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_block_apply(const int* __re
   if (blockIdx.x == nb - 1 && threadIdx.x == 0) out[n] = totals[nb];
 }
 
+// The per-block scan with the block's offset = sum of totals[0 .. b-1], reduced by the block itself.
+constexpr int SCAN_DIRECT_MAX = 4096;
+__global__ __launch_bounds__(SCAN_THREADS) void scan_block_apply_direct(const int* __restrict__ in, int64_t n,
+                                                                        const int* __restrict__ totals,
+                                                                        int* __restrict__ out, int nb) {
+  __shared__ int lw[SCAN_THREADS / 64];
+  __shared__ int red[SCAN_THREADS / 64];
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // offset of this block (and, in the last block, the grand total): integer sums, any order is exact
+  const int lim = b == nb - 1 ? nb : b;
+  int part = 0;
+  for (int i = threadIdx.x; i < lim; i += SCAN_THREADS) part += totals[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+  if (lane == 0) red[wid] = part;
+  const int64_t base = (int64_t)b * SCAN_TILE + threadIdx.x * SCAN_ITEMS;
+  int v[SCAN_ITEMS];
+  int s = 0;
+#pragma unroll
+  for (int i = 0; i < SCAN_ITEMS; ++i) {
+    v[i] = (base + i < n) ? in[base + i] : 0;
+    s += v[i];
+  }
+  int tot;
+  const int excl = block_excl_scan(s, lw, &tot);   // its barriers also publish red[]
+  int off = 0;
+#pragma unroll
+  for (int w = 0; w < SCAN_THREADS / 64; ++w) off += red[w];
+  // the last block summed all nb totals: its own offset is that minus its own total
+  if (b == nb - 1) {
+    if (threadIdx.x == 0) out[n] = off;
+    off -= tot;
+  }
+  int run = excl + off;
+#pragma unroll
+  for (int i = 0; i < SCAN_ITEMS; ++i) {
+    if (base + i < n) out[base + i] = run;
+    run += v[i];
+  }
+}
+
 size_t scan_workspace_bytes(int64_t n) {
   int64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
   return (size_t)(nb + 1) * sizeof(int);
@@ -111,6 +156,10 @@ int scan_exclusive_i32(const int* in, int* out, int64_t n, void* ws, hipStream_t
   int nb = ceil_div(n, SCAN_TILE);
   int* totals = (int*)ws;
   hipLaunchKernelGGL(scan_block_totals, dim3(nb), dim3(SCAN_THREADS), 0, s, in, n, totals);
+  if (nb <= SCAN_DIRECT_MAX) {
+    hipLaunchKernelGGL(scan_block_apply_direct, dim3(nb), dim3(SCAN_THREADS), 0, s, in, n, totals, out, nb);
+    return launch_status();
+  }
   hipLaunchKernelGGL(scan_totals_single, dim3(1), dim3(1024), 0, s, totals, nb);
   hipLaunchKernelGGL(scan_block_apply, dim3(nb), dim3(SCAN_THREADS), 0, s, in, n, totals, out, nb);
   return launch_status();

@@ -1369,3 +1369,20 @@ def test_lbs_train_kernel_vs_torch_autograd(dev, J):
     for name, a, b in zip(("W", "theta", "T", "global_t"), grad_f, grad_t):
         assert a is not None and b is not None, name
         assert float((a - b).abs().max()) <= 1e-4 * float(b.abs().max()), (name, float((a - b).abs().max()))
+
+
+@pytest.mark.parametrize("n", [1, 7, 2047, 2048, 2049, 300_001, 1 << 20, 9_000_001])
+def test_scan_exclusive_matches_cumsum(dev, n):
+    """apn_scan_exclusive_i32 (grid cells, rays, kNN blocks): the two-launch form (<= 4096 blocks of
+    2048) and the three-launch form (9M elements) against numpy's cumulative sum, with the total in
+    out[n]."""
+    from apn_amd import _lib as L
+    rng = np.random.default_rng(n)
+    x = rng.integers(0, 50, n, dtype=np.int32)
+    x[rng.random(n) < 0.3] = 0
+    xin = torch.from_numpy(x).to(dev)
+    out = torch.full((n + 1,), -7, dtype=torch.int32, device=dev)
+    ws = torch.empty(int(L.load().apn_scan_workspace_bytes(n)) + 256, dtype=torch.uint8, device=dev)
+    L.call("apn_scan_exclusive_i32", L.ptr(xin), L.ptr(out), n, L.ptr(ws), L.stream_ptr(dev))
+    ref = np.concatenate([[0], np.cumsum(x, dtype=np.int64)]).astype(np.int32)
+    assert np.array_equal(out.cpu().numpy(), ref)
