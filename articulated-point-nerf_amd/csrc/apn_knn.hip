@@ -178,7 +178,10 @@ constexpr bool kBufferPoints = false;
 constexpr bool kBufferPoints = true;
 #endif
 // Buffer-descriptor loads for the ball scans: 32-bit byte offsets (no 64-bit address arithmetic per
-// load); reads past num_records return zeros.
+// load); reads past num_records return zeros. num_records and offsets are int32 byte counts, so a
+// cloud of more than KNN_MAX_POINTS points (16 B each) would wrap and read zeros: apn_grid_build
+// and apn_knn_radius refuse such clouds (APN_ERR_ARG) rather than return a wrong kNN.
+constexpr int64_t KNN_MAX_POINTS = 0x7fffffffLL / 16;
 typedef float knn_f4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t knn_rsrc(const void* p, int bytes) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, bytes, 0x00020000);
@@ -2127,6 +2130,7 @@ static GridWs grid_ws(void* ws, int64_t N, int cap) {
 extern "C" int apn_grid_build(const float* xyz, int64_t n_points, const int32_t* bbox_ord, float query_radius,
                               int32_t cell_cap, float* sorted_pts4, void* workspace, void* stream) {
   if (n_points <= 0 || cell_cap <= 0 || !xyz || !bbox_ord || !sorted_pts4 || !workspace) return APN_ERR_ARG;
+  if (n_points > KNN_MAX_POINTS) return APN_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   GridWs w = grid_ws(workspace, n_points, cell_cap);
   APN_TRY(fill4_i32(w.counts, cell_cap, w.cursor, cell_cap, nullptr, 0, nullptr, 0, s));
@@ -2167,6 +2171,7 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
                               void* stream) {
   (void)query_radius;  // the grid was built for it (GridParams.r2)
   if (n_queries < 0 || !grid_workspace || !workspace) return APN_ERR_ARG;
+  if (n_points > KNN_MAX_POINTS) return APN_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   if (n_queries == 0) {
     APN_TRY(fill_i32(n_survivors_dev, 0, 1, s));

@@ -470,6 +470,44 @@ def latest_traffic(stem):
     return None, None
 
 
+def knn_report(model, S_kept, inbbox, knn_ms):
+    """The kNN next to its work (apn_amd/knn_work.py): the perfect-scan work of
+    this frame's survivors and its VALU-issue floor, and the executed VALU instructions of the kNN
+    kernels from the newest committed PMC summary (labelled with its file: not measured in this run)."""
+    from apn_amd.knn_work import knn_work, valu_issue_ms
+    import glob
+    bufs = model._ws.bufs
+    if not all(k in bufs for k in ("sorted4", "s_pos", "s_nbr")) or S_kept <= 0:
+        return None
+    s4 = bufs["sorted4"].view(-1, 4)
+    idx = s4[:, 3].contiguous().view(torch.int32).long()
+    cloud = torch.empty(s4.shape[0], 3, device=s4.device)
+    cloud[idx] = s4[:, :3]
+    w = knn_work(cloud, bufs["s_pos"].view(-1, 4)[:S_kept, :3], bufs["s_nbr"].view(-1, 8)[:S_kept],
+                 0.01)   # the frame's query_radius (forward's default, which bench renders with)
+    out = {"ms": round(knn_ms, 4), "queries": inbbox, "survivors": S_kept, "perfect_scan": w,
+           "note": "perfect scan = survivors' final-ball x-chord rows/points on an r/8 grid (7 VALU lane ops per "
+                   "point, 4 per row), rejected samples 0 points; floor_ms = its VALU issue time at the PMC clock"}
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_summary_c2*.json")))
+    for path in reversed(files):
+        pmc = read_traffic(path) or {}
+        ks = {k: v for k, v in pmc.items() if ("knn" in k or "cell_bound" in k or "classify" in k)
+              and "SQ_INSTS_VALU" in v}
+        if not ks:
+            continue
+        clk = max(v.get("eff_clock_GHz", 2.4) for v in ks.values())
+        insts = sum(v["SQ_INSTS_VALU"] for v in ks.values())
+        out.update({"floor_ms": round(valu_issue_ms(w["valu_lane_ops"], clk), 4),
+                    "executed_valu_insts": insts,
+                    "executed_issue_ms": round(insts * 2 / 1024 / (clk * 1e9) * 1e3, 4),
+                    "lane_efficiency": w["valu_lane_ops"] / (64 * insts),
+                    "pmc_source": os.path.relpath(path, ROOT) + " (kNN kernels' SQ_INSTS_VALU per launch, "
+                                                                 "earlier run of this build's kernels)"})
+        out["floor_frac"] = out["floor_ms"] / knn_ms if knn_ms > 0 else None
+        break
+    return out
+
+
 def read_traffic(path):
     try:
         with open(path) as f:
@@ -725,6 +763,12 @@ def main():
             same = same_cloud_error(out, rk, model.last_palette_perm, orc, sub, t_cpu, sel)
         except Exception as e:  # never lose the GPU line over the baseline leg
             log(f"cpu baseline failed: {e!r}")
+    knn = None
+    if world == 1:
+        try:
+            knn = knn_report(model, S_kept, stats.get("inbbox_samples"), stage_ms.get("knn", 0.0))
+        except Exception as e:  # never lose the GPU line over a diagnostic
+            log(f"knn work report failed: {e!r}")
     others = None
     if world == 1 and args.config == "C2" and not args.no_other_configs:
         others = other_configs(dev)
@@ -768,6 +812,7 @@ def main():
         "frame_roofline_frac": frame_roof["frac"],
         "frame_roofline": frame_roof,
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
+        **({"knn": knn} if knn is not None else {}),
         **({"shards": shard_diag} if shard_diag is not None else {}),
         "cpu_baseline": cpu,
         "psnr_vs_oracle": psnr,

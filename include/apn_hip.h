@@ -228,7 +228,9 @@ int apn_inbbox_fill_capped(const float* rays_o, const float* rays_d, const float
                            void* stream);
 
 /* Uniform grid over the warped cloud (cell >= sqrt(query_radius)): counting sort into
- * sorted_pts4 [N,4] {x,y,z,bits(idx)}. cell_cap bounds the number of cells. */
+ * sorted_pts4 [N,4] {x,y,z,bits(idx)}. cell_cap bounds the number of cells. The ball scans
+ * address the cloud with 32-bit byte offsets: n_points > 2^27 - 1 is APN_ERR_ARG here and in
+ * apn_knn_radius. */
 size_t apn_grid_workspace_bytes(int64_t n_points, int32_t cell_cap);
 int apn_grid_build(const float* xyz, int64_t n_points, const int32_t* bbox_ord, float query_radius,
                    int32_t cell_cap, float* sorted_pts4, void* workspace, void* stream);

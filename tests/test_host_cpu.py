@@ -61,6 +61,13 @@ def test_invalid_arguments_rejected_without_gpu():
     assert lib.apn_lbs_skin(None, None, 0, 0, None, 0.0, None, None, None, None, None, None, None, 0.0, 0,
                             None, None, None, None, None, None, None, None) == 1
     assert lib.apn_lbs_workspace_bytes(300_000) == 6 * 4 * ((300_000 + 63) // 64)   # one partial per 64-point block
+    # clouds past the 32-bit buffer-descriptor range are refused before any device work
+    import ctypes
+    buf = ctypes.create_string_buffer(64)
+    p = ctypes.cast(buf, ctypes.c_void_p)
+    big = 1 << 27
+    assert lib.apn_grid_build(p, big, p, 0.01, 1024, p, p, None) == 1
+    assert lib.apn_knn_radius(p, p, 16, p, p, big, 1024, p, 0.01, p, p, p, p, p, None) == 1
 
 
 def test_missing_library_fails_loudly(monkeypatch):
