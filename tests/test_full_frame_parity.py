@@ -9,7 +9,10 @@ stage-wise and bit-exact, over the WHOLE frame rather than a band:
   re-ranked in float32, every full window certified or re-searched over its whole ball:
   oracle.apn_oracle.knn_radius_certified) over all ~8M in-bbox samples on the GPU's warped cloud
   (temporalpoints.py:433-447). The frame runs the shipped library's mode 9 (fine-grid pass A,
-  anisotropic-grid pass B, cost-ranked lanes)."""
+  anisotropic-grid pass B, cost-ranked lanes);
+* ray shards of that frame (the "blocks" split at 4 and 8 ranks, ~2M and ~1M in-bbox samples: the
+  launch sizes where the kNN orders its workgroups heavy-first and the cell bounds run 16 lanes
+  per cell): every survivor of a shard equals the full frame's survivor of the same ray and step."""
 import numpy as np
 import pytest
 import torch
@@ -51,7 +54,7 @@ def c2_frame():
         "s_pos": ws["s_pos"][:4 * ns].view(ns, 4).cpu().numpy(),
         "s_ray": ws["s_ray"][:ns].cpu().numpy(),
         "s_nbr": ws["s_nbr"][:8 * ns].view(ns, 8).cpu().numpy(),
-        "nq": nq, "ns": ns,
+        "nq": nq, "ns": ns, "model": model, "t": t, "rk_dev": rk,
     }
     return fr
 
@@ -82,3 +85,31 @@ def test_c2_full_frame_knn_survivors_bit_exact(c2_frame):
     assert np.array_equal(fr["s_ray"], fr["q_ray"][keep])
     assert np.array_equal(fr["s_pos"], q[keep])
     assert np.array_equal(fr["s_nbr"], idx[keep].astype(np.int32))
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_c2_ray_block_shard_knn_matches_full_frame(c2_frame, world):
+    from apn_amd.shard import RAY_BLOCK
+    fr = c2_frame
+    m = fr["model"]
+    m._force_exact = True
+    try:
+        with torch.no_grad():
+            m(fr["t"], render_depth=True, render_kwargs=fr["rk_dev"], render_weights=True,
+              ray_shard=(world - 1, world, RAY_BLOCK))
+        torch.cuda.synchronize()
+    finally:
+        m._force_exact = False
+    st = m.last_stats.resolved()
+    nq, ns = st["inbbox_samples"], st["kept_samples"]
+    assert (1 << 18) < nq <= (3 << 20)          # above the small-batch pass B, below the one-lane cell bounds
+    ws = m._ws.bufs
+    rays = m.last_ray_index.cpu().numpy()      # global ray of each local ray (ascending)
+    s_ray = rays[ws["s_ray"][:ns].cpu().numpy()]
+    s_pos = ws["s_pos"][:4 * ns].view(ns, 4).cpu().numpy()
+    s_nbr = ws["s_nbr"][:8 * ns].view(ns, 8).cpu().numpy()
+    sel = np.isin(fr["s_ray"], rays)
+    assert ns == int(sel.sum()) > 100_000
+    assert np.array_equal(s_ray, fr["s_ray"][sel])
+    assert np.array_equal(s_pos, fr["s_pos"][sel])
+    assert np.array_equal(s_nbr, fr["s_nbr"][sel])
