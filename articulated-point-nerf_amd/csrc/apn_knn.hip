@@ -342,6 +342,7 @@ struct KeyList {
     for (int k = 0; k < K; ++k) kk[k] = knn_key(INFINITY, 0x7fffffff);
   }
   __device__ __forceinline__ float worst() const { return __uint_as_float((unsigned)(kk[K - 1] >> 32)); }
+  __device__ __forceinline__ float dist(int k) const { return __uint_as_float((unsigned)(kk[k] >> 32)); }
   __device__ __forceinline__ int index(int k) const { return (int)(unsigned)kk[k]; }
   template <bool DUP>
   __device__ __forceinline__ void insert(float d, int id) {
@@ -376,6 +377,7 @@ struct PairList {
     for (int k = 0; k < K; ++k) { bd[k] = INFINITY; bi[k] = 0x7fffffff; }
   }
   __device__ __forceinline__ float worst() const { return bd[K - 1]; }
+  __device__ __forceinline__ float dist(int k) const { return bd[k]; }
   __device__ __forceinline__ int index(int k) const { return bi[k]; }
   template <bool DUP>
   __device__ __forceinline__ void insert(float d, int id) {
@@ -1161,11 +1163,12 @@ __global__ void k_agrid_scatter(const float4* __restrict__ sorted, int64_t N, co
 
 // scan_ball_flat2 on the anisotropic grid (cell sides hx, hy, hz): the same lock-step row/point
 // state machine, nearest-first slabs, running K-th-best culling with 1e-4 slack.
-// PTS points per point step (2 or 4).
-template <int K, bool STATS, int PTS, bool DUP, class L>
+// PTS points per point step (2 or 4). S > 1: one of S lanes sharing the query, walking the y slots
+// slice, slice + S, ... of every slab (as scan_ball_flat2_l).
+template <int K, bool STATS, int PTS, bool DUP, class L, int S = 1>
 __device__ __forceinline__ void scan_ball_aniso_l(const AGrid& g, const int* __restrict__ cell_start,
                                                   const float4* __restrict__ sorted, float qx, float qy, float qz,
-                                                  float R2, L& lst, unsigned* ctr = nullptr) {
+                                                  float R2, L& lst, unsigned* ctr = nullptr, int slice = 0) {
   const float R = bound_sqrt(R2);
   const __amdgpu_buffer_rsrc_t prs = knn_rsrc(sorted, g.np * 16);
   const __amdgpu_buffer_rsrc_t crs = knn_rsrc(cell_start, (g.nf + 1) * 4);
@@ -1213,7 +1216,7 @@ __device__ __forceinline__ void scan_ball_aniso_l(const AGrid& g, const int* __r
       const float tau = fminf(lst.worst(), R2) * 1.0001f;
       if (iy >= nyz) {
         ++iz;
-        iy = 0;
+        iy = S == 1 ? 0 : slice;
         nyz = 0;
         if (iz < nz) {
           z = fz + nf_offset(iz);
@@ -1227,7 +1230,7 @@ __device__ __forceinline__ void scan_ball_aniso_l(const AGrid& g, const int* __r
         }
       } else {
         const int y = fy + nf_offset(iy);
-        ++iy;
+        iy += S;
         if (y >= y0 && y <= y1) {
           const float dyz2 = dz2 + slab_d2(qy, g.oy, g.hy, y, y);
           if (dyz2 <= tau) {
@@ -1367,6 +1370,7 @@ __global__ __launch_bounds__(KNN_THREADS) void k_cell_bound3(const GridParams* _
 // On a full frame the list is long and the plain kernel is load-throughput bound (the 16-lane
 // form measured 2x slower there), so apn_knn_radius picks by query count.
 constexpr int CB_LANES = 16;
+template <int CB_LANES>
 __global__ __launch_bounds__(KNN_THREADS) void k_cell_bound3w(const GridParams* __restrict__ gp,
                                                              const int* __restrict__ cell_start,
                                                              const int* __restrict__ list,
@@ -1493,7 +1497,7 @@ __global__ __launch_bounds__(ORDER_THREADS) void k_order_blocks(const int* __res
 #ifdef APN_KNN_B_W7   // A/B: pass B at the compiler's 68 VGPRs
 #define APN_KNN_PASS_B_ATTR
 #else
-#define APN_KNN_PASS_B_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))
+#define APN_KNN_PASS_B_ATTR __attribute__((amdgpu_waves_per_eu(PTS > 4 ? 4 : 8, 8)))
 #endif
 #ifndef APN_KNN_A_PTS
 #define APN_KNN_A_PTS 4
@@ -2018,6 +2022,101 @@ __global__ __launch_bounds__(KNN_THREADS) APN_KNN_PASS_B_ATTR void k_knn_pass_b9
   }
 }
 
+#ifdef APN_DEBUG_BUILD   // measured and not kept: S lanes per hard query of pass B (APN_KNN_B_LANES)
+template <int S, class L>
+__device__ __forceinline__ void group_merge_list(L& lst) {
+  const L snap = lst;
+  const int lane = threadIdx.x & 63, base = lane & ~(S - 1), me = lane & (S - 1);
+#pragma unroll
+  for (int o = 1; o < S; ++o) {
+    const int src = base | ((me + o) & (S - 1));
+#pragma unroll
+    for (int k = 0; k < KNN_K; ++k) {
+      const float d = __shfl(snap.dist(k), src, 64);
+      const int id = __shfl(snap.index(k), src, 64);
+      lst.template insert<true>(d, id);
+    }
+  }
+}
+
+// k_knn_pass_b9 with S lanes per hard query: each lane walks its share of every slab's rows
+// (scan_ball_aniso_l's slices), the lists are merged after each ball (pruning with the lane-local
+// K-th best is exact), lane 0 writes. Workgroup b covers part b % S of list block perm[b / S].
+template <int S, int PTS>
+__global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_b9s(
+    const float4* __restrict__ q_pos, const int* __restrict__ cand, const int* __restrict__ hard,
+    const int* __restrict__ n_hard, const int* __restrict__ hard2, const int* __restrict__ n_hard2,
+    const AGrid* __restrict__ agp, const int* __restrict__ cell_start2, const float4* __restrict__ sorted2,
+    int* __restrict__ flag, int* __restrict__ t_nbr, const int* __restrict__ perm, const int* __restrict__ ccell,
+    const int* __restrict__ u1, const int* __restrict__ u2) {
+  constexpr int NQ = KNN_THREADS / S;
+  const int blk = blockIdx.x / S, part = blockIdx.x % S;
+  const int base = (perm ? perm[blk] : blk) * KNN_THREADS + part * NQ;
+  const int n1 = *n_hard, n2 = hard2 ? *n_hard2 : 0;
+  if (base >= n1 + n2) return;
+  const int tid = threadIdx.x, grp = tid / S, slice = tid & (S - 1);
+  int i = base + grp;
+  if (kSortB && ccell) {
+    __shared__ unsigned skey[NQ];
+    if (tid < NQ) {
+      unsigned w = 0;
+      const int e = base + tid;
+      if (e < n1 + n2) {
+        const int hc = e < n1 ? hard[e] : hard2[e - n1];
+        const int cell = ccell[hc >> 1];
+        w = (hc & 1) ? (unsigned)u1[cell] : (unsigned)(u2[cell] + u1[cell]);
+      }
+      skey[tid] = ((0xffffffu - min(w, 0xffffffu)) << 8) | (unsigned)tid;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 2; k <= NQ; k <<= 1) {
+#pragma unroll
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        const int p = tid ^ j;
+        if (tid < NQ && p > tid) {
+          const unsigned a = skey[tid], b = skey[p];
+          if ((a > b) == ((tid & k) == 0)) { skey[tid] = b; skey[p] = a; }
+        }
+        __syncthreads();
+      }
+    }
+    i = base + (int)(skey[grp] & 0xffu);
+  }
+  if (i >= n1 + n2) return;
+  const AGrid g = *agp;
+  const int hc = i < n1 ? hard[i] : hard2[i - n1];
+  const int c = hc >> 1;
+  const float4 q = q_pos[cand[c]];
+  KnnList lst;
+  lst.init();
+  bool first = true;
+  if ((hc & 1) == 0) {
+    scan_ball_aniso_l<KNN_K, false, PTS, !kFirstScanNoDup, KnnList, S>(g, cell_start2, sorted2, q.x, q.y, q.z,
+                                                                     0.25f * g.r2, lst, nullptr, slice);
+    group_merge_list<S>(lst);
+    first = false;
+  }
+  if (first || !(lst.worst() < 0.25f * g.r2 * (1.f - 2e-4f))) {
+    if (first)
+      scan_ball_aniso_l<KNN_K, false, PTS, !kFirstScanNoDup, KnnList, S>(g, cell_start2, sorted2, q.x, q.y, q.z,
+                                                                       g.r2, lst, nullptr, slice);
+    else
+      scan_ball_aniso_l<KNN_K, false, PTS, true, KnnList, S>(g, cell_start2, sorted2, q.x, q.y, q.z, g.r2, lst,
+                                                            nullptr, slice);
+    group_merge_list<S>(lst);
+  }
+  if (slice != 0) return;
+  const bool surv = lst.worst() <= g.r2;
+  flag[c] = surv;
+  if (surv) {
+    int4* nb = (int4*)(t_nbr + (int64_t)c * KNN_K);
+    nb[0] = make_int4(lst.index(0), lst.index(1), lst.index(2), lst.index(3));
+    nb[1] = make_int4(lst.index(4), lst.index(5), lst.index(6), lst.index(7));
+  }
+}
+#endif  // APN_DEBUG_BUILD
+
 __global__ void k_bbox_from_points(const float* __restrict__ xyz, int64_t N, int* __restrict__ bbox_ord) {
   const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -2241,10 +2340,21 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
       const char* e = apn_env("APN_CELL_BOUND16_MAX");
       return e ? (int64_t)atoll(e) : (int64_t)3 << 20;
     }();
-    if (n_queries <= cb16_max)
-      hipLaunchKernelGGL(k_cell_bound3w,
-                         dim3(std::max<int64_t>(1, std::min<int64_t>(256 * 16, ceil_div(std::min<int64_t>(cell_cap, slots) * CB_LANES, KNN_THREADS)))),
+    if (n_queries <= cb16_max) {
+#ifdef APN_DEBUG_BUILD
+      static const int cbl = [] {   // A/B: lanes per cell of the short-list cell bounds (16, 32 or 64)
+        const char* e = apn_env("APN_CB_LANES");
+        const int v = e ? atoi(e) : CB_LANES;
+        return (v == 32 || v == 64) ? v : CB_LANES;
+      }();
+#else
+      constexpr int cbl = CB_LANES;
+#endif
+      auto cb = cbl == 64 ? k_cell_bound3w<64> : (cbl == 32 ? k_cell_bound3w<32> : k_cell_bound3w<CB_LANES>);
+      hipLaunchKernelGGL(cb,
+                         dim3(std::max<int64_t>(1, std::min<int64_t>(256 * 16, ceil_div(std::min<int64_t>(cell_cap, slots) * cbl, KNN_THREADS)))),
                          dim3(KNN_THREADS), 0, s, g.gp, g.cell_start, g.tile_list, g.n_tile_list, u1, u2, u4);
+    }
     else
       hipLaunchKernelGGL(k_cell_bound3, dim3(ceil_div(std::min<int64_t>(cell_cap, slots), KNN_THREADS)),
                          dim3(KNN_THREADS), 0, s, g.gp, g.cell_start, g.tile_list, g.n_tile_list, u1, u2, u4);
@@ -2278,12 +2388,14 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
                          n_hard_r, g.gp, g.cell_start, (const float4*)sorted_pts4, flag, t_nbr);
     } else if (aniso) {
 #ifdef APN_DEBUG_BUILD
-      static const int pts = [] {   // points per step of the scan (A/B: APN_KNN_PTS=2)
+      static const int pts = [] {   // points per step of the scan (A/B: APN_KNN_PTS=2 or 8)
         const char* e = apn_env("APN_KNN_PTS");
-        return e && atoi(e) == 2 ? 2 : 4;
+        const int v = e ? atoi(e) : 4;
+        return (v == 2 || v == 8) ? v : 4;
       }();
       auto pass_b = stats ? (pts == 4 ? k_knn_pass_b9<true, 4> : k_knn_pass_b9<true, 2>)
-                          : (pts == 4 ? k_knn_pass_b9<false, 4> : k_knn_pass_b9<false, 2>);
+                          : (pts == 4 ? k_knn_pass_b9<false, 4>
+                                      : (pts == 8 ? k_knn_pass_b9<false, 8> : k_knn_pass_b9<false, 2>));
 #else
       auto pass_b = k_knn_pass_b9<false, 4>;
 #endif
@@ -2303,6 +2415,18 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
                              n_hard, g.gp, ccell, u1, u2, u4, blk_cnt);
           hipLaunchKernelGGL(k_order_blocks, dim3(1), dim3(ORDER_THREADS), 0, s, blk_cnt, nb, perm);
         }
+#ifdef APN_DEBUG_BUILD
+        static const int lanes = [] {   // A/B: APN_KNN_B_LANES = 2 or 4 lanes per hard query
+          const char* e = apn_env("APN_KNN_B_LANES");
+          const int v = e ? atoi(e) : 1;
+          return (v == 2 || v == 4) ? v : 1;
+        }();
+        if (lanes > 1) {
+          auto pass_bs = lanes == 2 ? k_knn_pass_b9s<2, 4> : k_knn_pass_b9s<4, 4>;
+          hipLaunchKernelGGL(pass_bs, dim3(nb * lanes), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard_r,
+                             n_hard_r, hard, n_hard, g.ag, g.cell_start2, g.sorted2, flag, t_nbr, perm, ccell, u1, u2);
+        } else
+#endif
         hipLaunchKernelGGL(pass_b, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, cand, hard_r,
                            n_hard_r, hard, n_hard, g.ag, g.cell_start2, g.sorted2, flag, t_nbr, perm, ccell, u1, u2);
       }
