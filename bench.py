@@ -488,7 +488,9 @@ def knn_report(model, S_kept, inbbox, knn_ms):
     out = {"ms": round(knn_ms, 4), "queries": inbbox, "survivors": S_kept, "perfect_scan": w,
            "note": "perfect scan = survivors' final-ball x-chord rows/points on an r/8 grid (7 VALU lane ops per "
                    "point, 4 per row), rejected samples 0 points; floor_ms = its VALU issue time at the PMC clock"}
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_summary_c2*.json")))
+    # newest round first and, within a round, its final-state summary
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_summary_c2*.json")),
+                   key=lambda f: (os.path.basename(f)[:3], "final" in os.path.basename(f), f))
     for path in reversed(files):
         pmc = read_traffic(path) or {}
         ks = {k: v for k, v in pmc.items() if ("knn" in k or "cell_bound" in k or "classify" in k)
@@ -502,7 +504,7 @@ def knn_report(model, S_kept, inbbox, knn_ms):
                     "executed_issue_ms": round(insts * 2 / 1024 / (clk * 1e9) * 1e3, 4),
                     "lane_efficiency": w["valu_lane_ops"] / (64 * insts),
                     "pmc_source": os.path.relpath(path, ROOT) + " (kNN kernels' SQ_INSTS_VALU per launch, "
-                                                                 "earlier run of this build's kernels)"})
+                                                                 "earlier run, not this one)"})
         out["floor_frac"] = out["floor_ms"] / knn_ms if knn_ms > 0 else None
         break
     return out

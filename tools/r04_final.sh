@@ -1,0 +1,18 @@
+# Round-4 closing measurements on one GPU (outputs under gpurun_out/r04_final/):
+# GPU test suite, the default bench line, its rocprofv3 kernel stats, the PMC passes, a roctx
+# marker summary and the 2-rank gloo rehearsal of the ray-sharded step on one card.
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT || exit 1
+O=gpurun_out/r04_final; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/gpu_tests.log 2>&1
+tail -3 $O/gpu_tests.log
+timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || exit 1
+tail -c 600 $O/bench.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-other-configs > $O/trace_bench.json 2> $O/trace_bench.err || exit 1
+timeout -k 10 300 rocprofv3 --marker-trace --kernel-trace --stats -d $O/marker -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-other-configs > $O/marker_bench.json 2> $O/marker_bench.err || exit 1
+bash tools/pmc_profile.sh $O/pmc > $O/pmc.log 2>&1 || exit 1
+APN_DIST_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu-baseline --no-other-configs > $O/gloo2.json 2> $O/gloo2.err || exit 1
+# gpurun returns at most 64 MiB: keep the summaries, drop the per-dispatch traces
+find $O -name "*kernel_trace.csv" -delete; find $O -name "*counter_collection.csv" -delete
+find $O -name "*marker_api_trace.csv" -delete; find $O -name "*_trace.csv" -size +4M -delete
+du -sh $O
+echo done
