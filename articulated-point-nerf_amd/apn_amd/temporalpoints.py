@@ -883,11 +883,16 @@ class TemporalPoints(torch.nn.Module):
             if idx is None or idx.device != dev:
                 from .shard import block_rays
                 idx = self._block_index[block_key] = block_rays(R, rank, world, block).to(dev)
-            ro, rd, vd = ro.index_select(0, idx), rd.index_select(0, idx), vd.index_select(0, idx)
-            self.last_ray_index, self.last_ray_range, self.last_ray_count = idx, None, idx.numel()
             R = idx.numel()
+            self.last_ray_index, self.last_ray_range, self.last_ray_count = idx, None, R
             if R == 0:
                 raise NoPointsException("No rays in this shard.")
+            # the three ray arrays gathered in one launch (apn_gather_rays)
+            g_o = ws.get("shard_rays_o", R * 3, torch.float32, dev).view(R, 3)
+            g_d = ws.get("shard_rays_d", R * 3, torch.float32, dev).view(R, 3)
+            g_v = ws.get("shard_viewdirs", R * 3, torch.float32, dev).view(R, 3)
+            call("apn_gather_rays", ptr(ro), ptr(rd), ptr(vd), ptr(idx), R, ptr(g_o), ptr(g_d), ptr(g_v), s)
+            ro, rd, vd = g_o, g_d, g_v
         qr = float(query_radius)
         stepdist = float(rk['stepsize']) * float(self.voxel_size)
         interval = float(rk['stepsize']) * float(self.tineuvox.voxel_size_ratio)

@@ -1811,9 +1811,11 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_flag_count(const int* __res
 __global__ __launch_bounds__(KNN_THREADS) void k_knn_flag_compact(
     const float4* __restrict__ q_pos, const int* __restrict__ q_ray, const int* __restrict__ cand,
     const int* __restrict__ n_cand_dev, const int* __restrict__ flag, const int* __restrict__ t_nbr,
-    const int* __restrict__ blk_off, float4* __restrict__ s_pos, int* __restrict__ s_ray, int* __restrict__ s_nbr) {
+    const int* __restrict__ blk_off, float4* __restrict__ s_pos, int* __restrict__ s_ray, int* __restrict__ s_nbr,
+    int nb, int* __restrict__ n_surv) {
   __shared__ int wave_cnt[KNN_THREADS / 64];
   const int c = blockIdx.x * KNN_THREADS + threadIdx.x;
+  if (c == 0) *n_surv = blk_off[nb];   // the survivor count (the scan's total), no copy launch
   const bool f = c < *n_cand_dev && flag[c];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const unsigned long long bal = __ballot(f);
@@ -2445,8 +2447,8 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
     st = scan_exclusive_i32(blk_cnt, blk_off, nb, sws, s);
     if (st) return st;
     hipLaunchKernelGGL(k_knn_flag_compact, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, q_ray, cand,
-                       cblk_off + nb, flag, t_nbr, blk_off, (float4*)s_pos4, s_ray, s_nbr);
-    APN_TRY(copy_i32(blk_off + nb, n_survivors_dev, 1, s));
+                       cblk_off + nb, flag, t_nbr, blk_off, (float4*)s_pos4, s_ray, s_nbr, nb,
+                       n_survivors_dev);
     return launch_status();
   }
 #ifndef APN_DEBUG_BUILD
@@ -2480,8 +2482,8 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
     st = scan_exclusive_i32(blk_cnt, blk_off, nb, sws, s);
     if (st) return st;
     hipLaunchKernelGGL(k_knn_flag_compact, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, q_ray, cand,
-                       cblk_off + nb, flag, t_nbr, blk_off, (float4*)s_pos4, s_ray, s_nbr);
-    APN_TRY(copy_i32(blk_off + nb, n_survivors_dev, 1, s));
+                       cblk_off + nb, flag, t_nbr, blk_off, (float4*)s_pos4, s_ray, s_nbr, nb,
+                       n_survivors_dev);
     return launch_status();
   }
   if (knn_mode() == 5) {
@@ -2506,8 +2508,8 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
     st = scan_exclusive_i32(blk_cnt, blk_off, nb, sws, s);
     if (st) return st;
     hipLaunchKernelGGL(k_knn_flag_compact, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, q_ray, cand,
-                       cblk_off + nb, flag, t_nbr, blk_off, (float4*)s_pos4, s_ray, s_nbr);
-    APN_TRY(copy_i32(blk_off + nb, n_survivors_dev, 1, s));
+                       cblk_off + nb, flag, t_nbr, blk_off, (float4*)s_pos4, s_ray, s_nbr, nb,
+                       n_survivors_dev);
     return launch_status();
   }
   if (knn_mode() == 4) {
@@ -2523,8 +2525,8 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
     st = scan_exclusive_i32(blk_cnt, blk_off, nb, sws, s);
     if (st) return st;
     hipLaunchKernelGGL(k_knn_flag_compact, dim3(nb), dim3(KNN_THREADS), 0, s, (const float4*)q_pos4, q_ray, cand,
-                       cblk_off + nb, flag, t_nbr, blk_off, (float4*)s_pos4, s_ray, s_nbr);
-    APN_TRY(copy_i32(blk_off + nb, n_survivors_dev, 1, s));
+                       cblk_off + nb, flag, t_nbr, blk_off, (float4*)s_pos4, s_ray, s_nbr, nb,
+                       n_survivors_dev);
     return launch_status();
   }
   if (knn_mode() == 3)

@@ -209,14 +209,24 @@ __global__ void k_inbbox_count(const float* __restrict__ ro, const float* __rest
   cnt[r] = c;
 }
 
+// frame_info = {min(total, cap), total, total > cap} from the exclusive scan's last entry (written
+// by the fill's first thread: the capped fill's own launch)
+__device__ __forceinline__ void frame_info_store(int n, int cap, int* __restrict__ info) {
+  info[0] = n < cap ? n : cap;
+  info[1] = n;
+  info[2] = n > cap ? 1 : 0;
+}
+
 #ifdef APN_DEBUG_BUILD   // one ray per thread: debug build only (A/B against the block-cooperative fill)
 // q_pos[i] = (x, y, z, bits(step_id)); q_ray[i] = ray id. Sorted by ray, then step.
 // cap: samples at positions >= cap are not written (the capacity-bounded, sync-free render path:
 // apn_inbbox_fill_capped); INT_MAX = every sample.
+
 __global__ void k_inbbox_fill(const float* __restrict__ ro, const float* __restrict__ rd,
                               const float* __restrict__ bbox6, float near, float far,
                               float stepdist, int64_t n_rays, const int* __restrict__ off,
-                              float4* __restrict__ q_pos, int* __restrict__ q_ray, int cap) {
+                              float4* __restrict__ q_pos, int* __restrict__ q_ray, int cap, int* __restrict__ info) {
+  if (info && blockIdx.x == 0 && threadIdx.x == 0) frame_info_store(off[n_rays], cap, info);
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n_rays) return;
   int o = off[r];
@@ -247,7 +257,7 @@ __global__ __launch_bounds__(FILL_RAYS) void k_inbbox_fill_blk(const float* __re
                                                              const float* __restrict__ bbox6, float near,
                                                              float far, float stepdist, int64_t n_rays,
                                                              const int* __restrict__ off, float4* __restrict__ q_pos,
-                                                             int* __restrict__ q_ray, int cap) {
+                                                             int* __restrict__ q_ray, int cap, int* __restrict__ info) {
   __shared__ int sOff[FILL_RAYS + 1];
   __shared__ int sK0[FILL_RAYS];
   __shared__ float sG[6][FILL_RAYS];
@@ -255,6 +265,7 @@ __global__ __launch_bounds__(FILL_RAYS) void k_inbbox_fill_blk(const float* __re
   const int nr = (int)min((int64_t)FILL_RAYS, n_rays - r0);
   const int t = threadIdx.x;
   const float lo[3] = {bbox6[0], bbox6[1], bbox6[2]}, hi[3] = {bbox6[3], bbox6[4], bbox6[5]};
+  if (info && blockIdx.x == 0 && t == 0) frame_info_store(off[n_rays], cap, info);   // no launch of its own
   if (t < nr) sOff[t] = off[r0 + t];
   if (t == 0 && nr > 0) sOff[nr] = off[r0 + nr];
   if (t < nr) {
@@ -302,15 +313,6 @@ static bool inbbox_fill_per_ray() {   // A/B: APN_INBBOX_FILL=ray selects the on
 #else
 #define APN_INBBOX_FILL_KERNEL k_inbbox_fill_blk
 #endif
-
-// frame_info = {min(total, cap), total, total > cap} from the exclusive scan's last entry.
-__global__ void k_frame_info(const int* __restrict__ total, int cap, int* __restrict__ info) {
-  if (threadIdx.x != 0) return;
-  const int n = *total;
-  info[0] = n < cap ? n : cap;
-  info[1] = n;
-  info[2] = n > cap ? 1 : 0;
-}
 
 // bbox_ord: ordered-int encoded [min x,y,z, max x,y,z] of the warped cloud (apn_lbs.hip);
 // padded by query_radius exactly as temporalpoints.py:424 (float32 subtract / add).
@@ -437,7 +439,7 @@ extern "C" int apn_inbbox_fill(const float* rays_o, const float* rays_d, const f
   if (n_rays <= 0) return APN_ERR_ARG;
   hipLaunchKernelGGL(APN_INBBOX_FILL_KERNEL, dim3(ceil_div(n_rays, 256)), dim3(256),
                      0, (hipStream_t)stream, rays_o, rays_d, bbox6, near, far, stepdist, n_rays, offsets,
-                     (float4*)q_pos4, q_ray, INT_MAX);
+                     (float4*)q_pos4, q_ray, INT_MAX, nullptr);
   return launch_status();
 }
 
@@ -447,10 +449,36 @@ extern "C" int apn_inbbox_fill_capped(const float* rays_o, const float* rays_d, 
                                       void* stream) {
   if (n_rays <= 0 || capacity < 0 || capacity > INT_MAX || !frame_info) return APN_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_frame_info, dim3(1), dim3(64), 0, s, offsets + n_rays, (int)capacity, frame_info);
   hipLaunchKernelGGL(APN_INBBOX_FILL_KERNEL, dim3(ceil_div(n_rays, 256)), dim3(256),
                      0, s, rays_o, rays_d, bbox6, near, far, stepdist, n_rays, offsets, (float4*)q_pos4, q_ray,
-                     (int)capacity);
+                     (int)capacity, frame_info);
+  return launch_status();
+}
+
+namespace apn {
+// One thread per gathered ray: 3 x 12 B in, 3 x 12 B out.
+__global__ void k_gather_rays(const float* __restrict__ a, const float* __restrict__ b, const float* __restrict__ c,
+                              const int64_t* __restrict__ idx, int64_t n, float* __restrict__ oa,
+                              float* __restrict__ ob, float* __restrict__ oc) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t r = idx[i];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    oa[3 * i + k] = a[3 * r + k];
+    ob[3 * i + k] = b[3 * r + k];
+    oc[3 * i + k] = c[3 * r + k];
+  }
+}
+}  // namespace apn
+
+extern "C" int apn_gather_rays(const float* rays_o, const float* rays_d, const float* viewdirs, const int64_t* index,
+                               int64_t n, float* out_o, float* out_d, float* out_v, void* stream) {
+  if (n < 0 || (n > 0 && (!rays_o || !rays_d || !viewdirs || !index || !out_o || !out_d || !out_v)))
+    return APN_ERR_ARG;
+  if (n == 0) return APN_OK;
+  hipLaunchKernelGGL(k_gather_rays, dim3(ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream, rays_o, rays_d,
+                     viewdirs, index, n, out_o, out_d, out_v);
   return launch_status();
 }
 

@@ -18,6 +18,7 @@ namespace apn {
 constexpr int SK_THREADS = 1024;
 constexpr int SK_OUT = 256;                      // max GEMV width (hidden, (J+1)*4, t_dim)
 constexpr int SK_SLICES = SK_THREADS / SK_OUT;   // K-slices per output feature
+constexpr int SK_KMAX = SK_OUT / SK_SLICES;      // inputs per K-slice (in_dim <= SK_OUT)
 constexpr int SK_MAX_J = 64;
 constexpr int SK_MAX_VIEWS = 16;
 constexpr int SK_MAX_DEPTH = 32;
@@ -101,6 +102,8 @@ __global__ __launch_bounds__(SK_THREADS) void k_skeleton_pose(
     // order), the slices added pairwise
     const float* w = tnw;
     const int o = tid % SK_OUT, sl = tid / SK_OUT;
+    const int n_w = t_dim * hidden + hidden + (n_layers - 2) * (hidden * hidden + hidden) + hidden * (J + 1) * 4;
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)tnw, 0, n_w * 4, 0x00020000);
     int in_dim = t_dim, cur = 0;
     for (int l = 0; l < n_layers; ++l) {
       const bool last = l == n_layers - 1;
@@ -108,9 +111,24 @@ __global__ __launch_bounds__(SK_THREADS) void k_skeleton_pose(
       const int kper = (in_dim + SK_SLICES - 1) / SK_SLICES;
       const int k0 = sl * kper, k1 = min(in_dim, k0 + kper);
       float a = 0.f;
-      if (o < out_dim) {
+      if (k1 - k0 == SK_KMAX) {   // the hidden and last layers (in_dim = 256): the slice's 64 weights
+        // as one batch of buffer loads (a running 32-bit VGPR offset): one load latency per layer
+        // instead of one per 16-load batch. Threads past out_dim read column out_dim - 1, unused.
+        float wr[SK_KMAX];
+        int off = (int)((w - tnw) + (size_t)k0 * out_dim + min(o, out_dim - 1)) * 4;
+        const int st4 = out_dim * 4;
+#pragma unroll
+        for (int u = 0; u < SK_KMAX; ++u) {
+          wr[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wrs, off, 0, 0));
+          off += st4;
+          asm volatile("" : "+v"(off));   // not 64 hoisted scalar products
+        }
+        if (o < out_dim) {
+#pragma unroll
+          for (int u = 0; u < SK_KMAX; ++u) a += wr[u] * h[cur][k0 + u];   // k order, as before
+        }
+      } else if (o < out_dim) {   // the time-embedding layer (in_dim = t_dim): short slices
         const float* wc = w + o;
-#pragma unroll 16
         for (int k = k0; k < k1; ++k) a += wc[(size_t)k * out_dim] * h[cur][k];
       }
       sPart[sl][o] = a;

@@ -207,6 +207,12 @@ int apn_skeleton_frame(const float* t, const float* time_poc, int32_t n_freq, co
 /* Padded sampling bbox = bbox_ord -/+ query_radius (temporalpoints.py:424) as 6 floats. */
 int apn_bbox_unpack(const int32_t* bbox_ord, float query_radius, float* out6, void* stream);
 
+/* The rays of a ray shard (shard.py "blocks" split): rows index[0..n) of rays_o, rays_d and
+ * viewdirs [R,3] gathered into out_o, out_d, out_v [n,3] in one launch (replaces three
+ * index_select calls of the render loop, run.py:136-151 slicing). index: int64, in [0, R). */
+int apn_gather_rays(const float* rays_o, const float* rays_d, const float* viewdirs, const int64_t* index,
+                    int64_t n, float* out_o, float* out_d, float* out_v, void* stream);
+
 /* In-bbox ray samples (sample_ray, temporalpoints.py:373-399, with the boolean compaction
  * done on device): per-ray counts -> offsets [n_rays+1]; then q_pos4 {x,y,z,bits(step)},
  * q_ray, sorted by (ray, step). bbox6 = {lo xyz, hi xyz} (device).

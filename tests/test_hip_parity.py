@@ -1371,11 +1371,11 @@ def test_lbs_train_kernel_vs_torch_autograd(dev, J):
         assert float((a - b).abs().max()) <= 1e-4 * float(b.abs().max()), (name, float((a - b).abs().max()))
 
 
-@pytest.mark.parametrize("n", [1, 7, 2047, 2048, 2049, 300_001, 1 << 20, 9_000_001])
+@pytest.mark.parametrize("n", [1, 7, 2047, 2048, 2049, 8192, 8193, 40_000, 300_001, 1 << 20, 9_000_001])
 def test_scan_exclusive_matches_cumsum(dev, n):
-    """apn_scan_exclusive_i32 (grid cells, rays, kNN blocks): the two-launch form (<= 4096 blocks of
-    2048) and the three-launch form (9M elements) against numpy's cumulative sum, with the total in
-    out[n]."""
+    """apn_scan_exclusive_i32 (grid cells, rays, kNN blocks): the one-workgroup form (<= 8192),
+    the two-launch form (<= 4096 blocks of 2048) and the three-launch form (9M elements) against
+    numpy's cumulative sum, with the total in out[n]."""
     from apn_amd import _lib as L
     rng = np.random.default_rng(n)
     x = rng.integers(0, 50, n, dtype=np.int32)
