@@ -1372,6 +1372,23 @@ def test_lbs_train_kernel_vs_torch_autograd(dev, J):
         assert float((a - b).abs().max()) <= 1e-4 * float(b.abs().max()), (name, float((a - b).abs().max()))
 
 
+@pytest.mark.parametrize("world,rank", [(8, 0), (8, 7), (3, 1)])
+def test_gather_rays_matches_index_select(dev, world, rank):
+    """apn_gather_rays (a ray shard's rays in one launch) equals index_select of the three arrays."""
+    from apn_amd import _lib as L
+    from apn_amd.shard import block_rays
+    R = 640_000
+    g = torch.Generator(device="cpu").manual_seed(world * 10 + rank)
+    ro, rd, vd = (torch.randn(R, 3, generator=g).to(dev) for _ in range(3))
+    idx = block_rays(R, rank, world, 4096).to(dev)
+    n = idx.numel()
+    out = [torch.full((n, 3), float("nan"), device=dev) for _ in range(3)]
+    L.call("apn_gather_rays", L.ptr(ro), L.ptr(rd), L.ptr(vd), L.ptr(idx), n, *(L.ptr(o) for o in out),
+           L.stream_ptr(dev))
+    for a, o in zip((ro, rd, vd), out):
+        assert torch.equal(o, a.index_select(0, idx))
+
+
 @pytest.mark.parametrize("n", [1, 7, 2047, 2048, 2049, 8192, 8193, 40_000, 300_001, 1 << 20, 9_000_001])
 def test_scan_exclusive_matches_cumsum(dev, n):
     """apn_scan_exclusive_i32 (grid cells, rays, kNN blocks): the one-workgroup form (<= 8192),
