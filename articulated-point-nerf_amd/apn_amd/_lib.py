@@ -45,6 +45,9 @@ SIGNATURES = {
     "apn_grid_build": (C.c_int, [P, I64, P, F32, I32, P, P, P]),
     "apn_knn_workspace_bytes": (SZ, [I64]),
     "apn_knn_radius": (C.c_int, [P, P, I64, P, P, I64, I32, P, F32, P, P, P, P, P, P]),
+    "apn_knn_uses_agrid": (I32, [I64]),
+    "apn_knn_agrid_build": (C.c_int, [P, I64, I32, P, P]),
+    "apn_knn_radius_ev": (C.c_int, [P, P, I64, P, P, I64, I32, P, F32, P, P, P, P, P, P, P]),
     "apn_nn1_distance": (C.c_int, [P, I64, F32, I32, P, P, P, P, P]),
     "apn_knn_points": (C.c_int, [P, I64, P, I64, I32, I32, P, P, P, P, P, P]),
     "apn_mlp_weight_layout": (C.c_int, [P]),

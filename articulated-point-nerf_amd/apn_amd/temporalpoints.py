@@ -27,6 +27,8 @@ from .shard import SplitTracker
 from .tineuvox import poc_fre
 
 CELL_CAP = int(os.environ.get("APN_CELL_CAP", 1 << 20))
+# the kNN's second grid on the grid's side stream (A/B: APN_AGRID_SIDE=0 builds it inside the kNN call)
+AGRID_SIDE = os.environ.get("APN_AGRID_SIDE", "1") != "0"
 
 
 class NoPointsException(Exception):
@@ -922,6 +924,8 @@ class TemporalPoints(torch.nn.Module):
             with torch.cuda.stream(side):
                 call("apn_grid_build", ptr(xyz), N, ptr(bbox_ord), qr, CELL_CAP, ptr(sorted4), ptr(gws),
                      stream_ptr(dev))
+                grid_ready = torch.cuda.Event()
+                grid_ready.record(side)
         else:
             call("apn_grid_build", ptr(xyz), N, ptr(bbox_ord), qr, CELL_CAP, ptr(sorted4), ptr(gws), s)
         self._mark("grid")
@@ -984,16 +988,30 @@ class TemporalPoints(torch.nn.Module):
             self.last_stats = FrameStats({"rays": R}, info=info)
         self._mark("sampling")
         roctx.end("sampling")
+        agrid_ready = None
         if side is not None:
-            cur.wait_stream(side)
+            # the kNN's second grid (needed by launches of more than 2^18 queries) continues on the
+            # side stream, beside the kNN's first passes; apn_knn_radius_ev waits for it before the
+            # passes that read it. The kNN itself waits only for the fine grid.
+            if AGRID_SIDE and lib.apn_knn_uses_agrid(Q):
+                with torch.cuda.stream(side):
+                    call("apn_knn_agrid_build", ptr(gws), N, CELL_CAP, ptr(sorted4), stream_ptr(dev))
+                    agrid_ready = torch.cuda.Event()
+                    agrid_ready.record(side)
+            cur.wait_event(grid_ready)
         roctx.begin("knn")
         # radius kNN + compaction of survivors
         s_pos = ws.get("s_pos", Q * 4, torch.float32, dev)
         s_ray = ws.get("s_ray", Q, torch.int32, dev)
         s_nbr = ws.get("s_nbr", Q * 8, torch.int32, dev)
         kws = ws.bytes("knn_ws", lib.apn_knn_workspace_bytes(Q), dev)
-        call("apn_knn_radius", ptr(q_pos), ptr(q_ray), Q, nq_dev, ptr(gws), N,
-             CELL_CAP, ptr(sorted4), qr, ptr(s_pos), ptr(s_ray), ptr(s_nbr), ptr(nsurv), ptr(kws), s)
+        if agrid_ready is not None:
+            call("apn_knn_radius_ev", ptr(q_pos), ptr(q_ray), Q, nq_dev, ptr(gws), N, CELL_CAP, ptr(sorted4), qr,
+                 ptr(s_pos), ptr(s_ray), ptr(s_nbr), ptr(nsurv), ptr(kws), C.c_void_p(agrid_ready.cuda_event), s)
+            cur.wait_stream(side)   # the side stream's work is joined before the frame ends
+        else:
+            call("apn_knn_radius", ptr(q_pos), ptr(q_ray), Q, nq_dev, ptr(gws), N,
+                 CELL_CAP, ptr(sorted4), qr, ptr(s_pos), ptr(s_ray), ptr(s_nbr), ptr(nsurv), ptr(kws), s)
         self._mark("knn")
         roctx.end("knn")
         roctx.begin("mlp")

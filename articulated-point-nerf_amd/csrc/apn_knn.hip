@@ -2265,11 +2265,46 @@ extern "C" size_t apn_knn_workspace_bytes(int64_t n_queries) {
 // Queries: q_pos4[n_queries] {x,y,z,bits(step)} and q_ray. n_queries is an upper bound used for
 // the launch; the live count is read on device from *n_queries_dev. Survivors (sorted by query
 // order) go to s_pos4/s_ray/s_nbr and their count to *n_survivors_dev.
-extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t n_queries,
-                              const int32_t* n_queries_dev, const void* grid_workspace, int64_t n_points,
-                              int32_t cell_cap, const float* sorted_pts4, float query_radius, float* s_pos4,
-                              int32_t* s_ray, int32_t* s_nbr, int32_t* n_survivors_dev, void* workspace,
-                              void* stream) {
+static int64_t knn_small_max() {
+  static const int64_t v = [] {
+    const char* e = apn_env("APN_KNN_SMALL_MAX");
+    return e ? (int64_t)atoll(e) : KNN_SPLIT_MAX_QUERIES;
+  }();
+  return v;
+}
+// small batches (the 8192-ray training steps) take the 8-lane fine-grid pass B; larger launches of
+// mode 9 read the anisotropic second grid. Up to 2^18 queries: a ray shard of a full frame (~0.5-1M
+// in-bbox samples at C2 over 8 GPUs) ran its kNN 2.3x slower on the 8-lane pass than on mode 9's
+// (tools/shard_balance.py); APN_KNN_SMALL_MAX overrides in the debug build.
+static bool knn_uses_agrid(int64_t n_queries) {
+  return knn_mode() == 9 && !(!kKnnStats && n_queries <= knn_small_max());
+}
+
+// The second grid (k_agrid_*): cells of AG_F x AG_F fine cells in y and z, counting-sorted from the
+// fine grid's sorted points. Reads only the fine grid (gp, sorted points) and writes only its own
+// buffers (counts2, cursor2, cell_start2, pcell2, sorted2, the grid scan scratch).
+static int agrid_build(GridWs& g, int64_t n_points, int cell_cap, const float* sorted_pts4, hipStream_t s) {
+  static const int f = [] {
+    const char* e = apn_env("APN_KNN_ANISO");
+    const int v = e ? atoi(e) : 2;
+    return (v == 1 || v == 2 || v == 4) ? v : 2;
+  }();
+  APN_TRY(fill4_i32(g.counts2, cell_cap, g.cursor2, cell_cap, nullptr, 0, nullptr, 0, s));
+  hipLaunchKernelGGL(k_agrid_params, dim3(1), dim3(64), 0, s, g.gp, f, (int)n_points, g.ag);
+  hipLaunchKernelGGL(k_agrid_count, dim3(ceil_div(n_points, 256)), dim3(256), 0, s, (const float4*)sorted_pts4,
+                     n_points, g.gp, f, g.counts2, g.pcell2);
+  const int st = scan_exclusive_i32(g.counts2, g.cell_start2, cell_cap, g.scan, s);
+  if (st) return st;
+  hipLaunchKernelGGL(k_agrid_scatter, dim3(ceil_div(n_points, 256)), dim3(256), 0, s, (const float4*)sorted_pts4,
+                     n_points, g.pcell2, g.cell_start2, g.cursor2, g.sorted2);
+  return launch_status();
+}
+
+static int knn_radius_impl(const float* q_pos4, const int32_t* q_ray, int64_t n_queries,
+                           const int32_t* n_queries_dev, const void* grid_workspace, int64_t n_points,
+                           int32_t cell_cap, const float* sorted_pts4, float query_radius, float* s_pos4,
+                           int32_t* s_ray, int32_t* s_nbr, int32_t* n_survivors_dev, void* workspace,
+                           void* agrid_ready, void* stream) {
   (void)query_radius;  // the grid was built for it (GridParams.r2)
   if (n_queries < 0 || !grid_workspace || !workspace) return APN_ERR_ARG;
   if (n_points > KNN_MAX_POINTS) return APN_ERR_ARG;
@@ -2303,26 +2338,11 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
     // small batches (the 8192-ray training steps): 8 lanes per hard query. Up to 2^18 queries:
     // a ray shard of a full frame (~0.5-1M in-bbox samples at C2 over 8 GPUs) ran its kNN 2.3x
     // slower on the 8-lane pass than on mode 9's (tools/shard_balance.py); APN_KNN_SMALL_MAX overrides
-    static const int64_t small_max = [] {
-      const char* e = apn_env("APN_KNN_SMALL_MAX");
-      return e ? (int64_t)atoll(e) : KNN_SPLIT_MAX_QUERIES;
-    }();
-    const bool small = !stats && n_queries <= small_max;
-    const bool aniso = knn_mode() == 9 && !small;
-    if (aniso) {   // the anisotropic second grid for pass B (built from the fine grid's sorted points)
-      static const int f = [] {
-        const char* e = apn_env("APN_KNN_ANISO");
-        const int v = e ? atoi(e) : 2;
-        return (v == 1 || v == 2 || v == 4) ? v : 2;
-      }();
-      APN_TRY(fill4_i32(g.counts2, cell_cap, g.cursor2, cell_cap, nullptr, 0, nullptr, 0, s));
-      hipLaunchKernelGGL(k_agrid_params, dim3(1), dim3(64), 0, s, g.gp, f, (int)n_points, g.ag);
-      hipLaunchKernelGGL(k_agrid_count, dim3(ceil_div(n_points, 256)), dim3(256), 0, s, (const float4*)sorted_pts4,
-                         n_points, g.gp, f, g.counts2, g.pcell2);
-      st = scan_exclusive_i32(g.counts2, g.cell_start2, cell_cap, g.scan, s);
+    const bool aniso = knn_uses_agrid(n_queries);
+    const bool small = !stats && n_queries <= knn_small_max();
+    if (aniso && !agrid_ready) {   // the second grid, here on the kNN's stream
+      st = agrid_build(g, n_points, cell_cap, sorted_pts4, s);
       if (st) return st;
-      hipLaunchKernelGGL(k_agrid_scatter, dim3(ceil_div(n_points, 256)), dim3(256), 0, s, (const float4*)sorted_pts4,
-                         n_points, g.pcell2, g.cell_start2, g.cursor2, g.sorted2);
     }
     int* flag = t_ray;
     int* hard = cand_blk;
@@ -2378,6 +2398,7 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
 #else
     auto pass_a = k_knn_pass_a8<false>;
 #endif
+    if (aniso && agrid_ready) APN_HIP_TRY(hipStreamWaitEvent(s, (hipEvent_t)agrid_ready, 0));   // built on another stream
     hipLaunchKernelGGL(pass_a, dim3(nb), dim3(KNN_THREADS), 0,
                        s, (const float4*)q_pos4, cand, cblk_off + nb, g.gp, g.cell_start, (const float4*)sorted_pts4,
                        ccell, u1, u2, u4, flag, t_nbr, hard, n_hard, hard_r, n_hard_r, g.ag, g.cell_start2, g.sorted2,
@@ -2544,6 +2565,35 @@ extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t
   APN_TRY(copy_i32(blk_off + nb, n_survivors_dev, 1, s));
   return launch_status();
 #endif  // APN_DEBUG_BUILD
+}
+
+extern "C" int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t n_queries,
+                              const int32_t* n_queries_dev, const void* grid_workspace, int64_t n_points,
+                              int32_t cell_cap, const float* sorted_pts4, float query_radius, float* s_pos4,
+                              int32_t* s_ray, int32_t* s_nbr, int32_t* n_survivors_dev, void* workspace,
+                              void* stream) {
+  return knn_radius_impl(q_pos4, q_ray, n_queries, n_queries_dev, grid_workspace, n_points, cell_cap, sorted_pts4,
+                         query_radius, s_pos4, s_ray, s_nbr, n_survivors_dev, workspace, nullptr, stream);
+}
+
+extern "C" int32_t apn_knn_uses_agrid(int64_t n_queries) { return knn_uses_agrid(n_queries) ? 1 : 0; }
+
+extern "C" int apn_knn_agrid_build(const void* grid_workspace, int64_t n_points, int32_t cell_cap,
+                                   const float* sorted_pts4, void* stream) {
+  if (n_points <= 0 || cell_cap <= 0 || !grid_workspace || !sorted_pts4) return APN_ERR_ARG;
+  if (n_points > KNN_MAX_POINTS) return APN_ERR_ARG;
+  GridWs g = grid_ws((void*)grid_workspace, n_points, cell_cap);
+  return agrid_build(g, n_points, cell_cap, sorted_pts4, (hipStream_t)stream);
+}
+
+extern "C" int apn_knn_radius_ev(const float* q_pos4, const int32_t* q_ray, int64_t n_queries,
+                                 const int32_t* n_queries_dev, const void* grid_workspace, int64_t n_points,
+                                 int32_t cell_cap, const float* sorted_pts4, float query_radius, float* s_pos4,
+                                 int32_t* s_ray, int32_t* s_nbr, int32_t* n_survivors_dev, void* workspace,
+                                 void* agrid_ready, void* stream) {
+  if (!agrid_ready) return APN_ERR_ARG;
+  return knn_radius_impl(q_pos4, q_ray, n_queries, n_queries_dev, grid_workspace, n_points, cell_cap, sorted_pts4,
+                         query_radius, s_pos4, s_ray, s_nbr, n_survivors_dev, workspace, agrid_ready, stream);
 }
 
 // Construction-time: per-point nearest-other distance sqrt(d2 + eps) over the canonical cloud.

@@ -245,6 +245,20 @@ int apn_grid_build(const float* xyz, int64_t n_points, const int32_t* bbox_ord, 
  * (temporalpoints.py:433-447): survivors (8th-NN squared distance <= query_radius) in
  * query order -> s_pos4, s_ray, s_nbr [S,8]; S written to *n_survivors_dev. */
 size_t apn_knn_workspace_bytes(int64_t n_queries);
+
+/* The kNN's second (anisotropic) grid, built from the fine grid of apn_grid_build. Launches of more
+ * than 2^18 queries read it (apn_knn_uses_agrid(n_queries) = 1); apn_knn_radius builds it itself.
+ * apn_knn_agrid_build lets the host build it on another stream (beside the sampling and the kNN's
+ * first passes) and apn_knn_radius_ev then waits on agrid_ready (a hipEvent_t recorded after that
+ * build) right before the first pass that reads it. Same results as apn_knn_radius. */
+int32_t apn_knn_uses_agrid(int64_t n_queries);
+int apn_knn_agrid_build(const void* grid_workspace, int64_t n_points, int32_t cell_cap, const float* sorted_pts4,
+                        void* stream);
+int apn_knn_radius_ev(const float* q_pos4, const int32_t* q_ray, int64_t n_queries,
+                      const int32_t* n_queries_dev, const void* grid_workspace, int64_t n_points,
+                      int32_t cell_cap, const float* sorted_pts4, float query_radius, float* s_pos4,
+                      int32_t* s_ray, int32_t* s_nbr, int32_t* n_survivors_dev, void* workspace,
+                      void* agrid_ready, void* stream);
 int apn_knn_radius(const float* q_pos4, const int32_t* q_ray, int64_t n_queries,
                    const int32_t* n_queries_dev, const void* grid_workspace, int64_t n_points,
                    int32_t cell_cap, const float* sorted_pts4, float query_radius, float* s_pos4,

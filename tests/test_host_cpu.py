@@ -61,6 +61,8 @@ def test_invalid_arguments_rejected_without_gpu():
     assert lib.apn_lbs_skin(None, None, 0, 0, None, 0.0, None, None, None, None, None, None, None, 0.0, 0,
                             None, None, None, None, None, None, None, None) == 1
     assert lib.apn_lbs_workspace_bytes(300_000) == 6 * 4 * ((300_000 + 63) // 64)   # one partial per 64-point block
+    # the kNN's second grid: launches of more than 2^18 queries; the event form needs its event
+    assert lib.apn_knn_uses_agrid(1 << 18) == 0 and lib.apn_knn_uses_agrid((1 << 18) + 1) == 1
     # clouds past the 32-bit buffer-descriptor range are refused before any device work
     import ctypes
     buf = ctypes.create_string_buffer(64)
@@ -68,6 +70,8 @@ def test_invalid_arguments_rejected_without_gpu():
     big = 1 << 27
     assert lib.apn_grid_build(p, big, p, 0.01, 1024, p, p, None) == 1
     assert lib.apn_knn_radius(p, p, 16, p, p, big, 1024, p, 0.01, p, p, p, p, p, None) == 1
+    assert lib.apn_knn_radius_ev(p, p, 16, p, p, 1000, 1024, p, 0.01, p, p, p, p, p, None, None) == 1
+    assert lib.apn_knn_agrid_build(p, big, 1024, p, None) == 1
 
 
 def test_missing_library_fails_loudly(monkeypatch):
