@@ -10,6 +10,7 @@ tail -c 600 $O/bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-other-configs > $O/trace_bench.json 2> $O/trace_bench.err || exit 1
 timeout -k 10 300 rocprofv3 --marker-trace --kernel-trace --stats -d $O/marker -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-other-configs > $O/marker_bench.json 2> $O/marker_bench.err || exit 1
 bash tools/pmc_profile.sh $O/pmc > $O/pmc.log 2>&1 || exit 1
+timeout -k 10 300 python tools/shard_balance.py --split gilv4096 --worlds 2,4,8 --reps 10 > $O/shard_balance.log 2>&1 || exit 1
 APN_DIST_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu-baseline --no-other-configs > $O/gloo2.json 2> $O/gloo2.err || exit 1
 # gpurun returns at most 64 MiB: keep the summaries, drop the per-dispatch traces
 find $O -name "*kernel_trace.csv" -delete; find $O -name "*counter_collection.csv" -delete
