@@ -14,6 +14,14 @@ has every rank render its own frame instead (weak scaling, no data-path collecti
 (LBS-only) shards the points N/W per rank with no collective (strong scaling). The timing is
 barrier + synchronize bracketed and the max over ranks (all-reduce MAX of the elapsed time).
 
+Frames in flight (``--in-flight``, default 2): a frame's stages run in sequence (the kNN needs the
+warped cloud, the MLP the kNN's survivors), so one frame leaves the chip under-used while its kNN
+and small stages run. With two frames in flight two TemporalPoints of the same scene (own
+workspaces) replay their captured frames on two HIP streams, frame i on stream i % 2: one frame's
+MLP runs beside the next frame's kNN and sampling. Every frame is still rendered in full and is
+bit-identical to a serial frame (tests/test_frame_graph.py); ``config.serial_ms_per_step`` is the
+same frames one at a time on one stream. The ray-sharded steps (all-gather per frame) stay serial.
+
 Rank 0 prints ONE JSON line. Diagnostics go to stderr.
 
 Launch: ``python bench.py --gpus N`` with N > 1 and no WORLD_SIZE in the environment starts the N
@@ -374,7 +382,45 @@ def lbs_sweep(args, rank, world, dev):
     return line
 
 
-def frame_rate(config, dev, steps=10, warmup=2):
+def replay_frames(steps_in_flight, t_arg, k, streams=None):
+    """Replays k captured frames: one graph on the current stream, or graphs g_0, g_1 alternating
+    over two streams (frame i: graph i % 2 on stream i % 2; both join the current stream at the end).
+    Returns the last frame and the host seconds spent issuing."""
+    h = 0.0
+    out = None
+    if len(steps_in_flight) == 1:
+        for _ in range(k):
+            h0 = time.perf_counter()
+            out = steps_in_flight[0](t_arg)
+            h += time.perf_counter() - h0
+        return out, h
+    cur = torch.cuda.current_stream()
+    ev = torch.cuda.Event()
+    ev.record(cur)
+    for s in streams:
+        s.wait_event(ev)
+    for i in range(k):
+        h0 = time.perf_counter()
+        with torch.cuda.stream(streams[i % 2]):
+            out = steps_in_flight[i % 2](t_arg)
+        h += time.perf_counter() - h0
+    for s in streams:
+        cur.wait_stream(s)
+    return out, h
+
+
+def second_frame_graph(scene, dev, t_arg, rk, poses, Ks):
+    """A second TemporalPoints of the scene (same weights, own workspaces) with its frame captured
+    (the second frame in flight)."""
+    m2 = harness.build_model(scene, dev)
+    _ = m2.mean_min_distance
+    for _ in range(2):
+        m2(t_arg, render_depth=True, render_kwargs=rk, render_weights=True, poses=poses, Ks=Ks, get_skeleton=True)
+    torch.cuda.synchronize(dev)
+    return m2, m2.capture_frame(t_arg, rk, poses=poses, Ks=Ks, get_skeleton=True)
+
+
+def frame_rate(config, dev, steps=10, warmup=2, in_flight=2):
     """One GPU, one config (C3 / C4): whole frames replayed as one HIP graph, as the headline line,
     plus the MLP kernel's time from HIP events on eager frames and its F_alg roofline fraction.
     Rides along in the default line (`other_configs`), so every config has a driver-run number."""
@@ -398,12 +444,14 @@ def frame_rate(config, dev, steps=10, warmup=2):
     mlp_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / max(len(ev), 1)
     kept = int(ev[-1][2].item()) if ev else stats.get("kept_samples", 0)
     step = model.capture_frame(t_arg, rk, poses=poses, Ks=Ks, get_skeleton=True)
-    for _ in range(2):
-        step(t_arg)
+    graphs, streams = [step], None
+    if in_flight == 2:
+        _, step2 = second_frame_graph(scene, dev, t_arg, rk, poses, Ks)
+        graphs, streams = [step, step2], [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    replay_frames(graphs, t_arg, 2, streams)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(steps):
-        step(t_arg)
+    replay_frames(graphs, t_arg, steps, streams)
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     d_in = 191 + model.pose_embedding_dim
@@ -411,16 +459,16 @@ def frame_rate(config, dev, steps=10, warmup=2):
     return {"workload": S.CONFIGS[config].name + f" ({config})", "value": steps * R / elapsed, "unit": "rays/s",
             "ms_per_step": elapsed / steps * 1e3, "steps": steps, "rays_per_frame": R, "points": scene.cfg.N,
             "bones": scene.cfg.J, "inbbox_samples": stats.get("inbbox_samples"), "kept_samples": kept,
-            "timed_frames_overflowed": bool(step.overflowed()),
+            "timed_frames_overflowed": any(bool(g.overflowed()) for g in graphs), "frames_in_flight": len(graphs),
             "mlp_kernel_ms": mlp_ms, "mlp_roofline_frac": achieved / SPLIT3_PEAK_TFLOPS}
 
 
-def other_configs(dev):
+def other_configs(dev, in_flight=2):
     """C3, C4 (frames) and C5 (repose sweep) on this GPU, compact; a failure is reported, never fatal."""
     out = {}
     for cfg in ("C3", "C4"):
         try:
-            out[cfg] = frame_rate(cfg, dev)
+            out[cfg] = frame_rate(cfg, dev, in_flight=in_flight)
             log(f"[other configs] {cfg}: {out[cfg]['value'] / 1e6:.1f} M rays/s, {out[cfg]['ms_per_step']:.2f} ms/frame")
         except Exception as e:
             out[cfg] = {"error": repr(e)}
@@ -535,6 +583,9 @@ def main():
                     help="N>1: 'rays' (default) = the ranks split one frame's rays and all-gather the tiles "
                          "over RCCL (strong scaling, SURVEY.md 8(e)); 'frames' = every rank renders its own "
                          "frame (weak scaling, no data-path collective)")
+    ap.add_argument("--in-flight", type=int, choices=[1, 2], default=2,
+                    help="frames in flight (graph-replayed frames without the ray-shard all-gather): 2 = two "
+                         "captured frames on two streams, frame i on stream i %% 2; 1 = one after another")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                     help="replay the frame as one HIP graph (TemporalPoints.capture_frame; with --shard rays "
                          "each rank's blocks, shard.capture_sharded); auto = on unless the ranks use the "
@@ -605,12 +656,20 @@ def main():
                           device=dev if torch.distributed.get_backend() == "nccl" else "cpu")
         torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN)
         use_graph = bool(ok.item())
+    graphs, streams = [], None
     if use_graph:   # the whole frame as one HIP graph replay (no per-kernel host launches, no host sync)
         if not shard_rays:
             graph_step = model.capture_frame(t_arg, rk, poses=poses, Ks=Ks, get_skeleton=True)
+            graphs = [graph_step]
+            if args.in_flight == 2:   # the second frame in flight: its own model, workspaces and graph
+                _, graph_step2 = second_frame_graph(scene, dev, t_arg, rk, poses, Ks)
+                graphs = [graph_step, graph_step2]
+                streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
         step = lambda: graph_step(t_arg)   # noqa: E731
         for _ in range(2):
             step()
+        if graphs:
+            replay_frames(graphs, t_arg, 2, streams)
         torch.cuda.synchronize(dev)
 
     # stage / MLP-kernel timings come from HIP events on eager frames (events are not recorded
@@ -629,12 +688,15 @@ def main():
     if not use_graph:
         model.timing = timing
     eager_infos = []
-    for _ in range(args.steps):
-        h0 = time.perf_counter()
-        out = step()
-        host_s += time.perf_counter() - h0
-        if not use_graph and model._last_info is not None:
-            eager_infos.append(model._last_info)
+    if graphs:   # captured frames without a collective: one or two in flight
+        out, host_s = replay_frames(graphs, t_arg, args.steps, streams)
+    else:
+        for _ in range(args.steps):
+            h0 = time.perf_counter()
+            out = step()
+            host_s += time.perf_counter() - h0
+            if not use_graph and model._last_info is not None:
+                eager_infos.append(model._last_info)
     torch.cuda.synchronize(dev)
     if not use_graph:
         timing, model.timing = model.timing, None
@@ -642,7 +704,7 @@ def main():
     # would be timed short. The graph ORs every replay's overflow flag on the device; read it once.
     # (eager frames: the device frame_info of each timed frame, kept by the loop below)
     if use_graph:
-        overflowed = bool(graph_step.overflowed())
+        overflowed = any(bool(g.overflowed()) for g in (graphs or [graph_step]))
     else:
         overflowed = any(bool(i[2]) for i in torch.stack(eager_infos).cpu()) if eager_infos else False
     n_timed = min(args.steps, 10) if use_graph else args.steps
@@ -655,6 +717,15 @@ def main():
         elapsed, overflowed = float(t[0]), bool(t[1] > 0)
     if overflowed:
         log(f"[rank {rank}] WARNING: a timed frame overflowed its sample capacity (dropped samples)")
+    serial_ms = None
+    if len(graphs) == 2:   # the same frames one at a time on one stream: the reference for the in-flight gain
+        torch.cuda.synchronize(dev)
+        ts0 = time.perf_counter()
+        replay_frames(graphs[:1], t_arg, args.steps)
+        torch.cuda.synchronize(dev)
+        serial_ms = (time.perf_counter() - ts0) / args.steps * 1e3
+        log(f"[rank {rank}] frames in flight 2: {elapsed / args.steps * 1e3:.3f} ms/frame; one at a time "
+            f"{serial_ms:.3f} ms/frame")
     from apn_amd import _lib
     lib = _lib.load()
     debug_lib = hasattr(lib, "apn_debug_knn_stats")   # APN_HIP_LIB = libapn_hip_debug.so (tools/ A/B runs)
@@ -773,7 +844,7 @@ def main():
             log(f"knn work report failed: {e!r}")
     others = None
     if world == 1 and args.config == "C2" and not args.no_other_configs:
-        others = other_configs(dev)
+        others = other_configs(dev, args.in_flight)
     line = {
         "metric": f"rendered rays/sec at {scene.cfg.W}x{scene.cfg.H}, {scene.cfg.N // 1000}k pts, {scene.cfg.J} bones",
         "value": value, "unit": "rays/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -793,8 +864,12 @@ def main():
                    if world > 1 else "single",
                    "step": (("each rank's blocks replayed as one HIP graph (shard.capture_sharded), then the "
                              "all-gather" if shard_rays else
-                             "whole frame replayed as one HIP graph (TemporalPoints.capture_frame)") if use_graph
+                             "whole frame replayed as one HIP graph (TemporalPoints.capture_frame)"
+                             + ("; two frames in flight (two models' graphs on two streams, frame i on stream "
+                                "i % 2)" if len(graphs) == 2 else "")) if use_graph
                             else "eager launches"),
+                   "frames_in_flight": max(len(graphs), 1),
+                   "serial_ms_per_step": serial_ms,
                    "timed_frames_overflowed": overflowed,
                    "mlp_fp32_fallback_fired": mlp_fallback},
         "roofline": {"bound": "mfma", "kernel": kernel, "achieved": achieved, "peak": peak,

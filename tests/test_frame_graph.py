@@ -103,6 +103,34 @@ def test_captured_frame_back_to_back(dev):
             assert torch.equal(got[k], ref[k]), (i, k)
 
 
+def test_two_frames_in_flight_equal_eager(dev):
+    """bench.py --in-flight 2: two models of one scene (own workspaces), their captured frames
+    replayed on two streams, frame i on stream i % 2, so consecutive frames run concurrently: every
+    frame equals the eager frame at its time bit for bit."""
+    from apn_amd import harness
+    scene, a = _scene_model(dev)
+    b = harness.build_model(scene, dev)
+    rk = scene.render_kwargs(dev)
+    ts = [torch.tensor([scene.cfg.t + 0.05 * i], device=dev) for i in range(4)]
+    steps = [m.capture_frame(ts[0], rk) for m in (a, b)]
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    cur = torch.cuda.current_stream(dev)
+    for s in streams:
+        s.wait_stream(cur)
+    got = []
+    for i in range(8):
+        with torch.cuda.stream(streams[i % 2]):
+            g = steps[i % 2](ts[i % 4])
+            got.append({k: g[k].clone() for k in KEYS})
+    for s in streams:
+        cur.wait_stream(s)
+    torch.cuda.synchronize()
+    for i, frame in enumerate(got):
+        ref = _frame(a, ts[i % 4], rk)
+        for k in KEYS:
+            assert torch.equal(frame[k], ref[k]), (i, k)
+
+
 def test_captured_frame_overflow_recaptures(dev, monkeypatch):
     """A replay whose samples overflow the captured capacity is flagged (step.overflowed(), the OR
     of every replay's frame_info[2] accumulated inside the graph), its read re-renders it exactly,
