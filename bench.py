@@ -409,6 +409,15 @@ def replay_frames(steps_in_flight, t_arg, k, streams=None):
     return out, h
 
 
+def replay_sharded(steps_in_flight, t_arg, k, streams, comm):
+    """k ray-shard frames with two in flight (apn_amd.shard.replay_in_flight). Returns the last
+    frame and the host seconds spent issuing."""
+    from apn_amd.shard import replay_in_flight
+    h0 = time.perf_counter()
+    out = replay_in_flight(steps_in_flight, [t_arg] * k, streams, comm)[-1]
+    return out, time.perf_counter() - h0
+
+
 def second_frame_graph(scene, dev, t_arg, rk, poses, Ks):
     """A second TemporalPoints of the scene (same weights, own workspaces) with its frame captured
     (the second frame in flight)."""
@@ -644,9 +653,16 @@ def main():
     torch.cuda.synchronize(dev)
     stats = model.last_stats.resolved()
     log(f"[rank {rank}] scene: {stats}")
+    shard_graphs = []
     if use_graph and shard_rays:   # this rank's blocks as one graph replay, then the tile all-gather
         try:
             graph_step = SH.capture_sharded(model, t_arg, rk, rank, world, poses=poses, Ks=Ks, get_skeleton=True)
+            shard_graphs = [graph_step]
+            if args.in_flight == 2:   # a second model's shard graph: two frames in flight
+                model2 = harness.build_model(scene, dev)
+                _ = model2.mean_min_distance
+                shard_graphs.append(SH.capture_sharded(model2, t_arg, rk, rank, world, poses=poses, Ks=Ks,
+                                                       get_skeleton=True))
         except Exception as e:   # the eager shard frame runs the same kernels and the same collectives
             log(f"[rank {rank}] shard graph capture failed ({e!r}); timing eager shard frames")
             use_graph = False
@@ -670,6 +686,10 @@ def main():
             step()
         if graphs:
             replay_frames(graphs, t_arg, 2, streams)
+        if len(shard_graphs) == 2:
+            streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+            comm = torch.cuda.Stream(dev)
+            replay_sharded(shard_graphs, t_arg, 2, streams, comm)
         torch.cuda.synchronize(dev)
 
     # stage / MLP-kernel timings come from HIP events on eager frames (events are not recorded
@@ -690,6 +710,8 @@ def main():
     eager_infos = []
     if graphs:   # captured frames without a collective: one or two in flight
         out, host_s = replay_frames(graphs, t_arg, args.steps, streams)
+    elif use_graph and len(shard_graphs) == 2:   # ray shards, two frames in flight, one collective stream
+        out, host_s = replay_sharded(shard_graphs, t_arg, args.steps, streams, comm)
     else:
         for _ in range(args.steps):
             h0 = time.perf_counter()
@@ -704,7 +726,7 @@ def main():
     # would be timed short. The graph ORs every replay's overflow flag on the device; read it once.
     # (eager frames: the device frame_info of each timed frame, kept by the loop below)
     if use_graph:
-        overflowed = any(bool(g.overflowed()) for g in (graphs or [graph_step]))
+        overflowed = any(bool(g.overflowed()) for g in (graphs or shard_graphs or [graph_step]))
     else:
         overflowed = any(bool(i[2]) for i in torch.stack(eager_infos).cpu()) if eager_infos else False
     n_timed = min(args.steps, 10) if use_graph else args.steps
@@ -718,10 +740,13 @@ def main():
     if overflowed:
         log(f"[rank {rank}] WARNING: a timed frame overflowed its sample capacity (dropped samples)")
     serial_ms = None
-    if len(graphs) == 2:   # the same frames one at a time on one stream: the reference for the in-flight gain
+    if use_graph and (len(graphs) == 2 or len(shard_graphs) == 2):
+        # the same frames one at a time on one stream: the reference for the in-flight gain
+        if world > 1:
+            torch.distributed.barrier()
         torch.cuda.synchronize(dev)
         ts0 = time.perf_counter()
-        replay_frames(graphs[:1], t_arg, args.steps)
+        replay_frames([graph_step], t_arg, args.steps)
         torch.cuda.synchronize(dev)
         serial_ms = (time.perf_counter() - ts0) / args.steps * 1e3
         log(f"[rank {rank}] frames in flight 2: {elapsed / args.steps * 1e3:.3f} ms/frame; one at a time "
@@ -863,12 +888,14 @@ def main():
                                    if shard_rays else f"frames x{world} (no data-path collective)")
                    if world > 1 else "single",
                    "step": (("each rank's blocks replayed as one HIP graph (shard.capture_sharded), then the "
-                             "all-gather" if shard_rays else
+                             "all-gather" + ("; two frames in flight (two models' shard graphs on two streams, the "
+                                             "all-gathers in frame order on one collective stream)"
+                                             if len(shard_graphs) == 2 else "") if shard_rays else
                              "whole frame replayed as one HIP graph (TemporalPoints.capture_frame)"
                              + ("; two frames in flight (two models' graphs on two streams, frame i on stream "
                                 "i % 2)" if len(graphs) == 2 else "")) if use_graph
                             else "eager launches"),
-                   "frames_in_flight": max(len(graphs), 1),
+                   "frames_in_flight": max(len(graphs), len(shard_graphs) if use_graph else 1, 1),
                    "serial_ms_per_step": serial_ms,
                    "timed_frames_overflowed": overflowed,
                    "mlp_fp32_fallback_fired": mlp_fallback},

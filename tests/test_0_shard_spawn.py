@@ -35,7 +35,7 @@ def _worker(rank, world, port, outdir, split):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     import torch.distributed as dist
     from apn_amd import harness, synthetic as S
-    from apn_amd.shard import RAY_BLOCK, capture_sharded, pack_tile, render_sharded
+    from apn_amd.shard import RAY_BLOCK, capture_sharded, pack_tile, render_sharded, replay_in_flight
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         dev = torch.device("cuda", 0)
@@ -53,11 +53,19 @@ def _worker(rank, world, port, outdir, split):
             # sync-free path (previous frame's split, per-rank capacity); frame 3: rank 1 overflows
             # its capacity, which every rank must detect through the gathered frame_info rows
             # ("graph": the blocks split with each rank's frame replayed from a HIP graph, bench's step)
-            step = capture_sharded(model, t0, rk, rank, world, **kw) if split == "graph" else None
+            step = capture_sharded(model, t0, rk, rank, world, **kw) if split in ("graph", "graph2") else None
+            in_flight = None
+            if split == "graph2":   # two frames in flight: two models' graphs, one collective stream
+                model_b = harness.build_model(scene, dev)
+                steps = [step, capture_sharded(model_b, t0, rk, rank, world, **kw)]
+                streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+                in_flight = replay_in_flight(steps, (t0, t1, t0, t1), streams, torch.cuda.Stream(dev), keep=True)
             for i, t in enumerate((t0, t1, t0, t1)):
                 if i == 3 and rank == 1 and step is None:
                     model._capacity[(R, rank, world, RAY_BLOCK) if split == "blocks" else (R, rank, world)] = 64
-                if step is not None:
+                if in_flight is not None:
+                    out = in_flight[i]
+                elif step is not None:
                     out = step(t)
                 else:
                     out = render_sharded(model, t, rk, rank, world, split=split, **kw)
@@ -76,7 +84,7 @@ def _worker(rank, world, port, outdir, split):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("split", ["blocks", "ranges", "graph"])
+@pytest.mark.parametrize("split", ["blocks", "ranges", "graph", "graph2"])
 def test_render_sharded_two_processes_bit_identical(split):
     import torch.multiprocessing as mp
     with tempfile.TemporaryDirectory() as d:

@@ -3,7 +3,7 @@ workspaces), each frame captured as one HIP graph (capture_frame); K frames repl
 another on one stream vs alternating over two streams (frame i on stream i % 2, so one frame's
 MLP runs beside the next frame's kNN / sampling). Checks that both orders give the same frames.
 
-    python tools/frames_in_flight.py [--config C2] [--frames 20]
+    python tools/frames_in_flight.py [--config C2] [--frames 20] [--shard RANK,WORLD]
 """
 from __future__ import annotations
 
@@ -22,6 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C2")
     ap.add_argument("--frames", type=int, default=20)
+    ap.add_argument("--shard", default="", help="rank,world: replay that ray shard's graph (blocks split) instead")
     args = ap.parse_args()
     torch.set_grad_enabled(False)
     dev = torch.device("cuda", 0)
@@ -35,7 +36,11 @@ def main():
         _ = m.mean_min_distance
         for _ in range(2):
             m(t, render_depth=True, render_kwargs=rk, render_weights=True, poses=poses, Ks=Ks, get_skeleton=True)
-        steps.append(m.capture_frame(t, rk, poses=poses, Ks=Ks, get_skeleton=True))
+        shard = None
+        if args.shard:
+            rank, world = (int(v) for v in args.shard.split(","))
+            shard = (rank, world, 4096)
+        steps.append(m.capture_frame(t, rk, poses=poses, Ks=Ks, get_skeleton=True, ray_shard=shard))
     torch.cuda.synchronize(dev)
     cur = torch.cuda.current_stream(dev)
     streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
