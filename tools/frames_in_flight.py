@@ -22,6 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C2")
     ap.add_argument("--frames", type=int, default=20)
+    ap.add_argument("--n", type=int, default=2, help="frames in flight")
     ap.add_argument("--shard", default="", help="rank,world: replay that ray shard's graph (blocks split) instead")
     args = ap.parse_args()
     torch.set_grad_enabled(False)
@@ -30,7 +31,7 @@ def main():
     rk = scene.render_kwargs(dev)
     t = torch.tensor([scene.cfg.t], device=dev)
     poses, Ks = scene.c2w[None].to(dev), scene.K[None].to(dev)
-    models = [harness.build_model(scene, dev) for _ in range(2)]
+    models = [harness.build_model(scene, dev) for _ in range(args.n)]
     steps = []
     for m in models:
         _ = m.mean_min_distance
@@ -43,7 +44,7 @@ def main():
         steps.append(m.capture_frame(t, rk, poses=poses, Ks=Ks, get_skeleton=True, ray_shard=shard))
     torch.cuda.synchronize(dev)
     cur = torch.cuda.current_stream(dev)
-    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    streams = [torch.cuda.Stream(dev) for _ in range(args.n)]
 
     def serial(k):
         for _ in range(k):
@@ -55,8 +56,8 @@ def main():
         for s in streams:
             s.wait_event(ev)
         for i in range(k):
-            with torch.cuda.stream(streams[i % 2]):
-                steps[i % 2](t)
+            with torch.cuda.stream(streams[i % args.n]):
+                steps[i % args.n](t)
         for s in streams:
             cur.wait_stream(s)
 
@@ -73,7 +74,7 @@ def main():
     for rep in range(3):
         ts = timed(serial, args.frames)
         tp = timed(pipelined, args.frames)
-        print(f"rep {rep}: serial {ts:.3f} ms/frame, two in flight {tp:.3f} ms/frame ({ts / tp:.3f}x)")
+        print(f"rep {rep}: serial {ts:.3f} ms/frame, {args.n} in flight {tp:.3f} ms/frame ({ts / tp:.3f}x)")
     # the frames of both graphs equal a serial frame bit for bit
     outs = []
     for i in range(2):
