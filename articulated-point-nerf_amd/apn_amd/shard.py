@@ -330,29 +330,30 @@ def capture_sharded(model, t, render_kwargs, rank: int, world: int, group=None, 
 
 
 def replay_in_flight(steps, ts, streams, comm, keep: bool = False) -> list:
-    """Ray-shard frames with two in flight (bench.py --in-flight 2): frame i (time ts[i]) replays
-    steps[i % 2]'s graph (two capture_sharded steps of two models, own workspaces) on
-    streams[i % 2], and its tile all-gather (step.assemble) runs on the ONE collective stream
+    """Ray-shard frames with len(steps) frames in flight (bench.py --in-flight): frame i (time
+    ts[i]) replays steps[i % n]'s graph (capture_sharded steps of n models, own workspaces) on
+    streams[i % n], and its tile all-gather (step.assemble) runs on the ONE collective stream
     ``comm`` in frame order, so every rank issues the same collectives in the same order. A
     stream's next replay waits (event) for the assembly of its previous frame, whose tile it
     overwrites. Returns every assembled frame (``keep``) or the last one, in a list."""
+    n = len(steps)
     cur = torch.cuda.current_stream()
     ev = torch.cuda.Event()
     ev.record(cur)
     for s in list(streams) + [comm]:
         s.wait_event(ev)
-    done = [torch.cuda.Event(), torch.cuda.Event()]
+    done = [torch.cuda.Event() for _ in range(n)]
     frames = []
     for i, t in enumerate(ts):
-        s = streams[i % 2]
-        if i >= 2:
-            s.wait_event(done[i % 2])   # frame i - 2's tile has been packed and gathered
+        s = streams[i % n]
+        if i >= n:
+            s.wait_event(done[i % n])   # frame i - n's tile has been packed and gathered
         with torch.cuda.stream(s):
-            o = steps[i % 2].local(t)
+            o = steps[i % n].local(t)
         comm.wait_stream(s)
         with torch.cuda.stream(comm):
-            f = steps[i % 2].assemble(t, o)
-            done[i % 2].record(comm)
+            f = steps[i % n].assemble(t, o)
+            done[i % n].record(comm)
         frames = frames + [f] if keep else [f]
     for s in list(streams) + [comm]:
         cur.wait_stream(s)

@@ -383,8 +383,8 @@ def lbs_sweep(args, rank, world, dev):
 
 
 def replay_frames(steps_in_flight, t_arg, k, streams=None):
-    """Replays k captured frames: one graph on the current stream, or graphs g_0, g_1 alternating
-    over two streams (frame i: graph i % 2 on stream i % 2; both join the current stream at the end).
+    """Replays k captured frames: one graph on the current stream, or n graphs g_0 .. g_n-1 in turn
+    over n streams (frame i: graph i % n on stream i % n; all join the current stream at the end).
     Returns the last frame and the host seconds spent issuing."""
     h = 0.0
     out = None
@@ -399,10 +399,11 @@ def replay_frames(steps_in_flight, t_arg, k, streams=None):
     ev.record(cur)
     for s in streams:
         s.wait_event(ev)
+    n = len(steps_in_flight)
     for i in range(k):
         h0 = time.perf_counter()
-        with torch.cuda.stream(streams[i % 2]):
-            out = steps_in_flight[i % 2](t_arg)
+        with torch.cuda.stream(streams[i % n]):
+            out = steps_in_flight[i % n](t_arg)
         h += time.perf_counter() - h0
     for s in streams:
         cur.wait_stream(s)
@@ -410,8 +411,8 @@ def replay_frames(steps_in_flight, t_arg, k, streams=None):
 
 
 def replay_sharded(steps_in_flight, t_arg, k, streams, comm):
-    """k ray-shard frames with two in flight (apn_amd.shard.replay_in_flight). Returns the last
-    frame and the host seconds spent issuing."""
+    """k ray-shard frames with len(steps_in_flight) in flight (apn_amd.shard.replay_in_flight).
+    Returns the last frame and the host seconds spent issuing."""
     from apn_amd.shard import replay_in_flight
     h0 = time.perf_counter()
     out = replay_in_flight(steps_in_flight, [t_arg] * k, streams, comm)[-1]
@@ -419,8 +420,8 @@ def replay_sharded(steps_in_flight, t_arg, k, streams, comm):
 
 
 def second_frame_graph(scene, dev, t_arg, rk, poses, Ks):
-    """A second TemporalPoints of the scene (same weights, own workspaces) with its frame captured
-    (the second frame in flight)."""
+    """Another TemporalPoints of the scene (same weights, own workspaces) with its frame captured
+    (one more frame in flight)."""
     m2 = harness.build_model(scene, dev)
     _ = m2.mean_min_distance
     for _ in range(2):
@@ -454,9 +455,9 @@ def frame_rate(config, dev, steps=10, warmup=2, in_flight=2):
     kept = int(ev[-1][2].item()) if ev else stats.get("kept_samples", 0)
     step = model.capture_frame(t_arg, rk, poses=poses, Ks=Ks, get_skeleton=True)
     graphs, streams = [step], None
-    if in_flight == 2:
-        _, step2 = second_frame_graph(scene, dev, t_arg, rk, poses, Ks)
-        graphs, streams = [step, step2], [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    if in_flight > 1:
+        graphs += [second_frame_graph(scene, dev, t_arg, rk, poses, Ks)[1] for _ in range(in_flight - 1)]
+        streams = [torch.cuda.Stream(dev) for _ in graphs]
     replay_frames(graphs, t_arg, 2, streams)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -592,9 +593,10 @@ def main():
                     help="N>1: 'rays' (default) = the ranks split one frame's rays and all-gather the tiles "
                          "over RCCL (strong scaling, SURVEY.md 8(e)); 'frames' = every rank renders its own "
                          "frame (weak scaling, no data-path collective)")
-    ap.add_argument("--in-flight", type=int, choices=[1, 2], default=2,
-                    help="frames in flight (graph-replayed frames without the ray-shard all-gather): 2 = two "
-                         "captured frames on two streams, frame i on stream i %% 2; 1 = one after another")
+    ap.add_argument("--in-flight", type=int, choices=[1, 2, 3], default=2,
+                    help="frames in flight: n models' captured frames on n streams, frame i on stream i %% n "
+                         "(ray shards: the all-gathers in frame order on one collective stream); 1 = one "
+                         "after another")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                     help="replay the frame as one HIP graph (TemporalPoints.capture_frame; with --shard rays "
                          "each rank's blocks, shard.capture_sharded); auto = on unless the ranks use the "
@@ -658,7 +660,7 @@ def main():
         try:
             graph_step = SH.capture_sharded(model, t_arg, rk, rank, world, poses=poses, Ks=Ks, get_skeleton=True)
             shard_graphs = [graph_step]
-            if args.in_flight == 2:   # a second model's shard graph: two frames in flight
+            for _ in range(args.in_flight - 1):   # more models' shard graphs: frames in flight
                 model2 = harness.build_model(scene, dev)
                 _ = model2.mean_min_distance
                 shard_graphs.append(SH.capture_sharded(model2, t_arg, rk, rank, world, poses=poses, Ks=Ks,
@@ -677,17 +679,16 @@ def main():
         if not shard_rays:
             graph_step = model.capture_frame(t_arg, rk, poses=poses, Ks=Ks, get_skeleton=True)
             graphs = [graph_step]
-            if args.in_flight == 2:   # the second frame in flight: its own model, workspaces and graph
-                _, graph_step2 = second_frame_graph(scene, dev, t_arg, rk, poses, Ks)
-                graphs = [graph_step, graph_step2]
-                streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+            if args.in_flight > 1:   # more frames in flight: their own models, workspaces and graphs
+                graphs += [second_frame_graph(scene, dev, t_arg, rk, poses, Ks)[1] for _ in range(args.in_flight - 1)]
+                streams = [torch.cuda.Stream(dev) for _ in graphs]
         step = lambda: graph_step(t_arg)   # noqa: E731
         for _ in range(2):
             step()
         if graphs:
             replay_frames(graphs, t_arg, 2, streams)
-        if len(shard_graphs) == 2:
-            streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+        if len(shard_graphs) > 1:
+            streams = [torch.cuda.Stream(dev) for _ in shard_graphs]
             comm = torch.cuda.Stream(dev)
             replay_sharded(shard_graphs, t_arg, 2, streams, comm)
         torch.cuda.synchronize(dev)
@@ -710,7 +711,7 @@ def main():
     eager_infos = []
     if graphs:   # captured frames without a collective: one or two in flight
         out, host_s = replay_frames(graphs, t_arg, args.steps, streams)
-    elif use_graph and len(shard_graphs) == 2:   # ray shards, two frames in flight, one collective stream
+    elif use_graph and len(shard_graphs) > 1:   # ray shards, frames in flight, one collective stream
         out, host_s = replay_sharded(shard_graphs, t_arg, args.steps, streams, comm)
     else:
         for _ in range(args.steps):
@@ -740,7 +741,7 @@ def main():
     if overflowed:
         log(f"[rank {rank}] WARNING: a timed frame overflowed its sample capacity (dropped samples)")
     serial_ms = None
-    if use_graph and (len(graphs) == 2 or len(shard_graphs) == 2):
+    if use_graph and (len(graphs) > 1 or len(shard_graphs) > 1):
         # the same frames one at a time on one stream: the reference for the in-flight gain
         if world > 1:
             torch.distributed.barrier()
@@ -749,7 +750,8 @@ def main():
         replay_frames([graph_step], t_arg, args.steps)
         torch.cuda.synchronize(dev)
         serial_ms = (time.perf_counter() - ts0) / args.steps * 1e3
-        log(f"[rank {rank}] frames in flight 2: {elapsed / args.steps * 1e3:.3f} ms/frame; one at a time "
+        log(f"[rank {rank}] frames in flight {max(len(graphs), len(shard_graphs))}: "
+            f"{elapsed / args.steps * 1e3:.3f} ms/frame; one at a time "
             f"{serial_ms:.3f} ms/frame")
     from apn_amd import _lib
     lib = _lib.load()
@@ -888,12 +890,12 @@ def main():
                                    if shard_rays else f"frames x{world} (no data-path collective)")
                    if world > 1 else "single",
                    "step": (("each rank's blocks replayed as one HIP graph (shard.capture_sharded), then the "
-                             "all-gather" + ("; two frames in flight (two models' shard graphs on two streams, the "
-                                             "all-gathers in frame order on one collective stream)"
-                                             if len(shard_graphs) == 2 else "") if shard_rays else
+                             "all-gather" + (f"; {len(shard_graphs)} frames in flight ({len(shard_graphs)} models' "
+                                             "shard graphs on as many streams, the all-gathers in frame order on "
+                                             "one collective stream)" if len(shard_graphs) > 1 else "") if shard_rays else
                              "whole frame replayed as one HIP graph (TemporalPoints.capture_frame)"
-                             + ("; two frames in flight (two models' graphs on two streams, frame i on stream "
-                                "i % 2)" if len(graphs) == 2 else "")) if use_graph
+                             + (f"; {len(graphs)} frames in flight ({len(graphs)} models' graphs on as many "
+                                "streams, frame i on stream i % n)" if len(graphs) > 1 else "")) if use_graph
                             else "eager launches"),
                    "frames_in_flight": max(len(graphs), len(shard_graphs) if use_graph else 1, 1),
                    "serial_ms_per_step": serial_ms,
