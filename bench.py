@@ -14,13 +14,14 @@ has every rank render its own frame instead (weak scaling, no data-path collecti
 (LBS-only) shards the points N/W per rank with no collective (strong scaling). The timing is
 barrier + synchronize bracketed and the max over ranks (all-reduce MAX of the elapsed time).
 
-Frames in flight (``--in-flight``, default 2): a frame's stages run in sequence (the kNN needs the
+Frames in flight (``--in-flight``, default 3): a frame's stages run in sequence (the kNN needs the
 warped cloud, the MLP the kNN's survivors), so one frame leaves the chip under-used while its kNN
-and small stages run. With two frames in flight two TemporalPoints of the same scene (own
-workspaces) replay their captured frames on two HIP streams, frame i on stream i % 2: one frame's
-MLP runs beside the next frame's kNN and sampling. Every frame is still rendered in full and is
+and small stages run. With n frames in flight n TemporalPoints of the same scene (own workspaces)
+replay their captured frames on n HIP streams, frame i on stream i % n: one frame's MLP runs
+beside the next frames' kNN and sampling. Every frame is still rendered in full and is
 bit-identical to a serial frame (tests/test_frame_graph.py); ``config.serial_ms_per_step`` is the
-same frames one at a time on one stream. The ray-sharded steps (all-gather per frame) stay serial.
+same frames one at a time on one stream. Ray shards keep their per-frame all-gathers on one
+collective stream in frame order (apn_amd.shard.replay_in_flight).
 
 Rank 0 prints ONE JSON line. Diagnostics go to stderr.
 
@@ -430,7 +431,7 @@ def second_frame_graph(scene, dev, t_arg, rk, poses, Ks):
     return m2, m2.capture_frame(t_arg, rk, poses=poses, Ks=Ks, get_skeleton=True)
 
 
-def frame_rate(config, dev, steps=10, warmup=2, in_flight=2):
+def frame_rate(config, dev, steps=10, warmup=2, in_flight=3):
     """One GPU, one config (C3 / C4): whole frames replayed as one HIP graph, as the headline line,
     plus the MLP kernel's time from HIP events on eager frames and its F_alg roofline fraction.
     Rides along in the default line (`other_configs`), so every config has a driver-run number."""
@@ -473,7 +474,7 @@ def frame_rate(config, dev, steps=10, warmup=2, in_flight=2):
             "mlp_kernel_ms": mlp_ms, "mlp_roofline_frac": achieved / SPLIT3_PEAK_TFLOPS}
 
 
-def other_configs(dev, in_flight=2):
+def other_configs(dev, in_flight=3):
     """C3, C4 (frames) and C5 (repose sweep) on this GPU, compact; a failure is reported, never fatal."""
     out = {}
     for cfg in ("C3", "C4"):
@@ -593,7 +594,7 @@ def main():
                     help="N>1: 'rays' (default) = the ranks split one frame's rays and all-gather the tiles "
                          "over RCCL (strong scaling, SURVEY.md 8(e)); 'frames' = every rank renders its own "
                          "frame (weak scaling, no data-path collective)")
-    ap.add_argument("--in-flight", type=int, choices=[1, 2, 3], default=2,
+    ap.add_argument("--in-flight", type=int, choices=[1, 2, 3], default=3,
                     help="frames in flight: n models' captured frames on n streams, frame i on stream i %% n "
                          "(ray shards: the all-gathers in frame order on one collective stream); 1 = one "
                          "after another")

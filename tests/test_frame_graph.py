@@ -103,24 +103,25 @@ def test_captured_frame_back_to_back(dev):
             assert torch.equal(got[k], ref[k]), (i, k)
 
 
-def test_two_frames_in_flight_equal_eager(dev):
-    """bench.py --in-flight 2: two models of one scene (own workspaces), their captured frames
-    replayed on two streams, frame i on stream i % 2, so consecutive frames run concurrently: every
+@pytest.mark.parametrize("n", [2, 3])
+def test_two_frames_in_flight_equal_eager(dev, n):
+    """bench.py --in-flight n: n models of one scene (own workspaces), their captured frames
+    replayed on n streams, frame i on stream i % n, so consecutive frames run concurrently: every
     frame equals the eager frame at its time bit for bit."""
     from apn_amd import harness
     scene, a = _scene_model(dev)
-    b = harness.build_model(scene, dev)
+    models = [a] + [harness.build_model(scene, dev) for _ in range(n - 1)]
     rk = scene.render_kwargs(dev)
     ts = [torch.tensor([scene.cfg.t + 0.05 * i], device=dev) for i in range(4)]
-    steps = [m.capture_frame(ts[0], rk) for m in (a, b)]
-    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    steps = [m.capture_frame(ts[0], rk) for m in models]
+    streams = [torch.cuda.Stream(dev) for _ in range(n)]
     cur = torch.cuda.current_stream(dev)
     for s in streams:
         s.wait_stream(cur)
     got = []
     for i in range(8):
-        with torch.cuda.stream(streams[i % 2]):
-            g = steps[i % 2](ts[i % 4])
+        with torch.cuda.stream(streams[i % n]):
+            g = steps[i % n](ts[i % 4])
             got.append({k: g[k].clone() for k in KEYS})
     for s in streams:
         cur.wait_stream(s)
