@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--worlds", default="2,4,8")
     ap.add_argument("--split", default="inbbox,cost")
     ap.add_argument("--kept-weights", default="", help="comma list of shard.KEPT_WEIGHT values to try (cost split)")
+    ap.add_argument("--in-flight", type=int, default=1,
+                    help="gilv splits: replay each shard's frames with this many in flight (models' graphs on "
+                         "as many streams, bench.py --in-flight; no all-gather)")
     args = ap.parse_args()
     torch.set_grad_enabled(False)
     dev = torch.device("cuda", 0)
@@ -64,6 +67,19 @@ def main():
                 stages[name] = stages.get(name, 0.0) + a.elapsed_time(b)
         return ms, out
 
+    extra = [harness.build_model(scene, dev) for _ in range(args.in_flight - 1)]
+    fl_streams = [torch.cuda.Stream(dev) for _ in range(args.in_flight)]
+
+    def in_flight(gsteps):
+        cur = torch.cuda.current_stream(dev)
+        for s in fl_streams:
+            s.wait_stream(cur)
+        for i in range(len(gsteps) * 4):
+            with torch.cuda.stream(fl_streams[i % len(gsteps)]):
+                gsteps[i % len(gsteps)](t)
+        for s in fl_streams:
+            cur.wait_stream(s)
+
     full_ms, out = timed(lambda: model(t, **kw), args.reps)
     st = model.last_stats.resolved()
     print(f"full frame {full_ms:.3f} ms, {st}")
@@ -85,6 +101,10 @@ def main():
                     fk = {n: v for n, v in kw.items() if n not in ("render_kwargs", "render_depth", "render_weights")}
                     gstep = model.capture_frame(t, rk, ray_shard=(k, world, B), **fk)
                     fn = lambda: gstep(t)   # noqa: E731
+                    if extra:   # frames in flight: timed per frame (4 rounds of len(gsteps) frames per call)
+                        gsteps = [gstep] + [m.capture_frame(t, rk, ray_shard=(k, world, B), **fk) for m in extra]
+                        fl_ms, _ = timed(lambda: in_flight(gsteps), args.reps)
+                        print(f"   shard {k}: {args.in_flight} in flight {fl_ms / (4 * len(gsteps)):.3f} ms/frame")
                 else:
                     fn = lambda: model(t, ray_shard=(k, world, B), **kw)   # noqa: E731
                 ms, o = timed(fn, args.reps)
