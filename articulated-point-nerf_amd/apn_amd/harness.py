@@ -260,16 +260,33 @@ def _joint_record(out, joints, i, HW, render_kwargs):
     return out.get("bones")
 
 
+def _view_rays(i, HW, Ks, c2w, ndc, inverse_y, flip_x, flip_y, fixed_viewdirs, dev):
+    """View i's rays, generated on ``dev`` (the reference generates them on the poses' device)."""
+    from .tineuvox import get_rays_of_a_view
+    H, W = int(HW[i][0]), int(HW[i][1])
+    K = Ks[i].to(dev, torch.float32)
+    c2w = torch.as_tensor(c2w).to(dev, torch.float32)
+    ro, rd, vd = get_rays_of_a_view(H, W, K, c2w, ndc, inverse_y=inverse_y, flip_x=flip_x, flip_y=flip_y)
+    if fixed_viewdirs is not None:
+        vd = torch.as_tensor(fixed_viewdirs).to(dev)
+    return H, W, K, c2w, ro.reshape(-1, 3), rd.reshape(-1, 3), vd.reshape(-1, 3)
+
+
 @torch.no_grad()
 def render_viewpoints(model, render_poses, HW, Ks, ndc, render_kwargs, gt_imgs=None, savedir=None, test_times=None,
                       render_factor=0, eval_psnr=False, eval_ssim=False, eval_lpips_alex=False,
                       eval_lpips_vgg=False, inverse_y=False, flip_x=False, flip_y=False, batch_size=4096 * 2,
-                      verbose=True, render_pcd_direct=False, render_flow=False, fixed_viewdirs=None):
+                      verbose=True, render_pcd_direct=False, render_flow=False, fixed_viewdirs=None, in_flight=3):
     """run.py:80-239: every view's rays (tineuvox.get_rays_of_a_view), the model at that view's
     time, rgb / depth / weight-visualisation images, optional PSNR / SSIM against gt_imgs, PNGs
-    in savedir, the skeleton drawn on the weight images. Returns (rgbs, depths, weights, flows)."""
+    in savedir, the skeleton drawn on the weight images. Returns (rgbs, depths, weights, flows).
+
+    A TemporalPoints model renders with ``in_flight`` frames in flight (apn_amd.pipeline): view
+    i + 1 .. i + in_flight - 1 are queued on the GPU while view i is read back and scored, all
+    from one model (its frame captured once per workspace, reused across calls while the model's
+    parameters are unchanged). Every image equals the model's own frame for that view bit for bit
+    (tests/test_pipeline.py). ``in_flight=1``: one eager forward per view, as the reference."""
     import numpy as np
-    from .tineuvox import get_rays_of_a_view
     if eval_lpips_alex or eval_lpips_vgg:
         raise NotImplementedError("LPIPS needs the torchvision / lpips network weights, absent here")
     if render_flow:
@@ -278,22 +295,65 @@ def render_viewpoints(model, render_poses, HW, Ks, ndc, render_kwargs, gt_imgs=N
     HW, Ks = _scaled_views(HW, Ks, render_factor)
     is_tp = isinstance(model, TemporalPoints)
     rgbs, depths, weights, psnrs, ssims, joints, bones = [], [], [], [], [], {}, None
+
+    def score(i, rgb):
+        if gt_imgs is not None and render_factor == 0:
+            if eval_psnr:
+                psnrs.append(float(-10.0 * np.log10(np.mean(np.square(rgb - gt_imgs[i])))))
+            if eval_ssim:
+                ssims.append(rgb_ssim(rgb, gt_imgs[i], max_val=1))
+
+    if is_tp and in_flight > 1 and len(render_poses) > 1 and len({(int(h), int(w)) for h, w in HW}) == 1:
+        from .pipeline import cached_pipeline
+        dev = model.canonical_feat.device
+        rgb_key = "rgb_marched_direct" if render_pcd_direct else "rgb_marched"
+        pipe, pending = None, []
+
+        def fetch():
+            i, H, W, h = pending.pop(0)
+            r = h.result()
+            if "joints" in r:
+                b = _joint_record({"joints": r["joints"], "bones": model.bones if model.joints_to_keep is None
+                                   else model.new_bones}, joints, i, HW, render_kwargs)
+                nonlocal bones
+                bones = b if b is not None else bones
+            rgb = r[rgb_key].reshape(H, W, -1).numpy()
+            rgbs.append(rgb)
+            depths.append(r["depth"].reshape(H, W, -1).numpy())
+            weights.append(r["weights"].reshape(H, W, -1).numpy())
+            score(i, rgb)
+        for i, c2w in enumerate(render_poses):
+            H, W, K, c2w, ro, rd, vd = _view_rays(i, HW, Ks, c2w, ndc, inverse_y, flip_x, flip_y, fixed_viewdirs, dev)
+            t = torch.as_tensor(test_times[i], dtype=torch.float32, device=dev).reshape(1)
+            if pipe is None:
+                rk = dict(render_kwargs, rays_o=ro, rays_d=rd, viewdirs=vd)
+                pipe = cached_pipeline(model, t, rk, n=in_flight, render_depth=True, render_weights=True,
+                                       poses=c2w[None], Ks=K[None], get_skeleton=True,
+                                       readback=(rgb_key, "depth", "weights"))
+            pending.append((i, H, W, pipe.submit(t, (ro, rd, vd), c2w[None], K[None])))
+            if len(pending) >= in_flight:
+                fetch()
+        while pending:
+            fetch()
+        if verbose and psnrs:
+            print("Testing psnr", np.mean(psnrs), "(avg)")
+        if verbose and ssims:
+            print("Testing ssim", np.mean(ssims), "(avg)")
+        rgbs, depths, weights = _finish(rgbs, depths, weights, joints, bones, savedir, psnrs, ssims, eval_psnr,
+                                        eval_ssim)
+        return rgbs, depths, weights, np.array([])
+
     for i, c2w in enumerate(render_poses):
-        H, W = int(HW[i][0]), int(HW[i][1])
-        K = Ks[i].to(torch.float32)
-        ro, rd, vd = get_rays_of_a_view(H, W, K, c2w, ndc, inverse_y=inverse_y, flip_x=flip_x, flip_y=flip_y)
-        if fixed_viewdirs is not None:
-            vd = fixed_viewdirs
-        ro, rd, vd = ro.reshape(-1, 3), rd.reshape(-1, 3), vd.reshape(-1, 3)
+        dev = model.canonical_feat.device if is_tp else torch.as_tensor(c2w).device
+        H, W, K, c2w, ro, rd, vd = _view_rays(i, HW, Ks, c2w, ndc, inverse_y, flip_x, flip_y, fixed_viewdirs, dev)
         if is_tp:
-            dev = model.canonical_feat.device
-            rk = dict(render_kwargs, rays_o=ro.to(dev), rays_d=rd.to(dev), viewdirs=vd.to(dev))
+            rk = dict(render_kwargs, rays_o=ro, rays_d=rd, viewdirs=vd)
             px = torch.stack(torch.meshgrid(torch.arange(0, W), torch.arange(0, H), indexing="ij"), -1)
             rk["pixel_coords"] = px.reshape(-1, 2).float().to(dev)
             t = torch.as_tensor(test_times[i], dtype=torch.float32, device=dev).reshape(1)
             out = model(t, render_depth=True, render_kwargs=rk, render_weights=True,
-                        render_pcd_direct=render_pcd_direct, poses=torch.as_tensor(c2w)[None].to(dev),
-                        Ks=Ks[i][None].to(dev), cam_per_ray=torch.zeros(len(ro))[:, None], get_skeleton=True)
+                        render_pcd_direct=render_pcd_direct, poses=c2w[None], Ks=K[None],
+                        cam_per_ray=torch.zeros(len(ro))[:, None], get_skeleton=True)
             b = _joint_record(out, joints, i, HW, render_kwargs)
             bones = b if b is not None else bones
             rgb = (out["rgb_marched_direct"] if render_pcd_direct else out["rgb_marched"]).reshape(H, W, -1)
@@ -311,11 +371,7 @@ def render_viewpoints(model, render_poses, HW, Ks, ndc, render_kwargs, gt_imgs=N
         depths.append(res["depth"].cpu().numpy())
         if "weights" in res:
             weights.append(res["weights"].cpu().numpy())
-        if gt_imgs is not None and render_factor == 0:
-            if eval_psnr:
-                psnrs.append(float(-10.0 * np.log10(np.mean(np.square(rgb - gt_imgs[i])))))
-            if eval_ssim:
-                ssims.append(rgb_ssim(rgb, gt_imgs[i], max_val=1))
+        score(i, rgb)
     if verbose and psnrs:
         print("Testing psnr", np.mean(psnrs), "(avg)")
     if verbose and ssims:

@@ -29,6 +29,7 @@ class Workspace:
 
     def __init__(self):
         self.bufs = {}
+        self.meta = {}         # host-side keys of what the buffers hold (e.g. the packed weights' version)
         self.retired = []      # [(buffer, tokens of the graphs that may hold its address)]
         self._holders = set()  # tokens of the live graphs
         self._n = 0

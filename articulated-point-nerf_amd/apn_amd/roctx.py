@@ -70,6 +70,30 @@ def end(name: str):
             lib.roctxRangePop()
 
 
+class Sequence:
+    """Consecutive stages of one call: ``switch(name)`` closes the open stage's ranges and opens
+    the next one's (``switch(None)`` only closes); leaving the ``with`` block -- normally or by an
+    exception raised between two switches -- closes whatever is still open, so a failed call never
+    leaves pushed ranges behind for later markers to nest under."""
+
+    def __init__(self):
+        self._open = None
+
+    def switch(self, name):
+        if self._open is not None:
+            end(self._open)
+        self._open = name
+        if name is not None:
+            begin(name)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.switch(None)
+        return False
+
+
 @contextlib.contextmanager
 def stage(name: str):
     """Nested roctx ranges of the reference labels that fused stage ``name`` replaces."""

@@ -307,14 +307,15 @@ def render_sharded(model, t, render_kwargs, rank: int, world: int, group=None, s
 
 
 def capture_sharded(model, t, render_kwargs, rank: int, world: int, group=None, block: int = RAY_BLOCK,
-                    **forward_kwargs):
+                    workspace=None, **forward_kwargs):
     """The "blocks" split with this rank's frame captured as one HIP graph
     (TemporalPoints.capture_frame(ray_shard=(rank, world, block))): returns ``step(t)``, which
     replays the graph and all-gathers the tiles (the collective stays outside the graph, so the
     same step runs over RCCL or gloo) -> a ShardedFrame like render_sharded's. Capture again after
-    changing the model or the rays."""
+    changing the model or the rays. ``workspace``: the graph's per-frame buffers (frames in
+    flight on one model give each step its own, see replay_in_flight)."""
     local = model.capture_frame(t, render_kwargs, ray_shard=(rank, world, block), capture_error_mode="thread_local",
-                                **forward_kwargs)
+                                workspace=workspace, **forward_kwargs)
 
     def step(t):
         out = local(t)
@@ -331,7 +332,8 @@ def capture_sharded(model, t, render_kwargs, rank: int, world: int, group=None, 
 
 def replay_in_flight(steps, ts, streams, comm, keep: bool = False) -> list:
     """Ray-shard frames with len(steps) frames in flight (bench.py --in-flight): frame i (time
-    ts[i]) replays steps[i % n]'s graph (capture_sharded steps of n models, own workspaces) on
+    ts[i]) replays steps[i % n]'s graph (capture_sharded steps of one model, each captured into a
+    workspace of its own -- apn_amd.pipeline.capture_sharded_in_flight) on
     streams[i % n], and its tile all-gather (step.assemble) runs on the ONE collective stream
     ``comm`` in frame order, so every rank issues the same collectives in the same order. A
     stream's next replay waits (event) for the assembly of its previous frame, whose tile it
@@ -379,9 +381,16 @@ def _assemble(model, t, out, render_kwargs, rank, world, group, blocks, block, f
             tracker.submit_cost(model.last_full_offsets, full[:, TILE_WIDTH].to(torch.int64), world)
     else:
         full, infos = tile, (info.view(1, 4) if info is not None else None)
+        if invalidate is not None and infos is not None:
+            infos = infos.clone()   # a replayed graph's static frame_info: the next replay overwrites it
     res = unpack_tile(full)
     for k in ("t_hat_pcd", "joints", "bones"):
-        res[k] = out.raw(k) if hasattr(out, "raw") else out.get(k)
+        v = out.raw(k) if hasattr(out, "raw") else out.get(k)
+        if invalidate is not None and isinstance(v, torch.Tensor):
+            # a replayed graph's static buffer: copied (on this stream, before the caller records
+            # the frame's done event), so a kept frame keeps its own values after later replays
+            v = v.clone()
+        res[k] = v
 
     def rerender(infos):
         # grow this rank's capacity from its in-bbox total (frame_info[1]) for the frames to come

@@ -12,6 +12,8 @@ are built once per call instead of once per chunk.
 from __future__ import annotations
 
 import colorsys
+import contextlib
+import gc
 import os
 import ctypes as C
 
@@ -215,12 +217,21 @@ def weights_from_bones(joints, bones, pcd, eps):
     return torch.cat([torch.zeros((len(w), 1)), w], dim=-1)
 
 
-def _collect_graphs():
-    """Destroy unreachable HIP graphs now, before a capture starts: a graph freed by the cyclic
-    garbage collector in the middle of another capture (an earlier step's closure cycle) would call
-    hipGraphExecDestroy while the stream is capturing, which HIP refuses (the process aborts)."""
-    import gc
+@contextlib.contextmanager
+def _capture_guard():
+    """Around a HIP-graph capture: destroy unreachable graphs first, then keep the cyclic garbage
+    collector off until the capture has ended. A graph freed by the collector in the middle of a
+    capture (an earlier step's closure cycle; allocations inside the capture can trigger a
+    collection) would call hipGraphExecDestroy while the stream is capturing, which HIP refuses
+    (the process aborts). Re-enabled in ``finally`` only if it was enabled on entry."""
+    was = gc.isenabled()
     gc.collect()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 
 def _grow_capacity(n):
@@ -312,7 +323,8 @@ class TemporalPoints(torch.nn.Module):
                 torch.nn.Linear(pin // 2, pose_embedding_dim), torch.nn.LeakyReLU(inplace=True))
         self.beta = torch.nn.Parameter(torch.tensor([0.5]))
         self.beta_min = torch.nn.Parameter(torch.tensor([0.0001]), requires_grad=False)
-        self._ws = Workspace()
+        self._ws = self._ws_eager = Workspace()   # per-frame buffers (use_workspace swaps them)
+        self._ws_shared = Workspace()              # the layer-1 projection P, shared by every workspace
         self._palette_cache = {}
         self.palette_perm_device = None   # None: the weights' device (reference behaviour)
         self.timing = None          # set to {} to record HIP-event timings of the MLP launch
@@ -523,14 +535,14 @@ class TemporalPoints(torch.nn.Module):
             with torch.cuda.stream(side):   # warm-up: caches, workspaces, packed buffers
                 self.repose(rp)
             torch.cuda.current_stream(dev).wait_stream(side)
-            _collect_graphs()
-            graph = torch.cuda.CUDAGraph()
-            self._ws.hold(graph)   # the graph holds workspace addresses from here on
-            with torch.cuda.graph(graph):
-                if sweep is None:
-                    xyz, joints_rel = self.repose(rp)
-                else:
-                    xyz, joints_rel = self.repose(sweep, sweep_index=idx)
+            with _capture_guard():
+                graph = torch.cuda.CUDAGraph()
+                self._ws.hold(graph)   # the graph holds workspace addresses from here on
+                with torch.cuda.graph(graph):
+                    if sweep is None:
+                        xyz, joints_rel = self.repose(rp)
+                    else:
+                        xyz, joints_rel = self.repose(sweep, sweep_index=idx)
         if sweep is None:
             def step(rot_params):
                 rp.copy_(rot_params.reshape(J, rot_dim))
@@ -559,7 +571,7 @@ class TemporalPoints(torch.nn.Module):
         return step
 
     def capture_frame(self, t, render_kwargs, render_depth=True, render_weights=True, query_radius=0.01, poses=None,
-                      Ks=None, get_skeleton=False, ray_shard=None, capture_error_mode="global"):
+                      Ks=None, get_skeleton=False, ray_shard=None, capture_error_mode="global", workspace=None):
         """The render frame for a fixed ray set (skeleton, LBS, grid, sampling, kNN, MLP,
         compositing: the whole no-grad forward) captured once in a HIP graph: returns
         ``step(t) -> RenderOutput``, which copies the time into the graph's input and replays it.
@@ -572,7 +584,10 @@ class TemporalPoints(torch.nn.Module):
         this rank's frame of the "blocks" ray split (apn_amd.shard.capture_sharded); the
         contiguous-range split is not capturable (its split moves from frame to frame).
         ``capture_error_mode`` goes to torch.cuda.graph ("thread_local" where other threads of the
-        process -- a process group's watchdog -- may make HIP calls during the capture)."""
+        process -- a process group's watchdog -- may make HIP calls during the capture).
+        ``workspace`` (an ops.Workspace): the per-frame buffers the graph captures (default: the
+        model's own); frames in flight give each graph its own (apn_amd.pipeline). A frame that
+        overflowed is rendered again in the model's own workspace."""
         if ray_shard is not None and len(ray_shard) != 3:
             raise ValueError("capture_frame: ray_shard must be (rank, world, block) (the blocks split)")
         dev = self.canonical_feat.device
@@ -590,25 +605,28 @@ class TemporalPoints(torch.nn.Module):
         st = {}
 
         def capture():
-            with torch.no_grad():
+            with torch.no_grad(), self.use_workspace(workspace):
                 side = torch.cuda.Stream(dev)
                 side.wait_stream(torch.cuda.current_stream(dev))
                 with torch.cuda.stream(side):   # warm-up: capacity (first frame), caches, workspaces
                     self._forward_render(t_in, *args)
                     warm = self._forward_render(t_in, *args)
+                    # validate: an overflow renders again (the model's own workspace) and grows the
+                    # capacity; read on the warm-up stream, which is the one that wrote the frame
+                    warm.keys()
                 torch.cuda.current_stream(dev).wait_stream(side)
-                warm.keys()   # validate: an overflow renders again and grows the capacity
                 if self._capacity.get(cap_key) is None:
                     raise RuntimeError("capture_frame: no sample capacity for this ray set (empty frame?)")
                 st.pop("graph", None)   # a re-capture: drop the old graph first (its retired buffers go with it)
                 step.graph = None
-                _collect_graphs()
-                graph = torch.cuda.CUDAGraph()
-                self._ws.hold(graph)   # the graph holds workspace addresses from here on
-                with torch.cuda.graph(graph, capture_error_mode=capture_error_mode):
-                    out = self._forward_render(t_in, *args)
-                    if out._info is not None:
-                        torch.bitwise_or(ovf, out._info[2:3], out=ovf)
+                with _capture_guard():
+                    graph = torch.cuda.CUDAGraph()
+                    self._ws.hold(graph)          # the graph holds workspace addresses from here on
+                    self._ws_shared.hold(graph)   # (and the shared projection's)
+                    with torch.cuda.graph(graph, capture_error_mode=capture_error_mode):
+                        out = self._forward_render(t_in, *args)
+                        if out._info is not None:
+                            torch.bitwise_or(ovf, out._info[2:3], out=ovf)
             st.update(graph=graph, static={k: dict.__getitem__(out, k) for k in dict.keys(out)}, info=out._info,
                       n_rays=out._n_rays, bg=out._bg, cap=self._capacity.get(cap_key), stale=False)
             step.graph = graph
@@ -628,7 +646,7 @@ class TemporalPoints(torch.nn.Module):
                 st["stale"] = True
                 self._force_exact = True
                 try:
-                    with torch.no_grad():
+                    with torch.no_grad(), self.use_workspace(None):
                         return self._forward_render(tt, *args)
                 finally:
                     self._force_exact = False
@@ -735,15 +753,31 @@ class TemporalPoints(torch.nn.Module):
         params = [p for l in layers for p in (l.weight, l.bias)] + list(self.densitynet.parameters()) + \
             list(self.rgbnet.parameters()) + [self.canonical_feat]
         key = tuple((p.data_ptr(), p._version) for p in params)
+        # the packed buffer (0.5 MB) belongs to the frame's workspace: its b1 follows the frame's
+        # pose embedding and its range flag the frame's MLP launch, so frames in flight each keep
+        # their own; the projection P (N x 512 B) depends on the weights only and is shared
         buf = self._ws.get("mlp_w", mlp_layout()["TOTAL"], torch.float32, dev)
-        if key != getattr(self, "_pack_key", None):
+        if key != self._ws.meta.get("pack_key"):
             pack_mlp_weights(layers, self.densitynet, self.rgbnet, pose_embedding, out=buf)
-            proj = self._ws.get("feat_proj", self.canonical_feat.shape[0] * 128, torch.float32, dev)
-            feat_project(self.canonical_feat, buf, out=proj.view(-1, 128))
-            self._pack_key = key
+            self._ws.meta["pack_key"] = key
         elif pose_embedding is not None:   # same weights: only b1 follows the pose embedding
             fold_pose_bias(layers[0], pose_embedding, buf)
-        return buf, self._ws.bufs["feat_proj"]
+        if key != self._ws_shared.meta.get("proj_key") or "feat_proj" not in self._ws_shared.bufs:
+            proj = self._ws_shared.get("feat_proj", self.canonical_feat.shape[0] * 128, torch.float32, dev)
+            feat_project(self.canonical_feat, buf, out=proj.view(-1, 128))
+            self._ws_shared.meta["proj_key"] = key
+        return buf, self._ws_shared.bufs["feat_proj"]
+
+    @contextlib.contextmanager
+    def use_workspace(self, ws):
+        """Run the fused frame in workspace ``ws`` (None: the model's own, used by eager frames).
+        Frames in flight (apn_amd.pipeline.FramePipeline) each capture into a workspace of their
+        own, so their per-frame buffers never alias; the projection P is shared."""
+        prev, self._ws = self._ws, (self._ws_eager if ws is None else ws)
+        try:
+            yield self._ws
+        finally:
+            self._ws = prev
 
     def forward(self, t, render_depth=False, render_kwargs=None, query_radius=0.01, render_weights=False,
                 rot_params=None, render_pcd_direct=False, poses=None, Ks=None, cam_per_ray=None, calc_min_max=True,
@@ -865,6 +899,11 @@ class TemporalPoints(torch.nn.Module):
         self.timing.setdefault("marks", []).append((name, e))
 
     def _render(self, xyz, recs, query_radius, rk, pose_embedding, calc_min_max, shard=None):
+        # roctx ranges per stage; the Sequence closes an open one if a stage raises
+        with roctx.Sequence() as rx:
+            return self._render_stages(rx, xyz, recs, query_radius, rk, pose_embedding, calc_min_max, shard)
+
+    def _render_stages(self, rx, xyz, recs, query_radius, rk, pose_embedding, calc_min_max, shard):
         recA, recB, bbox_ord = recs
         dev = xyz.device
         lib = L.load()
@@ -901,7 +940,7 @@ class TemporalPoints(torch.nn.Module):
         bg = float(rk['bg'])
         near, far = float(rk['near']), float(rk['far'])
         # sampling bbox (temporalpoints.py:423-427)
-        roctx.begin("sampling")
+        rx.switch("sampling")
         if calc_min_max:
             bbox6 = ws.get("bbox6", 6, torch.float32, dev)
             call("apn_bbox_unpack", ptr(bbox_ord), qr, ptr(bbox6), s)
@@ -966,7 +1005,6 @@ class TemporalPoints(torch.nn.Module):
             n_bbox = int(offs[R].item())
             self.last_stats = FrameStats({"rays": R, "inbbox_samples": n_bbox})
             if n_bbox == 0:
-                roctx.end("sampling")
                 raise NoPointsException("No points.")
             self._capacity[cap_key] = max(self._capacity.get(cap_key, 0), _grow_capacity(n_bbox))
             Q = n_bbox
@@ -987,7 +1025,6 @@ class TemporalPoints(torch.nn.Module):
             nsurv = info[3:]
             self.last_stats = FrameStats({"rays": R}, info=info)
         self._mark("sampling")
-        roctx.end("sampling")
         agrid_ready = None
         if side is not None:
             # the kNN's second grid (needed by launches of more than 2^18 queries) continues on the
@@ -999,7 +1036,7 @@ class TemporalPoints(torch.nn.Module):
                     agrid_ready = torch.cuda.Event()
                     agrid_ready.record(side)
             cur.wait_event(grid_ready)
-        roctx.begin("knn")
+        rx.switch("knn")
         # radius kNN + compaction of survivors
         s_pos = ws.get("s_pos", Q * 4, torch.float32, dev)
         s_ray = ws.get("s_ray", Q, torch.int32, dev)
@@ -1013,8 +1050,7 @@ class TemporalPoints(torch.nn.Module):
             call("apn_knn_radius", ptr(q_pos), ptr(q_ray), Q, nq_dev, ptr(gws), N,
                  CELL_CAP, ptr(sorted4), qr, ptr(s_pos), ptr(s_ray), ptr(s_nbr), ptr(nsurv), ptr(kws), s)
         self._mark("knn")
-        roctx.end("knn")
-        roctx.begin("mlp")
+        rx.switch("mlp")
         # The survivor count stays on the device: the MLP and compositing kernels read it there and
         # Q bounds it, so no sync here. (If no sample survives, the kernels produce the
         # reference's NoPointsException values -- bg colour, depth 0 -- and RenderOutput gives
@@ -1040,8 +1076,7 @@ class TemporalPoints(torch.nn.Module):
             e1.record()
             self.timing.setdefault("mlp_events", []).append((e0, e1, nsurv))
             self.timing["marks"].append(("mlp", e1))
-        roctx.end("mlp")
-        roctx.begin("composite")
+        rx.switch("composite")
         # compositing
         rgb = torch.empty(R, 3, device=dev); rgb_d = torch.empty(R, 3, device=dev)
         depth = torch.empty(R, device=dev); wvis = torch.empty(R, 3, device=dev)
@@ -1051,5 +1086,5 @@ class TemporalPoints(torch.nn.Module):
         call("apn_composite", ptr(out12), ptr(s_pos), ptr(s_ray), S, ptr(nsurv), R, float(self.fast_color_thres), bg,
              ptr(rgb), ptr(rgb_d), ptr(depth), ptr(wvis), ptr(last), ptr(last_d), ptr(rws), s)
         self._mark("composite")
-        roctx.end("composite")
+        rx.switch(None)
         return rgb, rgb_d, depth, wvis, last, last_d

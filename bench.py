@@ -16,12 +16,15 @@ barrier + synchronize bracketed and the max over ranks (all-reduce MAX of the el
 
 Frames in flight (``--in-flight``, default 3): a frame's stages run in sequence (the kNN needs the
 warped cloud, the MLP the kNN's survivors), so one frame leaves the chip under-used while its kNN
-and small stages run. With n frames in flight n TemporalPoints of the same scene (own workspaces)
-replay their captured frames on n HIP streams, frame i on stream i % n: one frame's MLP runs
+and small stages run. With n frames in flight ONE TemporalPoints replays its frame, captured n
+times into n per-frame workspaces (apn_amd.pipeline.FramePipeline; the canonical tables and the
+layer-1 projection are shared), on n HIP streams, frame i on stream i % n: one frame's MLP runs
 beside the next frames' kNN and sampling. Every frame is still rendered in full and is
-bit-identical to a serial frame (tests/test_frame_graph.py); ``config.serial_ms_per_step`` is the
-same frames one at a time on one stream. Ray shards keep their per-frame all-gathers on one
-collective stream in frame order (apn_amd.shard.replay_in_flight).
+bit-identical to a serial frame (tests/test_pipeline.py); ``config.serial_ms_per_step`` is the
+same frames one at a time on one stream, ``render_viewpoints`` the drop-in render loop
+(harness.render_viewpoints: 8 views at distinct times, host readback) on the same pipeline. Ray
+shards keep their per-frame all-gathers on one collective stream in frame order
+(apn_amd.shard.replay_in_flight).
 
 Rank 0 prints ONE JSON line. Diagnostics go to stderr.
 
@@ -383,32 +386,46 @@ def lbs_sweep(args, rank, world, dev):
     return line
 
 
+def device_identity(dev):
+    """This rank's GPU as the runtime names it: PCI domain / bus / device ids and UUID (a driver
+    run with N ranks shows N distinct devices behind the all-gather), plus the host name."""
+    import socket
+    p = torch.cuda.get_device_properties(dev)
+    ident = {"index": dev.index, "name": p.name, "hostname": socket.gethostname(),
+             "visible_devices": os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES")}
+    for a in ("pci_domain_id", "pci_bus_id", "pci_device_id", "gcnArchName"):
+        v = getattr(p, a, None)
+        if v is not None:
+            ident[a] = v if isinstance(v, (int, str)) else str(v)
+    u = getattr(p, "uuid", None)
+    if u is not None:
+        ident["uuid"] = str(u)
+    return ident
+
+
 def replay_frames(steps_in_flight, t_arg, k, streams=None):
-    """Replays k captured frames: one graph on the current stream, or n graphs g_0 .. g_n-1 in turn
-    over n streams (frame i: graph i % n on stream i % n; all join the current stream at the end).
-    Returns the last frame and the host seconds spent issuing."""
+    """Replays k captured frames of one graph on the current stream (the serial reference of the
+    in-flight gain). Returns the last frame and the host seconds spent issuing."""
     h = 0.0
     out = None
-    if len(steps_in_flight) == 1:
-        for _ in range(k):
-            h0 = time.perf_counter()
-            out = steps_in_flight[0](t_arg)
-            h += time.perf_counter() - h0
-        return out, h
-    cur = torch.cuda.current_stream()
-    ev = torch.cuda.Event()
-    ev.record(cur)
-    for s in streams:
-        s.wait_event(ev)
-    n = len(steps_in_flight)
-    for i in range(k):
+    for _ in range(k):
         h0 = time.perf_counter()
-        with torch.cuda.stream(streams[i % n]):
-            out = steps_in_flight[i % n](t_arg)
+        out = steps_in_flight[0](t_arg)
         h += time.perf_counter() - h0
-    for s in streams:
-        cur.wait_stream(s)
     return out, h
+
+
+def replay_pipeline(pipe, t_arg, k):
+    """k frames through one model's FramePipeline (apn_amd.pipeline: n captured frames, each in a
+    workspace of its own, frame i on stream i % n); the current stream joins them at the end.
+    Returns the last frame's handle and the host seconds spent issuing."""
+    h0 = time.perf_counter()
+    h = None
+    for _ in range(k):
+        h = pipe.submit(t_arg)
+    host = time.perf_counter() - h0
+    pipe.join()
+    return h, host
 
 
 def replay_sharded(steps_in_flight, t_arg, k, streams, comm):
@@ -420,15 +437,30 @@ def replay_sharded(steps_in_flight, t_arg, k, streams, comm):
     return out, time.perf_counter() - h0
 
 
-def second_frame_graph(scene, dev, t_arg, rk, poses, Ks):
-    """Another TemporalPoints of the scene (same weights, own workspaces) with its frame captured
-    (one more frame in flight)."""
-    m2 = harness.build_model(scene, dev)
-    _ = m2.mean_min_distance
-    for _ in range(2):
-        m2(t_arg, render_depth=True, render_kwargs=rk, render_weights=True, poses=poses, Ks=Ks, get_skeleton=True)
+def viewpoint_rate(model, scene, dev, n_views=8, in_flight=3):
+    """harness.render_viewpoints (run.py:80-239) over n_views views at distinct times -- rays made
+    on the device per view, n frames in flight on the model's FramePipeline, rgb / depth / weights
+    read back to host numpy per view -- timed after one untimed sweep (the captures). The drop-in
+    render loop's rate next to the timed loop's."""
+    from apn_amd.tineuvox import get_rays_of_a_view  # noqa: F401  (the harness's ray maker)
+    H, W = scene.cfg.H, scene.cfg.W
+    rk = {k: v for k, v in scene.render_kwargs(dev).items() if k not in ("rays_o", "rays_d", "viewdirs")}
+    poses = scene.c2w[None].repeat(n_views, 1, 1)
+    HW = [[H, W]] * n_views
+    Ks = scene.K[None].repeat(n_views, 1, 1)
+    times = [scene.cfg.t + 0.01 * i for i in range(n_views)]
+    kw = dict(test_times=times, verbose=False, inverse_y=bool(rk.get("inverse_y", False)), in_flight=in_flight)
+    harness.render_viewpoints(model, poses, HW, Ks, False, dict(rk), **kw)   # captures the pipeline
     torch.cuda.synchronize(dev)
-    return m2, m2.capture_frame(t_arg, rk, poses=poses, Ks=Ks, get_skeleton=True)
+    t0 = time.perf_counter()
+    harness.render_viewpoints(model, poses, HW, Ks, False, dict(rk), **kw)
+    el = time.perf_counter() - t0
+    return {"views": n_views, "distinct_times": n_views, "frames_in_flight": in_flight,
+            "ms_per_frame": el / n_views * 1e3, "rays_per_s": n_views * H * W / el,
+            "note": "harness.render_viewpoints over views at distinct times, one model (apn_amd.pipeline."
+                    "FramePipeline: per-frame workspaces, shared canonical tables / projection), per view: rays "
+                    "on the device, frame submitted, rgb / depth / weights read back to host numpy; second call "
+                    "timed (the first captures)"}
 
 
 def frame_rate(config, dev, steps=10, warmup=2, in_flight=3):
@@ -454,15 +486,12 @@ def frame_rate(config, dev, steps=10, warmup=2, in_flight=3):
     ev = timing.get("mlp_events", [])
     mlp_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / max(len(ev), 1)
     kept = int(ev[-1][2].item()) if ev else stats.get("kept_samples", 0)
-    step = model.capture_frame(t_arg, rk, poses=poses, Ks=Ks, get_skeleton=True)
-    graphs, streams = [step], None
-    if in_flight > 1:
-        graphs += [second_frame_graph(scene, dev, t_arg, rk, poses, Ks)[1] for _ in range(in_flight - 1)]
-        streams = [torch.cuda.Stream(dev) for _ in graphs]
-    replay_frames(graphs, t_arg, 2, streams)
+    from apn_amd.pipeline import FramePipeline
+    pipe = FramePipeline(model, t_arg, rk, n=in_flight, poses=poses, Ks=Ks, get_skeleton=True, readback=None)
+    replay_pipeline(pipe, t_arg, 2)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    replay_frames(graphs, t_arg, steps, streams)
+    replay_pipeline(pipe, t_arg, steps)
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     d_in = 191 + model.pose_embedding_dim
@@ -470,7 +499,7 @@ def frame_rate(config, dev, steps=10, warmup=2, in_flight=3):
     return {"workload": S.CONFIGS[config].name + f" ({config})", "value": steps * R / elapsed, "unit": "rays/s",
             "ms_per_step": elapsed / steps * 1e3, "steps": steps, "rays_per_frame": R, "points": scene.cfg.N,
             "bones": scene.cfg.J, "inbbox_samples": stats.get("inbbox_samples"), "kept_samples": kept,
-            "timed_frames_overflowed": any(bool(g.overflowed()) for g in graphs), "frames_in_flight": len(graphs),
+            "timed_frames_overflowed": pipe.overflowed(), "frames_in_flight": pipe.n,
             "mlp_kernel_ms": mlp_ms, "mlp_roofline_frac": achieved / SPLIT3_PEAK_TFLOPS}
 
 
@@ -589,13 +618,15 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-other-configs", action="store_true",
                     help="skip the compact C3 / C4 / C5 measurements the default one-GPU C2 line carries")
+    ap.add_argument("--no-viewpoints", action="store_true",
+                    help="skip the harness.render_viewpoints leg (8 views, frames in flight, host readback)")
     ap.add_argument("-o", "--out", default=None, help="also write the JSON line to this file")
     ap.add_argument("--shard", choices=["frames", "rays"], default="rays",
                     help="N>1: 'rays' (default) = the ranks split one frame's rays and all-gather the tiles "
                          "over RCCL (strong scaling, SURVEY.md 8(e)); 'frames' = every rank renders its own "
                          "frame (weak scaling, no data-path collective)")
     ap.add_argument("--in-flight", type=int, choices=[1, 2, 3], default=3,
-                    help="frames in flight: n models' captured frames on n streams, frame i on stream i %% n "
+                    help="frames in flight: one model's frame captured into n workspaces, frame i on stream i %% n "
                          "(ray shards: the all-gathers in frame order on one collective stream); 1 = one "
                          "after another")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
@@ -656,43 +687,48 @@ def main():
     torch.cuda.synchronize(dev)
     stats = model.last_stats.resolved()
     log(f"[rank {rank}] scene: {stats}")
-    shard_graphs = []
+    shard_graphs, pipe, mem = [], None, {}
+    mem["model_bytes"] = torch.cuda.memory_allocated(dev)
     if use_graph and shard_rays:   # this rank's blocks as one graph replay, then the tile all-gather
         try:
-            graph_step = SH.capture_sharded(model, t_arg, rk, rank, world, poses=poses, Ks=Ks, get_skeleton=True)
-            shard_graphs = [graph_step]
-            for _ in range(args.in_flight - 1):   # more models' shard graphs: frames in flight
-                model2 = harness.build_model(scene, dev)
-                _ = model2.mean_min_distance
-                shard_graphs.append(SH.capture_sharded(model2, t_arg, rk, rank, world, poses=poses, Ks=Ks,
-                                                       get_skeleton=True))
+            # frames in flight: n shard graphs of this one model, each captured into its own
+            # per-frame workspace (apn_amd.pipeline)
+            from apn_amd.pipeline import capture_sharded_in_flight
+            shard_graphs = capture_sharded_in_flight(model, t_arg, rk, rank, world, n=args.in_flight, poses=poses,
+                                                     Ks=Ks, get_skeleton=True)
+            graph_step = shard_graphs[0]
         except Exception as e:   # the eager shard frame runs the same kernels and the same collectives
             log(f"[rank {rank}] shard graph capture failed ({e!r}); timing eager shard frames")
             use_graph = False
+            shard_graphs = []
             torch.cuda.synchronize(dev)
         # every rank must run the same step (same collectives): graphs only if all ranks captured
         ok = torch.tensor([1 if use_graph else 0], dtype=torch.int32,
                           device=dev if torch.distributed.get_backend() == "nccl" else "cpu")
         torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN)
         use_graph = bool(ok.item())
-    graphs, streams = [], None
+    streams = None
     if use_graph:   # the whole frame as one HIP graph replay (no per-kernel host launches, no host sync)
         if not shard_rays:
-            graph_step = model.capture_frame(t_arg, rk, poses=poses, Ks=Ks, get_skeleton=True)
-            graphs = [graph_step]
-            if args.in_flight > 1:   # more frames in flight: their own models, workspaces and graphs
-                graphs += [second_frame_graph(scene, dev, t_arg, rk, poses, Ks)[1] for _ in range(args.in_flight - 1)]
-                streams = [torch.cuda.Stream(dev) for _ in graphs]
+            # n frames in flight on this one model (apn_amd.pipeline.FramePipeline): n captures of the
+            # frame, each in a per-frame workspace of its own, frame i on stream i % n
+            from apn_amd.pipeline import FramePipeline
+            pipe = FramePipeline(model, t_arg, rk, n=args.in_flight, poses=poses, Ks=Ks, get_skeleton=True,
+                                 readback=None)
+            graph_step = pipe.steps[0]
         step = lambda: graph_step(t_arg)   # noqa: E731
         for _ in range(2):
             step()
-        if graphs:
-            replay_frames(graphs, t_arg, 2, streams)
+        if pipe is not None:
+            replay_pipeline(pipe, t_arg, 2)
         if len(shard_graphs) > 1:
             streams = [torch.cuda.Stream(dev) for _ in shard_graphs]
             comm = torch.cuda.Stream(dev)
             replay_sharded(shard_graphs, t_arg, 2, streams, comm)
         torch.cuda.synchronize(dev)
+    mem["with_frames_in_flight_bytes"] = torch.cuda.memory_allocated(dev)
+    mem["per_frame_workspace_bytes"] = ([sum(b.numel() * b.element_size() for b in ws.bufs.values())
+                                         for ws in pipe.workspaces] if pipe is not None else None)
 
     # stage / MLP-kernel timings come from HIP events on eager frames (events are not recorded
     # inside a graph replay); the timed loop below runs the step as configured
@@ -710,8 +746,9 @@ def main():
     if not use_graph:
         model.timing = timing
     eager_infos = []
-    if graphs:   # captured frames without a collective: one or two in flight
-        out, host_s = replay_frames(graphs, t_arg, args.steps, streams)
+    if pipe is not None:   # captured frames without a collective, n in flight on one model
+        out, host_s = replay_pipeline(pipe, t_arg, args.steps)
+        out = out.device()
     elif use_graph and len(shard_graphs) > 1:   # ray shards, frames in flight, one collective stream
         out, host_s = replay_sharded(shard_graphs, t_arg, args.steps, streams, comm)
     else:
@@ -728,7 +765,7 @@ def main():
     # would be timed short. The graph ORs every replay's overflow flag on the device; read it once.
     # (eager frames: the device frame_info of each timed frame, kept by the loop below)
     if use_graph:
-        overflowed = any(bool(g.overflowed()) for g in (graphs or shard_graphs or [graph_step]))
+        overflowed = pipe.overflowed() if pipe is not None else any(bool(g.overflowed()) for g in (shard_graphs or [graph_step]))
     else:
         overflowed = any(bool(i[2]) for i in torch.stack(eager_infos).cpu()) if eager_infos else False
     n_timed = min(args.steps, 10) if use_graph else args.steps
@@ -742,7 +779,8 @@ def main():
     if overflowed:
         log(f"[rank {rank}] WARNING: a timed frame overflowed its sample capacity (dropped samples)")
     serial_ms = None
-    if use_graph and (len(graphs) > 1 or len(shard_graphs) > 1):
+    n_flight = pipe.n if pipe is not None else (len(shard_graphs) if use_graph else 1)
+    if use_graph and n_flight > 1:
         # the same frames one at a time on one stream: the reference for the in-flight gain
         if world > 1:
             torch.distributed.barrier()
@@ -751,7 +789,7 @@ def main():
         replay_frames([graph_step], t_arg, args.steps)
         torch.cuda.synchronize(dev)
         serial_ms = (time.perf_counter() - ts0) / args.steps * 1e3
-        log(f"[rank {rank}] frames in flight {max(len(graphs), len(shard_graphs))}: "
+        log(f"[rank {rank}] frames in flight {n_flight}: "
             f"{elapsed / args.steps * 1e3:.3f} ms/frame; one at a time "
             f"{serial_ms:.3f} ms/frame")
     from apn_amd import _lib
@@ -794,13 +832,17 @@ def main():
         g1.record()
         torch.cuda.synchronize(dev)
         ag_ms = g0.elapsed_time(g1) / 10
-        mine = {"rank": rank, "rays": n_local, "kept_samples": S_kept, "allgather_ms": round(ag_ms, 4),
+        mine = {"rank": rank, "world_size": torch.distributed.get_world_size(), "device": device_identity(dev),
+                "rays": n_local, "kept_samples": S_kept, "allgather_ms": round(ag_ms, 4),
                 "replicated_ms": round(sum(stage_ms.get(k, 0.0) for k in ("lbs", "bbox", "grid")), 4),
                 "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()}}
         per_rank = [None] * world
         torch.distributed.all_gather_object(per_rank, mine)
         kept_total = sum(p["kept_samples"] for p in per_rank)
         shard_diag = {"per_rank": per_rank, "allgather_ms_max": max(p["allgather_ms"] for p in per_rank),
+                      "world_size": torch.distributed.get_world_size(),
+                      "distinct_devices": len({(p["device"].get("hostname"), p["device"].get("pci_bus_id"),
+                                                p["device"].get("uuid")) for p in per_rank}),
                       "rerenders": getattr(model, "sharded_rerenders", 0),
                       "note": "stage_ms from HIP events on eager shard frames; allgather_ms = one gather_blocks "
                               "(the frame's tile all-gather) alone, mean of 10; replicated_ms = lbs + bbox + grid, "
@@ -850,7 +892,9 @@ def main():
         peak_note = "peak = fp16 dense MFMA peak / 3 (three fp16 MFMA terms per fp32-accurate product)"
     from apn_amd.ops import mlp_range_fallback
     # the split kernel's range guard hands a launch to the FP32 MFMA kernel; the line says if it fired
-    mlp_fallback = bool(mlp_range_fallback(model._ws.bufs["mlp_w"])) if "mlp_w" in model._ws.bufs else None
+    wss = [model._ws_eager] + (pipe.workspaces if pipe is not None else [])
+    mlp_fallback = (any(bool(mlp_range_fallback(w.bufs["mlp_w"])) for w in wss if "mlp_w" in w.bufs)
+                    if any("mlp_w" in w.bufs for w in wss) else None)
     traffic, traffic_src = latest_traffic("point_mlp_traffic")
     ms_per_step = elapsed / args.steps * 1e3
     frame_roof = frame_roofline(scene.cfg.N, scene.cfg.J, R, kept_total * flop_per_kept_sample(d_in), ms_per_step,
@@ -870,6 +914,14 @@ def main():
             knn = knn_report(model, S_kept, stats.get("inbbox_samples"), stage_ms.get("knn", 0.0))
         except Exception as e:  # never lose the GPU line over a diagnostic
             log(f"knn work report failed: {e!r}")
+    views = None
+    if world == 1 and use_graph and not args.no_viewpoints:
+        try:
+            views = viewpoint_rate(model, scene, dev, in_flight=args.in_flight)
+            log(f"[render_viewpoints] {views['ms_per_frame']:.3f} ms/frame over {views['views']} views "
+                f"({views['frames_in_flight']} in flight, host readback)")
+        except Exception as e:  # never lose the GPU line over a diagnostic
+            log(f"render_viewpoints leg failed: {e!r}")
     others = None
     if world == 1 and args.config == "C2" and not args.no_other_configs:
         others = other_configs(dev, args.in_flight)
@@ -891,14 +943,16 @@ def main():
                                    if shard_rays else f"frames x{world} (no data-path collective)")
                    if world > 1 else "single",
                    "step": (("each rank's blocks replayed as one HIP graph (shard.capture_sharded), then the "
-                             "all-gather" + (f"; {len(shard_graphs)} frames in flight ({len(shard_graphs)} models' "
-                                             "shard graphs on as many streams, the all-gathers in frame order on "
-                                             "one collective stream)" if len(shard_graphs) > 1 else "") if shard_rays else
-                             "whole frame replayed as one HIP graph (TemporalPoints.capture_frame)"
-                             + (f"; {len(graphs)} frames in flight ({len(graphs)} models' graphs on as many "
-                                "streams, frame i on stream i % n)" if len(graphs) > 1 else "")) if use_graph
+                             "all-gather" + (f"; {n_flight} frames in flight (one model's shard graphs, each in its "
+                                             "own per-frame workspace, on as many streams, the all-gathers in frame "
+                                             "order on one collective stream)" if n_flight > 1 else "") if shard_rays
+                             else "whole frame replayed as one HIP graph (TemporalPoints.capture_frame)"
+                             + (f"; {n_flight} frames in flight on ONE model (apn_amd.pipeline.FramePipeline: the "
+                                "frame captured into n per-frame workspaces, canonical tables and the layer-1 "
+                                "projection shared; frame i on stream i % n)" if n_flight > 1 else "")) if use_graph
                             else "eager launches"),
-                   "frames_in_flight": max(len(graphs), len(shard_graphs) if use_graph else 1, 1),
+                   "frames_in_flight": n_flight,
+                   "memory": mem,
                    "serial_ms_per_step": serial_ms,
                    "timed_frames_overflowed": overflowed,
                    "mlp_fp32_fallback_fired": mlp_fallback},
@@ -924,6 +978,7 @@ def main():
         "cpu_baseline": cpu,
         "psnr_vs_oracle": psnr,
         "same_cloud_vs_oracle": same,
+        **({"render_viewpoints": views} if views is not None else {}),
         **({"other_configs": others} if others is not None else {}),
     }
     emit(line, args)

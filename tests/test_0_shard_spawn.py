@@ -53,14 +53,23 @@ def _worker(rank, world, port, outdir, split):
             # sync-free path (previous frame's split, per-rank capacity); frame 3: rank 1 overflows
             # its capacity, which every rank must detect through the gathered frame_info rows
             # ("graph": the blocks split with each rank's frame replayed from a HIP graph, bench's step)
-            step = capture_sharded(model, t0, rk, rank, world, **kw) if split in ("graph", "graph2") else None
+            step = capture_sharded(model, t0, rk, rank, world, **kw) if split == "graph" else None
             in_flight = None
-            if split == "graph2":   # two frames in flight: two models' graphs, one collective stream
-                model_b = harness.build_model(scene, dev)
-                steps = [step, capture_sharded(model_b, t0, rk, rank, world, **kw)]
+            seq = (0, 1, 0, 1)
+            if split == "graph2":
+                # two frames in flight on ONE model (its shard graph captured into two workspaces),
+                # one collective stream. Times (t0, t0, t1, t1): each graph renders both times, so a
+                # replay that overwrote a frame's tile before its all-gather read it would show
+                # (with (t0, t1, t0, t1) each graph always rendered the same time)
+                from apn_amd.pipeline import capture_sharded_in_flight
+                steps = capture_sharded_in_flight(model, t0, rk, rank, world, n=2, **kw)
+                step = steps[0]
+                seq = (0, 0, 1, 1)
                 streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
-                in_flight = replay_in_flight(steps, (t0, t1, t0, t1), streams, torch.cuda.Stream(dev), keep=True)
-            for i, t in enumerate((t0, t1, t0, t1)):
+                in_flight = replay_in_flight(steps, [(t0, t1)[j] for j in seq], streams, torch.cuda.Stream(dev),
+                                             keep=True)
+            for i, t in enumerate([(t0, t1)[j] for j in seq]):
+                tiles[f"tidx{i}"] = torch.tensor(seq[i])
                 if i == 3 and rank == 1 and step is None:
                     model._capacity[(R, rank, world, RAY_BLOCK) if split == "blocks" else (R, rank, world)] = 64
                 if in_flight is not None:
@@ -91,7 +100,7 @@ def test_render_sharded_two_processes_bit_identical(split):
         mp.spawn(_worker, args=(WORLD, _free_port(), d, split), nprocs=WORLD, join=True)
         res = [torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=True) for r in range(WORLD)]
     for i in range(4):
-        single = res[0][f"single{i % 2}"]
+        single = res[0][f"single{int(res[0][f'tidx{i}'])}"]
         R = single.shape[0]
         if split == "ranges":
             bounds = res[0][f"bounds{i}"].tolist()

@@ -105,9 +105,12 @@ def test_captured_frame_back_to_back(dev):
 
 @pytest.mark.parametrize("n", [2, 3])
 def test_two_frames_in_flight_equal_eager(dev, n):
-    """bench.py --in-flight n: n models of one scene (own workspaces), their captured frames
-    replayed on n streams, frame i on stream i % n, so consecutive frames run concurrently: every
-    frame equals the eager frame at its time bit for bit."""
+    """n models of one scene (own workspaces), their captured frames replayed on n streams, frame i
+    on stream i % n, ALL frames issued before anything is read (a read validates the
+    frame through a host sync, which had serialised the frames): each frame's outputs are cloned
+    on its own stream with RenderOutput.raw (no validation, no sync) right after its replay, the
+    overflow flags are checked once after the streams are joined, and every frame equals the
+    eager frame at its time bit for bit."""
     from apn_amd import harness
     scene, a = _scene_model(dev)
     models = [a] + [harness.build_model(scene, dev) for _ in range(n - 1)]
@@ -122,10 +125,11 @@ def test_two_frames_in_flight_equal_eager(dev, n):
     for i in range(8):
         with torch.cuda.stream(streams[i % n]):
             g = steps[i % n](ts[i % 4])
-            got.append({k: g[k].clone() for k in KEYS})
+            got.append({k: g.raw(k).clone() for k in KEYS})
     for s in streams:
         cur.wait_stream(s)
     torch.cuda.synchronize()
+    assert not any(st.overflowed() for st in steps)
     for i, frame in enumerate(got):
         ref = _frame(a, ts[i % 4], rk)
         for k in KEYS:
@@ -287,5 +291,35 @@ def test_successive_captures_with_aggressive_gc(dev):
                             ray_shard=(k, world, block))
             for key in KEYS:
                 assert torch.equal(got[key], ref[key]), (k, key)
+    finally:
+        gc.set_threshold(*old)
+
+
+def test_shard_steps_dropped_inside_in_flight_replays_with_aggressive_gc(dev):
+    """with the collector at its most aggressive, capture_sharded steps of one
+    model (frames in flight, each in its own workspace) are dropped and captured again while
+    replay_in_flight loops run: captures keep the collector off (temporalpoints._capture_guard),
+    so no freed graph is destroyed mid-capture, and every assembled frame equals the eager one."""
+    import gc
+    from apn_amd.pipeline import capture_sharded_in_flight
+    from apn_amd.shard import replay_in_flight
+    scene, model = _scene_model(dev)
+    rk = scene.render_kwargs(dev)
+    ts = [torch.tensor([scene.cfg.t + 0.05 * i], device=dev) for i in range(3)]
+    refs = [_frame(model, t, rk) for t in ts]
+    old = gc.get_threshold()
+    gc.set_threshold(1, 1, 1)
+    try:
+        for rnd in range(3):
+            steps = capture_sharded_in_flight(model, ts[0], rk, 0, 1, n=3)   # drops the previous round's
+            streams = [torch.cuda.Stream(dev) for _ in steps]
+            comm = torch.cuda.Stream(dev)
+            seq = [0, 0, 1, 1, 2, 2, 0]   # period 2 does not divide n = 3: every slot sees every time
+            frames = replay_in_flight(steps, [ts[j] for j in seq], streams, comm, keep=True)
+            torch.cuda.synchronize()
+            assert gc.isenabled()
+            for i, f in enumerate(frames):
+                for k in KEYS:
+                    assert torch.equal(f[k], refs[seq[i]][k]), (rnd, i, k)
     finally:
         gc.set_threshold(*old)

@@ -43,8 +43,10 @@ def test_render_viewpoints_matches_model_frames(gm, tmp_path):
     assert rgbs.shape == (2, 40, 48, 3) and depths.shape == (2, 40, 48, 1) and weights.shape == (2, 40, 48, 3)
     for i in range(2):
         H, W = HW[i]
-        ro, rd, vd = get_rays_of_a_view(H, W, Ks[i], poses[i], False, inverse_y=rk["inverse_y"])
-        sub = dict(rk, rays_o=ro.reshape(-1, 3).cuda(), rays_d=rd.reshape(-1, 3).cuda(), viewdirs=vd.reshape(-1, 3).cuda())
+        # the harness makes each view's rays on the model's device (as the reference does on its poses')
+        ro, rd, vd = get_rays_of_a_view(H, W, Ks[i].float().cuda(), poses[i].float().cuda(), False,
+                                        inverse_y=rk["inverse_y"])
+        sub = dict(rk, rays_o=ro.reshape(-1, 3), rays_d=rd.reshape(-1, 3), viewdirs=vd.reshape(-1, 3))
         out = m(torch.tensor([times[i]], device="cuda"), render_depth=True, render_kwargs=sub, render_weights=True)
         assert np.array_equal(rgbs[i], out["rgb_marched"].reshape(H, W, 3).cpu().numpy())
         assert np.array_equal(depths[i], out["depth"].reshape(H, W, 1).cpu().numpy())

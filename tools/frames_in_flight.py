@@ -1,7 +1,8 @@
-"""Probe: frame throughput with two frames in flight. Two TemporalPoints of the same scene (own
-workspaces), each frame captured as one HIP graph (capture_frame); K frames replayed one after
-another on one stream vs alternating over two streams (frame i on stream i % 2, so one frame's
-MLP runs beside the next frame's kNN / sampling). Checks that both orders give the same frames.
+"""Probe: frame throughput with n frames in flight. ONE TemporalPoints, its frame captured as a HIP
+graph into n per-frame workspaces (capture_frame(workspace=...), as apn_amd.pipeline does); K
+frames replayed one after another on one stream vs over n streams (frame i on stream i % n, so one
+frame's MLP runs beside the next frames' kNN / sampling). Checks every graph's frame against an
+eager frame of the model.
 
     python tools/frames_in_flight.py [--config C2] [--frames 20] [--shard RANK,WORLD]
 """
@@ -31,17 +32,17 @@ def main():
     rk = scene.render_kwargs(dev)
     t = torch.tensor([scene.cfg.t], device=dev)
     poses, Ks = scene.c2w[None].to(dev), scene.K[None].to(dev)
-    models = [harness.build_model(scene, dev) for _ in range(args.n)]
-    steps = []
-    for m in models:
-        _ = m.mean_min_distance
-        for _ in range(2):
-            m(t, render_depth=True, render_kwargs=rk, render_weights=True, poses=poses, Ks=Ks, get_skeleton=True)
-        shard = None
-        if args.shard:
-            rank, world = (int(v) for v in args.shard.split(","))
-            shard = (rank, world, 4096)
-        steps.append(m.capture_frame(t, rk, poses=poses, Ks=Ks, get_skeleton=True, ray_shard=shard))
+    from apn_amd.ops import Workspace
+    m = harness.build_model(scene, dev)
+    _ = m.mean_min_distance
+    for _ in range(2):
+        m(t, render_depth=True, render_kwargs=rk, render_weights=True, poses=poses, Ks=Ks, get_skeleton=True)
+    shard = None
+    if args.shard:
+        rank, world = (int(v) for v in args.shard.split(","))
+        shard = (rank, world, 4096)
+    steps = [m.capture_frame(t, rk, poses=poses, Ks=Ks, get_skeleton=True, ray_shard=shard, workspace=Workspace())
+             for _ in range(args.n)]
     torch.cuda.synchronize(dev)
     cur = torch.cuda.current_stream(dev)
     streams = [torch.cuda.Stream(dev) for _ in range(args.n)]
@@ -75,16 +76,18 @@ def main():
         ts = timed(serial, args.frames)
         tp = timed(pipelined, args.frames)
         print(f"rep {rep}: serial {ts:.3f} ms/frame, {args.n} in flight {tp:.3f} ms/frame ({ts / tp:.3f}x)")
-    # the frames of both graphs equal a serial frame bit for bit
-    outs = []
-    for i in range(2):
+    # every graph's frame equals an eager frame of the model bit for bit
+    keys = ("rgb_marched", "depth", "alphainv_last")
+    eager = m(t, render_depth=True, render_kwargs=rk, render_weights=True, poses=poses, Ks=Ks, get_skeleton=True,
+              ray_shard=shard)
+    ref = {k: eager[k].clone() for k in keys}
+    same = []
+    for i in range(args.n):
         with torch.cuda.stream(streams[i]):
             o = steps[i](t)
         torch.cuda.synchronize(dev)
-        outs.append({k: o[k].clone() for k in ("rgb_marched", "depth", "alphainv_last")})
-    same = all(torch.equal(outs[0][k], outs[1][k]) for k in outs[0])
-    print(f"frames of the two graphs identical: {same}")
-
+        same.append(all(torch.equal(o[k], ref[k]) for k in keys))
+    print(f"frames of the {args.n} graphs identical to the eager frame: {same}")
 
 if __name__ == "__main__":
     main()
