@@ -241,7 +241,7 @@ def _finish(rgbs, depths, weights, joints, bones, savedir, psnrs, ssims, eval_ps
             write_png(os.path.join(savedir, f"img_{i:03d}.png"), to8b(rgb))
         for i, w in enumerate(weights):
             write_png(os.path.join(savedir, f"weights_{i:03d}.png"), to8b(w))
-    rgbs, depths, weights = np.array(rgbs), np.array(depths), np.array(weights)
+    rgbs, depths, weights = np.asarray(rgbs), np.asarray(depths), np.asarray(weights)
     J = np.array([joints[i] for i in range(len(joints))]).astype(np.int32)
     if len(J) > 0 and bones is not None:
         for i in range(len(weights)):
@@ -286,6 +286,7 @@ def render_viewpoints(model, render_poses, HW, Ks, ndc, render_kwargs, gt_imgs=N
     from one model (its frame captured once per workspace, reused across calls while the model's
     parameters are unchanged). Every image equals the model's own frame for that view bit for bit
     (tests/test_pipeline.py). ``in_flight=1``: one eager forward per view, as the reference."""
+    import os
     import numpy as np
     if eval_lpips_alex or eval_lpips_vgg:
         raise NotImplementedError("LPIPS needs the torchvision / lpips network weights, absent here")
@@ -307,21 +308,31 @@ def render_viewpoints(model, render_poses, HW, Ks, ndc, render_kwargs, gt_imgs=N
         from .pipeline import cached_pipeline
         dev = model.canonical_feat.device
         rgb_key = "rgb_marched_direct" if render_pcd_direct else "rgb_marched"
-        pipe, pending = None, []
+        pipe, pending, stack = None, [], {}
+        n_views = len(render_poses)
 
         def fetch():
+            # frame i is fetched while frames i + 1 .. i + n - 1 render: its images go straight from
+            # the pinned readback into the result stacks, and its PNGs / skeleton overlay are made
+            # here (in the order _finish would: PNGs first), overlapped with the GPU's next frames
+            nonlocal bones
             i, H, W, h = pending.pop(0)
-            r = h.result()
+            if not stack:
+                stack.update(rgb=np.empty((n_views, H, W, 3), np.float32),
+                             depth=np.empty((n_views, H, W, 1), np.float32),
+                             weights=np.empty((n_views, H, W, 3), np.float32))
+            r = h.result(into={rgb_key: stack["rgb"][i], "depth": stack["depth"][i],
+                               "weights": stack["weights"][i]})
             if "joints" in r:
                 b = _joint_record({"joints": r["joints"], "bones": model.bones if model.joints_to_keep is None
                                    else model.new_bones}, joints, i, HW, render_kwargs)
-                nonlocal bones
                 bones = b if b is not None else bones
-            rgb = r[rgb_key].reshape(H, W, -1).numpy()
-            rgbs.append(rgb)
-            depths.append(r["depth"].reshape(H, W, -1).numpy())
-            weights.append(r["weights"].reshape(H, W, -1).numpy())
-            score(i, rgb)
+            score(i, stack["rgb"][i])
+            if savedir is not None:
+                write_png(os.path.join(savedir, f"img_{i:03d}.png"), to8b(stack["rgb"][i]))
+                write_png(os.path.join(savedir, f"weights_{i:03d}.png"), to8b(stack["weights"][i]))
+            if i in joints and bones is not None:
+                draw_skeleton(stack["weights"][i], np.asarray(joints[i]).astype(np.int32), bones)
         for i, c2w in enumerate(render_poses):
             H, W, K, c2w, ro, rd, vd = _view_rays(i, HW, Ks, c2w, ndc, inverse_y, flip_x, flip_y, fixed_viewdirs, dev)
             t = torch.as_tensor(test_times[i], dtype=torch.float32, device=dev).reshape(1)
@@ -339,9 +350,8 @@ def render_viewpoints(model, render_poses, HW, Ks, ndc, render_kwargs, gt_imgs=N
             print("Testing psnr", np.mean(psnrs), "(avg)")
         if verbose and ssims:
             print("Testing ssim", np.mean(ssims), "(avg)")
-        rgbs, depths, weights = _finish(rgbs, depths, weights, joints, bones, savedir, psnrs, ssims, eval_psnr,
-                                        eval_ssim)
-        return rgbs, depths, weights, np.array([])
+        _finish([], [], [], {}, None, savedir, psnrs, ssims, eval_psnr, eval_ssim)   # results.txt
+        return stack["rgb"], stack["depth"], stack["weights"], np.array([])
 
     for i, c2w in enumerate(render_poses):
         dev = model.canonical_feat.device if is_tp else torch.as_tensor(c2w).device

@@ -22,6 +22,7 @@ overwritten under a reader. ``harness.render_viewpoints`` and bench.py's timed l
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 from .ops import Workspace
@@ -46,8 +47,15 @@ class FrameHandle:
             raise RuntimeError("FrameHandle.device(): the slot has been reused by a later frame")
         return self._out
 
-    def result(self) -> dict:
+    def result(self, into=None) -> dict:
+        """Wait for this frame, validate it, return its outputs as CPU tensors -- or, with ``into``
+        ({key: numpy array}), copy them straight from the pinned buffers into those arrays (one host
+        copy; harness.render_viewpoints fills its result stacks this way) and return ``into``."""
         if self._res is not None:
+            if into is not None:
+                for k, a in into.items():
+                    np.copyto(a, self._res[k].numpy().reshape(a.shape))
+                return into
             return self._res
         slot = self._slot
         if slot["handle"] is not self:
@@ -65,10 +73,23 @@ class FrameHandle:
             if self._pipe.get_skeleton:
                 res["joints"] = fresh["joints"].detach().cpu().clone()
             self._pipe.rerenders += 1
+        elif into is not None:
+            for k, a in into.items():
+                np.copyto(a, host[k].numpy().reshape(a.shape))
+            res = dict(into)
+            if "joints" in host and "joints" not in into:
+                res["joints"] = host["joints"].clone()
+            res["kept_samples"], res["inbbox_samples"] = info[3], info[1]
+            self._res = {k: (torch.from_numpy(v) if isinstance(v, np.ndarray) else v) for k, v in res.items()}
+            return res
         else:
             res = {k: host[k].clone() for k in host if k != "_info"}
         res["kept_samples"], res["inbbox_samples"] = info[3], info[1]
         self._res = res
+        if into is not None:
+            for k, a in into.items():
+                np.copyto(a, res[k].numpy().reshape(a.shape))
+            return dict(into, **{k: v for k, v in res.items() if k not in into})
         return res
 
 

@@ -31,6 +31,8 @@ from .tineuvox import poc_fre
 CELL_CAP = int(os.environ.get("APN_CELL_CAP", 1 << 20))
 # the kNN's second grid on the grid's side stream (A/B: APN_AGRID_SIDE=0 builds it inside the kNN call)
 AGRID_SIDE = os.environ.get("APN_AGRID_SIDE", "1") != "0"
+# exact early ray termination of the neighbour MLP (apn_point_mlp_ert; APN_ERT=0: every kept sample)
+ERT = os.environ.get("APN_ERT", "1") != "0"
 
 
 class NoPointsException(Exception):
@@ -339,6 +341,10 @@ class TemporalPoints(torch.nn.Module):
         self._block_index = {}      # (ray count, rank, world, block) -> ray indices of the "blocks" split
         self._force_exact = False
         self._last_info = None
+        # the neighbour MLP only on the kept samples the compositing reads (apn_point_mlp_ert: every
+        # ray's samples up to its T < 1e-3 break, in passes); the frame is bit-identical either way
+        self.early_termination = ERT
+        self.last_mlp_rows = None   # device int32 [6]: samples per early-termination pass of the last frame
 
     # view_poc / pos_poc alias the TiNeuVox buffers (temporalpoints.py:148-150); as properties
     # they follow .to(device) (the reference relies on a CUDA default tensor type instead).
@@ -1069,12 +1075,22 @@ class TemporalPoints(torch.nn.Module):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             self.timing.setdefault("marks", []).append(("mlp_setup", e0))
-        call("apn_point_mlp", ptr(s_pos), ptr(s_ray), ptr(s_nbr), S, ptr(nsurv), ptr(recA), ptr(recB), ptr(feat),
-             128, ptr(vd), ptr(vemb), ptr(wbuf), self._eps, float(self.tineuvox.act_shift), interval, 0,
-             ptr(out12), s)
+        if self.early_termination:
+            ews = ws.bytes("ert_ws", lib.apn_point_mlp_ert_workspace_bytes(S, R), dev)
+            rows = ws.get("ert_rows", 8, torch.int32, dev)
+            self.last_mlp_rows = rows[:6]
+            call("apn_point_mlp_ert", ptr(s_pos), ptr(s_ray), ptr(s_nbr), S, ptr(nsurv), R, ptr(recA), ptr(recB),
+                 ptr(feat), 128, ptr(vd), ptr(vemb), ptr(wbuf), self._eps, float(self.tineuvox.act_shift), interval,
+                 float(self.fast_color_thres), ptr(out12), ptr(ews), ptr(rows), s)
+        else:
+            self.last_mlp_rows = None
+            call("apn_point_mlp", ptr(s_pos), ptr(s_ray), ptr(s_nbr), S, ptr(nsurv), ptr(recA), ptr(recB), ptr(feat),
+                 128, ptr(vd), ptr(vemb), ptr(wbuf), self._eps, float(self.tineuvox.act_shift), interval, 0,
+                 ptr(out12), s)
         if self.timing is not None:
             e1.record()
-            self.timing.setdefault("mlp_events", []).append((e0, e1, nsurv))
+            rows = self.last_mlp_rows.clone() if self.last_mlp_rows is not None else None
+            self.timing.setdefault("mlp_events", []).append((e0, e1, nsurv, rows))
             self.timing["marks"].append(("mlp", e1))
         rx.switch("composite")
         # compositing

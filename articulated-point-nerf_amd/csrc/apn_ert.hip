@@ -1,0 +1,213 @@
+// Early ray termination for the neighbour MLP (exact): the reference's compositing
+// (temporalpoints.py:611-651 -> Alphas2Weights, render_utils_kernel.cu:430-459) walks each ray's
+// kept samples front to back and stops after the sample whose update takes T below 1e-3; the
+// Point-NeRF columns {rgb, alpha} of every later sample of that ray are never read. The reference
+// still runs feat_net / densitynet / rgbnet on them (temporalpoints.py:452-519). Here the MLP runs
+// in passes over each ray's kept samples in step order -- local indices [0, 4), [4, 8), [8, 12),
+// [12, 20), [20, 36), [36, ...) -- and after each pass a per-ray walk with the compositing's own
+// arithmetic (pre-mask alpha > thr, T in double, the same break test) retires the rays that
+// terminated; the next pass lists only the live rays' next samples. Every sample the compositing
+// reads has exactly the values a full MLP launch would give it (a sample's MLP rows do not depend
+// on the other rows of its tile), so apn_composite's output is bit-identical (tests/test_ert.py).
+//
+// The direct path (alpha_d, rgb_d, temporalpoints.py:459-470) and the weight-visualisation colour
+// (517-519) are cheap record blends; k_direct_blend computes them for every kept sample (the direct
+// path has its own termination point), with the MLP kernel's arithmetic and order.
+#include "apn_mlp_layout.h"
+
+namespace apn {
+
+// out12 columns 4..11 = {r_d, g_d, b_d, alpha_d, wr, wg, wb, 0} of sample i, the arithmetic of the
+// fused MLP kernel's gather (apn_mlp_h4.hip gather_q: squared distance, direct weight) and its
+// epilogue (IDW weights, sequential sums over the 8 neighbours in order).
+__global__ __launch_bounds__(256) void k_direct_blend(const float4* __restrict__ s_pos, const int* __restrict__ s_nbr,
+                                                      const int* __restrict__ n_dev, const float4* __restrict__ recA,
+                                                      const float4* __restrict__ recB, float eps,
+                                                      float4* __restrict__ out) {
+  const int n = *n_dev;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const float4 q = s_pos[i];
+    const int4 nb0 = ((const int4*)s_nbr)[2 * (size_t)i], nb1 = ((const int4*)s_nbr)[2 * (size_t)i + 1];
+    const int nbs[8] = {nb0.x, nb0.y, nb0.z, nb0.w, nb1.x, nb1.y, nb1.z, nb1.w};
+    float to[8], dw[8], al[8];
+    float3 cd[8], cw[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int nb = nbs[k];
+      const size_t m = (size_t)max(nb, 0);
+      const float4 a0 = recA[4 * m], a3 = recA[4 * m + 3], b0 = recB[2 * m], b1 = recB[2 * m + 1];
+      if (nb >= 0) {
+        const float dx = q.x - a0.x, dy = q.y - a0.y, dz = q.z - a0.z;
+        const float tn = (dx * dx + dy * dy) + dz * dz;
+        to[k] = tn;
+        dw[k] = expf(-(tn * tn) / a0.w);   // temporalpoints.py:461 (to_nn is already squared)
+        al[k] = a3.y;
+        cd[k] = make_float3(b0.x, b0.y, b0.z);
+        cw[k] = make_float3(b1.x, b1.y, b1.z);
+      } else {
+        to[k] = 1.f;
+        dw[k] = 0.f;
+        al[k] = 0.f;
+        cd[k] = make_float3(0.f, 0.f, 0.f);
+        cw[k] = make_float3(0.f, 0.f, 0.f);
+      }
+    }
+    float w[8], sum = 0.f, sumd = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      w[k] = __builtin_amdgcn_rcpf(to[k] + eps);   // v_rcp_f32, as the MLP kernel's IDW weights
+      sum += w[k];
+    }
+    const float inv = __builtin_amdgcn_rcpf(sum);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sumd += dw[k];
+    const float idn = __builtin_amdgcn_rcpf(sumd + 1e-12f);
+    float ad = 0.f, rd = 0.f, gd = 0.f, bd = 0.f, wr = 0.f, wg = 0.f, wb = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      ad += (0.125f * dw[k]) * al[k];
+      rd += (dw[k] * idn) * cd[k].x;
+      gd += (dw[k] * idn) * cd[k].y;
+      bd += (dw[k] * idn) * cd[k].z;
+      const float iw = w[k] * inv;
+      wr += iw * cw[k].x;
+      wg += iw * cw[k].y;
+      wb += iw * cw[k].z;
+    }
+    out[3 * (size_t)i + 1] = make_float4(rd, gd, bd, ad);
+    out[3 * (size_t)i + 2] = make_float4(wr, wg, wb, 0.f);
+  }
+}
+
+// pass 0: every ray starts at its first kept sample with T = 1
+__global__ __launch_bounds__(256) void k_ert_begin(int64_t n_rays, const int* __restrict__ beg,
+                                                   const int* __restrict__ end, int* __restrict__ pos,
+                                                   float* __restrict__ T, int* __restrict__ cnt, int B) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= n_rays) return;
+  const int b = beg[r], e = end[r];
+  pos[r] = b;
+  T[r] = 1.f;
+  cnt[r] = min(e - b, B);
+}
+
+// the pass's sample list: ray r's cnt[r] next samples at offs[r]; the pass size (offs[n_rays]) is
+// also the MLP launch's device count (and goes to stats[pass] when asked)
+__global__ __launch_bounds__(256) void k_ert_fill(int64_t n_rays, const int* __restrict__ pos,
+                                                  const int* __restrict__ cnt, const int* __restrict__ offs,
+                                                  int* __restrict__ list, int* __restrict__ stat) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r == 0 && stat) *stat = offs[n_rays];
+  if (r >= n_rays) return;
+  const int c = cnt[r];
+  if (c <= 0) return;
+  const int o = offs[r], p = pos[r];
+  for (int j = 0; j < c; ++j) list[o + j] = p + j;
+}
+
+// after a pass: walk ray r's samples of the pass with the compositing's arithmetic
+// (apn_composite.hip k_composite_lds, Point-NeRF path): a ray whose T fell below 1e-3 is retired,
+// the others get their next B samples (cnt = 0: retired or out of samples)
+__global__ __launch_bounds__(256) void k_ert_step(int64_t n_rays, const float4* __restrict__ out, float thr,
+                                                  int use_mask, int* __restrict__ pos, const int* __restrict__ end,
+                                                  float* __restrict__ T, int* __restrict__ cnt, int B) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= n_rays) return;
+  const int c = cnt[r];
+  if (c <= 0) return;
+  int p = pos[r];
+  float t = T[r];
+  bool dead = false;
+  for (int i = p; i < p + c; ++i) {
+    const float a = out[3 * (size_t)i].w;
+    if (!use_mask || a > thr) {
+      t = (float)((double)t * (1.0 - (double)a));
+      if ((double)t < 1e-3) {
+        dead = true;
+        break;
+      }
+    }
+  }
+  p += c;
+  pos[r] = p;
+  T[r] = t;
+  cnt[r] = dead ? 0 : min(end[r] - p, B);
+}
+
+__global__ void k_ray_bounds_ert(const int* __restrict__ s_ray, const int* __restrict__ n_dev, int* __restrict__ beg,
+                                 int* __restrict__ end) {
+  const int n = *n_dev;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int r = s_ray[i];
+  if (i == 0 || s_ray[i - 1] != r) beg[r] = i;
+  if (i == n - 1 || s_ray[i + 1] != r) end[r] = i + 1;
+}
+
+int scan_exclusive_i32(const int* in, int* out, int64_t n, void* ws, hipStream_t s);
+size_t scan_workspace_bytes(int64_t n);
+
+// workspace: beg, end, pos, cnt [n_rays] i32, T [n_rays] f32, offs [n_rays + 1] i32, list
+// [max_samples] i32, the scan's workspace
+static size_t ert_ws_layout(int64_t max_samples, int64_t n_rays, size_t* off) {
+  size_t o = 0;
+  auto take = [&](size_t bytes) {
+    size_t at = o;
+    o += (bytes + 255) / 256 * 256;
+    return at;
+  };
+  off[0] = take(4 * (size_t)n_rays);            // beg
+  off[1] = take(4 * (size_t)n_rays);            // end
+  off[2] = take(4 * (size_t)n_rays);            // pos
+  off[3] = take(4 * (size_t)n_rays);            // cnt
+  off[4] = take(4 * (size_t)n_rays);            // T
+  off[5] = take(4 * ((size_t)n_rays + 1));      // offs
+  off[6] = take(4 * (size_t)max_samples);       // list
+  off[7] = take(scan_workspace_bytes(n_rays));  // scan
+  return o;
+}
+
+size_t ert_workspace_bytes(int64_t max_samples, int64_t n_rays) {
+  size_t off[8];
+  return ert_ws_layout(max_samples, n_rays, off);
+}
+
+// Per-ray local index ranges of the passes: [0,4), [4,8), [8,12), [12,20), [20,36), [36,...).
+static const int ERT_PASS[ERT_PASSES] = {4, 4, 4, 8, 16, 1 << 30};
+
+int ert_run(const float4* s_pos, const int* s_ray, const int* s_nbr, int64_t max_samples, const int* n_samples_dev,
+            int64_t n_rays, const float4* recA, const float4* recB, float eps, float thr, float4* out, void* ws,
+            int* stats, hipStream_t s, const MlpPass& mlp) {
+  size_t off[8];
+  ert_ws_layout(max_samples, n_rays, off);
+  char* w = (char*)ws;
+  int* beg = (int*)(w + off[0]);
+  int* end = (int*)(w + off[1]);
+  int* pos = (int*)(w + off[2]);
+  int* cnt = (int*)(w + off[3]);
+  float* T = (float*)(w + off[4]);
+  int* offs = (int*)(w + off[5]);
+  int* list = (int*)(w + off[6]);
+  void* sws = w + off[7];
+  const int rb = ceil_div(n_rays, 256);
+  const int use_mask = thr > 0.f ? 1 : 0;
+  APN_TRY(fill_i32(beg, 0, n_rays, s));   // rays without kept samples: beg = end = 0
+  APN_TRY(fill_i32(end, 0, n_rays, s));
+  hipLaunchKernelGGL(k_ray_bounds_ert, dim3(ceil_div(max_samples, 256)), dim3(256), 0, s, s_ray, n_samples_dev, beg,
+                     end);
+  // direct path + weight colour of every kept sample (read up to the direct path's own break)
+  hipLaunchKernelGGL(k_direct_blend, dim3(ceil_div(max_samples, 256) < 256 * 16 ? ceil_div(max_samples, 256) : 256 * 16),
+                     dim3(256), 0, s, s_pos, s_nbr, n_samples_dev, recA, recB, eps, out);
+  hipLaunchKernelGGL(k_ert_begin, dim3(rb), dim3(256), 0, s, n_rays, beg, end, pos, T, cnt, ERT_PASS[0]);
+  for (int p = 0; p < ERT_PASSES; ++p) {
+    if (p > 0)
+      hipLaunchKernelGGL(k_ert_step, dim3(rb), dim3(256), 0, s, n_rays, (const float4*)out, thr, use_mask, pos, end,
+                         T, cnt, ERT_PASS[p]);
+    APN_TRY(scan_exclusive_i32(cnt, offs, n_rays, sws, s));
+    hipLaunchKernelGGL(k_ert_fill, dim3(rb), dim3(256), 0, s, n_rays, pos, cnt, offs, list, stats ? stats + p : nullptr);
+    APN_TRY(mlp(list, offs + n_rays));
+  }
+  return launch_status();
+}
+
+}  // namespace apn

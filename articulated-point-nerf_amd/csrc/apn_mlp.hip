@@ -594,6 +594,50 @@ extern "C" int apn_point_mlp(const float* s_pos4, const int32_t* s_ray, const in
   return launch_status();
 }
 
+extern "C" size_t apn_point_mlp_ert_workspace_bytes(int64_t max_samples, int64_t n_rays) {
+  return ert_workspace_bytes(max_samples > 0 ? max_samples : 1, n_rays > 0 ? n_rays : 1);
+}
+
+// apn_point_mlp with early ray termination (apn_ert.hip): the MLP's {rgb, alpha} columns for the
+// kept samples the compositing reads (every ray's samples up to its T < 1e-3 break), in ERT_PASSES
+// passes over the live rays; the direct-path and weight-colour columns for every kept sample. With
+// apn_composite on the same samples the frame is bit-identical to apn_point_mlp's.
+extern "C" int apn_point_mlp_ert(const float* s_pos4, const int32_t* s_ray, const int32_t* s_nbr, int64_t max_samples,
+                                 const int32_t* n_samples_dev, int64_t n_rays, const float* recA16, const float* recB8,
+                                 const float* feat_proj, int32_t feat_dim, const float* viewdirs,
+                                 const float* vemb_const, const float* wbuf, float eps, float act_shift,
+                                 float interval, float fast_color_thres, float* out12, void* workspace,
+                                 int32_t* pass_rows, void* stream) {
+  if (feat_dim != FEAT || n_rays <= 0) return APN_ERR_ARG;
+  if (max_samples <= 0) return APN_OK;
+  if (!s_pos4 || !s_ray || !s_nbr || !n_samples_dev || !recA16 || !recB8 || !feat_proj || !wbuf || !out12 ||
+      !workspace || (!viewdirs && !vemb_const))
+    return APN_ERR_ARG;
+  if (mlp_variant() != 0)   // the pass lists exist for the default (128-row split) kernel only
+    return apn_point_mlp(s_pos4, s_ray, s_nbr, max_samples, n_samples_dev, recA16, recB8, feat_proj, feat_dim,
+                         viewdirs, vemb_const, wbuf, eps, act_shift, interval, 0, out12, stream);
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t ntiles = (max_samples + 15) / 16;
+  const int blocks = (int)(ntiles < 256 * 64 ? ntiles : 256 * 64);
+  MlpPass pass = [&](const int* list, const int* n_list) {
+    launch_point_mlp_h4(blocks, false, s, (const float4*)s_pos4, s_ray, s_nbr, n_list, (const float4*)recA16,
+                        (const float4*)recB8, (const float4*)feat_proj, viewdirs, vemb_const, wbuf, eps, act_shift,
+                        interval, (float4*)out12, list);
+    return launch_status();
+  };
+  APN_TRY(ert_run((const float4*)s_pos4, s_ray, s_nbr, max_samples, n_samples_dev, n_rays, (const float4*)recA16,
+                  (const float4*)recB8, eps, fast_color_thres, (float4*)out12, workspace, pass_rows, s, pass));
+  // range fallback (apn_mlp_layout.h OFF_FLAG): if any pass flagged an out-of-fp16-range value, the
+  // FP32 MFMA kernel redoes every kept sample (all 12 columns, a superset of the passes); otherwise
+  // its workgroups exit at once
+  const int fb = blocks < 256 * 8 ? blocks : 256 * 8;
+  auto fp32_kernel = k_point_mlp<2, 2>;
+  hipLaunchKernelGGL(fp32_kernel, dim3(fb), dim3(MLP_THREADS), 0, s, (const float4*)s_pos4, s_ray, s_nbr,
+                     n_samples_dev, (const float4*)recA16, (const float4*)recB8, (const float4*)feat_proj, viewdirs,
+                     vemb_const, wbuf, eps, act_shift, interval, (float4*)out12, (const int*)(wbuf + OFF_FLAG));
+  return launch_status();
+}
+
 #ifdef APN_DEBUG_BUILD
 // Profiling aid: copy (and reset) the per-phase cycle sums of the timed MLP variants
 // (APN_MLP_VARIANT=2, 3): {gather, layer 1, layers 2-4, epilogue, tiles, kernel} summed over

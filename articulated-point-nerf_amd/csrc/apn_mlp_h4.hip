@@ -67,7 +67,7 @@ __device__ __forceinline__ void gather_load(int p, int k, int nb, int ray, Gathe
 // P is wave-uniform, so argument indices, frequencies and coordinate choices are compile-time
 // constants. Also writes the row's squared distance (sTo), the direct-blend terms (sRow) and the
 // sample's view-embedding element 4k + P (sV).
-template <int P, int HALF>
+template <int P, int HALF, bool DIRECT>
 __device__ __forceinline__ void gather_q(int nb, float4 q, const GatherRegs& G, char* __restrict__ PE,
                                          float* __restrict__ sTo, float* __restrict__ sRow, float* __restrict__ sV,
                                          const float* __restrict__ vemb_const) {
@@ -84,7 +84,7 @@ __device__ __forceinline__ void gather_q(int nb, float4 q, const GatherRegs& G, 
                          (a2.z * dx + a2.w * dy) + a3.x * dz};
     if constexpr (P == 0) {
       sTo[r] = (dx * dx + dy * dy) + dz * dz;
-    } else if constexpr (P == 1) {
+    } else if constexpr (P == 1 && DIRECT) {
       const float tn = (dx * dx + dy * dy) + dz * dz;
       float* rw = sRow + RS * r;
       rw[0] = expf(-(tn * tn) / a0.w);   // temporalpoints.py:461 (to_nn is already squared)
@@ -134,21 +134,21 @@ __device__ __forceinline__ void gather_q(int nb, float4 q, const GatherRegs& G, 
     sV[s * 32 + 4 * k + P] = 0.f;
     if constexpr (P == 0) {
       sTo[r] = 1.f;
-    } else if constexpr (P == 1) {
+    } else if constexpr (P == 1 && DIRECT) {
       for (int c = 0; c < 8; ++c) sRow[RS * r + c] = 0.f;
     }
   }
 }
 
-template <int HALF>
+template <int HALF, bool DIRECT>
 __device__ __forceinline__ void gather(int p, int nb, float4 q, const GatherRegs& G, char* __restrict__ PE,
                                        float* __restrict__ sTo, float* __restrict__ sRow, float* __restrict__ sV,
                                        const float* __restrict__ vemb_const) {
   switch (p) {
-    case 0: gather_q<0, HALF>(nb, q, G, PE, sTo, sRow, sV, vemb_const); break;
-    case 1: gather_q<1, HALF>(nb, q, G, PE, sTo, sRow, sV, vemb_const); break;
-    case 2: gather_q<2, HALF>(nb, q, G, PE, sTo, sRow, sV, vemb_const); break;
-    default: gather_q<3, HALF>(nb, q, G, PE, sTo, sRow, sV, vemb_const); break;
+    case 0: gather_q<0, HALF, DIRECT>(nb, q, G, PE, sTo, sRow, sV, vemb_const); break;
+    case 1: gather_q<1, HALF, DIRECT>(nb, q, G, PE, sTo, sRow, sV, vemb_const); break;
+    case 2: gather_q<2, HALF, DIRECT>(nb, q, G, PE, sTo, sRow, sV, vemb_const); break;
+    default: gather_q<3, HALF, DIRECT>(nb, q, G, PE, sTo, sRow, sV, vemb_const); break;
   }
 }
 
@@ -245,10 +245,13 @@ __device__ __forceinline__ void init_bias(f32x4 (&acc)[MT][2], int ot0, const fl
 // layer 1, layers 2-4, epilogue, tiles, whole kernel} over workgroups (wave 0's clock).
 __device__ unsigned long long g_phase4[6];
 
-template <bool SCALED, bool TIMED>
+// LISTED: the tile slots are the entries of ``list`` (sample indices, n_samples_dev entries) -- an
+// early-ray-termination pass (apn_ert.hip) -- and only the Point-NeRF columns {rgb, alpha} of each
+// sample are written (the direct-blend and weight-colour columns come from k_direct_blend).
+template <bool SCALED, bool TIMED, bool LISTED>
 __device__ __forceinline__ void mlp_tiles(
     const float4* __restrict__ s_pos, const int* __restrict__ s_ray, const int* __restrict__ s_nbr,
-    const int* __restrict__ n_samples_dev, const float4* __restrict__ recA, const float4* __restrict__ recB,
+    const int* __restrict__ list, const int* __restrict__ n_samples_dev, const float4* __restrict__ recA, const float4* __restrict__ recB,
     const float4* __restrict__ pproj, const float* __restrict__ viewdirs, const float* __restrict__ vemb_const,
     const float* __restrict__ wbuf, float eps, float shift, float interval, float4* __restrict__ out,
     char* const X, float* const sTo, float* const sIdw, float* const sRow, float* const sOut, float* const sV,
@@ -297,16 +300,20 @@ __device__ __forceinline__ void mlp_tiles(
     for (int h = 0; h < 2; ++h) {
       const int gs = tc * TS4 + 8 * h + (lane >> 3);
       const int gc = min(gs, nS - 1);
+      const int si = LISTED ? list[gc] : gc;
       pf_ok[h] = tl < t_end && gs < nS;
-      pf_nb[h] = s_nbr[(size_t)gc * 8 + (lane & 7)];
-      pf_q[h] = s_pos[gc];
-      pf_ray[h] = s_ray[gc];
+      pf_nb[h] = s_nbr[(size_t)si * 8 + (lane & 7)];
+      pf_q[h] = s_pos[si];
+      pf_ray[h] = s_ray[si];
     }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const int m = 16 * mt + li;
       pf_pok[mt] = tl < t_end && tc * TS4 + (m >> 3) < nS;
-      pf_pn[mt] = s_nbr[min((size_t)tc * TR4 + m, (size_t)nS * 8 - 1)];
+      if (LISTED)
+        pf_pn[mt] = s_nbr[(size_t)list[min(tc * TS4 + (m >> 3), nS - 1)] * 8 + (m & 7)];
+      else
+        pf_pn[mt] = s_nbr[min((size_t)tc * TR4 + m, (size_t)nS * 8 - 1)];
     }
   };
   int tile = t_beg + blockIdx.x / nx;
@@ -344,8 +351,8 @@ __device__ __forceinline__ void mlp_tiles(
     for (int mt = 0; mt < MT; ++mt) { pn_tile[mt] = pf_pn[mt]; pok_tile[mt] = pf_pok[mt]; }
     fetch(tile + per_xcd);
     // ------------------------------------------------ gather + posenc + direct-blend terms
-    gather<0>(wid, nb0, q0, g0, X, sTo, sRow, sV, vemb_const);
-    gather<1>(wid, nb1, q1, g1, X, sTo, sRow, sV, vemb_const);
+    gather<0, !LISTED>(wid, nb0, q0, g0, X, sTo, sRow, sV, vemb_const);
+    gather<1, !LISTED>(wid, nb1, q1, g1, X, sTo, sRow, sV, vemb_const);
     // layer-1 accumulators = P[nbr] (global -> VGPR), loaded after the gather's register peak
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -366,8 +373,12 @@ __device__ __forceinline__ void mlp_tiles(
     __syncthreads();
     APN_PHASE(0)
     // ------------------------------------------------ outputs of the previous tile, IDW weights
-    if (prev_s0 >= 0 && tid < TS4 * 3 && prev_s0 + tid / 3 < nS)
+    if (LISTED) {
+      if (prev_s0 >= 0 && tid < TS4 && prev_s0 + tid < nS)
+        out[(size_t)list[prev_s0 + tid] * 3] = *(const float4*)(sOut + 12 * tid);
+    } else if (prev_s0 >= 0 && tid < TS4 * 3 && prev_s0 + tid / 3 < nS) {
       out[(size_t)prev_s0 * 3 + tid] = *(const float4*)(sOut + 4 * tid);
+    }
     if (tid < TS4) {  // IDW weights (temporalpoints.py:473-475)
       float w[8], sum = 0.f;
 #pragma unroll
@@ -458,7 +469,7 @@ __device__ __forceinline__ void mlp_tiles(
     }
     // direct blend + weight-vis colour (temporalpoints.py:459-470, 517-519): waves 1-2, lane =
     // (sample, quantity); sums over the 8 neighbours in order
-    if (wid == 1 || wid == 2) {
+    if (!LISTED && (wid == 1 || wid == 2)) {
       const int sl = (wid - 1) * 64 + lane;
       const int s = sl >> 3, qn = sl & 7;
       const float* rw = sRow + 8 * RS * s;
@@ -554,17 +565,21 @@ __device__ __forceinline__ void mlp_tiles(
     for (int i = 0; i < 6; ++i) atomicAdd(&g_phase4[i], ph[i]);
   }
   __syncthreads();
-  if (prev_s0 >= 0 && tid < TS4 * 3 && prev_s0 + tid / 3 < nS)
+  if (LISTED) {
+    if (prev_s0 >= 0 && tid < TS4 && prev_s0 + tid < nS)
+      out[(size_t)list[prev_s0 + tid] * 3] = *(const float4*)(sOut + 12 * tid);
+  } else if (prev_s0 >= 0 && tid < TS4 * 3 && prev_s0 + tid / 3 < nS) {
     out[(size_t)prev_s0 * 3 + tid] = *(const float4*)(sOut + 4 * tid);
+  }
   if (range_bad) __builtin_amdgcn_raw_buffer_store_b32(1, rs, 0, H_TOTAL * 2, 0);   // the range flag (OFF_FLAG)
 }
 
 // One instantiation per weight-scale mode; apn_point_mlp launches both and the one that does not
 // match wbuf's mode exits at once (as does every workgroup once the range flag is set).
-template <bool SCALED, bool TIMED>
+template <bool SCALED, bool TIMED, bool LISTED>
 __global__ __launch_bounds__(MLP_THREADS, 2) void k_point_mlp_h4(
     const float4* __restrict__ s_pos, const int* __restrict__ s_ray, const int* __restrict__ s_nbr,
-    const int* __restrict__ n_samples_dev, const float4* __restrict__ recA, const float4* __restrict__ recB,
+    const int* __restrict__ list, const int* __restrict__ n_samples_dev, const float4* __restrict__ recA, const float4* __restrict__ recB,
     const float4* __restrict__ pproj, const float* __restrict__ viewdirs, const float* __restrict__ vemb_const,
     const float* __restrict__ wbuf, float eps, float shift, float interval, float4* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) char X[TR4 * XB];
@@ -580,7 +595,7 @@ __global__ __launch_bounds__(MLP_THREADS, 2) void k_point_mlp_h4(
     s_skip = __builtin_nontemporal_load((const int*)(wbuf + OFF_FLAG)) != 0 || (wbuf[OFF_SCALE + 6] != 0.f) != SCALED;
   __syncthreads();
   if (s_skip) return;
-  mlp_tiles<SCALED, TIMED>(s_pos, s_ray, s_nbr, n_samples_dev, recA, recB, pproj, viewdirs, vemb_const, wbuf, eps, shift,
+  mlp_tiles<SCALED, TIMED, LISTED>(s_pos, s_ray, s_nbr, list, n_samples_dev, recA, recB, pproj, viewdirs, vemb_const, wbuf, eps, shift,
                     interval, out, X, sTo, sIdw, sRow, sOut, sV, sW, sPart);
 }
 
@@ -589,23 +604,28 @@ __global__ __launch_bounds__(MLP_THREADS, 2) void k_point_mlp_h4(
 void launch_point_mlp_h4(int blocks, bool timed, hipStream_t stream, const float4* s_pos, const int* s_ray, const int* s_nbr,
                          const int* n_samples_dev, const float4* recA, const float4* recB, const float4* pproj,
                          const float* viewdirs, const float* vemb_const, const float* wbuf, float eps, float shift,
-                         float interval, float4* out) {
+                         float interval, float4* out, const int* list) {
   auto go = [&](auto kern, int nb) {
-    hipLaunchKernelGGL(kern, dim3(nb), dim3(MLP_THREADS), 0, stream, s_pos, s_ray, s_nbr, n_samples_dev, recA, recB,
-                       pproj, viewdirs, vemb_const, wbuf, eps, shift, interval, out);
+    hipLaunchKernelGGL(kern, dim3(nb), dim3(MLP_THREADS), 0, stream, s_pos, s_ray, s_nbr, list, n_samples_dev, recA,
+                       recB, pproj, viewdirs, vemb_const, wbuf, eps, shift, interval, out);
   };
   const int nb_scaled = blocks < 256 * 8 ? blocks : 256 * 8;
+  if (list) {
+    go(t128::k_point_mlp_h4<false, false, true>, blocks);
+    go(t128::k_point_mlp_h4<true, false, true>, nb_scaled);
+    return;
+  }
 #ifdef APN_DEBUG_BUILD
   if (timed) {
-    go(t128::k_point_mlp_h4<false, true>, blocks);
-    go(t128::k_point_mlp_h4<true, true>, nb_scaled);
+    go(t128::k_point_mlp_h4<false, true, false>, blocks);
+    go(t128::k_point_mlp_h4<true, true, false>, nb_scaled);
     return;
   }
 #else
   (void)timed;
 #endif
-  go(t128::k_point_mlp_h4<false, false>, blocks);
-  go(t128::k_point_mlp_h4<true, false>, nb_scaled);
+  go(t128::k_point_mlp_h4<false, false, false>, blocks);
+  go(t128::k_point_mlp_h4<true, false, false>, nb_scaled);
 }
 
 int debug_phase_cycles_h4(uint64_t* out6) {

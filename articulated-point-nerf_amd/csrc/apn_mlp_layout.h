@@ -2,6 +2,8 @@
 // MFMA; apn_mlp_h3.hip: 3-term fp16-split MFMA) and apn_amd/ops.py:pack_mlp_weights (through
 // apn_mlp_weight_layout()).
 #pragma once
+#include <functional>
+
 #include "apn_common.h"
 
 namespace apn {
@@ -92,10 +94,20 @@ void launch_point_mlp_h3(int blocks, bool timed, hipStream_t stream, const float
                          const float4* pproj, const float* viewdirs, const float* vemb_const, const float* wbuf,
                          float eps, float shift, float interval, float4* out);
 // Launcher of the fp16-split kernel on 128-row tiles (apn_mlp_h4.hip).
+// ``list`` (optional): the launch's tile slots are these sample indices (n_samples_dev of them) and
+// only each sample's {rgb, alpha} columns are written (early-ray-termination passes, apn_ert.hip).
 void launch_point_mlp_h4(int blocks, bool timed, hipStream_t stream, const float4* s_pos, const int* s_ray, const int* s_nbr,
                          const int* n_samples_dev, const float4* recA, const float4* recB, const float4* pproj,
                          const float* viewdirs, const float* vemb_const, const float* wbuf, float eps, float shift,
-                         float interval, float4* out);
+                         float interval, float4* out, const int* list = nullptr);
+// Early ray termination (apn_ert.hip): the MLP in ERT_PASSES passes over the live rays' next
+// kept samples; ``MlpPass(list, n_list_dev)`` launches the MLP on one pass's sample list.
+constexpr int ERT_PASSES = 6;
+typedef std::function<int(const int*, const int*)> MlpPass;
+size_t ert_workspace_bytes(int64_t max_samples, int64_t n_rays);
+int ert_run(const float4* s_pos, const int* s_ray, const int* s_nbr, int64_t max_samples, const int* n_samples_dev,
+            int64_t n_rays, const float4* recA, const float4* recB, float eps, float thr, float4* out, void* ws,
+            int* stats, hipStream_t s, const MlpPass& mlp);
 // Largest magnitude the fp16-split kernel carries through its hi/lo halves (fp16 max finite).
 constexpr float H3_RANGE = 65504.f;
 // Adds (and resets) the phase-timed fp16-split kernel's cycle sums into out6.

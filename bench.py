@@ -146,6 +146,13 @@ def flop_per_kept_sample(d_in=191, width=128):
     return 8 * 2 * (d_in * width + 3 * width * width) + 2 * (128 + 128 * 128 + 155 * 64 + 64 * 3)
 
 
+def mlp_pass_rows(ev, kept):
+    """Samples the neighbour MLP ran on in the last timed eager frame, per early-termination pass
+    (apn_point_mlp_ert's pass_rows), or [kept] when every kept sample went through it."""
+    rows = ev[-1][3] if ev and len(ev[-1]) > 3 else None
+    return [int(v) for v in rows.tolist()] if rows is not None else [int(kept)]
+
+
 def mfma_executed_flop(n_samples, variant=0):
     """MFMA flops the MLP kernel issues per launch, 4 waves per tile.
     variant 1 (FP32 MFMA, 8-sample tiles): 16x16x4 f32 MFMAs for layer 1 (K=64), layers 2-4 (K=128)
@@ -437,7 +444,7 @@ def replay_sharded(steps_in_flight, t_arg, k, streams, comm):
     return out, time.perf_counter() - h0
 
 
-def viewpoint_rate(model, scene, dev, n_views=8, in_flight=3):
+def viewpoint_rate(model, scene, dev, n_views=16, in_flight=3):
     """harness.render_viewpoints (run.py:80-239) over n_views views at distinct times -- rays made
     on the device per view, n frames in flight on the model's FramePipeline, rgb / depth / weights
     read back to host numpy per view -- timed after one untimed sweep (the captures). The drop-in
@@ -484,8 +491,9 @@ def frame_rate(config, dev, steps=10, warmup=2, in_flight=3):
     torch.cuda.synchronize(dev)
     timing, model.timing = model.timing, None
     ev = timing.get("mlp_events", [])
-    mlp_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / max(len(ev), 1)
+    mlp_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / max(len(ev), 1)
     kept = int(ev[-1][2].item()) if ev else stats.get("kept_samples", 0)
+    rows = mlp_pass_rows(ev, kept)
     from apn_amd.pipeline import FramePipeline
     pipe = FramePipeline(model, t_arg, rk, n=in_flight, poses=poses, Ks=Ks, get_skeleton=True, readback=None)
     replay_pipeline(pipe, t_arg, 2)
@@ -495,10 +503,11 @@ def frame_rate(config, dev, steps=10, warmup=2, in_flight=3):
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     d_in = 191 + model.pose_embedding_dim
-    achieved = kept * flop_per_kept_sample(d_in) / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else 0.0
+    achieved = sum(rows) * flop_per_kept_sample(d_in) / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else 0.0
     return {"workload": S.CONFIGS[config].name + f" ({config})", "value": steps * R / elapsed, "unit": "rays/s",
             "ms_per_step": elapsed / steps * 1e3, "steps": steps, "rays_per_frame": R, "points": scene.cfg.N,
             "bones": scene.cfg.J, "inbbox_samples": stats.get("inbbox_samples"), "kept_samples": kept,
+            "mlp_rows_per_pass": rows, "mlp_samples": sum(rows),
             "timed_frames_overflowed": pipe.overflowed(), "frames_in_flight": pipe.n,
             "mlp_kernel_ms": mlp_ms, "mlp_roofline_frac": achieved / SPLIT3_PEAK_TFLOPS}
 
@@ -618,6 +627,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-other-configs", action="store_true",
                     help="skip the compact C3 / C4 / C5 measurements the default one-GPU C2 line carries")
+    ap.add_argument("--no-full-mlp-leg", action="store_true",
+                    help="skip timing the same frames without early ray termination (full_mlp_ms_per_step)")
     ap.add_argument("--no-viewpoints", action="store_true",
                     help="skip the harness.render_viewpoints leg (8 views, frames in flight, host readback)")
     ap.add_argument("-o", "--out", default=None, help="also write the JSON line to this file")
@@ -792,6 +803,25 @@ def main():
         log(f"[rank {rank}] frames in flight {n_flight}: "
             f"{elapsed / args.steps * 1e3:.3f} ms/frame; one at a time "
             f"{serial_ms:.3f} ms/frame")
+    full_mlp_ms = None
+    if world == 1 and pipe is not None and model.early_termination and not args.no_full_mlp_leg:
+        # the same frames with the neighbour MLP on EVERY kept sample (the reference's work: no early
+        # ray termination), n in flight on their own pipeline: the gain of apn_point_mlp_ert
+        from apn_amd.pipeline import FramePipeline
+        model.early_termination = False
+        try:
+            pfull = FramePipeline(model, t_arg, rk, n=args.in_flight, poses=poses, Ks=Ks, get_skeleton=True,
+                                  readback=None)
+            replay_pipeline(pfull, t_arg, 2)
+            torch.cuda.synchronize(dev)
+            tf0 = time.perf_counter()
+            replay_pipeline(pfull, t_arg, args.steps)
+            torch.cuda.synchronize(dev)
+            full_mlp_ms = (time.perf_counter() - tf0) / args.steps * 1e3
+            del pfull
+        finally:
+            model.early_termination = True
+        log(f"[rank {rank}] full MLP (no early ray termination): {full_mlp_ms:.3f} ms/frame")
     from apn_amd import _lib
     lib = _lib.load()
     debug_lib = hasattr(lib, "apn_debug_knn_stats")   # APN_HIP_LIB = libapn_hip_debug.so (tools/ A/B runs)
@@ -811,8 +841,10 @@ def main():
             stage_ms[name] = stage_ms.get(name, 0.0) + a.elapsed_time(b) / n_timed
     log(f"[rank {rank}] stage ms/frame (HIP events, eager frames): " + ", ".join(f"{k} {v:.3f}" for k, v in stage_ms.items()))
     ev = timing.get("mlp_events", [])
-    mlp_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / max(len(ev), 1)
+    mlp_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / max(len(ev), 1)
     S_kept = int(ev[-1][2].item()) if ev else stats.get("kept_samples", 0)
+    pass_rows = mlp_pass_rows(ev, S_kept)
+    S_mlp = sum(pass_rows)   # the samples the MLP ran on (early ray termination: those the compositing reads)
     kept_total = S_kept * (world if not shard_rays else 1)
     shard_diag = None
     if shard_rays:
@@ -833,7 +865,7 @@ def main():
         torch.cuda.synchronize(dev)
         ag_ms = g0.elapsed_time(g1) / 10
         mine = {"rank": rank, "world_size": torch.distributed.get_world_size(), "device": device_identity(dev),
-                "rays": n_local, "kept_samples": S_kept, "allgather_ms": round(ag_ms, 4),
+                "rays": n_local, "kept_samples": S_kept, "mlp_samples": S_mlp, "allgather_ms": round(ag_ms, 4),
                 "replicated_ms": round(sum(stage_ms.get(k, 0.0) for k in ("lbs", "bbox", "grid")), 4),
                 "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()}}
         per_rank = [None] * world
@@ -879,9 +911,10 @@ def main():
     d_in = 191  # pose embedding folded into the bias for ZJU; F_alg still counts the reference D_in
     if model.pose_embedding_dim > 0:
         d_in = 191 + model.pose_embedding_dim
-    flop = S_kept * flop_per_kept_sample(d_in)
+    flop = S_mlp * flop_per_kept_sample(d_in)
     achieved = flop / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else 0.0
-    executed = mfma_executed_flop(S_kept, variant) / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else 0.0
+    executed = (sum(mfma_executed_flop(r, variant) for r in pass_rows) / (mlp_ms * 1e-3) / 1e12
+                if mlp_ms > 0 else 0.0)
     if variant in (1, 2):
         kernel, peak, mfma_peak = "k_point_mlp (fp32 MFMA)", FP32_MFMA_PEAK_TFLOPS, FP32_MFMA_PEAK_TFLOPS
         peak_note = "peak = FP32 matrix peak"
@@ -897,7 +930,10 @@ def main():
                     if any("mlp_w" in w.bufs for w in wss) else None)
     traffic, traffic_src = latest_traffic("point_mlp_traffic")
     ms_per_step = elapsed / args.steps * 1e3
-    frame_roof = frame_roofline(scene.cfg.N, scene.cfg.J, R, kept_total * flop_per_kept_sample(d_in), ms_per_step,
+    mlp_total = kept_total if len(pass_rows) == 1 else (S_mlp if shard_rays else S_mlp * world)
+    if shard_rays and len(pass_rows) > 1:
+        mlp_total = sum(p.get("mlp_samples", p["kept_samples"]) for p in shard_diag["per_rank"])
+    frame_roof = frame_roofline(scene.cfg.N, scene.cfg.J, R, mlp_total * flop_per_kept_sample(d_in), ms_per_step,
                                 world if shard_rays else 1)
     value = (1 if shard_rays else world) * args.steps * R / elapsed
     cpu = psnr = same = None
@@ -937,6 +973,8 @@ def main():
         "config": {"workload": S.CONFIGS[args.config].name + f" ({args.config})", "rays_per_frame": R,
                    "points": scene.cfg.N, "bones": scene.cfg.J, "inbbox_samples": stats.get("inbbox_samples"),
                    "kept_samples": S_kept,
+                   "early_ray_termination": len(pass_rows) > 1,
+                   "mlp_samples": S_mlp, "mlp_rows_per_pass": pass_rows,
                    "parallelism": (f"rays x{world} ({SH.DEFAULT_SPLIT} split"
                                    + (f" of {SH.RAY_BLOCK}-ray blocks" if SH.DEFAULT_SPLIT == "blocks" else "")
                                    + f") + {backend} all_gather_into_tensor of the per-ray tiles"
@@ -954,6 +992,7 @@ def main():
                    "frames_in_flight": n_flight,
                    "memory": mem,
                    "serial_ms_per_step": serial_ms,
+                   "full_mlp_ms_per_step": full_mlp_ms,
                    "timed_frames_overflowed": overflowed,
                    "mlp_fp32_fallback_fired": mlp_fallback},
         "roofline": {"bound": "mfma", "kernel": kernel, "achieved": achieved, "peak": peak,
@@ -964,10 +1003,12 @@ def main():
                                         f"{traffic.get('avg_ms', float('nan')):.2f} ms then); NOT measured in this run"
                                         if traffic else None),
                      "flop_per_launch": flop, "avg_launch_ms": mlp_ms,
-                     "note": "achieved = reference F_alg (SURVEY.md 8(d), fp32 flops) / avg MLP kernel time (HIP "
-                             "events on the launch stream); " + peak_note + "; the kernel issues fewer MFMA flops "
-                             "than F_alg (per-point layer-1 projection, folded rgb head, padded 16-row head "
-                             "tile): executed_tflops / mfma_util",
+                     "note": "achieved = reference F_alg (SURVEY.md 8(d), fp32 flops) per sample x the samples the "
+                             "MLP ran on (mlp_samples: with early ray termination the kept samples the compositing "
+                             "reads, in passes) / the MLP stage's time (HIP events on the launch stream around all "
+                             "its launches: the direct-blend kernel, the passes' list kernels and MLP launches); "
+                             + peak_note + "; the kernel issues fewer MFMA flops than F_alg (per-point layer-1 "
+                             "projection, folded rgb head): executed_tflops / mfma_util",
                      "executed_tflops": executed,
                      "mfma_util": executed / mfma_peak},
         "frame_roofline_frac": frame_roof["frac"],

@@ -1,0 +1,116 @@
+"""Exact early ray termination of the neighbour MLP (apn_point_mlp_ert, apn_ert.hip).
+
+The reference runs feat_net / densitynet / rgbnet on every kept sample (temporalpoints.py:452-519)
+and its compositing then stops each ray at the sample whose update takes T below 1e-3
+(render_utils_kernel.cu:445-451); the {rgb, alpha} of later samples are never read. The render
+path runs the MLP only on the samples the compositing reads (passes over the live rays' next
+samples) and the direct / weight-colour columns on every kept sample. The frame must be
+bit-identical to the one that runs the MLP on every kept sample -- on golden scenes, with and
+without the fast_color_thres masks, on a scene whose rays never terminate, and on the whole C2
+frame -- and the MLP must have skipped exactly the samples after each ray's break."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+KEYS = ("rgb_marched", "rgb_marched_direct", "depth", "weights", "alphainv_last", "alphainv_last_direct")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch.device("cuda")
+
+
+def _frame(model, t, rk, ert):
+    model.early_termination = ert
+    try:
+        with torch.no_grad():
+            o = model(t, render_depth=True, render_kwargs=rk, render_weights=True)
+        out = {k: o[k].clone() for k in KEYS}
+        ns = int(model.last_stats["kept_samples"])
+        out12 = model._ws.bufs["out12"][:12 * ns].view(ns, 12).clone()
+        s_ray = model._ws.bufs["s_ray"][:ns].clone()
+        rows = model.last_mlp_rows.clone() if ert else None
+    finally:
+        model.early_termination = True
+    return out, out12, s_ray, rows
+
+
+def _breaks(alpha, s_ray, n_rays, thr):
+    """Per kept sample: is it at or before its ray's break (the samples the compositing reads on the
+    Point-NeRF path), by the compositing's own arithmetic (float T updated in double)."""
+    a = alpha.astype(np.float32)
+    need = np.zeros(len(a), bool)
+    starts = np.searchsorted(s_ray, np.arange(n_rays))
+    ends = np.searchsorted(s_ray, np.arange(n_rays), side="right")
+    for r in np.nonzero(ends > starts)[0]:
+        T = np.float32(1)
+        for i in range(starts[r], ends[r]):
+            need[i] = True
+            if thr <= 0 or a[i] > np.float32(thr):
+                T = np.float32(np.float64(T) * (1.0 - np.float64(a[i])))
+                if np.float64(T) < 1e-3:
+                    break
+    return need
+
+
+def _check(model, t, rk, thr):
+    full, f12, f_ray, _ = _frame(model, t, rk, False)
+    ert, e12, e_ray, rows = _frame(model, t, rk, True)
+    for k in KEYS:
+        assert torch.equal(full[k], ert[k]), k
+    assert torch.equal(f_ray, e_ray)
+    f12, e12 = f12.cpu().numpy(), e12.cpu().numpy()
+    # direct-path and weight-colour columns: every kept sample, bit-identical to the fused kernel's
+    assert np.array_equal(f12[:, 4:], e12[:, 4:])
+    # the MLP's columns: identical on every sample the compositing reads, and the passes ran on
+    # exactly those plus at most the rest of the pass in which the ray broke
+    need = _breaks(f12[:, 3], f_ray.cpu().numpy(), len(rk["rays_o"]), thr)
+    assert np.array_equal(f12[need, :4], e12[need, :4])
+    n_rows = int(rows.sum())
+    assert need.sum() <= n_rows <= len(f12)
+    return len(f12), int(need.sum()), n_rows, rows.tolist()
+
+
+@pytest.mark.parametrize("name", ["G1", "G2", "G3", "G4", "C1"])
+def test_ert_frame_bit_identical(dev, name):
+    from apn_amd import harness, synthetic as S
+    scene = S.make_scene(name)
+    model = harness.build_model(scene, dev)
+    rk = scene.render_kwargs(dev)
+    for dt in (0.0, 0.13):
+        t = torch.tensor([scene.cfg.t + dt], device=dev)
+        kept, need, rows, per = _check(model, t, rk, model.fast_color_thres)
+        print(f"{name} t+{dt}: kept {kept}, read by the compositing {need}, MLP rows {rows} {per}")
+
+
+def test_ert_without_masks_and_without_termination(dev):
+    """fast_color_thres = 0 (no pre/post masks: every sample enters the walk), and a scene whose
+    densities are pushed down so that no ray terminates (every pass runs, the MLP sees every
+    kept sample): both bit-identical."""
+    from apn_amd import harness, synthetic as S
+    scene = S.make_scene("G3")
+    model = harness.build_model(scene, dev)
+    rk = scene.render_kwargs(dev)
+    t = torch.tensor([scene.cfg.t], device=dev)
+    model.fast_color_thres = 0
+    _check(model, t, rk, 0)
+    model.fast_color_thres = S.FAST_COLOR_THRES
+    with torch.no_grad():
+        model.densitynet.bias.sub_(30.0)   # alpha ~ 0: T stays near 1 on every ray
+    kept, need, rows, _ = _check(model, t, rk, model.fast_color_thres)
+    assert rows == kept == need
+
+
+def test_ert_full_c2_frame_bit_identical(dev):
+    from apn_amd import harness, synthetic as S
+    scene = S.make_scene("C2")
+    model = harness.build_model(scene, dev)
+    rk = scene.render_kwargs(dev)
+    t = torch.tensor([scene.cfg.t], device=dev)
+    kept, need, rows, per = _check(model, t, rk, model.fast_color_thres)
+    print(f"C2: kept {kept}, read by the compositing {need} ({need / kept:.3f}), MLP rows {rows} "
+          f"({rows / kept:.3f}) per pass {per}")
+    assert rows < kept

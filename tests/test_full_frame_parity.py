@@ -164,7 +164,18 @@ def test_c2_every_ray_vs_oracle(frame):
             sub[k] = rk[k][sel].contiguous()
         ref = orc.forward(torch.tensor([scene.cfg.t]), render_depth=True, render_kwargs=sub, render_weights=True,
                           t_hat_override=xyz, knn_tree=True, perm=model.last_palette_perm)
-        kept += len(orc.trace.get("ray_id", []))
+        if "alpha" not in orc.trace:
+            # no kNN survivor in these rows (the oracle's NoPointsException dict, an artefact of the
+            # chunking: the whole frame has survivors, so the GPU composited empty rays): background
+            # colour, depth 0, transmittance 1 on every ray of the chunk
+            bg = np.float32(rk["bg"])
+            for key in ("rgb_marched", "rgb_marched_direct", "weights"):
+                assert (fr["out"][key][sel] == bg).all(), key
+            assert (fr["out"]["depth"][sel] == 0).all()
+            for key in ("alphainv_last", "alphainv_last_direct"):
+                assert (fr["out"][key][sel] == 1).all(), key
+            continue
+        kept += len(orc.trace["ray_id"])
         for key in KEYS:
             nb, w = assert_flips_explained(key, fr["out"][key][sel], ref[key].numpy(), orc.trace)
             n_bad[key] += nb

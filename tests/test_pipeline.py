@@ -62,6 +62,7 @@ def test_pipeline_shares_tables_not_frames(dev):
     scene, model = _scene_model(dev)
     rk = scene.render_kwargs(dev)
     t = torch.tensor([scene.cfg.t], device=dev)
+    _eager(model, t, rk)   # the model's own workspace (eager frames, re-renders)
     pipe = FramePipeline(model, t, rk, n=3, readback=None)
     assert "feat_proj" in model._ws_shared.bufs
     wss = pipe.workspaces
