@@ -149,7 +149,30 @@ def read_png(path):
 
 
 def _draw_line(img, p0, p1, color):
-    """8-connected line (cv2.LINE_8 style) from p0 to p1 = (x, y), clipped to the image."""
+    """8-connected line (cv2.LINE_8 style) from p0 to p1 = (x, y), clipped to the image: the pixels
+    of the integer error-term walk (x, y or both advance per step), in closed form -- along the
+    major axis i = 0 .. d, the minor coordinate moves floor((2 i d_minor + d) / (2 d)) steps (the
+    walk's own pixels, tests/test_harness_cpu.py::test_draw_line_closed_form_equals_walk)."""
+    import numpy as np
+    x0, y0 = int(p0[0]), int(p0[1])
+    x1, y1 = int(p1[0]), int(p1[1])
+    dx, dy = abs(x1 - x0), abs(y1 - y0)
+    sx, sy = (1 if x0 < x1 else -1), (1 if y0 < y1 else -1)
+    if dx >= dy:
+        i = np.arange(dx + 1)
+        k = (2 * i * dy + dx) // (2 * dx) if dx > 0 else np.zeros(1, np.int64)
+        xs, ys = x0 + sx * i, y0 + sy * k
+    else:
+        i = np.arange(dy + 1)
+        k = (2 * i * dx + dy) // (2 * dy)
+        xs, ys = x0 + sx * k, y0 + sy * i
+    H, W = img.shape[:2]
+    m = (xs >= 0) & (xs < W) & (ys >= 0) & (ys < H)
+    img[ys[m], xs[m]] = color
+
+
+def _draw_line_walk(img, p0, p1, color):
+    """The step-by-step error-term walk _draw_line restates in closed form (kept for the test)."""
     x0, y0 = int(p0[0]), int(p0[1])
     x1, y1 = int(p1[0]), int(p1[1])
     dx, dy = abs(x1 - x0), -abs(y1 - y0)
@@ -308,7 +331,7 @@ def render_viewpoints(model, render_poses, HW, Ks, ndc, render_kwargs, gt_imgs=N
         from .pipeline import cached_pipeline
         dev = model.canonical_feat.device
         rgb_key = "rgb_marched_direct" if render_pcd_direct else "rgb_marched"
-        pipe, pending, stack = None, [], {}
+        pipe, pending, stack, pinned = None, [], {}, {}
         n_views = len(render_poses)
 
         def fetch():
@@ -317,12 +340,7 @@ def render_viewpoints(model, render_poses, HW, Ks, ndc, render_kwargs, gt_imgs=N
             # here (in the order _finish would: PNGs first), overlapped with the GPU's next frames
             nonlocal bones
             i, H, W, h = pending.pop(0)
-            if not stack:
-                stack.update(rgb=np.empty((n_views, H, W, 3), np.float32),
-                             depth=np.empty((n_views, H, W, 1), np.float32),
-                             weights=np.empty((n_views, H, W, 3), np.float32))
-            r = h.result(into={rgb_key: stack["rgb"][i], "depth": stack["depth"][i],
-                               "weights": stack["weights"][i]})
+            r = h.result()   # the frame's images are already in the pinned stacks (DMA at submit)
             if "joints" in r:
                 b = _joint_record({"joints": r["joints"], "bones": model.bones if model.joints_to_keep is None
                                    else model.new_bones}, joints, i, HW, render_kwargs)
@@ -341,7 +359,13 @@ def render_viewpoints(model, render_poses, HW, Ks, ndc, render_kwargs, gt_imgs=N
                 pipe = cached_pipeline(model, t, rk, n=in_flight, render_depth=True, render_weights=True,
                                        poses=c2w[None], Ks=K[None], get_skeleton=True,
                                        readback=(rgb_key, "depth", "weights"))
-            pending.append((i, H, W, pipe.submit(t, (ro, rd, vd), c2w[None], K[None])))
+                # the returned image stacks, in pinned memory (torch's host cache reuses it from call to
+                # call): each frame's readback is a DMA straight into its slice, no host copy
+                for k, c in (("rgb", 3), ("depth", 1), ("weights", 3)):
+                    pinned[k] = torch.empty((n_views, H, W, c), dtype=torch.float32, pin_memory=True)
+                    stack[k] = pinned[k].numpy()
+            dest = {rgb_key: pinned["rgb"][i], "depth": pinned["depth"][i], "weights": pinned["weights"][i]}
+            pending.append((i, H, W, pipe.submit(t, (ro, rd, vd), c2w[None], K[None], dest=dest)))
             if len(pending) >= in_flight:
                 fetch()
         while pending:

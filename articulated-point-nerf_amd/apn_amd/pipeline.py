@@ -35,8 +35,9 @@ class FrameHandle:
     (+ ``joints`` with get_skeleton); ``device()``: the frame's RenderOutput on the device, valid
     until its slot is reused n frames later."""
 
-    def __init__(self, pipe, slot, out, t):
+    def __init__(self, pipe, slot, out, t, dest=None):
         self._pipe, self._slot, self._out, self._t = pipe, slot, out, t
+        self._dest = dest   # submit(dest=...): the readback went straight into these pinned tensors
         self._res = None
 
     def done(self) -> bool:
@@ -65,6 +66,20 @@ class FrameHandle:
         slot["done"].synchronize()
         host = slot["host"]
         info = host["_info"].tolist()   # {queries, in-bbox total, overflow, survivors}
+        if self._dest is not None:
+            # the frame's outputs are already in the caller's pinned tensors (no host copy)
+            if info[2]:
+                fresh = self._out._rerender()
+                for k, v in self._dest.items():
+                    v.copy_(fresh[k].detach().reshape(v.shape))
+                self._pipe.rerenders += 1
+            res = dict(self._dest)
+            if "joints" in host:
+                res["joints"] = (fresh["joints"].detach().cpu().clone() if info[2] and self._pipe.get_skeleton
+                                 else host["joints"].clone())
+            res["kept_samples"], res["inbbox_samples"] = info[3], info[1]
+            self._res = res
+            return res
         if info[2]:
             # overflowed the captured capacity: the exact render (the model's own workspace; its
             # rerender also marks the slot's graph for a capture before its next replay)
@@ -165,10 +180,13 @@ class FramePipeline:
         for s in self._slots:
             cur.wait_stream(s["stream"])
 
-    def submit(self, t, rays=None, poses=None, Ks=None) -> FrameHandle:
+    def submit(self, t, rays=None, poses=None, Ks=None, dest=None) -> FrameHandle:
         """Queue the next frame: time ``t`` (and, when they change per view, ``rays`` =
         (rays_o, rays_d, viewdirs) [R, 3] each, ``poses`` [V, 4, 4], ``Ks`` [V, 3, 3]) on the next
-        slot's stream. Inputs made on the caller's stream are ordered before the frame."""
+        slot's stream. Inputs made on the caller's stream are ordered before the frame. ``dest``
+        ({readback key: pinned CPU tensor}): the frame's outputs are copied by DMA straight into
+        those tensors instead of the slot's pinned buffers (no host copy; harness.render_viewpoints
+        hands in slices of its result stacks)."""
         slot = self._slots[self._count % self.n]
         self._count += 1
         prev = slot["handle"]
@@ -195,7 +213,10 @@ class FramePipeline:
             if self.readback:
                 host = slot["host"]
                 for k in self.readback:
-                    host[k].copy_(out.raw(k).reshape(host[k].shape), non_blocking=True)
+                    if dest is not None and k in dest:
+                        dest[k].copy_(out.raw(k).reshape(dest[k].shape), non_blocking=True)
+                    else:
+                        host[k].copy_(out.raw(k).reshape(host[k].shape), non_blocking=True)
                 if self.get_skeleton:
                     j = out.raw("joints")
                     if host["joints"] is None or host["joints"].shape != j.shape:
@@ -205,7 +226,7 @@ class FramePipeline:
                                                                                            device=self.dev),
                                     non_blocking=True)
             slot["done"].record(s)
-        h = FrameHandle(self, slot, out, t)
+        h = FrameHandle(self, slot, out, t, dest)
         slot["handle"] = h
         return h
 

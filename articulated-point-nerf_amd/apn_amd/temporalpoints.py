@@ -33,6 +33,7 @@ CELL_CAP = int(os.environ.get("APN_CELL_CAP", 1 << 20))
 AGRID_SIDE = os.environ.get("APN_AGRID_SIDE", "1") != "0"
 # exact early ray termination of the neighbour MLP (apn_point_mlp_ert; APN_ERT=0: every kept sample)
 ERT = os.environ.get("APN_ERT", "1") != "0"
+ERT_PASSES = 9   # apn_mlp_layout.h ERT_PASSES
 
 
 class NoPointsException(Exception):
@@ -344,7 +345,7 @@ class TemporalPoints(torch.nn.Module):
         # the neighbour MLP only on the kept samples the compositing reads (apn_point_mlp_ert: every
         # ray's samples up to its T < 1e-3 break, in passes); the frame is bit-identical either way
         self.early_termination = ERT
-        self.last_mlp_rows = None   # device int32 [6]: samples per early-termination pass of the last frame
+        self.last_mlp_rows = None   # device int32 [ERT_PASSES]: samples per early-termination pass of the last frame
 
     # view_poc / pos_poc alias the TiNeuVox buffers (temporalpoints.py:148-150); as properties
     # they follow .to(device) (the reference relies on a CUDA default tensor type instead).
@@ -1077,11 +1078,18 @@ class TemporalPoints(torch.nn.Module):
             self.timing.setdefault("marks", []).append(("mlp_setup", e0))
         if self.early_termination:
             ews = ws.bytes("ert_ws", lib.apn_point_mlp_ert_workspace_bytes(S, R), dev)
-            rows = ws.get("ert_rows", 8, torch.int32, dev)
-            self.last_mlp_rows = rows[:6]
+            rows = ws.get("ert_rows", ERT_PASSES, torch.int32, dev)
+            self.last_mlp_rows = rows[:ERT_PASSES]
+            pass_ev = evs = None
+            if self.timing is not None:   # HIP events around each pass's MLP launches (bench's roofline)
+                pass_ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * ERT_PASSES)]
+                for e in pass_ev:
+                    e.record()   # creates the event (the library records it again at its place)
+                evs = (C.c_void_p * (2 * ERT_PASSES))(*[e.cuda_event for e in pass_ev])
+                self.timing.setdefault("mlp_pass_events", []).append(pass_ev)
             call("apn_point_mlp_ert", ptr(s_pos), ptr(s_ray), ptr(s_nbr), S, ptr(nsurv), R, ptr(recA), ptr(recB),
                  ptr(feat), 128, ptr(vd), ptr(vemb), ptr(wbuf), self._eps, float(self.tineuvox.act_shift), interval,
-                 float(self.fast_color_thres), ptr(out12), ptr(ews), ptr(rows), s)
+                 float(self.fast_color_thres), ptr(out12), ptr(ews), ptr(rows), evs, s)
         else:
             self.last_mlp_rows = None
             call("apn_point_mlp", ptr(s_pos), ptr(s_ray), ptr(s_nbr), S, ptr(nsurv), ptr(recA), ptr(recB), ptr(feat),

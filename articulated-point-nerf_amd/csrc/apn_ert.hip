@@ -3,8 +3,8 @@
 // kept samples front to back and stops after the sample whose update takes T below 1e-3; the
 // Point-NeRF columns {rgb, alpha} of every later sample of that ray are never read. The reference
 // still runs feat_net / densitynet / rgbnet on them (temporalpoints.py:452-519). Here the MLP runs
-// in passes over each ray's kept samples in step order -- local indices [0, 4), [4, 8), [8, 12),
-// [12, 20), [20, 36), [36, ...) -- and after each pass a per-ray walk with the compositing's own
+// in passes over each ray's kept samples in step order -- two samples at a time up to local index
+// 12, then [12, 16), [16, 24), [24, ...) -- and after each pass a per-ray walk with the compositing's own
 // arithmetic (pre-mask alpha > thr, T in double, the same break test) retires the rays that
 // terminated; the next pass lists only the live rays' next samples. Every sample the compositing
 // reads has exactly the values a full MLP launch would give it (a sample's MLP rows do not depend
@@ -79,59 +79,73 @@ __global__ __launch_bounds__(256) void k_direct_blend(const float4* __restrict__
   }
 }
 
-// pass 0: every ray starts at its first kept sample with T = 1
-__global__ __launch_bounds__(256) void k_ert_begin(int64_t n_rays, const int* __restrict__ beg,
-                                                   const int* __restrict__ end, int* __restrict__ pos,
-                                                   float* __restrict__ T, int* __restrict__ cnt, int B) {
+// One launch per pass. Pass 0 starts every ray at its first kept sample with T = 1; every later
+// pass first walks ray r's samples of the previous pass with the compositing's arithmetic
+// (apn_composite.hip k_composite_lds, Point-NeRF path: pre-mask, T in double, the break test) and
+// retires the ray if its T fell below 1e-3. Then the ray's next min(B, left) samples go to the
+// pass's list: a block scan of the counts, one atomic per block for the block's place in the list
+// (the list's order between blocks varies from run to run; a sample's MLP result does not depend
+// on its tile-mates, so the frame does not), and the pass size accumulates in *count -- the MLP
+// launch's device count.
+__global__ __launch_bounds__(256) void k_ert_pass(int64_t n_rays, int first, const int* __restrict__ beg,
+                                                  const int* __restrict__ end, const float4* __restrict__ out,
+                                                  float thr, int use_mask, int* __restrict__ pos,
+                                                  float* __restrict__ T, int* __restrict__ cnt, int B,
+                                                  int* __restrict__ list, int* __restrict__ count) {
+  __shared__ int s_wave[4];
+  __shared__ int s_base;
   const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (r >= n_rays) return;
-  const int b = beg[r], e = end[r];
-  pos[r] = b;
-  T[r] = 1.f;
-  cnt[r] = min(e - b, B);
-}
-
-// the pass's sample list: ray r's cnt[r] next samples at offs[r]; the pass size (offs[n_rays]) is
-// also the MLP launch's device count (and goes to stats[pass] when asked)
-__global__ __launch_bounds__(256) void k_ert_fill(int64_t n_rays, const int* __restrict__ pos,
-                                                  const int* __restrict__ cnt, const int* __restrict__ offs,
-                                                  int* __restrict__ list, int* __restrict__ stat) {
-  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (r == 0 && stat) *stat = offs[n_rays];
-  if (r >= n_rays) return;
-  const int c = cnt[r];
-  if (c <= 0) return;
-  const int o = offs[r], p = pos[r];
-  for (int j = 0; j < c; ++j) list[o + j] = p + j;
-}
-
-// after a pass: walk ray r's samples of the pass with the compositing's arithmetic
-// (apn_composite.hip k_composite_lds, Point-NeRF path): a ray whose T fell below 1e-3 is retired,
-// the others get their next B samples (cnt = 0: retired or out of samples)
-__global__ __launch_bounds__(256) void k_ert_step(int64_t n_rays, const float4* __restrict__ out, float thr,
-                                                  int use_mask, int* __restrict__ pos, const int* __restrict__ end,
-                                                  float* __restrict__ T, int* __restrict__ cnt, int B) {
-  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (r >= n_rays) return;
-  const int c = cnt[r];
-  if (c <= 0) return;
-  int p = pos[r];
-  float t = T[r];
-  bool dead = false;
-  for (int i = p; i < p + c; ++i) {
-    const float a = out[3 * (size_t)i].w;
-    if (!use_mask || a > thr) {
-      t = (float)((double)t * (1.0 - (double)a));
-      if ((double)t < 1e-3) {
-        dead = true;
-        break;
+  int c = 0, p = 0;
+  if (r < n_rays) {
+    const int e = end[r];
+    if (first) {
+      p = beg[r];
+      T[r] = 1.f;
+      c = min(e - p, B);
+    } else {
+      const int cp = cnt[r];
+      p = pos[r];
+      if (cp > 0) {
+        float t = T[r];
+        bool dead = false;
+        for (int i = p; i < p + cp; ++i) {
+          const float a = out[3 * (size_t)i].w;
+          if (!use_mask || a > thr) {
+            t = (float)((double)t * (1.0 - (double)a));
+            if ((double)t < 1e-3) {
+              dead = true;
+              break;
+            }
+          }
+        }
+        p += cp;
+        T[r] = t;
+        c = dead ? 0 : min(e - p, B);
       }
     }
+    pos[r] = p;
+    cnt[r] = c;
   }
-  p += c;
-  pos[r] = p;
-  T[r] = t;
-  cnt[r] = dead ? 0 : min(end[r] - p, B);
+  // block-wide exclusive scan of c
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int inc = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += v;
+  }
+  if (lane == 63) s_wave[wid] = inc;
+  __syncthreads();
+  int wbase = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    wbase += w < wid ? s_wave[w] : 0;
+    tot += s_wave[w];
+  }
+  if (threadIdx.x == 0) s_base = tot > 0 ? atomicAdd(count, tot) : 0;
+  __syncthreads();
+  const int o = s_base + wbase + inc - c;
+  for (int j = 0; j < c; ++j) list[o + j] = p + j;
 }
 
 __global__ void k_ray_bounds_ert(const int* __restrict__ s_ray, const int* __restrict__ n_dev, int* __restrict__ beg,
@@ -147,8 +161,8 @@ __global__ void k_ray_bounds_ert(const int* __restrict__ s_ray, const int* __res
 int scan_exclusive_i32(const int* in, int* out, int64_t n, void* ws, hipStream_t s);
 size_t scan_workspace_bytes(int64_t n);
 
-// workspace: beg, end, pos, cnt [n_rays] i32, T [n_rays] f32, offs [n_rays + 1] i32, list
-// [max_samples] i32, the scan's workspace
+// workspace: beg, end, pos, cnt [n_rays] i32, T [n_rays] f32, the passes' list sizes
+// [ERT_PASSES] i32, list [max_samples] i32
 static size_t ert_ws_layout(int64_t max_samples, int64_t n_rays, size_t* off) {
   size_t o = 0;
   auto take = [&](size_t bytes) {
@@ -156,29 +170,29 @@ static size_t ert_ws_layout(int64_t max_samples, int64_t n_rays, size_t* off) {
     o += (bytes + 255) / 256 * 256;
     return at;
   };
-  off[0] = take(4 * (size_t)n_rays);            // beg
-  off[1] = take(4 * (size_t)n_rays);            // end
-  off[2] = take(4 * (size_t)n_rays);            // pos
-  off[3] = take(4 * (size_t)n_rays);            // cnt
-  off[4] = take(4 * (size_t)n_rays);            // T
-  off[5] = take(4 * ((size_t)n_rays + 1));      // offs
-  off[6] = take(4 * (size_t)max_samples);       // list
-  off[7] = take(scan_workspace_bytes(n_rays));  // scan
+  off[0] = take(4 * (size_t)n_rays);        // beg
+  off[1] = take(4 * (size_t)n_rays);        // end
+  off[2] = take(4 * (size_t)n_rays);        // pos
+  off[3] = take(4 * (size_t)n_rays);        // cnt
+  off[4] = take(4 * (size_t)n_rays);        // T
+  off[5] = take(4 * (size_t)ERT_PASSES);    // pass sizes
+  off[6] = take(4 * (size_t)max_samples);   // list
   return o;
 }
 
 size_t ert_workspace_bytes(int64_t max_samples, int64_t n_rays) {
-  size_t off[8];
+  size_t off[7];
   return ert_ws_layout(max_samples, n_rays, off);
 }
 
-// Per-ray local index ranges of the passes: [0,4), [4,8), [8,12), [12,20), [20,36), [36,...).
-static const int ERT_PASS[ERT_PASSES] = {4, 4, 4, 8, 16, 1 << 30};
+// Per-ray local index ranges of the passes: two samples at a time for the first twelve (a ray's
+// surplus over its break is at most one sample there), then 4, 8 and the rest.
+static const int ERT_PASS[ERT_PASSES] = {2, 2, 2, 2, 2, 2, 4, 8, 1 << 30};
 
 int ert_run(const float4* s_pos, const int* s_ray, const int* s_nbr, int64_t max_samples, const int* n_samples_dev,
             int64_t n_rays, const float4* recA, const float4* recB, float eps, float thr, float4* out, void* ws,
-            int* stats, hipStream_t s, const MlpPass& mlp) {
-  size_t off[8];
+            int* stats, void* const* events, hipStream_t s, const MlpPass& mlp) {
+  size_t off[7];
   ert_ws_layout(max_samples, n_rays, off);
   char* w = (char*)ws;
   int* beg = (int*)(w + off[0]);
@@ -186,27 +200,26 @@ int ert_run(const float4* s_pos, const int* s_ray, const int* s_nbr, int64_t max
   int* pos = (int*)(w + off[2]);
   int* cnt = (int*)(w + off[3]);
   float* T = (float*)(w + off[4]);
-  int* offs = (int*)(w + off[5]);
+  int* sizes = (int*)(w + off[5]);
   int* list = (int*)(w + off[6]);
-  void* sws = w + off[7];
   const int rb = ceil_div(n_rays, 256);
   const int use_mask = thr > 0.f ? 1 : 0;
   APN_TRY(fill_i32(beg, 0, n_rays, s));   // rays without kept samples: beg = end = 0
   APN_TRY(fill_i32(end, 0, n_rays, s));
+  APN_TRY(fill_i32(sizes, 0, ERT_PASSES, s));
   hipLaunchKernelGGL(k_ray_bounds_ert, dim3(ceil_div(max_samples, 256)), dim3(256), 0, s, s_ray, n_samples_dev, beg,
                      end);
   // direct path + weight colour of every kept sample (read up to the direct path's own break)
   hipLaunchKernelGGL(k_direct_blend, dim3(ceil_div(max_samples, 256) < 256 * 16 ? ceil_div(max_samples, 256) : 256 * 16),
                      dim3(256), 0, s, s_pos, s_nbr, n_samples_dev, recA, recB, eps, out);
-  hipLaunchKernelGGL(k_ert_begin, dim3(rb), dim3(256), 0, s, n_rays, beg, end, pos, T, cnt, ERT_PASS[0]);
   for (int p = 0; p < ERT_PASSES; ++p) {
-    if (p > 0)
-      hipLaunchKernelGGL(k_ert_step, dim3(rb), dim3(256), 0, s, n_rays, (const float4*)out, thr, use_mask, pos, end,
-                         T, cnt, ERT_PASS[p]);
-    APN_TRY(scan_exclusive_i32(cnt, offs, n_rays, sws, s));
-    hipLaunchKernelGGL(k_ert_fill, dim3(rb), dim3(256), 0, s, n_rays, pos, cnt, offs, list, stats ? stats + p : nullptr);
-    APN_TRY(mlp(list, offs + n_rays));
+    hipLaunchKernelGGL(k_ert_pass, dim3(rb), dim3(256), 0, s, n_rays, p == 0 ? 1 : 0, beg, end, (const float4*)out,
+                       thr, use_mask, pos, T, cnt, ERT_PASS[p], list, sizes + p);
+    if (events) APN_HIP_TRY(hipEventRecord((hipEvent_t)events[2 * p], s));
+    APN_TRY(mlp(list, sizes + p));
+    if (events) APN_HIP_TRY(hipEventRecord((hipEvent_t)events[2 * p + 1], s));
   }
+  if (stats) APN_TRY(copy_i32(sizes, stats, ERT_PASSES, s));
   return launch_status();
 }
 

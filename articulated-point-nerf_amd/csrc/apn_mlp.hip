@@ -607,7 +607,7 @@ extern "C" int apn_point_mlp_ert(const float* s_pos4, const int32_t* s_ray, cons
                                  const float* feat_proj, int32_t feat_dim, const float* viewdirs,
                                  const float* vemb_const, const float* wbuf, float eps, float act_shift,
                                  float interval, float fast_color_thres, float* out12, void* workspace,
-                                 int32_t* pass_rows, void* stream) {
+                                 int32_t* pass_rows, void* const* pass_events, void* stream) {
   if (feat_dim != FEAT || n_rays <= 0) return APN_ERR_ARG;
   if (max_samples <= 0) return APN_OK;
   if (!s_pos4 || !s_ray || !s_nbr || !n_samples_dev || !recA16 || !recB8 || !feat_proj || !wbuf || !out12 ||
@@ -618,7 +618,10 @@ extern "C" int apn_point_mlp_ert(const float* s_pos4, const int32_t* s_ray, cons
                          viewdirs, vemb_const, wbuf, eps, act_shift, interval, 0, out12, stream);
   hipStream_t s = (hipStream_t)stream;
   const int64_t ntiles = (max_samples + 15) / 16;
-  const int blocks = (int)(ntiles < 256 * 64 ? ntiles : 256 * 64);
+  // a pass's size is known on the device only: a grid of ERT_MLP_BLOCKS workgroups (grid-stride
+  // over the pass's tiles) instead of one per tile, so the passes that find few or no live rays
+  // cost a few microseconds, not the dispatch of 16k workgroups that exit at once
+  const int blocks = (int)(ntiles < ERT_MLP_BLOCKS ? ntiles : ERT_MLP_BLOCKS);
   MlpPass pass = [&](const int* list, const int* n_list) {
     launch_point_mlp_h4(blocks, false, s, (const float4*)s_pos4, s_ray, s_nbr, n_list, (const float4*)recA16,
                         (const float4*)recB8, (const float4*)feat_proj, viewdirs, vemb_const, wbuf, eps, act_shift,
@@ -626,7 +629,8 @@ extern "C" int apn_point_mlp_ert(const float* s_pos4, const int32_t* s_ray, cons
     return launch_status();
   };
   APN_TRY(ert_run((const float4*)s_pos4, s_ray, s_nbr, max_samples, n_samples_dev, n_rays, (const float4*)recA16,
-                  (const float4*)recB8, eps, fast_color_thres, (float4*)out12, workspace, pass_rows, s, pass));
+                  (const float4*)recB8, eps, fast_color_thres, (float4*)out12, workspace, pass_rows, pass_events, s,
+                  pass));
   // range fallback (apn_mlp_layout.h OFF_FLAG): if any pass flagged an out-of-fp16-range value, the
   // FP32 MFMA kernel redoes every kept sample (all 12 columns, a superset of the passes); otherwise
   // its workgroups exit at once

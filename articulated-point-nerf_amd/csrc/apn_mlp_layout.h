@@ -102,12 +102,16 @@ void launch_point_mlp_h4(int blocks, bool timed, hipStream_t stream, const float
                          float interval, float4* out, const int* list = nullptr);
 // Early ray termination (apn_ert.hip): the MLP in ERT_PASSES passes over the live rays' next
 // kept samples; ``MlpPass(list, n_list_dev)`` launches the MLP on one pass's sample list.
-constexpr int ERT_PASSES = 6;
+constexpr int ERT_PASSES = 9;
+#ifndef APN_ERT_MLP_BLOCKS
+#define APN_ERT_MLP_BLOCKS 2048
+#endif
+constexpr int ERT_MLP_BLOCKS = APN_ERT_MLP_BLOCKS;   // workgroups per pass launch (8 per CU)
 typedef std::function<int(const int*, const int*)> MlpPass;
 size_t ert_workspace_bytes(int64_t max_samples, int64_t n_rays);
 int ert_run(const float4* s_pos, const int* s_ray, const int* s_nbr, int64_t max_samples, const int* n_samples_dev,
             int64_t n_rays, const float4* recA, const float4* recB, float eps, float thr, float4* out, void* ws,
-            int* stats, hipStream_t s, const MlpPass& mlp);
+            int* stats, void* const* events, hipStream_t s, const MlpPass& mlp);
 // Largest magnitude the fp16-split kernel carries through its hi/lo halves (fp16 max finite).
 constexpr float H3_RANGE = 65504.f;
 // Adds (and resets) the phase-timed fp16-split kernel's cycle sums into out6.

@@ -153,6 +153,16 @@ def mlp_pass_rows(ev, kept):
     return [int(v) for v in rows.tolist()] if rows is not None else [int(kept)]
 
 
+def mlp_pass_ms(timing):
+    """Per-pass MLP kernel ms (mean over the timed eager frames) from the HIP events apn_point_mlp_ert
+    records around each early-termination pass's MLP launches; None without early termination."""
+    fr = timing.get("mlp_pass_events")
+    if not fr:
+        return None
+    n = len(fr[0]) // 2
+    return [sum(f[2 * p].elapsed_time(f[2 * p + 1]) for f in fr) / len(fr) for p in range(n)]
+
+
 def mfma_executed_flop(n_samples, variant=0):
     """MFMA flops the MLP kernel issues per launch, 4 waves per tile.
     variant 1 (FP32 MFMA, 8-sample tiles): 16x16x4 f32 MFMAs for layer 1 (K=64), layers 2-4 (K=128)
@@ -457,13 +467,30 @@ def viewpoint_rate(model, scene, dev, n_views=16, in_flight=3):
     Ks = scene.K[None].repeat(n_views, 1, 1)
     times = [scene.cfg.t + 0.01 * i for i in range(n_views)]
     kw = dict(test_times=times, verbose=False, inverse_y=bool(rk.get("inverse_y", False)), in_flight=in_flight)
-    harness.render_viewpoints(model, poses, HW, Ks, False, dict(rk), **kw)   # captures the pipeline
+    for _ in range(2):   # the first call captures the pipeline, the second warms the pinned stacks
+        harness.render_viewpoints(model, poses, HW, Ks, False, dict(rk), **kw)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     harness.render_viewpoints(model, poses, HW, Ks, False, dict(rk), **kw)
     el = time.perf_counter() - t0
+    # the same pipeline's bare submit loop, every frame's rgb / depth / weights read back into the
+    # slots' pinned buffers and nothing else: the PCIe readback's own cost (ROCm runs these
+    # device-to-host copies as blit kernels on the CUs), without the harness
+    pipe = next(iter(model._pipelines.values()))[1]
+    t_arg = torch.tensor([scene.cfg.t], device=dev)
+    for _ in range(2):
+        pipe.submit(t_arg)
+    pipe.join()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    for _ in range(n_views):
+        pipe.submit(t_arg)
+    pipe.join()
+    torch.cuda.synchronize(dev)
+    bare = (time.perf_counter() - t1) / n_views * 1e3
     return {"views": n_views, "distinct_times": n_views, "frames_in_flight": in_flight,
             "ms_per_frame": el / n_views * 1e3, "rays_per_s": n_views * H * W / el,
+            "pipeline_readback_ms_per_frame": bare,
             "note": "harness.render_viewpoints over views at distinct times, one model (apn_amd.pipeline."
                     "FramePipeline: per-frame workspaces, shared canonical tables / projection), per view: rays "
                     "on the device, frame submitted, rgb / depth / weights read back to host numpy; second call "
@@ -494,6 +521,9 @@ def frame_rate(config, dev, steps=10, warmup=2, in_flight=3):
     mlp_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / max(len(ev), 1)
     kept = int(ev[-1][2].item()) if ev else stats.get("kept_samples", 0)
     rows = mlp_pass_rows(ev, kept)
+    pms = mlp_pass_ms(timing)
+    if pms is not None:
+        mlp_ms = sum(pms)
     from apn_amd.pipeline import FramePipeline
     pipe = FramePipeline(model, t_arg, rk, n=in_flight, poses=poses, Ks=Ks, get_skeleton=True, readback=None)
     replay_pipeline(pipe, t_arg, 2)
@@ -845,6 +875,10 @@ def main():
     S_kept = int(ev[-1][2].item()) if ev else stats.get("kept_samples", 0)
     pass_rows = mlp_pass_rows(ev, S_kept)
     S_mlp = sum(pass_rows)   # the samples the MLP ran on (early ray termination: those the compositing reads)
+    mlp_stage_ms = mlp_ms
+    pass_ms = mlp_pass_ms(timing)
+    if pass_ms is not None:   # the MLP kernel launches alone (HIP events around each pass's launches)
+        mlp_ms = sum(pass_ms)
     kept_total = S_kept * (world if not shard_rays else 1)
     shard_diag = None
     if shard_rays:
@@ -1003,10 +1037,14 @@ def main():
                                         f"{traffic.get('avg_ms', float('nan')):.2f} ms then); NOT measured in this run"
                                         if traffic else None),
                      "flop_per_launch": flop, "avg_launch_ms": mlp_ms,
+                     "per_pass": ({"rows": pass_rows, "ms": [round(v, 4) for v in pass_ms]} if pass_ms else None),
+                     "mlp_stage_ms": mlp_stage_ms,
                      "note": "achieved = reference F_alg (SURVEY.md 8(d), fp32 flops) per sample x the samples the "
-                             "MLP ran on (mlp_samples: with early ray termination the kept samples the compositing "
-                             "reads, in passes) / the MLP stage's time (HIP events on the launch stream around all "
-                             "its launches: the direct-blend kernel, the passes' list kernels and MLP launches); "
+                             "MLP kernel ran on in the frame (mlp_samples: with early ray termination the kept "
+                             "samples the compositing reads, over the passes' launches) / those launches' summed "
+                             "time (avg_launch_ms: HIP events recorded by apn_point_mlp_ert on the launch stream "
+                             "around each pass's launches, mean over the timed eager frames; per_pass lists both); "
+                             "mlp_stage_ms = the whole stage (direct-blend kernel, pass-list kernels, launches); "
                              + peak_note + "; the kernel issues fewer MFMA flops than F_alg (per-point layer-1 "
                              "projection, folded rgb head): executed_tflops / mfma_util",
                      "executed_tflops": executed,

@@ -320,21 +320,22 @@ int apn_point_mlp(const float* s_pos4, const int32_t* s_ray, const int32_t* s_nb
 /* apn_point_mlp with exact early ray termination (the render path's default; replaces the same
  * stage, temporalpoints.py:452-519, followed by the compositing's break at T < 1e-3,
  * render_utils_kernel.cu:445-451, as apn_composite applies it). The {rgb, alpha} columns are
- * computed only for the kept samples the compositing reads: the MLP runs in passes over each
- * ray's kept samples in step order (local indices [0,4) [4,8) [8,12) [12,20) [20,36) [36,..)),
+ * computed only for the kept samples the compositing reads: the MLP runs in 9 passes over each
+ * ray's kept samples in step order (two at a time up to local index 12, then [12,16) [16,24) [24,..)),
  * and after each pass a per-ray walk with apn_composite's arithmetic (fast_color_thres pre-mask,
  * T in double) retires the rays that terminated. The direct-path and weight-colour columns are
  * computed for every kept sample. apn_composite on the result gives exactly apn_point_mlp's frame.
  * Survivors must be sorted by ray (apn_knn_radius's order); n_rays bounds their ray ids.
  * workspace: apn_point_mlp_ert_workspace_bytes(max_samples, n_rays). pass_rows (optional, device
- * int32 [6]): the samples each pass ran the MLP on. */
+ * int32 [9]): the samples each pass ran the MLP on. pass_events (optional, eager calls only):
+ * 18 hipEvent_t recorded on `stream` right before / after each pass's MLP launches. */
 size_t apn_point_mlp_ert_workspace_bytes(int64_t max_samples, int64_t n_rays);
 int apn_point_mlp_ert(const float* s_pos4, const int32_t* s_ray, const int32_t* s_nbr,
                       int64_t max_samples, const int32_t* n_samples_dev, int64_t n_rays,
                       const float* recA16, const float* recB8, const float* feat_proj, int32_t feat_dim,
                       const float* viewdirs, const float* vemb_const, const float* wbuf, float eps,
                       float act_shift, float interval, float fast_color_thres, float* out12,
-                      void* workspace, int32_t* pass_rows, void* stream);
+                      void* workspace, int32_t* pass_rows, void* const* pass_events, void* stream);
 
 /* Select the apn_point_mlp kernel (process-wide, default 0): 0 = 3-term fp16-split MFMA with the
  * FP32 range fallback, 1 = FP32 MFMA alone. (The debug build, include/apn_hip_debug.h, also takes

@@ -34,6 +34,18 @@ def test_draw_skeleton_lines_and_discs():
     assert (far[2] == 0).all() and (far[0] == 1).all()
 
 
+def test_draw_line_closed_form_equals_walk():
+    """The vectorised line rasteriser draws exactly the pixels of the error-term walk, every octant,
+    degenerate and clipped lines included."""
+    rng = np.random.default_rng(7)
+    for _ in range(3000):
+        x0, y0, x1, y1 = (int(v) for v in rng.integers(-15, 45, 4))
+        a, b = np.ones((30, 30)), np.ones((30, 30))
+        Hn._draw_line(a, (x0, y0), (x1, y1), 0.0)
+        Hn._draw_line_walk(b, (x0, y0), (x1, y1), 0.0)
+        assert np.array_equal(a, b), (x0, y0, x1, y1)
+
+
 def test_rgb_ssim():
     rng = np.random.default_rng(1)
     a = rng.uniform(0, 1, (32, 40, 3))
