@@ -55,7 +55,9 @@ SIGNATURES = {
     "apn_feat_project": (C.c_int, [P, I64, I32, P, P, P]),
     "apn_point_mlp": (C.c_int, [P, P, P, I64, P, P, P, P, I32, P, P, P, F32, F32, F32, I32, P, P]),
     "apn_point_mlp_ert_workspace_bytes": (SZ, [I64, I64]),
-    "apn_point_mlp_ert": (C.c_int, [P, P, P, I64, P, I64, P, P, P, I32, P, P, P, F32, F32, F32, F32, P, P, P, P, P]),
+    "apn_point_mlp_ert": (C.c_int, [P, P, P, I64, P, I64, P, P, P, I32, P, P, P, F32, F32, F32, F32, I32, P, P, P, P,
+                                    P]),
+    "apn_direct_blend": (C.c_int, [P, P, I64, P, P, P, F32, P, P]),
     "apn_composite": (C.c_int, [P, P, P, I64, P, I64, F32, F32, P, P, P, P, P, P, P, P]),
     "apn_set_mlp_variant": (C.c_int, [I32]),
     "apn_adam_upd": (C.c_int, [P, P, P, P, I64, I32, F32, F32, F32, F32, P]),

@@ -1087,9 +1087,12 @@ class TemporalPoints(torch.nn.Module):
                     e.record()   # creates the event (the library records it again at its place)
                 evs = (C.c_void_p * (2 * ERT_PASSES))(*[e.cuda_event for e in pass_ev])
                 self.timing.setdefault("mlp_pass_events", []).append(pass_ev)
+            # the direct-blend kernel runs inside, on this stream: on the grid's side stream beside the
+            # passes (apn_direct_blend + with_direct = 0) the captured frames in flight stopped
+            # overlapping (C2, 3 in flight: 6.58-6.60 vs 5.91-5.95 ms/frame, tools/ab_direct_side.sh)
             call("apn_point_mlp_ert", ptr(s_pos), ptr(s_ray), ptr(s_nbr), S, ptr(nsurv), R, ptr(recA), ptr(recB),
                  ptr(feat), 128, ptr(vd), ptr(vemb), ptr(wbuf), self._eps, float(self.tineuvox.act_shift), interval,
-                 float(self.fast_color_thres), ptr(out12), ptr(ews), ptr(rows), evs, s)
+                 float(self.fast_color_thres), 1, ptr(out12), ptr(ews), ptr(rows), evs, s)
         else:
             self.last_mlp_rows = None
             call("apn_point_mlp", ptr(s_pos), ptr(s_ray), ptr(s_nbr), S, ptr(nsurv), ptr(recA), ptr(recB), ptr(feat),

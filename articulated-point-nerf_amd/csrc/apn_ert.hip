@@ -158,8 +158,12 @@ __global__ void k_ray_bounds_ert(const int* __restrict__ s_ray, const int* __res
   if (i == n - 1 || s_ray[i + 1] != r) end[r] = i + 1;
 }
 
-int scan_exclusive_i32(const int* in, int* out, int64_t n, void* ws, hipStream_t s);
-size_t scan_workspace_bytes(int64_t n);
+int direct_blend(const float4* s_pos, const int* s_nbr, int64_t max_samples, const int* n_samples_dev,
+                 const float4* recA, const float4* recB, float eps, float4* out, hipStream_t s) {
+  const int blocks = ceil_div(max_samples, 256) < 256 * 16 ? ceil_div(max_samples, 256) : 256 * 16;
+  hipLaunchKernelGGL(k_direct_blend, dim3(blocks), dim3(256), 0, s, s_pos, s_nbr, n_samples_dev, recA, recB, eps, out);
+  return launch_status();
+}
 
 // workspace: beg, end, pos, cnt [n_rays] i32, T [n_rays] f32, the passes' list sizes
 // [ERT_PASSES] i32, list [max_samples] i32
@@ -191,7 +195,7 @@ static const int ERT_PASS[ERT_PASSES] = {2, 2, 2, 2, 2, 2, 4, 8, 1 << 30};
 
 int ert_run(const float4* s_pos, const int* s_ray, const int* s_nbr, int64_t max_samples, const int* n_samples_dev,
             int64_t n_rays, const float4* recA, const float4* recB, float eps, float thr, float4* out, void* ws,
-            int* stats, void* const* events, hipStream_t s, const MlpPass& mlp) {
+            int with_direct, int* stats, void* const* events, hipStream_t s, const MlpPass& mlp) {
   size_t off[7];
   ert_ws_layout(max_samples, n_rays, off);
   char* w = (char*)ws;
@@ -209,9 +213,9 @@ int ert_run(const float4* s_pos, const int* s_ray, const int* s_nbr, int64_t max
   APN_TRY(fill_i32(sizes, 0, ERT_PASSES, s));
   hipLaunchKernelGGL(k_ray_bounds_ert, dim3(ceil_div(max_samples, 256)), dim3(256), 0, s, s_ray, n_samples_dev, beg,
                      end);
-  // direct path + weight colour of every kept sample (read up to the direct path's own break)
-  hipLaunchKernelGGL(k_direct_blend, dim3(ceil_div(max_samples, 256) < 256 * 16 ? ceil_div(max_samples, 256) : 256 * 16),
-                     dim3(256), 0, s, s_pos, s_nbr, n_samples_dev, recA, recB, eps, out);
+  // direct path + weight colour of every kept sample (read up to the direct path's own break);
+  // with_direct = 0: the caller runs apn_direct_blend itself (e.g. on a second stream beside the passes)
+  if (with_direct) APN_TRY(direct_blend(s_pos, s_nbr, max_samples, n_samples_dev, recA, recB, eps, out, s));
   for (int p = 0; p < ERT_PASSES; ++p) {
     hipLaunchKernelGGL(k_ert_pass, dim3(rb), dim3(256), 0, s, n_rays, p == 0 ? 1 : 0, beg, end, (const float4*)out,
                        thr, use_mask, pos, T, cnt, ERT_PASS[p], list, sizes + p);

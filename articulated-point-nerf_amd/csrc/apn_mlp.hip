@@ -594,6 +594,18 @@ extern "C" int apn_point_mlp(const float* s_pos4, const int32_t* s_ray, const in
   return launch_status();
 }
 
+// The direct-path and weight-colour columns (4..11) of out12 for every kept sample
+// (temporalpoints.py:459-470, 517-519), the fused MLP kernel's arithmetic; apn_point_mlp_ert
+// runs it itself unless with_direct = 0.
+extern "C" int apn_direct_blend(const float* s_pos4, const int32_t* s_nbr, int64_t max_samples,
+                                const int32_t* n_samples_dev, const float* recA16, const float* recB8, float eps,
+                                float* out12, void* stream) {
+  if (max_samples <= 0) return APN_OK;
+  if (!s_pos4 || !s_nbr || !n_samples_dev || !recA16 || !recB8 || !out12) return APN_ERR_ARG;
+  return direct_blend((const float4*)s_pos4, s_nbr, max_samples, n_samples_dev, (const float4*)recA16,
+                      (const float4*)recB8, eps, (float4*)out12, (hipStream_t)stream);
+}
+
 extern "C" size_t apn_point_mlp_ert_workspace_bytes(int64_t max_samples, int64_t n_rays) {
   return ert_workspace_bytes(max_samples > 0 ? max_samples : 1, n_rays > 0 ? n_rays : 1);
 }
@@ -606,8 +618,8 @@ extern "C" int apn_point_mlp_ert(const float* s_pos4, const int32_t* s_ray, cons
                                  const int32_t* n_samples_dev, int64_t n_rays, const float* recA16, const float* recB8,
                                  const float* feat_proj, int32_t feat_dim, const float* viewdirs,
                                  const float* vemb_const, const float* wbuf, float eps, float act_shift,
-                                 float interval, float fast_color_thres, float* out12, void* workspace,
-                                 int32_t* pass_rows, void* const* pass_events, void* stream) {
+                                 float interval, float fast_color_thres, int32_t with_direct, float* out12,
+                                 void* workspace, int32_t* pass_rows, void* const* pass_events, void* stream) {
   if (feat_dim != FEAT || n_rays <= 0) return APN_ERR_ARG;
   if (max_samples <= 0) return APN_OK;
   if (!s_pos4 || !s_ray || !s_nbr || !n_samples_dev || !recA16 || !recB8 || !feat_proj || !wbuf || !out12 ||
@@ -629,8 +641,8 @@ extern "C" int apn_point_mlp_ert(const float* s_pos4, const int32_t* s_ray, cons
     return launch_status();
   };
   APN_TRY(ert_run((const float4*)s_pos4, s_ray, s_nbr, max_samples, n_samples_dev, n_rays, (const float4*)recA16,
-                  (const float4*)recB8, eps, fast_color_thres, (float4*)out12, workspace, pass_rows, pass_events, s,
-                  pass));
+                  (const float4*)recB8, eps, fast_color_thres, (float4*)out12, workspace, with_direct, pass_rows,
+                  pass_events, s, pass));
   // range fallback (apn_mlp_layout.h OFF_FLAG): if any pass flagged an out-of-fp16-range value, the
   // FP32 MFMA kernel redoes every kept sample (all 12 columns, a superset of the passes); otherwise
   // its workgroups exit at once

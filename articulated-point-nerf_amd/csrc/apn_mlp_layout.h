@@ -111,7 +111,9 @@ typedef std::function<int(const int*, const int*)> MlpPass;
 size_t ert_workspace_bytes(int64_t max_samples, int64_t n_rays);
 int ert_run(const float4* s_pos, const int* s_ray, const int* s_nbr, int64_t max_samples, const int* n_samples_dev,
             int64_t n_rays, const float4* recA, const float4* recB, float eps, float thr, float4* out, void* ws,
-            int* stats, void* const* events, hipStream_t s, const MlpPass& mlp);
+            int with_direct, int* stats, void* const* events, hipStream_t s, const MlpPass& mlp);
+int direct_blend(const float4* s_pos, const int* s_nbr, int64_t max_samples, const int* n_samples_dev,
+                 const float4* recA, const float4* recB, float eps, float4* out, hipStream_t s);
 // Largest magnitude the fp16-split kernel carries through its hi/lo halves (fp16 max finite).
 constexpr float H3_RANGE = 65504.f;
 // Adds (and resets) the phase-timed fp16-split kernel's cycle sums into out6.

@@ -666,7 +666,7 @@ def main():
                     help="N>1: 'rays' (default) = the ranks split one frame's rays and all-gather the tiles "
                          "over RCCL (strong scaling, SURVEY.md 8(e)); 'frames' = every rank renders its own "
                          "frame (weak scaling, no data-path collective)")
-    ap.add_argument("--in-flight", type=int, choices=[1, 2, 3], default=3,
+    ap.add_argument("--in-flight", type=int, choices=[1, 2, 3, 4], default=3,
                     help="frames in flight: one model's frame captured into n workspaces, frame i on stream i %% n "
                          "(ray shards: the all-gathers in frame order on one collective stream); 1 = one "
                          "after another")

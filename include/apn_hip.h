@@ -324,7 +324,8 @@ int apn_point_mlp(const float* s_pos4, const int32_t* s_ray, const int32_t* s_nb
  * ray's kept samples in step order (two at a time up to local index 12, then [12,16) [16,24) [24,..)),
  * and after each pass a per-ray walk with apn_composite's arithmetic (fast_color_thres pre-mask,
  * T in double) retires the rays that terminated. The direct-path and weight-colour columns are
- * computed for every kept sample. apn_composite on the result gives exactly apn_point_mlp's frame.
+ * computed for every kept sample (with_direct = 1; 0: by the caller's apn_direct_blend). apn_composite
+ * on the result gives exactly apn_point_mlp's frame.
  * Survivors must be sorted by ray (apn_knn_radius's order); n_rays bounds their ray ids.
  * workspace: apn_point_mlp_ert_workspace_bytes(max_samples, n_rays). pass_rows (optional, device
  * int32 [9]): the samples each pass ran the MLP on. pass_events (optional, eager calls only):
@@ -334,8 +335,16 @@ int apn_point_mlp_ert(const float* s_pos4, const int32_t* s_ray, const int32_t* 
                       int64_t max_samples, const int32_t* n_samples_dev, int64_t n_rays,
                       const float* recA16, const float* recB8, const float* feat_proj, int32_t feat_dim,
                       const float* viewdirs, const float* vemb_const, const float* wbuf, float eps,
-                      float act_shift, float interval, float fast_color_thres, float* out12,
-                      void* workspace, int32_t* pass_rows, void* const* pass_events, void* stream);
+                      float act_shift, float interval, float fast_color_thres, int32_t with_direct,
+                      float* out12, void* workspace, int32_t* pass_rows, void* const* pass_events,
+                      void* stream);
+/* The direct-path / weight-colour columns 4..11 of out12 (temporalpoints.py:459-470, 517-519) for
+ * every kept sample, with the fused MLP kernel's arithmetic: what apn_point_mlp_ert computes first
+ * when with_direct = 1; with 0 the caller runs this instead (TemporalPoints: on a second stream,
+ * beside the MLP passes; both must finish before apn_composite). */
+int apn_direct_blend(const float* s_pos4, const int32_t* s_nbr, int64_t max_samples,
+                     const int32_t* n_samples_dev, const float* recA16, const float* recB8, float eps,
+                     float* out12, void* stream);
 
 /* Select the apn_point_mlp kernel (process-wide, default 0): 0 = 3-term fp16-split MFMA with the
  * FP32 range fallback, 1 = FP32 MFMA alone. (The debug build, include/apn_hip_debug.h, also takes
