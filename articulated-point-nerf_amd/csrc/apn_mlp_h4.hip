@@ -611,8 +611,10 @@ void launch_point_mlp_h4(int blocks, bool timed, hipStream_t stream, const float
   };
   const int nb_scaled = blocks < 256 * 8 ? blocks : 256 * 8;
   if (list) {
+    // early-ray-termination passes (9 per frame): the scaled instantiation, which exits at once
+    // unless the weights needed scales, on 256 workgroups (an empty launch: ~3 us, not ~5)
     go(t128::k_point_mlp_h4<false, false, true>, blocks);
-    go(t128::k_point_mlp_h4<true, false, true>, nb_scaled);
+    go(t128::k_point_mlp_h4<true, false, true>, blocks < 256 ? blocks : 256);
     return;
   }
 #ifdef APN_DEBUG_BUILD

@@ -114,3 +114,24 @@ def test_ert_full_c2_frame_bit_identical(dev):
     print(f"C2: kept {kept}, read by the compositing {need} ({need / kept:.3f}), MLP rows {rows} "
           f"({rows / kept:.3f}) per pass {per}")
     assert rows < kept
+
+
+def test_direct_blend_entry_equals_inside(dev):
+    """apn_direct_blend (the C-ABI form a caller runs itself with with_direct = 0) writes exactly the
+    columns 4..11 apn_point_mlp_ert writes inside (and leaves the MLP's columns 0..3 alone)."""
+    from apn_amd import harness, synthetic as S
+    from apn_amd._lib import call, ptr, stream_ptr
+    scene = S.make_scene("G4")
+    model = harness.build_model(scene, dev)
+    rk = scene.render_kwargs(dev)
+    t = torch.tensor([scene.cfg.t], device=dev)
+    _, f12, _, _ = _frame(model, t, rk, True)
+    ws = model._ws.bufs
+    ns = f12.shape[0]
+    nsurv = torch.tensor([ns], dtype=torch.int32, device=dev)
+    out = torch.full((ns, 12), -7.0, device=dev)
+    call("apn_direct_blend", ptr(ws["s_pos"]), ptr(ws["s_nbr"]), ns, ptr(nsurv), ptr(ws["recA"]), ptr(ws["recB"]),
+         model._eps, ptr(out), stream_ptr(dev))
+    torch.cuda.synchronize()
+    assert torch.equal(out[:, 4:], f12[:, 4:])
+    assert (out[:, :4] == -7.0).all()

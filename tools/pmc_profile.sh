@@ -4,7 +4,7 @@
 # Each counter group runs in its own pass (FETCH_SIZE and WRITE_SIZE cannot share a pass).
 set -o pipefail
 OUT=${1:-gpurun_out/pmc}; shift
-ARGS=${@:-"--steps 2 --warmup 1 --no-cpu-baseline --no-other-configs"}
+ARGS=${@:-"--steps 2 --warmup 1 --in-flight 1 --no-cpu-baseline --no-other-configs --no-viewpoints --no-full-mlp-leg"}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p "$OUT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/trace_bench.json" 2> "$OUT/trace_bench.err" || exit $?
