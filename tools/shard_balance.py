@@ -31,8 +31,9 @@ def main():
     ap.add_argument("--split", default="inbbox,cost")
     ap.add_argument("--kept-weights", default="", help="comma list of shard.KEPT_WEIGHT values to try (cost split)")
     ap.add_argument("--in-flight", type=int, default=1,
-                    help="gilv splits: replay each shard's frames with this many in flight (models' graphs on "
-                         "as many streams, bench.py --in-flight; no all-gather)")
+                    help="gilv splits: replay each shard's frames with this many in flight (the shard's graph "
+                         "captured into as many workspaces of one model, on as many streams, bench.py --in-flight; "
+                         "no all-gather)")
     args = ap.parse_args()
     torch.set_grad_enabled(False)
     dev = torch.device("cuda", 0)
@@ -67,7 +68,8 @@ def main():
                 stages[name] = stages.get(name, 0.0) + a.elapsed_time(b)
         return ms, out
 
-    extra = [harness.build_model(scene, dev) for _ in range(args.in_flight - 1)]
+    from apn_amd.ops import Workspace
+    extra = [Workspace() for _ in range(args.in_flight - 1)]   # frames in flight: per-frame workspaces of one model
     fl_streams = [torch.cuda.Stream(dev) for _ in range(args.in_flight)]
 
     def in_flight(gsteps):
@@ -102,7 +104,8 @@ def main():
                     gstep = model.capture_frame(t, rk, ray_shard=(k, world, B), **fk)
                     fn = lambda: gstep(t)   # noqa: E731
                     if extra:   # frames in flight: timed per frame (4 rounds of len(gsteps) frames per call)
-                        gsteps = [gstep] + [m.capture_frame(t, rk, ray_shard=(k, world, B), **fk) for m in extra]
+                        gsteps = [gstep] + [model.capture_frame(t, rk, ray_shard=(k, world, B), workspace=w, **fk)
+                                            for w in extra]
                         fl_ms, _ = timed(lambda: in_flight(gsteps), args.reps)
                         print(f"   shard {k}: {args.in_flight} in flight {fl_ms / (4 * len(gsteps)):.3f} ms/frame")
                 else:
