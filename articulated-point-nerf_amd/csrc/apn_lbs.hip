@@ -12,6 +12,7 @@
 //   recB[n] = {clip(rgb,0,1), 0, pcol, 0}                                     (32 B)
 // HBM-bound: per point it reads 12 + 4J + 4 + 12 + 4 bytes and writes 12 + 4J + 96 bytes.
 #include "apn_common.h"
+#include "apn_mlp_split.h"   // split4 (the hi/lo fp16 split of the 3-term MFMA)
 
 #include <algorithm>
 
@@ -388,6 +389,142 @@ void k_lbs_skin_quad(
   if (bbox_part) lbs_bbox_partial(bmin, bmax, bbox_part);
 }
 
+// MFMA variant of the record-free softmax blend (repose / LBS-only sweeps: x' only, no weights,
+// G, colours, records or bbox written). A wave skins 16 points per step: lane (n, g) = (lane & 15,
+// lane >> 4) holds joints g*JL .. g*JL + JL - 1 of point n -- the quad kernel's per-lane 48-B
+// segment of the row, so the loads are the same -- and the blend G^T[12 x 16 points] =
+// T^T[12 x J] W^T[J x 16] is one 16x16 product on v_mfma_f32_16x16x32_f16 with the 3-term fp16
+// split (hi*hi + hi*lo + lo*hi, fp32 accumulate; apn_mlp_h3.hip), K = the lane's joints in one or
+// two 8-wide chunks. In the product's B layout lane (n, g) holds exactly its own weights and in the
+// A layout lane (m, g) bone element m of the same joints (registers, once per launch), so no
+// operand moves between lanes; the result lane (n, g) holds row g of point n's G, i.e. x'[g]
+// directly. Against the quad kernel this removes the 12 FMA per joint of the VALU blend and the
+// bone-row LDS reads (36 ds_read_b128 per 16 points); the softmax stays on the VALU (max and sum
+// across the point's four lanes by permlane swaps, grouped (g0 + g1) + (g2 + g3) as the quad's
+// DPP sums), its normalisation applied to the 12 blended values instead of the J weights. The
+// exponentials are split as e 2^12 (exact; e <= 1) so that no weight above 2^-36 meets an fp16
+// subnormal. Bar: fp32 reassociation (~2^-22 relative per product, tests/test_hip_parity.py).
+typedef _Float16 lbs_h8 __attribute__((ext_vector_type(8)));
+typedef float lbs_f4 __attribute__((ext_vector_type(4)));
+#ifndef MFMA_WAVES_PER_EU
+#define MFMA_WAVES_PER_EU 5
+#endif
+#ifndef LBS_MFMA_PF
+#define LBS_MFMA_PF 1   // 16-point groups in flight ahead of the one being skinned, per wave
+#endif
+
+__device__ __forceinline__ float xor16_max(float v) {
+  const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(s[0]), __uint_as_float(s[1]));
+}
+__device__ __forceinline__ float xor32_max(float v) {
+  const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(s[0]), __uint_as_float(s[1]));
+}
+// s[0] + s[1] is (lower row + upper row) on both lanes of the pair: all four lanes of a point end
+// with the same bits
+__device__ __forceinline__ float xor16_sum(float v) {
+  const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(s[0]) + __uint_as_float(s[1]);
+}
+__device__ __forceinline__ float xor32_sum(float v) {
+  const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(s[0]) + __uint_as_float(s[1]);
+}
+
+template <int JL>
+__global__ __launch_bounds__(LBS_THREADS) __attribute__((amdgpu_waves_per_eu(MFMA_WAVES_PER_EU)))
+void k_lbs_skin_mfma(const float* __restrict__ pcd, const float* __restrict__ W, int64_t N,
+                     const float* __restrict__ theta_weight, float eps, const float* __restrict__ boneT12,
+                     const float* __restrict__ global_t, float* __restrict__ xyz_out) {
+  constexpr int J = 4 * JL, NC = (JL + 7) / 8;
+  const int lane = threadIdx.x & 63, n16 = lane & 15, g = lane >> 4;
+  // A fragments: lane (m, g) holds T[g*JL + 8c + i][m] (rows m >= 12 and joints past JL are 0)
+  lbs_h8 ahi[NC], alo[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int jj = 8 * c + i;
+      const float v = (jj < JL && n16 < 12) ? boneT12[(g * JL + jj) * 12 + n16] : 0.f;
+      const _Float16 h = (_Float16)v;
+      ahi[c][i] = h;
+      alo[c][i] = (_Float16)(v - (float)h);
+    }
+  }
+  const float th = fmaxf(eps, theta_weight[0]);
+  const float rth = 1.f / th;
+  const float gt = global_t[g < 3 ? g : 0];
+  const int64_t groups = (N + 15) / 16;
+  const int64_t step = (int64_t)gridDim.x * (LBS_THREADS / 64);
+  int64_t gi = (int64_t)blockIdx.x * (LBS_THREADS / 64) + (threadIdx.x >> 6);
+  auto fetch = [&](int64_t gg, float (&row)[JL], float (&pc)[3]) {
+    const int64_t p = min(gg * 16 + n16, N - 1);
+    quad_load_row<JL>(W + p * J + g * JL, row);
+    pc[0] = pcd[3 * p]; pc[1] = pcd[3 * p + 1]; pc[2] = pcd[3 * p + 2];
+  };
+  auto skin = [&](int64_t gg, const float (&w)[JL], const float (&pc)[3]) {
+    const int64_t p = gg * 16 + n16;
+    float row[JL];
+    // softmax(W / th) (temporalpoints.py:403): the quotient as in k_lbs_skin_quad
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < JL; ++j) {
+      const float q = w[j] * rth;
+      row[j] = fmaf(fmaf(-q, th, w[j]), rth, q);
+      m = fmaxf(m, row[j]);
+    }
+    m = xor32_max(xor16_max(m));
+    float sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < JL; ++j) {
+      row[j] = __builtin_amdgcn_exp2f((row[j] - m) * 1.4426950408889634f);
+      sum += row[j];
+    }
+    sum = xor32_sum(xor16_sum(sum));
+    const float sc = (1.f / sum) * 0x1p-12f;
+    lbs_f4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      mlpx::h4 hq[2], lq[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int j0 = 8 * c + 4 * u;
+        if (j0 < JL) {
+          const mlpx::f32x4 v = {row[j0] * 4096.f, j0 + 1 < JL ? row[j0 + 1] * 4096.f : 0.f,
+                                 j0 + 2 < JL ? row[j0 + 2] * 4096.f : 0.f, j0 + 3 < JL ? row[j0 + 3] * 4096.f : 0.f};
+          mlpx::split4(v, hq[u], lq[u]);
+        } else {
+          hq[u] = lq[u] = mlpx::h4{0, 0, 0, 0};
+        }
+      }
+      const lbs_h8 bhi = __builtin_shufflevector(hq[0], hq[1], 0, 1, 2, 3, 4, 5, 6, 7);
+      const lbs_h8 blo = __builtin_shufflevector(lq[0], lq[1], 0, 1, 2, 3, 4, 5, 6, 7);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi[c], bhi, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi[c], blo, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo[c], bhi, acc, 0, 0, 0);
+    }
+    // lane (n, g): row g of point n's G (pointwarper.py:241-266), then x'[g] = G_g [x; 1] + t[g]
+    const float x = ((acc[0] * sc * pc[0] + acc[1] * sc * pc[1]) + acc[2] * sc * pc[2]) + acc[3] * sc;
+    if (g < 3 && p < N) xyz_out[3 * p + g] = x + gt;
+  };
+  // LBS_MFMA_PF + 1 register buffers, the loop unrolled over them: buffer b is refilled with the
+  // group LBS_MFMA_PF + 1 steps ahead right after it is skinned (no register rotation)
+  constexpr int NB = LBS_MFMA_PF + 1;
+  float buf[NB][JL], pcb[NB][3];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) fetch(gi + b * step, buf[b], pcb[b]);
+  for (;;) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      if (gi >= groups) return;   // wave-uniform
+      skin(gi, buf[b], pcb[b]);
+      fetch(gi + NB * step, buf[b], pcb[b]);
+      gi += step;
+    }
+  }
+}
+
 extern "C" int apn_lbs_skin(const float* canonical_pcd, const float* raw_weights, int64_t n_points, int32_t n_joints,
                             const float* theta_weight, float eps, const int32_t* merge_rules, const float* bone_T34,
                             const float* global_t, const float* joint_colors, const float* canonical_alpha,
@@ -409,6 +546,38 @@ extern "C" int apn_lbs_skin(const float* canonical_pcd, const float* raw_weights
   // sequential sums reproduce the oracle's skinned cloud bit for bit, and the sampling bbox --
   // hence every sample position -- follows that cloud (bbox sensitivity).
   static const bool quad_ok = apn_env("APN_LBS_LDS") == nullptr;
+  static const bool mfma_ok = apn_env("APN_LBS_QUAD") == nullptr;   // debug A/B: the VALU quad blend
+  if (mfma_ok && quad_ok && !recA16 && !merge_rules && !weights_final && !weights_out && !G_out && !joint_colors &&
+      !bbox_ord && J % 4 == 0 && J <= 64 && ((uintptr_t)raw_weights % 16) == 0) {
+    static const int per_cu = [] {
+      const char* e = apn_env("APN_LBS_BLOCKS_PER_CU");
+      return e ? atoi(e) : 8;
+    }();
+    const int mblocks = (int)std::min<int64_t>(ceil_div(ceil_div(n_points, 16), LBS_THREADS / 64), 256 * per_cu);
+    auto mf = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(mblocks), dim3(LBS_THREADS), 0, s, canonical_pcd, raw_weights, n_points,
+                         theta_weight, eps, bone_T34, global_t, xyz_out);
+    };
+    switch (J / 4) {
+      case 1: mf(k_lbs_skin_mfma<1>); break;
+      case 2: mf(k_lbs_skin_mfma<2>); break;
+      case 3: mf(k_lbs_skin_mfma<3>); break;
+      case 4: mf(k_lbs_skin_mfma<4>); break;
+      case 5: mf(k_lbs_skin_mfma<5>); break;
+      case 6: mf(k_lbs_skin_mfma<6>); break;
+      case 7: mf(k_lbs_skin_mfma<7>); break;
+      case 8: mf(k_lbs_skin_mfma<8>); break;
+      case 9: mf(k_lbs_skin_mfma<9>); break;
+      case 10: mf(k_lbs_skin_mfma<10>); break;
+      case 11: mf(k_lbs_skin_mfma<11>); break;
+      case 12: mf(k_lbs_skin_mfma<12>); break;
+      case 13: mf(k_lbs_skin_mfma<13>); break;
+      case 14: mf(k_lbs_skin_mfma<14>); break;
+      case 15: mf(k_lbs_skin_mfma<15>); break;
+      default: mf(k_lbs_skin_mfma<16>); break;
+    }
+    return launch_status();
+  }
   if (quad_ok && !recA16 && !merge_rules && J % 4 == 0 && ((uintptr_t)raw_weights % 16) == 0) {
     // grid-stride blocks (one row ahead); <= 1 partial per block. 32 blocks per CU: the launch
     // then carries more rows in flight per CU than the 4-per-CU persistent grid (C5, 1M points,

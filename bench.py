@@ -297,7 +297,7 @@ def lbs_sweep(args, rank, world, dev):
     = one pose of the sweep through TemporalPoints.repose (skeleton + fused LBS, 1M points, 48
     bones). With N>1 GPUs the points are sharded N/W per rank (SURVEY.md §8(e): LBS is per point;
     the skeleton stage is replicated, no collective) and every rank runs the same poses -- strong
-    scaling. Roofline: k_lbs_skin_quad against HBM with B_alg = N*(24 + 4J) bytes per pose
+    scaling. Roofline: k_lbs_skin_mfma against HBM with B_alg = N*(24 + 4J) bytes per pose
     (SURVEY.md 8(d)), per rank N_r points."""
     scene = S.make_scene(args.config)
     N_total = scene.cfg.N
@@ -387,7 +387,7 @@ def lbs_sweep(args, rank, world, dev):
                    "step": "skeleton + LBS captured in one HIP graph reading the sweep's next pose (TemporalPoints.capture_repose(sweep=...))",
                    "lbs_kernel_ms": lbs_ms,
                    "parallelism": f"points x{world} (no collective)" if world > 1 else "single"},
-        "roofline": {"bound": "hbm", "kernel": "k_lbs_skin_quad",
+        "roofline": {"bound": "hbm", "kernel": "k_lbs_skin_mfma",
                      "achieved": b_alg / (lbs_ms * 1e-3) / 1e9 if lbs_ms > 0 else 0.0,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": b_alg / (lbs_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if lbs_ms > 0 else 0.0,

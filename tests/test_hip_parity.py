@@ -778,10 +778,11 @@ def test_knn_modes_identical_full_scene(dev, mode):
 
 @pytest.mark.parametrize("J", [8, 24, 32, 48])
 def test_repose_quad_lbs_vs_oracle(dev, J):
-    """LBS-only repose (the C5 path, k_lbs_skin_quad: four lanes per point, weights in registers)
-    at the BASELINE bone counts, including 48 (three 16-B loads per lane), vs the oracle's
-    get_weights + PointWarper on CPU. The quad regroups the softmax and blend sums by quarter, so
-    the bar is fp32 reassociation: 2e-6 on positions (|x| <= ~1.5), 1e-6 on joints."""
+    """LBS-only repose (the C5 path, k_lbs_skin_mfma: four lanes per point, weights in registers,
+    the blend as a 16x16 product on the 3-term fp16 MFMA) at the BASELINE bone counts, including
+    48 (three 16-B loads per lane, two K chunks), vs the oracle's get_weights + PointWarper on CPU.
+    The kernel regroups the softmax sums by quarter and the blend by MFMA, so the bar is fp32
+    reassociation: 2e-6 on positions (|x| <= ~1.5), 1e-6 on joints."""
     import sys
     import os
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),

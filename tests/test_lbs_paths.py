@@ -5,8 +5,9 @@
   and on the record-free repose path, against the reference's own ``get_weights_merged`` fixture
   and the oracle's merged LBS;
 * the C5 configuration at full size (BASELINE configs[4]: 1M points, 48 bones, the repose sweep
-  of run.py:1364-1377) through ``k_lbs_skin_quad``'s persistent grid-stride loop: several trips
-  per lane, the next-row prefetch clamp ``min(n + stride, N - 1)`` and the ``n_end`` tail. The
+  of run.py:1364-1377) through ``k_lbs_skin_mfma``'s persistent grid-stride loop: several trips
+  per wave, the register ring's clamped prefetch ``min(16 g + n, N - 1)`` and the wave-uniform
+  exit. The
   oracle (CPU) checks a strided 50k-point subset plus the last point -- LBS is per point, so a
   subset model is exact."""
 import numpy as np

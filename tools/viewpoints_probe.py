@@ -37,9 +37,11 @@ def main():
     harness.render_viewpoints(model, poses, HW, Ks, False, dict(rk), **kw)
     torch.cuda.synchronize()
     for rep in range(2):
-        t0 = time.perf_counter()
-        harness.render_viewpoints(model, poses, HW, Ks, False, dict(rk), **kw)
-        print(f"render_viewpoints: {(time.perf_counter() - t0) / n * 1e3:.3f} ms/frame")
+        for nf in sorted({args.in_flight, 4}):
+            t0 = time.perf_counter()
+            harness.render_viewpoints(model, poses, HW, Ks, False, dict(rk), **dict(kw, in_flight=nf))
+            torch.cuda.synchronize()
+            print(f"render_viewpoints ({nf} in flight): {(time.perf_counter() - t0) / n * 1e3:.3f} ms/frame")
     pr = cProfile.Profile()
     pr.enable()
     t0 = time.perf_counter()
@@ -48,7 +50,7 @@ def main():
     pr.disable()
     print(f"profiled: {el / n * 1e3:.3f} ms/frame")
     pstats.Stats(pr).sort_stats("tottime").print_stats(18)
-    pipe = next(iter(model._pipelines.values()))[1]
+    pipe = next(p for p in (v[1] for v in model._pipelines.values()) if p.n == args.in_flight)
     t_arg = torch.tensor([scene.cfg.t], device=dev)
     for rep in range(2):
         torch.cuda.synchronize()
@@ -59,6 +61,17 @@ def main():
         torch.cuda.synchronize()
         print(f"bare submit loop (readback of rgb/depth/weights into the slots, no fetch): "
               f"{(time.perf_counter() - t0) / n * 1e3:.3f} ms/frame")
+    ro = pipe.readback
+    pipe.readback = ()
+    for rep in range(2):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(n):
+            pipe.submit(t_arg)
+        pipe.join()
+        torch.cuda.synchronize()
+        print(f"bare submit loop, no readback: {(time.perf_counter() - t0) / n * 1e3:.3f} ms/frame")
+    pipe.readback = ro
 
 
 if __name__ == "__main__":
