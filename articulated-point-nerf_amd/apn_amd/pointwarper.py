@@ -32,11 +32,19 @@ class TransformNet(torch.nn.Module):
         self.net = torch.nn.Sequential(*layers)
 
     def forward(self, x):
+        from .linear import sequential
         b = x.shape[0]
-        out = self.net(x)
+        out = sequential(self.net, x)
         if b > 1:
             return out.reshape(b, self.num_components, self.num_params_per_component)
         return out.reshape(self.num_components, self.num_params_per_component)
+
+
+def small_mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a @ b for the skeleton's 3x3 / 4x4 / 4x1 batches as a broadcast product and sum: elementwise
+    kernels only (no library GEMM, whose argument uploads cannot sit inside the training step's
+    captured warp graph, train.py)."""
+    return (a.unsqueeze(-1) * b.unsqueeze(-3)).sum(-2)
 
 
 def rodrigues(rvec: torch.Tensor):
@@ -104,7 +112,7 @@ class PointWarper(torch.nn.Module):
         L_ = m.shape[1]
         if L_ == 1:
             return m
-        return cls.matrix_chain_product(m[:, :L_ // 2]) @ cls.matrix_chain_product(m[:, L_ // 2:])
+        return small_mm(cls.matrix_chain_product(m[:, :L_ // 2]), cls.matrix_chain_product(m[:, L_ // 2:]))
 
     def calc_rec_abs_T_fast(self, R_t, joints):
         """pointwarper.py:156-193: M_j = [R_j | p - R_j p] about the parent joint p, chained
@@ -112,7 +120,7 @@ class PointWarper(torch.nn.Module):
         J = R_t.shape[0]
         dev = R_t.device
         joints_old = torch.cat((self.hom_row[None, :3].to(dev), joints), 0)[self.parent_joint_ex + 1]
-        M = torch.cat((torch.cat((R_t, joints_old[..., None] + R_t @ -joints_old[..., None]), -1),
+        M = torch.cat((torch.cat((R_t, joints_old[..., None] + small_mm(R_t, -joints_old[..., None])), -1),
                        self.hom_row[None, None].to(dev).repeat(J, 1, 1)), -2)
         M = torch.cat((torch.eye(4, device=dev)[None], M), 0)
         return self.matrix_chain_product(M[self.parent_indices + 1])[:, 0]
@@ -249,12 +257,13 @@ class PointWarper(torch.nn.Module):
             R_t, self.prev_thetas = self.Rodrigues(rot_params)
         R_t = R_t[self.sibling_mask]
         if self.rot_mask is not None:
-            R_t[self.rot_mask] = torch.eye(3, device=R_t.device)
+            # R_t[rot_mask] = I (pointwarper.py:230-231) without the boolean index's host sync
+            R_t = torch.where(self.rot_mask.to(R_t.device)[:, None, None], torch.eye(3, device=R_t.device), R_t)
         bone_Ts = self.calc_rec_abs_T_fast(R_t, joints)
         if global_t is None:
             global_t = torch.zeros(3, dtype=torch.float32, device=bone_Ts.device)
         jh = torch.cat([joints, torch.ones((len(joints), 1), device=joints.device)], -1)
-        joints_rel = torch.bmm(bone_Ts, jh.unsqueeze(-1)).squeeze(-1)[:, :3]
+        joints_rel = small_mm(bone_Ts, jh.unsqueeze(-1)).squeeze(-1)[:, :3]
         return bone_Ts, global_t, joints_rel
 
     def forward(self, weights, joints, t=None, rot_params=None, global_t=None, get_frames=False,

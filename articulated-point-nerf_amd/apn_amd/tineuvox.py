@@ -43,12 +43,13 @@ class RGBNet(nn.Module):
                                            nn.Linear(W // 2, self.output_ch))
 
     def forward(self, input_h, input_views=None):
-        feature = self.feature_linears(input_h)
+        from .linear import linear, sequential
+        feature = linear(input_h, self.feature_linears)
         if input_views is not None:
             feature = torch.cat([feature, input_views], dim=-1)
         else:
             assert self.input_ch_views == 0
-        return self.views_linears(feature)
+        return sequential(self.views_linears, feature)
 
 
 class TiNeuVoxHeads(nn.Module):

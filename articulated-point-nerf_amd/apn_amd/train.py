@@ -24,13 +24,14 @@ import ctypes as C
 import torch
 
 from . import _lib as L
+from . import linear as LIN
 from ._lib import call, ptr, stream_ptr
 from .ops import Alphas2Weights, Raw2Alpha
 from .tineuvox import poc_fre
 
 __all__ = ["forward_train", "LBSTrain", "lbs_train", "lbs_blend", "inv3x3", "radius_knn", "ordered_bbox",
            "reverse_csr", "NbrTVLoss", "ArapLoss",
-           "SplitKLinear", "feat_net_forward", "SparsityLoss"]
+           "feat_net_forward", "SparsityLoss"]
 
 
 def cloud_min_max(xyz: torch.Tensor):
@@ -214,67 +215,21 @@ class SparsityLoss(torch.autograd.Function):
         return dw, None
 
 
-SPLITK_ROWS = 4096   # rows per chunk of the split-K weight gradient
-
-
-def splitk_weight_grad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
-    """dW = dy^T x for tall [M,out] x [M,in] operands as a batched split-K product: M is cut into
-    S = M // SPLITK_ROWS chunks (one bmm, S output tiles in flight instead of one 128x128 tile
-    walking all M rows), summed over the chunk axis in a fixed order, plus the remainder rows.
-    Deterministic; at M = 212k rows 0.48 -> 0.075 ms and ~7x closer to the float64 product."""
-    M = dy.shape[0]
-    S = M // SPLITK_ROWS
-    if S <= 1:
-        return dy.t() @ x
-    Mc = S * (M // S)
-    out = torch.bmm(dy[:Mc].view(S, -1, dy.shape[1]).transpose(1, 2), x[:Mc].view(S, -1, x.shape[1])).sum(0)
-    if Mc < M:
-        out.addmm_(dy[Mc:].t(), x[Mc:])
-    return out
-
-
-class SplitKLinear(torch.autograd.Function):
-    """torch.nn.Linear (y = x W^T + b) whose weight gradient uses splitk_weight_grad: the
-    feat_net layers of the training forward (temporalpoints.py:491) run over survivors x 8
-    rows, where the library's single-tile dW GEMM was the largest kernel of the backward."""
-
-    @staticmethod
-    def forward(ctx, x, weight, bias):
-        ctx.save_for_backward(x, weight)
-        ctx.has_bias = bias is not None
-        return torch.nn.functional.linear(x, weight, bias)
-
-    @staticmethod
-    @torch.autograd.function.once_differentiable
-    def backward(ctx, dy):
-        x, weight = ctx.saved_tensors
-        dy = dy.contiguous()
-        dx = dy @ weight if ctx.needs_input_grad[0] else None
-        dw = splitk_weight_grad(dy, x.contiguous()) if ctx.needs_input_grad[1] else None
-        db = dy.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
-        return dx, dw, db
-
-
 def feat_net_forward(net: torch.nn.Module, x: torch.Tensor) -> torch.Tensor:
-    """Run a Sequential of Linear / LeakyReLU (nested) with SplitKLinear for the Linear layers;
-    same parameters, same arithmetic per output element as net(x)."""
-    for m in net:
-        if isinstance(m, torch.nn.Linear):
-            x = SplitKLinear.apply(x, m.weight, m.bias)
-        elif isinstance(m, torch.nn.LeakyReLU):
-            x = torch.nn.functional.leaky_relu(x, m.negative_slope)
-        elif isinstance(m, torch.nn.Sequential):
-            x = feat_net_forward(m, x)
-        else:
-            x = m(x)
-    return x
+    """Run a Sequential of Linear / LeakyReLU (nested) on the hand-written GEMM (linear.sequential):
+    same parameters, f32 products and sums per output element, the activation in the epilogue."""
+    return LIN.sequential(net, x)
 
 
-def lbs_train(model, bone_Ts, global_t):
+def lbs_train(model, bone_Ts, global_t, identity_rules=None):
     """(t_hat_pcd, Rinv, weights) of the training forward: the fused HIP Function for identity
-    merge rules and J <= 64, else the torch composition (get_weights + lbs_blend + inv3x3)."""
+    merge rules and J <= 64, else the torch composition (get_weights + lbs_blend + inv3x3).
+    ``identity_rules``: model._merge_rules() is None, when the caller already knows (inside a
+    graph capture the check's host copy is not allowed)."""
     J = bone_Ts.shape[0]
-    if model._merge_rules() is None and J <= 64:
+    if identity_rules is None:
+        identity_rules = model._merge_rules() is None
+    if identity_rules and J <= 64:
         pcd = model.forward_warp.canonical_pcd.detach().float().contiguous()
         th = model.theta_weight.reshape(1)
         gt = global_t.reshape(3)
@@ -284,6 +239,92 @@ def lbs_train(model, bone_Ts, global_t):
     weights = model.get_weights()
     xyz, G = lbs_blend(model.forward_warp.canonical_pcd, weights, bone_Ts, global_t)
     return xyz, inv3x3(G[:, :, :3]), weights
+
+
+# The warp stage of a training step -- skeleton (TransformNet, Rodrigues, masks, the kinematic
+# chain), fused LBS, pose embedding -- has the same shapes every step, so it runs as a captured
+# HIP graph pair (torch.cuda.make_graphed_callables: one forward replay, one backward replay)
+# instead of ~100 forward and ~250 backward launches from the host. Off: the eager composition.
+GRAPH_WARP = True
+
+
+class _WarpStage(torch.nn.Module):
+    """pointwarper.py:213-239 + temporalpoints.py:401-414, 569, 478 (+ the pose embedding
+    380-381) as one module over the parameters they read; forward(t_embed) returns every tensor
+    the rest of the step uses: (t_hat_pcd, Rinv, weights, bone_Ts, global_t, joints_rel, thetas,
+    params[, pose_embedding])."""
+
+    def __init__(self, model, identity_rules):
+        super().__init__()
+        self.fw = model.forward_warp
+        self.joints = model.joints
+        self.weights = model.weights
+        self.theta_weight = model.theta_weight
+        self.pe = model.pose_embedding_net if model.pose_embedding_dim > 0 else None
+        self._model = (model,)   # not a submodule: only the stage's own parameters are graph inputs
+        self._identity_rules = identity_rules
+
+    def forward(self, t_embed):
+        model = self._model[0]
+        bone_Ts, global_t, joints_rel = self.fw.pose_torch(self.joints, t_embed, None)
+        xyz, Rinv, weights = lbs_train(model, bone_Ts, global_t, identity_rules=self._identity_rules)
+        out = [xyz, Rinv, weights, bone_Ts, global_t, joints_rel, self.fw.prev_thetas, self.fw.prev_params]
+        # no reference to this pass's autograd graph may outlive it: a parameter's AccumulateGrad
+        # node kept alive from a pass on another stream makes the captured backward wait on that
+        # stream, which ends the capture (warp_stage sets the pose state from the replay's outputs)
+        self.fw.prev_thetas = self.fw.prev_params = self.fw.prev_global_t = None
+        if self.pe is not None:
+            delta_joint = (self.joints - joints_rel).clone().detach()
+            out.append(LIN.sequential(self.pe, poc_fre(delta_joint, model.pos_poc).view(1, -1)))
+        return tuple(out)
+
+
+def _graphed_warp(model, t_embed):
+    """The model's captured warp stage for this input shape, captured again when a parameter
+    tensor, its requires_grad, or the skeleton's masks change."""
+    fw = model.forward_warp
+    identity_rules = model._merge_rules() is None
+    params = [model.joints, model.weights, model.theta_weight] + list(fw.parameters())
+    if model.pose_embedding_dim > 0:
+        params += list(model.pose_embedding_net.parameters())
+    key = (tuple(t_embed.shape), identity_rules, tuple((p.data_ptr(), p.requires_grad) for p in params),
+           (fw.rot_mask.data_ptr(), fw.rot_mask._version), (fw.sibling_mask.data_ptr(), fw.sibling_mask._version),
+           model.training)
+    hit = model.__dict__.get("_warp_graph")
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    model.__dict__.pop("_warp_graph", None)
+    # drop the model's references to earlier steps' autograd graphs (pose state, LBS weights):
+    # their parameter AccumulateGrad nodes carry the stream those steps ran on (see _WarpStage)
+    fw.prev_thetas = fw.prev_params = fw.prev_global_t = None
+    model._last_weights = None
+    stage = _WarpStage(model, identity_rules)
+    stage.train(model.training)
+    sample = t_embed.detach().clone()
+    graphed = torch.cuda.make_graphed_callables(stage, (sample,), num_warmup_iters=2, allow_unused_input=True)
+    model.__dict__["_warp_graph"] = (key, graphed)
+    return graphed
+
+
+def warp_stage(model, t_embed):
+    """(t_hat_pcd, Rinv, weights, bone_Ts, global_t, joints_rel, pose_embedding) of the training
+    forward; sets the pose state the regularisers read (prev_thetas / prev_params / prev_global_t)
+    and model._last_weights, as the eager composition does."""
+    fw = model.forward_warp
+    if GRAPH_WARP and t_embed.is_cuda and torch.is_grad_enabled():
+        out = _graphed_warp(model, t_embed)(t_embed)
+        xyz, Rinv, weights, bone_Ts, global_t, joints_rel, thetas, params = out[:8]
+        fw.prev_thetas, fw.prev_params, fw.prev_global_t = thetas, params, global_t
+        pose_embedding = out[8] if len(out) > 8 else None
+    else:
+        bone_Ts, global_t, joints_rel = fw.pose_torch(model.joints, t_embed, None)
+        xyz, Rinv, weights = lbs_train(model, bone_Ts, global_t)
+        pose_embedding = None
+        if model.pose_embedding_dim > 0:
+            delta_joint = (model.joints - joints_rel).clone().detach()
+            pose_embedding = LIN.sequential(model.pose_embedding_net, poc_fre(delta_joint, model.pos_poc).view(1, -1))
+    model._last_weights = weights
+    return xyz, Rinv, weights, bone_Ts, global_t, joints_rel, pose_embedding
 
 
 def radius_knn(model, xyz, bbox6, rk, query_radius):
@@ -348,15 +389,18 @@ def forward_train(model, t, render_depth=False, render_kwargs=None, query_radius
     L.require_cuda(model.canonical_feat, what="TemporalPoints.forward")
     K = model.neighbours
     # skeleton + LBS (temporalpoints.py:547-569; pointwarper.py:213-279)
-    t_embed = poc_fre(t, model.time_poc) if rot_params is None else None
     fw = model.forward_warp
-    bone_Ts, global_t, joints_rel = fw.pose_torch(model.joints, t_embed, rot_params)
-    # get_weights + blend/apply + torch.inverse(G)[:, :3, :3] (569, 478)
-    t_hat_pcd, Rinv, weights = lbs_train(model, bone_Ts, global_t)
-    model._last_weights = weights
-    delta_joint = (model.joints - joints_rel).clone().detach()
-    pose_embedding = (model.pose_embedding_net(poc_fre(delta_joint, model.pos_poc).view(1, -1))
-                      if model.pose_embedding_dim > 0 else None)
+    if rot_params is None:
+        # get_weights + blend/apply + torch.inverse(G)[:, :3, :3] (569, 478), captured stage
+        t_hat_pcd, Rinv, weights, bone_Ts, global_t, joints_rel, pose_embedding = warp_stage(
+            model, poc_fre(t, model.time_poc))
+    else:
+        bone_Ts, global_t, joints_rel = fw.pose_torch(model.joints, None, rot_params)
+        t_hat_pcd, Rinv, weights = lbs_train(model, bone_Ts, global_t)
+        model._last_weights = weights
+        delta_joint = (model.joints - joints_rel).clone().detach()
+        pose_embedding = (LIN.sequential(model.pose_embedding_net, poc_fre(delta_joint, model.pos_poc).view(1, -1))
+                          if model.pose_embedding_dim > 0 else None)
     joints = bones = None
     if get_skeleton:
         joints = project_point_to_image_plane(joints_rel + global_t, poses.to(dev), Ks.to(dev, torch.float32))
@@ -401,7 +445,7 @@ def forward_train(model, t, render_depth=False, render_kwargs=None, query_radius
     out = feat_net_forward(model.feat_net, torch.cat(feat_in, dim=-1))
     h = (out.reshape(len(s_i), K, -1) * w).sum(dim=1)
     # heads (496-515)
-    density = model.densitynet(h).squeeze(-1)
+    density = LIN.linear(h, model.densitynet).squeeze(-1)
     interval = float(rk['stepsize']) * float(model.tineuvox.voxel_size_ratio)
     alpha = Raw2Alpha.apply(density.contiguous(), float(model.tineuvox.act_shift), interval)
     if model.no_view_dir:

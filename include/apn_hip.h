@@ -401,6 +401,26 @@ int apn_tnv_field(const float* pos4, const int32_t* s_ray, const int32_t* time_i
                   float act_shift, float interval, float* out12, float* delta_out, float* h_out,
                   float* vox_out, void* stream);
 
+/* fp32 GEMMs of the training step (forward and backward of the Linear layers that the reference
+ * trains through autograd: feat_net, densitynet, rgbnet, TransformNet, pose_embedding_net --
+ * temporalpoints.py:491-515, pointwarper.py:5-37, run.py:574-716), on the f32-input MFMA (exact
+ * f32 products and sums in the kernel's order):
+ *   C[m][n] = epi( sum_k opA[m][k] opB[k][n] ),  opA = A (M x K, lda) or A^T (trans_a: A is K x M),
+ *   opB = B (K x N, ldb) or B^T (trans_b: B is N x K);
+ *   A2 (optional, same layout as A): opA *= (A2 > 0 ? 1 : slope_mask) -- a LeakyReLU derivative
+ *   taken from the layer's output; epi: + bias[n] (optional), LeakyReLU(slope_act) when act. */
+int apn_gemm_f32(const float* A, const float* A2, const float* B, float* C, const float* bias, int64_t M,
+                 int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int32_t trans_a, int32_t trans_b,
+                 float slope_mask, int32_t act, float slope_act, void* stream);
+/* The same product with the reduction dimension K split over `splits` workgroup slices (weight
+ * gradients: K = the rows of a batch), partial products summed in a fixed order: C [M, N]
+ * (ldc = N); bias_grad (optional) [M] = sum_k opA[m][k] (the bias gradient, computed as one more
+ * column of ones in opB). workspace: apn_gemm_f32_splitk_workspace_bytes(M, N, splits). */
+size_t apn_gemm_f32_splitk_workspace_bytes(int64_t M, int64_t N, int32_t splits);
+int apn_gemm_f32_splitk(const float* A, const float* A2, const float* B, float* C, float* bias_grad, int64_t M,
+                        int64_t N, int64_t K, int64_t lda, int64_t ldb, int32_t trans_a, int32_t trans_b,
+                        float slope_mask, int32_t splits, void* workspace, void* stream);
+
 /* Utilities */
 size_t apn_scan_workspace_bytes(int64_t n);
 int apn_scan_exclusive_i32(const int32_t* in, int32_t* out, int64_t n, void* workspace, void* stream);

@@ -126,6 +126,140 @@ def test_temporalpoints_losses_route_to_hip():
 
 @pytest.mark.gpu
 @pytest.mark.autograd
+@pytest.mark.parametrize("slope", [None, 0.01, 0.0])
+@pytest.mark.parametrize("M,K,N", [(1, 155, 128), (300, 128, 128), (4096 * 2 + 5, 155, 128), (212736 + 7, 128, 128),
+                                   (26001, 128, 1), (1, 160, 64), (777, 33, 256), (5, 256, 97)])
+def test_gemm_linear_vs_float64(M, K, N, slope):
+    """apn_amd.linear (the training step's Linear layers on apn_gemm_f32 / apn_gemm_f32_splitk:
+    feat_net, densitynet (N = 1), rgbnet, TransformNet (M = 1), with LeakyReLU / ReLU / no
+    activation fused): output and all three gradients within fp32 rounding of float64. The
+    activation's kink is taken from the fp32 output on both sides (a pre-activation within an ulp
+    of 0 may have either sign), so the check isolates the products and sums."""
+    from apn_amd.linear import _GemmLinear
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(M * 7 + N)
+    x = torch.randn(M, K, generator=g)
+    w = torch.randn(N, K, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g)
+    dy = torch.randn(M, N, generator=g)
+    ps = [t.to(dev).requires_grad_(True) for t in (x, w, b)]
+    y = _GemmLinear.apply(*ps, slope)
+    y.backward(dy.to(dev))
+    x64, w64, b64 = (t.double().to(dev) for t in (x, w, b))
+    pre = x64 @ w64.t() + b64
+    if slope is None:
+        y64, m64 = pre, torch.ones_like(pre)
+    else:
+        pos = y.detach().double() > 0
+        y64 = torch.where(pos, pre, pre * slope)
+        m64 = torch.where(pos, torch.ones_like(pre), torch.full_like(pre, slope))
+    gd = dy.double().to(dev) * m64
+    refs = {"y": y64, "x": gd @ w64, "w": gd.t() @ x64, "b": gd.sum(0)}
+    for name, a in (("y", y), ("x", ps[0].grad), ("w", ps[1].grad), ("b", ps[2].grad)):
+        r = refs[name]
+        err = float((a.double() - r).abs().max() / r.abs().max().clamp_min(1e-30))
+        assert err < 2e-6, (name, err)
+
+
+def test_gemm_linear_sequential_matches_torch_on_cpu():
+    """linear.sequential pairs each Linear with the LeakyReLU / ReLU after it (nested Sequentials
+    flattened, the feat_net layout of temporalpoints.py:299-303); on CPU tensors it is torch's own
+    forward, so it must equal the module bit for bit."""
+    from apn_amd.linear import sequential
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(20, 16), torch.nn.LeakyReLU(),
+                              torch.nn.Sequential(torch.nn.Linear(16, 16), torch.nn.ReLU()),
+                              torch.nn.Linear(16, 8))
+    x = torch.randn(5, 20)
+    assert torch.equal(sequential(net, x), net(x))
+
+
+@pytest.mark.gpu
+@pytest.mark.autograd
+@pytest.mark.parametrize("n,J", [(1, 8), (777, 24), (20000, 24), (5000, 48)])
+def test_nbr_tv_loss_vs_torch(n, J):
+    dev = torch.device("cuda")
+    K = 8 if n >= 8 else 1
+    nn = _graph(n, K, n + J)
+    g = torch.Generator().manual_seed(J)
+    w = torch.softmax(torch.randn(n, J, generator=g) * 3, -1)
+    w[: n // 10] = w[0]      # exact ties: sign(0) = 0 on both sides
+    w64 = w.double().requires_grad_(True)
+    ref = _tv_ref(w64, nn)
+    ref.backward(torch.tensor(10.0, dtype=torch.float64))
+    rp, re = reverse_csr(nn.to(dev))
+    wd = w.to(dev).requires_grad_(True)
+    loss = NbrTVLoss.apply(wd, nn.to(dev), rp, re)
+    (10.0 * loss).backward()
+    assert abs(float(loss) - float(ref)) <= 1e-6 * max(1.0, float(ref))
+    scale = 10.0 / (n * K * J)
+    assert torch.allclose(wd.grad.cpu().double(), w64.grad, rtol=1e-6, atol=1e-6 * scale)
+    # deterministic: a second run is bit-identical
+    wd2 = w.to(dev).requires_grad_(True)
+    l2 = NbrTVLoss.apply(wd2, nn.to(dev), rp, re)
+    (10.0 * l2).backward()
+    assert float(l2) == float(loss) and torch.equal(wd2.grad, wd.grad)
+
+
+@pytest.mark.gpu
+@pytest.mark.autograd
+@pytest.mark.parametrize("n", [1, 777, 20000, 300000])
+def test_arap_loss_vs_torch(n):
+    from apn_amd.ops import knn_points
+    dev = torch.device("cuda")
+    K = 8 if n >= 8 else 1
+    g = torch.Generator().manual_seed(n)
+    pcd = torch.rand(n, 3, generator=g)
+    eps = float(torch.tensor(1e-6))
+    _, nn = knn_points(pcd.to(dev), pcd.to(dev), K)
+    nn = nn.cpu()
+    d0 = torch.sqrt(((pcd[:, None, :] - pcd[nn, :]) ** 2).sum(-1) + torch.tensor(1e-6))
+    warped = pcd + 0.01 * torch.randn(n, 3, generator=g)
+    x64 = warped.double().requires_grad_(True)
+    ref = _arap_ref(x64, nn, d0.double(), eps)
+    ref.backward(torch.tensor(5e-3, dtype=torch.float64))
+    rp, re = reverse_csr(nn.to(dev))
+    xd = warped.to(dev).requires_grad_(True)
+    loss = ArapLoss.apply(xd, nn.to(dev), d0.to(dev), eps, rp, re)
+    (5e-3 * loss).backward()
+    assert abs(float(loss) - float(ref)) <= 1e-5 * max(1.0, abs(float(ref)))
+    gref = x64.grad
+    # per-edge terms are +-dL * diff/s (|.| <= dL); fp32 rounding of diff/s ~1e-7 relative per
+    # term, summed over <= K + in-degree terms
+    tol = 5e-3 * 1e-5
+    bad = ((xd.grad.cpu().double() - gref).abs() > tol).float().mean()
+    assert float(bad) <= 1e-4, float(bad)   # sign flips where d0 == s within rounding
+    xd2 = warped.to(dev).requires_grad_(True)
+    l2 = ArapLoss.apply(xd2, nn.to(dev), d0.to(dev), eps, rp, re)
+    (5e-3 * l2).backward()
+    assert float(l2) == float(loss) and torch.equal(xd2.grad, xd.grad)
+
+
+@pytest.mark.gpu
+@pytest.mark.autograd
+def test_temporalpoints_losses_route_to_hip():
+    """The TemporalPoints methods take the fused path and agree with the reference expressions on
+    the model's own kNN graph."""
+    import sys
+    from golden_io import Golden
+    from model_io import model_from_golden
+    g = Golden("G1")
+    m = model_from_golden(g, "cuda")
+    nn_i, nn_d = m.nn_i, m.nn_distance
+    m._last_weights = torch.softmax(m.weights.detach(), -1).requires_grad_(True)
+    tv = m.get_neighbour_weight_tv_loss()
+    assert tv.grad_fn is not None and "NbrTVLoss" in type(tv.grad_fn).__name__
+    lw = m._last_weights.detach()
+    assert abs(float(tv) - float(_tv_ref(lw.double(), nn_i))) < 1e-6
+    x = m.canonical_pcd.detach().clone().requires_grad_(True)
+    arap = m.get_arap_loss(x)
+    assert "ArapLoss" in type(arap.grad_fn).__name__
+    assert abs(float(arap) - float(_arap_ref(x.detach().double(), nn_i, nn_d.double(), float(m.eps)))) < 1e-4
+    assert "apn_amd" in sys.modules
+
+
+@pytest.mark.gpu
+@pytest.mark.autograd
 @pytest.mark.parametrize("M,K", [(1, 155), (300, 128), (4096 * 2 + 5, 155), (212736 + 7, 128)])
 def test_splitk_linear_vs_float64(M, K):
     """SplitKLinear (training feat_net layers): output and all three gradients within fp32
