@@ -16,7 +16,18 @@ import torch
 from ._lib import call, load, ptr, stream_ptr
 
 SPLIT_ROWS = 512     # rows per split of the weight-gradient product (at least)
-SPLIT_TILES = 1024   # aim: output tiles x splits of about this many workgroups
+SPLIT_TILES = 512    # aim: output tiles x splits of about this many workgroups
+
+
+def _padded_rows(w: torch.Tensor) -> torch.Tensor:
+    """W [N, K] as a view of rows padded to a multiple of 4 floats (a copy only when K % 4 != 0):
+    16-B aligned rows take the product's vector loads."""
+    N, K = w.shape
+    if K % 4 == 0:
+        return w.contiguous()
+    buf = torch.zeros(N, -(-K // 4) * 4, device=w.device, dtype=w.dtype)
+    buf[:, :K] = w.detach()
+    return buf[:, :K]
 
 
 class _GemmLinear(torch.autograd.Function):
@@ -25,16 +36,19 @@ class _GemmLinear(torch.autograd.Function):
         if x.dtype != torch.float32 or weight.dtype != torch.float32:
             raise TypeError("apn linear: float32 only")
         dev = x.device
-        x2 = x.reshape(-1, x.shape[-1]).contiguous()
-        w = weight.contiguous()
+        x2 = x.reshape(-1, x.shape[-1])
+        if x2.stride(-1) != 1 or x2.stride(0) < x2.shape[1]:
+            x2 = x2.contiguous()
+        lda = x2.stride(0)   # rows may be padded (pad_cat): 16-B aligned rows take the vector loads
         M, K = x2.shape
-        N = w.shape[0]
-        if w.shape[1] != K:
-            raise ValueError(f"apn linear: input width {K} vs weight {tuple(w.shape)}")
+        N = weight.shape[0]
+        if weight.shape[1] != K:
+            raise ValueError(f"apn linear: input width {K} vs weight {tuple(weight.shape)}")
+        w = _padded_rows(weight)
         b = bias.contiguous() if bias is not None else None
         y = torch.empty(M, N, device=dev, dtype=torch.float32)
         act = slope is not None
-        call("apn_gemm_f32", ptr(x2), None, ptr(w), ptr(y), ptr(b), M, N, K, K, K, N, 0, 1, 0.0, int(act),
+        call("apn_gemm_f32", ptr(x2), None, ptr(w), ptr(y), ptr(b), M, N, K, lda, w.stride(0), N, 0, 1, 0.0, int(act),
              float(slope) if act else 0.0, stream_ptr(dev))
         ctx.save_for_backward(x2, w, y if act else None)
         ctx.slope, ctx.has_bias, ctx.in_shape = slope, bias is not None, x.shape
@@ -52,20 +66,41 @@ class _GemmLinear(torch.autograd.Function):
         s = stream_ptr(dev)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = torch.empty(M, K, device=dev, dtype=torch.float32)
-            call("apn_gemm_f32", ptr(dy), ptr(y), ptr(w), ptr(dx), None, M, K, N, N, K, K, 0, 0, sm, 0, 0.0, s)
-            dx = dx.reshape(ctx.in_shape)
+            Kp = -(-K // 4) * 4   # 16-B rows for the next product's vector loads
+            dx = torch.empty(M, Kp, device=dev, dtype=torch.float32)
+            call("apn_gemm_f32", ptr(dy), ptr(y), ptr(w), ptr(dx), None, M, K, N, N, w.stride(0), Kp, 0, 0, sm, 0, 0.0,
+                 s)
+            dx = dx[:, :K]
+            if len(ctx.in_shape) != 2:
+                dx = dx.reshape(ctx.in_shape)
         want_b = ctx.has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1] or want_b:
             dw = torch.empty(N, K, device=dev, dtype=torch.float32)
             db = torch.empty(N, device=dev, dtype=torch.float32) if want_b else None
-            tiles = -(-N // 64) * -(-(K + 1) // 64)
+            bn = 192 if -(-K // 192) < -(-K // 128) else 128   # the kernel's column tile (apn_gemm.hip run)
+            tiles = -(-N // 64) * -(-K // bn)
             splits = max(1, min(M // SPLIT_ROWS, SPLIT_TILES // tiles))
             ws = torch.empty(int(load().apn_gemm_f32_splitk_workspace_bytes(N, K, splits)) // 4 + 1,
                              device=dev, dtype=torch.float32)
-            call("apn_gemm_f32_splitk", ptr(dy), ptr(y), ptr(x), ptr(dw), ptr(db), N, K, M, N, K, 1, 0, sm, splits,
-                 ptr(ws), s)
+            call("apn_gemm_f32_splitk", ptr(dy), ptr(y), ptr(x), ptr(dw), ptr(db), N, K, M, N, x.stride(0), 1, 0, sm,
+                 splits, ptr(ws), s)
         return dx, (dw if ctx.needs_input_grad[1] else None), db, None
+
+
+def pad_cat(parts) -> torch.Tensor:
+    """torch.cat(parts, -1) for [M, k_i] tensors, written into rows padded to a multiple of 4 floats
+    (a view of width sum k_i): the first layer's product then reads 16-B aligned rows."""
+    M = parts[0].shape[0]
+    K = sum(p.shape[-1] for p in parts)
+    Kp = -(-K // 4) * 4
+    if Kp == K or not parts[0].is_cuda:
+        return torch.cat(parts, dim=-1)
+    buf = torch.empty(M, Kp, device=parts[0].device, dtype=parts[0].dtype)
+    c = 0
+    for p in parts:
+        buf[:, c:c + p.shape[-1]].copy_(p)
+        c += p.shape[-1]
+    return buf[:, :K]
 
 
 def linear(x: torch.Tensor, layer: torch.nn.Linear, slope=None) -> torch.Tensor:

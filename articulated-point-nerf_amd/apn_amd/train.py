@@ -127,6 +127,100 @@ def reverse_csr(nn_i: torch.Tensor):
     return rev_ptr, rev_edge
 
 
+def reverse_index(idx: torch.Tensor, n_targets: int):
+    """rev_ptr [n_targets+1], rev_edge: the positions of idx (flattened, int64) grouped by value,
+    ascending within a value (stable sort) -- the gather order of the per-point gradient sums."""
+    flat = idx.reshape(-1)
+    rev_edge = torch.argsort(flat, stable=True).contiguous()
+    rev_ptr = torch.zeros(n_targets + 1, dtype=torch.int64, device=idx.device)
+    rev_ptr[1:] = torch.cumsum(torch.bincount(flat, minlength=n_targets), 0)
+    return rev_ptr, rev_edge
+
+
+class NbrAggregate(torch.autograd.Function):
+    """temporalpoints.py:452-491 for the training forward as one HIP forward (apn_nbr_train_fwd) and
+    one HIP backward (apn_nbr_train_bwd): (ray_pts [S,3], s_i [S,8], xyz [N,3], Rinv [N,3,3],
+    canonical_feat [N,F], pose_emb [1,P] | None, sig [N], rgb_c [N,3], alpha_c [N] (clipped), poc,
+    eps) -> (w [S,8] IDW weights, rgb_d [S,3], alpha_d [S], feat_in [8S, 3+6L+F+P] in 16-B rows).
+    Per-point gradients are gathered over the reverse adjacency of s_i (no atomics)."""
+
+    @staticmethod
+    def forward(ctx, ray_pts, s_i, xyz, Rinv, feat, pose_emb, sig, rgb_c, alpha_c, poc, eps):
+        dev = xyz.device
+        S = s_i.shape[0]
+        F = feat.shape[1]
+        P = pose_emb.shape[-1] if pose_emb is not None else 0
+        L = poc.numel()
+        K = 3 + 6 * L + F + P
+        Kp = -(-K // 4) * 4
+        c = lambda x: x.detach().float().contiguous()
+        args = [c(ray_pts), s_i.contiguous(), c(xyz), c(Rinv), c(sig), c(rgb_c), c(alpha_c), c(poc)]
+        w = torch.empty(S, 8, device=dev)
+        rgbd = torch.empty(S, 3, device=dev)
+        alphad = torch.empty(S, device=dev)
+        buf = torch.empty(S * 8, Kp, device=dev)
+        pe = c(pose_emb) if pose_emb is not None else None
+        call("apn_nbr_train_fwd", S, ptr(args[0]), ptr(args[1]), ptr(args[2]), ptr(args[3]), ptr(c(feat)), F, ptr(pe),
+             P, ptr(args[4]), ptr(args[5]), ptr(args[6]), ptr(args[7]), L, float(eps), ptr(w), ptr(rgbd), ptr(alphad),
+             ptr(buf), Kp, stream_ptr(dev))
+        ctx.save_for_backward(*args)
+        ctx.meta = (S, xyz.shape[0], F, P, L, float(eps), K)
+        ctx.pose_shape = pose_emb.shape if pose_emb is not None else None
+        return w, rgbd, alphad, buf[:, :K]
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, d_w, d_rgbd, d_alphad, d_feat):
+        ray_pts, s_i, xyz, Rinv, sig, rgb_c, alpha_c, poc = ctx.saved_tensors
+        S, N, F, P, L, eps, K = ctx.meta
+        dev = xyz.device
+        c = lambda x: None if x is None else x.float().contiguous()
+        d_w, d_rgbd, d_alphad = c(d_w), c(d_rgbd), c(d_alphad)
+        if d_feat is not None and (d_feat.stride(-1) != 1 or d_feat.stride(0) < K):
+            d_feat = d_feat.contiguous()
+        ldd = d_feat.stride(0) if d_feat is not None else K
+        rev_ptr, rev_edge = reverse_index(s_i, N)
+        contrib = torch.empty(S * 8, 17, device=dev)
+        d_xyz = torch.empty(N, 3, device=dev)
+        d_R = torch.empty(N, 3, 3, device=dev)
+        d_sig = torch.empty(N, device=dev)
+        d_c = torch.empty(N, 3, device=dev)
+        d_a = torch.empty(N, device=dev)
+        want_feat = ctx.needs_input_grad[4] and d_feat is not None
+        d_featp = torch.empty(N, F, device=dev) if want_feat else None
+        call("apn_nbr_train_bwd", S, N, ptr(ray_pts), ptr(s_i), ptr(xyz), ptr(Rinv), ptr(sig), ptr(rgb_c), ptr(alpha_c),
+             ptr(poc), L, eps, ptr(d_w), ptr(d_rgbd), ptr(d_alphad), ptr(d_feat), ldd, F, ptr(rev_ptr), ptr(rev_edge),
+             ptr(contrib), ptr(d_xyz), ptr(d_R), ptr(d_sig), ptr(d_c), ptr(d_a), ptr(d_featp), stream_ptr(dev))
+        d_pose = None
+        if P > 0 and ctx.needs_input_grad[5] and d_feat is not None:
+            d_pose = d_feat[:, K - P:].sum(0).reshape(ctx.pose_shape)
+        return None, None, d_xyz, d_R, d_featp, d_pose, d_sig, d_c, d_a, None, None
+
+
+class IdwSum(torch.autograd.Function):
+    """h = sum_k w[s,k] out[8s+k] (temporalpoints.py:493-494) as apn_idw_sum_fwd / _bwd."""
+
+    @staticmethod
+    def forward(ctx, w, out):
+        S, C = w.shape[0], out.shape[-1]
+        w, out = w.contiguous(), out.reshape(S * 8, C).contiguous()
+        h = torch.empty(S, C, device=out.device)
+        call("apn_idw_sum_fwd", S, C, ptr(w), ptr(out), ptr(h), stream_ptr(out.device))
+        ctx.save_for_backward(w, out)
+        return h
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dh):
+        w, out = ctx.saved_tensors
+        S, C = w.shape[0], out.shape[-1]
+        d_out = torch.empty_like(out) if ctx.needs_input_grad[1] else None
+        d_w = torch.empty_like(w) if ctx.needs_input_grad[0] else None
+        call("apn_idw_sum_bwd", S, C, ptr(w), ptr(out), ptr(dh.contiguous()), ptr(d_out), ptr(d_w),
+             stream_ptr(out.device))
+        return d_w, d_out
+
+
 class NbrTVLoss(torch.autograd.Function):
     """get_neighbour_weight_tv_loss (temporalpoints.py:714-716): mean |w_i - w_nn(i,k)| over
     [N,K,J] as one fused HIP edge reduction (apn_nbr_tv_loss); backward apn_nbr_tv_loss_backward
@@ -426,24 +520,15 @@ def forward_train(model, t, render_depth=False, render_kwargs=None, query_radius
                 'rgb_marched_direct': torch.ones(R, 3, device=dev) * bg,
                 'depth': torch.zeros(R, device=dev), 'weights': torch.ones(R, 3, device=dev) * bg,
                 't_hat_pcd': t_hat_pcd, 'alphainv_last': None, 'grid': None, 'joints': joints, 'bones': bones}
-    rel_p = ray_pts[:, None, :] - t_hat_pcd[s_i, :]
-    to_nn = (rel_p ** 2).sum(-1)
-    # direct render blend (459-470, forced on at 592)
+    # direct render blend (459-470, forced on at 592), IDW weights (472-475), rel_c + posenc + the
+    # feat_net input rows (476-491): one HIP forward / backward (NbrAggregate)
     sig = model.mean_min_distance * torch.clamp(model.direct_eps, min=0.)
-    w_direct = torch.exp(-(to_nn ** 2) / (2 * (sig[s_i]) ** 2 + 1e-12))
-    w_direct_density = ((1. / K) * w_direct).unsqueeze(-1)
-    w_direct = (w_direct / (w_direct.sum(dim=-1) + 1e-12)[:, None]).unsqueeze(-1)
-    rgbs_direct = (w_direct * model.canonical_rgbs.clip(0, 1)[s_i, :]).sum(dim=1)
-    alpha_direct = (w_direct_density * model.canonical_alpha.clip(0, 1)[s_i].unsqueeze(-1)).sum(dim=1).squeeze(-1)
-    # point-NeRF aggregation (472-494)
-    w = 1 / (to_nn + model.eps.to(dev))
-    w = (w / w.sum(dim=-1)[:, None]).unsqueeze(-1)
-    rel_c = (Rinv[s_i] * rel_p[:, :, None, :]).sum(-1).reshape(-1, 3)
-    feat_in = [poc_fre(rel_c, model.pos_poc), model.canonical_feat[s_i].reshape(-1, model.canonical_feat.shape[-1])]
-    if pose_embedding is not None:
-        feat_in.append(pose_embedding.expand(len(rel_c), -1))
-    out = feat_net_forward(model.feat_net, torch.cat(feat_in, dim=-1))
-    h = (out.reshape(len(s_i), K, -1) * w).sum(dim=1)
+    w, rgbs_direct, alpha_direct, feat_in = NbrAggregate.apply(
+        ray_pts, s_i, t_hat_pcd, Rinv, model.canonical_feat, pose_embedding, sig, model.canonical_rgbs.clip(0, 1),
+        model.canonical_alpha.clip(0, 1), model.pos_poc, model._eps)
+    out = feat_net_forward(model.feat_net, feat_in)
+    h = IdwSum.apply(w, out)   # 493-494
+    w = w.unsqueeze(-1)
     # heads (496-515)
     density = LIN.linear(h, model.densitynet).squeeze(-1)
     interval = float(rk['stepsize']) * float(model.tineuvox.voxel_size_ratio)

@@ -421,6 +421,32 @@ int apn_gemm_f32_splitk(const float* A, const float* A2, const float* B, float* 
                         int64_t N, int64_t K, int64_t lda, int64_t ldb, int32_t trans_a, int32_t trans_b,
                         float slope_mask, int32_t splits, void* workspace, void* stream);
 
+/* The training forward's neighbour aggregation (temporalpoints.py:452-494 under autograd,
+ * run.py:574-716): per MLP row (sample s, neighbour k = s_i[s,k]) the IDW weight w [S,8], the
+ * direct blend rgb_d [S,3] / alpha_d [S] (459-470), and the feat_net input row
+ * feat_in[8s+k] = [rel_c | sin(rel_c f) | cos(rel_c f) | canonical_feat[n] | pose_emb] (L = pos
+ * frequencies poc[L], row stride ldf); sig = mean_min_distance * max(direct_eps, 0), rgb_c /
+ * alpha_c the clipped canonical colours. */
+int apn_nbr_train_fwd(int64_t S, const float* ray_pts, const int64_t* s_i, const float* xyz, const float* Rinv,
+                      const float* canonical_feat, int32_t F, const float* pose_emb, int32_t P, const float* sig,
+                      const float* rgb_c, const float* alpha_c, const float* poc, int32_t L, float eps, float* w_out,
+                      float* rgbd, float* alphad, float* feat_in, int64_t ldf, void* stream);
+/* Its backward: from d_w [S,8], d_rgbd [S,3], d_alphad [S], d_feat [8S, ldd] (any may be NULL)
+ * the per-point gradients d_xyz [N,3], d_R [N,9], d_sig [N], d_c [N,3], d_a [N] and d_featp [N,F]
+ * (canonical_feat), summed over each point's rows in the order of the reverse adjacency
+ * rev_ptr [N+1] / rev_edge [8S] (deterministic); contrib: workspace [8S, 17]. */
+int apn_nbr_train_bwd(int64_t S, int64_t N, const float* ray_pts, const int64_t* s_i, const float* xyz,
+                      const float* Rinv, const float* sig, const float* rgb_c, const float* alpha_c, const float* poc,
+                      int32_t L, float eps, const float* d_w, const float* d_rgbd, const float* d_alphad,
+                      const float* d_feat, int64_t ldd, int32_t F, const int64_t* rev_ptr, const int64_t* rev_edge,
+                      float* contrib, float* d_xyz, float* d_R, float* d_sig, float* d_c, float* d_a, float* d_featp,
+                      void* stream);
+/* h [S,C] = sum_k w[s,k] out[8s+k, :] (temporalpoints.py:493-494) and its backward
+ * (d_out = w d_h, d_w[s,k] = <out[8s+k], d_h[s]>). */
+int apn_idw_sum_fwd(int64_t S, int32_t C, const float* w, const float* out, float* h, void* stream);
+int apn_idw_sum_bwd(int64_t S, int32_t C, const float* w, const float* out, const float* dh, float* d_out, float* d_w,
+                    void* stream);
+
 /* Utilities */
 size_t apn_scan_workspace_bytes(int64_t n);
 int apn_scan_exclusive_i32(const int32_t* in, int32_t* out, int64_t n, void* workspace, void* stream);

@@ -303,3 +303,28 @@ def test_weight_sparsity_loss_vs_float64(n, J):
     assert abs(float(loss.detach()) - float(ref)) <= 2e-6 * max(1.0, abs(float(ref)))
     err = (wd.grad.cpu().double() - w64.grad).abs() / w64.grad.abs().clamp_min(0.2 / w.numel())
     assert float(err.max()) < 1e-5, float(err.max())
+
+
+@pytest.mark.gpu
+@pytest.mark.autograd
+def test_gemm_linear_padded_rows_equal_contiguous():
+    """linear.pad_cat (feat_net's first-layer input, temporalpoints.py:488-491: posenc 63 + feature
+    128 = 191 columns, written into 192-float rows): the product read through the padded 16-B rows
+    and the gradients it returns equal those of the contiguous torch.cat input bit for bit."""
+    from apn_amd.linear import _GemmLinear, pad_cat
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(3)
+    a, b = torch.randn(5000, 63, generator=g), torch.randn(5000, 128, generator=g)
+    w, bias = torch.randn(128, 191, generator=g) / 14, torch.randn(128, generator=g)
+    dy = torch.randn(5000, 128, generator=g).to(dev)
+    res = []
+    for padded in (False, True):
+        ps = [t.to(dev).requires_grad_(True) for t in (a, b, w, bias)]
+        x = pad_cat(ps[:2]) if padded else torch.cat(ps[:2], -1)
+        if padded:
+            assert x.stride(0) == 192 and x.shape[1] == 191
+        y = _GemmLinear.apply(x, ps[2], ps[3], 0.01)
+        y.backward(dy)
+        res.append([y.detach()] + [p.grad for p in ps])
+    for u, v in zip(*res):
+        assert torch.equal(u, v)

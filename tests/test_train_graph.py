@@ -61,3 +61,71 @@ def test_graphed_warp_stage_equals_eager(dev, name):
             for p in model.parameters():
                 if p.grad is not None:
                     p.add_(p.grad, alpha=-1e-3)
+
+
+def _torch_aggregate(ray_pts, s_i, xyz, Rinv, feat, pose, sig, rgb_c, alpha_c, poc, eps):
+    """The reference composition (temporalpoints.py:452-494) in torch ops."""
+    from apn_amd.tineuvox import poc_fre
+    K = 8
+    rel_p = ray_pts[:, None, :] - xyz[s_i, :]
+    to_nn = (rel_p ** 2).sum(-1)
+    w_direct = torch.exp(-(to_nn ** 2) / (2 * sig[s_i] ** 2 + 1e-12))
+    w_dd = ((1. / K) * w_direct).unsqueeze(-1)
+    w_direct = (w_direct / (w_direct.sum(dim=-1) + 1e-12)[:, None]).unsqueeze(-1)
+    rgbd = (w_direct * rgb_c[s_i, :]).sum(dim=1)
+    alphad = (w_dd * alpha_c[s_i].unsqueeze(-1)).sum(dim=1).squeeze(-1)
+    w = 1 / (to_nn + eps)
+    w = w / w.sum(dim=-1)[:, None]
+    rel_c = (Rinv[s_i] * rel_p[:, :, None, :]).sum(-1).reshape(-1, 3)
+    parts = [poc_fre(rel_c, poc), feat[s_i].reshape(-1, feat.shape[-1])]
+    if pose is not None:
+        parts.append(pose.expand(len(rel_c), -1))
+    return w, rgbd, alphad, torch.cat(parts, -1)
+
+
+@pytest.mark.parametrize("with_pose", [False, True])
+def test_nbr_aggregate_vs_float64_autograd(dev, with_pose):
+    """NbrAggregate + IdwSum (apn_nbr_train.hip: the training forward's direct blend, IDW weights,
+    rel_c posenc, feat_net input rows and the IDW sum, forward and backward) against the torch
+    composition of temporalpoints.py:452-494 run in float64 under autograd, on random clouds with
+    shared neighbours (every gradient is a sum over several rows per point)."""
+    from apn_amd.train import NbrAggregate, IdwSum
+    g = torch.Generator().manual_seed(5 + with_pose)
+    N, S, F, P, C = 3000, 2500, 32, 7, 16
+    xyz = torch.rand(N, 3, generator=g)
+    ray_pts = xyz[torch.randint(0, N, (S,), generator=g)] + 0.01 * torch.randn(S, 3, generator=g)
+    s_i = torch.randint(0, N, (S, 8), generator=g)
+    Rinv = torch.eye(3) + 0.2 * torch.randn(N, 3, 3, generator=g)
+    feat = torch.randn(N, F, generator=g)
+    pose = torch.randn(1, P, generator=g) if with_pose else None
+    sig = 0.01 + 0.02 * torch.rand(N, generator=g)
+    rgb_c, alpha_c = torch.rand(N, 3, generator=g), torch.rand(N, generator=g)
+    poc = torch.tensor([2.0 ** i for i in range(10)])
+    eps = 1e-6
+    mats = [xyz, Rinv, feat, pose, sig, rgb_c, alpha_c]
+    K = 3 + 60 + F + (P if with_pose else 0)
+    proj = torch.randn(K, C, generator=g)
+    grads_out = [torch.randn(S, 8, generator=g), torch.randn(S, 3, generator=g), torch.randn(S, generator=g),
+                 torch.randn(S, C, generator=g)]
+
+    def run(fn, dtype, device):
+        ts = [None if m is None else m.to(device, dtype).requires_grad_(True) for m in mats]
+        w, rgbd, ad, fin = fn(ray_pts.to(device, dtype), s_i.to(device), ts[0], ts[1], ts[2], ts[3], ts[4], ts[5], ts[6],
+                              poc.to(device, dtype), eps)
+        out = fin @ proj.to(device, dtype)
+        h = IdwSum.apply(w, out) if fn is NbrAggregate.apply else (out.reshape(S, 8, -1) * w.unsqueeze(-1)).sum(1)
+        loss = sum((a * b.to(device, dtype)).sum() for a, b in zip((w, rgbd, ad, h), grads_out))
+        loss.backward()
+        return [w, rgbd, ad, fin, h], [None if t is None else t.grad for t in ts]
+
+    outs, grads = run(NbrAggregate.apply, torch.float32, dev)
+    routs, rgrads = run(_torch_aggregate, torch.float64, dev)
+    touts, tgrads = run(_torch_aggregate, torch.float32, dev)   # fp32 conditioning floor (2^9 posenc)
+    rel = lambda a, r: float((a.double() - r).abs().max() / r.abs().max())
+    for i, (a, t, r) in enumerate(zip(outs, touts, routs)):
+        assert rel(a, r) <= max(1e-5, 3 * rel(t, r)), (i, rel(a, r), rel(t, r))
+    for i, (a, t, r) in enumerate(zip(grads, tgrads, rgrads)):
+        if r is None:
+            assert a is None
+            continue
+        assert rel(a, r) <= max(1e-5, 3 * rel(t, r)), (i, rel(a, r), rel(t, r))
