@@ -88,6 +88,7 @@ SIGNATURES = {
     "apn_nbr_train_fwd": (C.c_int, [I64, P, P, P, P, P, I32, P, I32, P, P, P, P, I32, F32, P, P, P, P, I64, P]),
     "apn_nbr_train_bwd": (C.c_int, [I64, I64, P, P, P, P, P, P, P, P, I32, F32, P, P, P, P, I64, I32, P, P, P, P, P,
                                     P, P, P, P, P]),
+    "apn_cloud_bbox": (C.c_int, [P, I64, P, P, P, P]),
     "apn_idw_sum_fwd": (C.c_int, [I64, I32, P, P, P, P]),
     "apn_idw_sum_bwd": (C.c_int, [I64, I32, P, P, P, P, P, P]),
     "apn_gemm_f32_splitk": (C.c_int, [P, P, P, P, P, I64, I64, I64, I64, I64, I32, I32, F32, I32, P, P]),

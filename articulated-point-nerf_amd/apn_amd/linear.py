@@ -32,7 +32,7 @@ def _padded_rows(w: torch.Tensor) -> torch.Tensor:
 
 class _GemmLinear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, slope):
+    def forward(ctx, x, weight, bias, slope, col_pos=None):
         if x.dtype != torch.float32 or weight.dtype != torch.float32:
             raise TypeError("apn linear: float32 only")
         dev = x.device
@@ -42,16 +42,21 @@ class _GemmLinear(torch.autograd.Function):
         lda = x2.stride(0)   # rows may be padded (pad_cat): 16-B aligned rows take the vector loads
         M, K = x2.shape
         N = weight.shape[0]
-        if weight.shape[1] != K:
-            raise ValueError(f"apn linear: input width {K} vs weight {tuple(weight.shape)}")
-        w = _padded_rows(weight)
+        if col_pos is not None:   # x holds weight column j at column col_pos[j]; other columns meet zeros
+            wx = torch.zeros(N, -(-K // 4) * 4, device=dev, dtype=torch.float32)
+            wx[:, col_pos] = weight.detach()
+            w = wx[:, :K]
+        else:
+            if weight.shape[1] != K:
+                raise ValueError(f"apn linear: input width {K} vs weight {tuple(weight.shape)}")
+            w = _padded_rows(weight)
         b = bias.contiguous() if bias is not None else None
         y = torch.empty(M, N, device=dev, dtype=torch.float32)
         act = slope is not None
         call("apn_gemm_f32", ptr(x2), None, ptr(w), ptr(y), ptr(b), M, N, K, lda, w.stride(0), N, 0, 1, 0.0, int(act),
              float(slope) if act else 0.0, stream_ptr(dev))
         ctx.save_for_backward(x2, w, y if act else None)
-        ctx.slope, ctx.has_bias, ctx.in_shape = slope, bias is not None, x.shape
+        ctx.slope, ctx.has_bias, ctx.in_shape, ctx.col_pos = slope, bias is not None, x.shape, col_pos
         return y.reshape(*x.shape[:-1], N)
 
     @staticmethod
@@ -84,7 +89,9 @@ class _GemmLinear(torch.autograd.Function):
                              device=dev, dtype=torch.float32)
             call("apn_gemm_f32_splitk", ptr(dy), ptr(y), ptr(x), ptr(dw), ptr(db), N, K, M, N, x.stride(0), 1, 0, sm,
                  splits, ptr(ws), s)
-        return dx, (dw if ctx.needs_input_grad[1] else None), db, None
+            if ctx.col_pos is not None:
+                dw = dw[:, ctx.col_pos]
+        return dx, (dw if ctx.needs_input_grad[1] else None), db, None, None
 
 
 def pad_cat(parts) -> torch.Tensor:
@@ -103,15 +110,19 @@ def pad_cat(parts) -> torch.Tensor:
     return buf[:, :K]
 
 
-def linear(x: torch.Tensor, layer: torch.nn.Linear, slope=None) -> torch.Tensor:
+def linear(x: torch.Tensor, layer: torch.nn.Linear, slope=None, col_pos=None) -> torch.Tensor:
     """act(x W^T + b) for a torch.nn.Linear ``layer``; ``slope``: None (no activation), 0 (ReLU)
-    or the LeakyReLU negative slope. CPU tensors: torch's own ops."""
+    or the LeakyReLU negative slope. ``col_pos`` (CUDA, int64 [in_features]): x is wider than the
+    layer and holds input j at column col_pos[j] (zero weight on the others). CPU tensors: torch's
+    own ops."""
     if not x.is_cuda:
+        if col_pos is not None:
+            x = x[..., col_pos]
         y = torch.nn.functional.linear(x, layer.weight, layer.bias)
         if slope is None:
             return y
         return torch.relu(y) if slope == 0 else torch.nn.functional.leaky_relu(y, slope)
-    return _GemmLinear.apply(x, layer.weight, layer.bias, slope)
+    return _GemmLinear.apply(x, layer.weight, layer.bias, slope, col_pos)
 
 
 def _flatten(net):
@@ -122,24 +133,26 @@ def _flatten(net):
             yield m
 
 
-def sequential(net: torch.nn.Module, x: torch.Tensor) -> torch.Tensor:
+def sequential(net: torch.nn.Module, x: torch.Tensor, col_pos=None) -> torch.Tensor:
     """A Sequential of Linear / LeakyReLU / ReLU (nested Sequentials flattened): each Linear runs
-    with the activation that follows it fused into its epilogue."""
+    with the activation that follows it fused into its epilogue (``col_pos``: the first layer's,
+    see linear)."""
     mods = list(_flatten(net))
     i = 0
     while i < len(mods):
         m = mods[i]
         if isinstance(m, torch.nn.Linear):
             nxt = mods[i + 1] if i + 1 < len(mods) else None
+            cp, col_pos = col_pos, None
             if isinstance(nxt, torch.nn.LeakyReLU):
-                x = linear(x, m, float(nxt.negative_slope))
+                x = linear(x, m, float(nxt.negative_slope), cp)
                 i += 2
                 continue
             if isinstance(nxt, torch.nn.ReLU):
-                x = linear(x, m, 0.0)
+                x = linear(x, m, 0.0, cp)
                 i += 2
                 continue
-            x = linear(x, m)
+            x = linear(x, m, None, cp)
         else:
             x = m(x)
         i += 1

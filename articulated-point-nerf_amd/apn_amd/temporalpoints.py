@@ -188,10 +188,10 @@ def hls_palette(n, h=0.01, l=0.6, s=0.65):
 
 def project_point_to_image_plane(points, pose, intrinsic):
     """utils.py:435-450."""
-    points = torch.repeat_interleave(points.unsqueeze(0), len(pose), 0)
     pose = torch.linalg.inv_ex(pose).inverse   # == pose.inverse() without its host-side singularity check (a sync)
-    points = torch.bmm(pose[:, :3, :3], points.transpose(1, 2)).transpose(1, 2) + pose[:, :3, 3:].transpose(1, 2)
-    points = torch.bmm(intrinsic, points.transpose(1, 2)).transpose(1, 2)
+    # the two bmm's as broadcast products over the 3-vectors (elementwise kernels, no library GEMM)
+    points = (pose[:, None, :3, :3] * points[None, :, None, :]).sum(-1) + pose[:, None, :3, 3]
+    points = (intrinsic[:, None, :, :] * points[:, :, None, :]).sum(-1)
     return points[:, :, :2] / points[:, :, 2:]
 
 

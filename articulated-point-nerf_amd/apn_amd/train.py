@@ -42,6 +42,18 @@ def cloud_min_max(xyz: torch.Tensor):
     return xt.amin(dim=1), xt.amax(dim=1)
 
 
+def cloud_bbox(xyz: torch.Tensor):
+    """(min/max [6] float, bbox_ord [8] int32) of an [N,3] device cloud in two launches
+    (apn_cloud_bbox: block partials, one final block); the values equal cloud_min_max's (min and
+    max are exact) and bbox_ord equals ordered_bbox's."""
+    xyz = xyz.detach().float().contiguous()
+    mm = torch.empty(6, device=xyz.device)
+    ordv = torch.empty(8, dtype=torch.int32, device=xyz.device)
+    ws = torch.empty(1024 * 6, device=xyz.device)
+    call("apn_cloud_bbox", ptr(xyz), xyz.shape[0], ptr(mm), ptr(ordv), ptr(ws), stream_ptr(xyz.device))
+    return mm, ordv
+
+
 def ordered_bbox(xyz: torch.Tensor) -> torch.Tensor:
     """Cloud min/max as the order-preserving int32 encoding the grid kernels read
     (``float_to_ordered`` in csrc/apn_common.h), 8 slots like the LBS kernel's bbox_ord."""
@@ -141,8 +153,10 @@ class NbrAggregate(torch.autograd.Function):
     """temporalpoints.py:452-491 for the training forward as one HIP forward (apn_nbr_train_fwd) and
     one HIP backward (apn_nbr_train_bwd): (ray_pts [S,3], s_i [S,8], xyz [N,3], Rinv [N,3,3],
     canonical_feat [N,F], pose_emb [1,P] | None, sig [N], rgb_c [N,3], alpha_c [N] (clipped), poc,
-    eps) -> (w [S,8] IDW weights, rgb_d [S,3], alpha_d [S], feat_in [8S, 3+6L+F+P] in 16-B rows).
-    Per-point gradients are gathered over the reverse adjacency of s_i (no atomics)."""
+    eps) -> (w [S,8] IDW weights, rgb_d [S,3], alpha_d [S], feat_in [8S, PE4+F+P] in 16-B rows:
+    posenc (PE = 3+6L columns) zero-padded to PE4 = 4 ceil(PE/4), then the features -- feat_in_columns
+    gives where each of feat_net's first-layer inputs sits). Per-point gradients are gathered over
+    the reverse adjacency of s_i (no atomics)."""
 
     @staticmethod
     def forward(ctx, ray_pts, s_i, xyz, Rinv, feat, pose_emb, sig, rgb_c, alpha_c, poc, eps):
@@ -151,7 +165,8 @@ class NbrAggregate(torch.autograd.Function):
         F = feat.shape[1]
         P = pose_emb.shape[-1] if pose_emb is not None else 0
         L = poc.numel()
-        K = 3 + 6 * L + F + P
+        PE4 = -(-(3 + 6 * L) // 4) * 4
+        K = PE4 + F + P
         Kp = -(-K // 4) * 4
         c = lambda x: x.detach().float().contiguous()
         args = [c(ray_pts), s_i.contiguous(), c(xyz), c(Rinv), c(sig), c(rgb_c), c(alpha_c), c(poc)]
@@ -195,6 +210,20 @@ class NbrAggregate(torch.autograd.Function):
         if P > 0 and ctx.needs_input_grad[5] and d_feat is not None:
             d_pose = d_feat[:, K - P:].sum(0).reshape(ctx.pose_shape)
         return None, None, d_xyz, d_R, d_featp, d_pose, d_sig, d_c, d_a, None, None
+
+
+_FEAT_COLS = {}
+
+
+def feat_in_columns(L, F, P, device):
+    """Column of feat_in (NbrAggregate) holding each of the reference's feat_net inputs
+    [posenc (3+6L) | canonical_feat (F) | pose embedding (P)] (cached on the device)."""
+    key = (L, F, P, str(device))
+    if key not in _FEAT_COLS:
+        PE = 3 + 6 * L
+        PE4 = -(-PE // 4) * 4
+        _FEAT_COLS[key] = torch.cat([torch.arange(PE), torch.arange(PE4, PE4 + F + P)]).to(device)
+    return _FEAT_COLS[key]
 
 
 class IdwSum(torch.autograd.Function):
@@ -421,9 +450,10 @@ def warp_stage(model, t_embed):
     return xyz, Rinv, weights, bone_Ts, global_t, joints_rel, pose_embedding
 
 
-def radius_knn(model, xyz, bbox6, rk, query_radius):
+def radius_knn(model, xyz, bbox6, rk, query_radius, bbox_ord=None):
     """Sampling in bbox6 + radius-bounded exact 8-NN on the HIP path (temporalpoints.py:423-447).
-    Returns (ray_pts [S,3], ray_id [S] i64, step_id [S] i64, s_i [S,8] i64, n_inbbox); S may be 0."""
+    Returns (ray_pts [S,3], ray_id [S] i64, step_id [S] i64, s_i [S,8] i64, n_inbbox); S may be 0.
+    ``bbox_ord``: the cloud's ordered bbox when the caller has it (cloud_bbox)."""
     from .temporalpoints import CELL_CAP
     dev = xyz.device
     lib = L.load()
@@ -437,7 +467,8 @@ def radius_knn(model, xyz, bbox6, rk, query_radius):
     qr = float(query_radius)
     stepdist = float(rk['stepsize']) * float(model.voxel_size)
     near, far = float(rk['near']), float(rk['far'])
-    bbox_ord = ordered_bbox(xyz)
+    if bbox_ord is None:
+        bbox_ord = ordered_bbox(xyz)
     gws = torch.empty(int(lib.apn_grid_workspace_bytes(N, CELL_CAP)), dtype=torch.uint8, device=dev)
     sorted4 = torch.empty(N, 4, device=dev)
     call("apn_grid_build", ptr(xyz), N, ptr(bbox_ord), qr, CELL_CAP, ptr(sorted4), ptr(gws), s)
@@ -506,13 +537,12 @@ def forward_train(model, t, render_depth=False, render_kwargs=None, query_radius
     bg = rk['bg']
     # sampling bbox (423-427) and kNN (433-447)
     qr = float(query_radius)
+    mm, bbox_ord = cloud_bbox(t_hat_pcd)
     if calc_min_max:
-        xd = t_hat_pcd.detach()
-        lo, hi = cloud_min_max(xd)
-        bbox6 = torch.cat([lo - qr, hi + qr]).float().contiguous()
+        bbox6 = torch.cat([mm[:3] - qr, mm[3:] + qr]).float().contiguous()
     else:
         bbox6 = torch.cat([model.xyz_min, model.xyz_max]).float().contiguous()
-    ray_pts, ray_id, step_id, s_i, n_bbox = radius_knn(model, t_hat_pcd, bbox6, rk, qr)
+    ray_pts, ray_id, step_id, s_i, n_bbox = radius_knn(model, t_hat_pcd, bbox6, rk, qr, bbox_ord=bbox_ord)
     model.last_stats = {"rays": R, "inbbox_samples": n_bbox, "survivors": len(s_i)}
     model.last_train_knn = (ray_id, s_i)
     if len(s_i) == 0:       # NoPointsException fallback (598-609)
@@ -526,7 +556,9 @@ def forward_train(model, t, render_depth=False, render_kwargs=None, query_radius
     w, rgbs_direct, alpha_direct, feat_in = NbrAggregate.apply(
         ray_pts, s_i, t_hat_pcd, Rinv, model.canonical_feat, pose_embedding, sig, model.canonical_rgbs.clip(0, 1),
         model.canonical_alpha.clip(0, 1), model.pos_poc, model._eps)
-    out = feat_net_forward(model.feat_net, feat_in)
+    cols = feat_in_columns(model.pos_poc.numel(), model.canonical_feat.shape[1],
+                           pose_embedding.shape[-1] if pose_embedding is not None else 0, dev)
+    out = LIN.sequential(model.feat_net, feat_in, col_pos=cols)
     h = IdwSum.apply(w, out)   # 493-494
     w = w.unsqueeze(-1)
     # heads (496-515)

@@ -9,12 +9,20 @@
 //   feat_in row = [posenc | canonical_feat_n | pose embedding]      488-491
 //   h = sum_k w_k feat_net(feat_in)_k                               493-494
 //
+// feat_in row layout: [posenc (PE = 3 + 6L) | 0 pad to PE4 = 4 ceil(PE / 4) | canonical_feat (F) |
+// pose embedding (P)], so the feature columns start 16-B aligned (the caller's weight map puts W1's
+// columns at those positions and a zero column on the pad, train.py). The sin/cos come from
+// sincos_pe (the render MLP's, ~1e-7 absolute).
 // One MLP row (sample s, neighbour k) per thread, the 8 rows of a sample in 8 adjacent lanes
-// (width-8 shuffles for the sums over k). The backward writes each row's gradient terms for its
-// neighbour point (position 3, Rinv 9, sigma 1, colour 3, alpha 1) and the per-point sums are
+// (width-8 shuffles for the sums over k); 128-row blocks stage the posenc columns through LDS so
+// that feat_in / d_feat are written and read row-contiguously (the backward recomputes the same
+// sin / cos). The backward writes each row's gradient terms for its neighbour point (position 3, Rinv 9, sigma 1, colour 3, alpha 1) and the per-point sums are
 // gathered over the reverse adjacency of s_i in a fixed order (rev_ptr / rev_edge, train.py
 // reverse_csr) -- no atomics, deterministic.
 #include "apn_common.h"
+#include "apn_mlp_split.h"   // sincos_pe: the render MLP's posenc sin/cos
+
+#include <algorithm>
 
 namespace apn {
 namespace nbrt {
@@ -46,15 +54,20 @@ __device__ __forceinline__ Geo geometry(const float* __restrict__ ray_pts, const
   return g;
 }
 
-__global__ __launch_bounds__(256) void k_nbr_train_fwd(int64_t S, const float* __restrict__ ray_pts,
-                                                       const int64_t* __restrict__ s_i, const float* __restrict__ xyz,
-                                                       const float* __restrict__ Rinv, const float* __restrict__ sig,
-                                                       const float* __restrict__ rgb_c, const float* __restrict__ alpha_c,
-                                                       const float* __restrict__ poc, int L, float eps,
-                                                       float* __restrict__ w_out, float* __restrict__ rgbd,
-                                                       float* __restrict__ alphad, float* __restrict__ feat_in,
-                                                       int64_t ldf) {
-  const int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
+constexpr int RB = 128;      // rows per block of the posenc kernels
+
+__global__ __launch_bounds__(RB) void k_nbr_train_fwd(int64_t S, const float* __restrict__ ray_pts,
+                                                      const int64_t* __restrict__ s_i, const float* __restrict__ xyz,
+                                                      const float* __restrict__ Rinv, const float* __restrict__ sig,
+                                                      const float* __restrict__ rgb_c, const float* __restrict__ alpha_c,
+                                                      const float* __restrict__ poc, int L, float eps,
+                                                      float* __restrict__ w_out, float* __restrict__ rgbd,
+                                                      float* __restrict__ alphad, float* __restrict__ feat_in,
+                                                      int64_t ldf) {
+  extern __shared__ float sPE[];   // [RB][LD]
+  const int PE = 3 + 6 * L, PE4 = (PE + 3) & ~3, LD = PE | 1;   // odd LDS row stride: own-row writes spread over banks
+  const int64_t row0 = (int64_t)blockIdx.x * RB;
+  const int64_t row = row0 + threadIdx.x;
   const int64_t s = row >> 3;
   const int k = (int)(row & 7);
   const bool valid = s < S;   // a sample's 8 lanes are valid together (S * 8 rows)
@@ -64,49 +77,74 @@ __global__ __launch_bounds__(256) void k_nbr_train_fwd(int64_t S, const float* _
   const float wd = g.e / (E + 1e-12f);
   float c0 = sum8(wd * rgb_c[3 * n]), c1 = sum8(wd * rgb_c[3 * n + 1]), c2 = sum8(wd * rgb_c[3 * n + 2]);
   const float ad = sum8((0.125f * g.e) * alpha_c[n]);
-  if (!valid) return;
-  w_out[row] = g.w0 / W0;
-  if (k == 0) {
-    rgbd[3 * s] = c0; rgbd[3 * s + 1] = c1; rgbd[3 * s + 2] = c2;
-    alphad[s] = ad;
+  if (valid) {
+    w_out[row] = g.w0 / W0;
+    if (k == 0) {
+      rgbd[3 * s] = c0; rgbd[3 * s + 1] = c1; rgbd[3 * s + 2] = c2;
+      alphad[s] = ad;
+    }
   }
   const float* R = Rinv + 9 * n;
   float rc[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) rc[i] = (R[3 * i] * g.rp[0] + R[3 * i + 1] * g.rp[1]) + R[3 * i + 2] * g.rp[2];
-  float* f = feat_in + row * ldf;
+  float* f = sPE + threadIdx.x * LD;
 #pragma unroll
   for (int d = 0; d < 3; ++d) f[d] = rc[d];
   for (int d = 0; d < 3; ++d)
     for (int l = 0; l < L; ++l) {
-      const float a = rc[d] * poc[l];
-      f[3 + d * L + l] = sinf(a);
-      f[3 + 3 * L + d * L + l] = cosf(a);
+      float sn, cs;
+      mlpx::sincos_pe(rc[d] * poc[l], sn, cs);
+      f[3 + d * L + l] = sn;
+      f[3 + 3 * L + d * L + l] = cs;
     }
+  __syncthreads();
+  const int64_t nrows = min((int64_t)RB, S * 8 - row0);
+  for (int i = threadIdx.x; i < nrows * PE4; i += RB) {
+    const int r = i / PE4, c = i - r * PE4;
+    feat_in[(row0 + r) * ldf + c] = c < PE ? sPE[r * LD + c] : 0.f;
+  }
 }
 
-// feat_in[row, col0 + c] = src[idx[row], c] (idx = s_i, or none: row 0 of src for every row --
-// the pose embedding), 64 lanes per row.
+// feat_in[row, col0 + c] = src[idx[row], c] (idx = s_i, or none: row 0 of src for every row -- the
+// pose embedding): one thread per 16-B chunk when F, col0 and ldd are multiples of 4, else per float.
 __global__ __launch_bounds__(256) void k_gather_rows(int64_t rows, const int64_t* __restrict__ idx,
                                                      const float* __restrict__ src, int F, float* __restrict__ dst,
-                                                     int64_t ldd, int col0) {
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= rows) return;
-  const float* a = src + (idx ? idx[r] : 0) * (int64_t)F;
-  float* b = dst + r * ldd + col0;
-  for (int c = threadIdx.x & 63; c < F; c += 64) b[c] = a[c];
+                                                     int64_t ldd, int col0, int vec) {
+  const int W = vec ? F / 4 : F;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < rows * W; t += (int64_t)gridDim.x * 256) {
+    const int64_t r = t / W;
+    const int c = (int)(t - r * W);
+    const float* a = src + (idx ? idx[r] : 0) * (int64_t)F;
+    float* b = dst + r * ldd + col0;
+    if (vec)
+      *(float4*)(b + 4 * c) = *(const float4*)(a + 4 * c);
+    else
+      b[c] = a[c];
+  }
 }
 
-__global__ __launch_bounds__(256) void k_nbr_train_bwd(int64_t S, const float* __restrict__ ray_pts,
-                                                       const int64_t* __restrict__ s_i, const float* __restrict__ xyz,
-                                                       const float* __restrict__ Rinv, const float* __restrict__ sig,
-                                                       const float* __restrict__ rgb_c, const float* __restrict__ alpha_c,
-                                                       const float* __restrict__ poc, int L, float eps,
-                                                       const float* __restrict__ d_w, const float* __restrict__ d_rgbd,
-                                                       const float* __restrict__ d_alphad,
-                                                       const float* __restrict__ d_feat, int64_t ldd,
-                                                       float* __restrict__ contrib) {
-  const int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
+__global__ __launch_bounds__(RB) void k_nbr_train_bwd(int64_t S, const float* __restrict__ ray_pts,
+                                                      const int64_t* __restrict__ s_i, const float* __restrict__ xyz,
+                                                      const float* __restrict__ Rinv, const float* __restrict__ sig,
+                                                      const float* __restrict__ rgb_c, const float* __restrict__ alpha_c,
+                                                      const float* __restrict__ poc, int L, float eps,
+                                                      const float* __restrict__ d_w, const float* __restrict__ d_rgbd,
+                                                      const float* __restrict__ d_alphad,
+                                                      const float* __restrict__ d_feat, int64_t ldd,
+                                                      float* __restrict__ contrib) {
+  extern __shared__ float sD[];   // [RB][LD]
+  const int PE = 3 + 6 * L, LD = PE | 1;
+  const int64_t row0 = (int64_t)blockIdx.x * RB;
+  const int64_t nrows = min((int64_t)RB, S * 8 - row0);
+  if (d_feat) {   // the block's posenc gradient and values, read row-contiguously
+    for (int i = threadIdx.x; i < nrows * PE; i += RB) {
+      const int r = i / PE, c = i - r * PE;
+      sD[r * LD + c] = d_feat[(row0 + r) * ldd + c];
+    }
+    __syncthreads();
+  }
+  const int64_t row = row0 + threadIdx.x;
   const int64_t s = row >> 3;
   const bool valid = s < S;
   const int64_t n = valid ? s_i[row] : 0;
@@ -123,7 +161,7 @@ __global__ __launch_bounds__(256) void k_nbr_train_bwd(int64_t S, const float* _
   const float ga = d_alphad ? d_alphad[ss] : 0.f;
   const float dwd = (g0 * c[0] + g1 * c[1]) + g2 * c[2];
   const float sum_dwd_wd = sum8(valid ? dwd * wd : 0.f);
-  float de = (dwd - sum_dwd_wd) / Ee + ga * 0.125f * a;
+  const float de = (dwd - sum_dwd_wd) / Ee + ga * 0.125f * a;
   // e = exp(-t^2 / D): d t, d D (-> d sig = dD * 4 sig)
   const float dt_direct = de * g.e * (-2.f * g.t / g.D);
   const float dD = de * g.e * (g.t * g.t) / (g.D * g.D);
@@ -133,20 +171,21 @@ __global__ __launch_bounds__(256) void k_nbr_train_bwd(int64_t S, const float* _
   const float sum_dw_w = sum8(valid ? dwv * w : 0.f);
   const float dw0 = (dwv - sum_dw_w) / W0;
   const float dt = dt_direct - dw0 * g.w0 * g.w0;
-  // posenc -> rel_c
+  // posenc -> rel_c: d/dx [x, sin(x f), cos(x f)] = [1, f cos, -f sin] (the forward's sincos_pe)
   const float* R = Rinv + 9 * n;
   float rc[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) rc[i] = (R[3 * i] * g.rp[0] + R[3 * i + 1] * g.rp[1]) + R[3 * i + 2] * g.rp[2];
   float drc[3] = {0.f, 0.f, 0.f};
   if (d_feat && valid) {
-    const float* df = d_feat + row * ldd;
+    const float* df = sD + threadIdx.x * LD;
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
       float acc = df[d];
       for (int l = 0; l < L; ++l) {
-        const float f = poc[l], x = rc[d] * f;
-        acc += f * (cosf(x) * df[3 + d * L + l] - sinf(x) * df[3 + 3 * L + d * L + l]);
+        float sn, cs;
+        mlpx::sincos_pe(rc[d] * poc[l], sn, cs);
+        acc += poc[l] * (cs * df[3 + d * L + l] - sn * df[3 + 3 * L + d * L + l]);
       }
       drc[d] = acc;
     }
@@ -194,17 +233,73 @@ __global__ __launch_bounds__(256) void k_nbr_train_gather(int64_t N, const int64
   d_a[n] = acc[16];
 }
 
-// d_feat_pt[n, c] = sum over n's rows of d_feat[row, col0 + c], 64 lanes per point.
+// d_feat_pt[n, c] = sum over n's rows of d_feat[row, col0 + c]: one thread per 16-B chunk of a
+// point's F columns when vec (F, col0, ldd multiples of 4), else per float.
 __global__ __launch_bounds__(256) void k_feat_gather(int64_t N, const int64_t* __restrict__ rev_ptr,
                                                      const int64_t* __restrict__ rev_edge, const float* __restrict__ d_feat,
-                                                     int64_t ldd, int col0, int F, float* __restrict__ out) {
-  const int64_t n = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (n >= N) return;
-  const int64_t e0 = rev_ptr[n], e1 = rev_ptr[n + 1];
-  for (int c = threadIdx.x & 63; c < F; c += 64) {
-    float acc = 0.f;
-    for (int64_t e = e0; e < e1; ++e) acc += d_feat[rev_edge[e] * ldd + col0 + c];
-    out[n * (int64_t)F + c] = acc;
+                                                     int64_t ldd, int col0, int F, int vec, float* __restrict__ out) {
+  const int W = vec ? F / 4 : F;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < N * W; t += (int64_t)gridDim.x * 256) {
+    const int64_t n = t / W;
+    const int c = (int)(t - n * W);
+    const int64_t e0 = rev_ptr[n], e1 = rev_ptr[n + 1];
+    if (vec) {
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int64_t e = e0; e < e1; ++e) {
+        const float4 v = *(const float4*)(d_feat + rev_edge[e] * ldd + col0 + 4 * c);
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+      *(float4*)(out + n * (int64_t)F + 4 * c) = acc;
+    } else {
+      float acc = 0.f;
+      for (int64_t e = e0; e < e1; ++e) acc += d_feat[rev_edge[e] * ldd + col0 + c];
+      out[n * (int64_t)F + c] = acc;
+    }
+  }
+}
+
+// Cloud bounding box: per-block min / max of xyz [N,3] (exact), then one block over the partials;
+// out6 = {min x, y, z, max x, y, z}, ord8 = the order-preserving int32 encoding of out6 (the grid
+// kernels' bbox_ord, apn_common.h float_to_ordered) or NULL.
+__global__ __launch_bounds__(256) void k_bbox_part(int64_t N, const float* __restrict__ xyz, float* __restrict__ part) {
+  float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < N; i += (int64_t)gridDim.x * 256)
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      const float v = xyz[3 * i + a];
+      lo[a] = fminf(lo[a], v);
+      hi[a] = fmaxf(hi[a], v);
+    }
+  __shared__ float sl[3][256], sh[3][256];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) { sl[a][threadIdx.x] = lo[a]; sh[a][threadIdx.x] = hi[a]; }
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o)
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        sl[a][threadIdx.x] = fminf(sl[a][threadIdx.x], sl[a][threadIdx.x + o]);
+        sh[a][threadIdx.x] = fmaxf(sh[a][threadIdx.x], sh[a][threadIdx.x + o]);
+      }
+    __syncthreads();
+  }
+  if (threadIdx.x < 3) {
+    part[6 * blockIdx.x + threadIdx.x] = sl[threadIdx.x][0];
+    part[6 * blockIdx.x + 3 + threadIdx.x] = sh[threadIdx.x][0];
+  }
+}
+
+__global__ __launch_bounds__(64) void k_bbox_final(int nb, const float* __restrict__ part, float* __restrict__ out6,
+                                                   int* __restrict__ ord8) {
+  if (threadIdx.x >= 6) return;
+  const int j = threadIdx.x;
+  float v = part[j];
+  for (int b = 1; b < nb; ++b) v = j < 3 ? fminf(v, part[6 * b + j]) : fmaxf(v, part[6 * b + j]);
+  out6[j] = v;
+  if (ord8) {
+    const int i = __float_as_int(v);
+    ord8[j] = i >= 0 ? i : (i ^ 0x7fffffff);
+    if (j < 2) ord8[6 + j] = 0;
   }
 }
 
@@ -259,19 +354,23 @@ extern "C" int apn_nbr_train_fwd(int64_t S, const float* ray_pts, const int64_t*
                                  int32_t P, const float* sig, const float* rgb_c, const float* alpha_c,
                                  const float* poc, int32_t L, float eps, float* w_out, float* rgbd, float* alphad,
                                  float* feat_in, int64_t ldf, void* stream) {
-  if (S < 0 || L < 0 || L > 64 || F < 0 || P < 0 || ldf < 3 + 6 * (int64_t)L + F + P) return APN_ERR_ARG;
+  if (S < 0 || L < 0 || L > 16 || F < 0 || P < 0 || ldf < ((3 + 6 * (int64_t)L + 3) & ~3) + F + P) return APN_ERR_ARG;
   if (S == 0) return APN_OK;
   hipStream_t st = (hipStream_t)stream;
   const int64_t rows = S * 8;
-  hipLaunchKernelGGL(nbrt::k_nbr_train_fwd, dim3((unsigned)ceil_div(rows, 256)), dim3(256), 0, st, S, ray_pts, s_i,
-                     xyz, Rinv, sig, rgb_c, alpha_c, poc, L, eps, w_out, rgbd, alphad, feat_in, ldf);
-  const int pe = 3 + 6 * L;
-  if (F > 0)
-    hipLaunchKernelGGL(nbrt::k_gather_rows, dim3((unsigned)ceil_div(rows, 4)), dim3(256), 0, st, rows, s_i,
-                       canonical_feat, F, feat_in, ldf, pe);
-  if (P > 0)
-    hipLaunchKernelGGL(nbrt::k_gather_rows, dim3((unsigned)ceil_div(rows, 4)), dim3(256), 0, st, rows,
-                       (const int64_t*)nullptr, pose_emb, P, feat_in, ldf, pe + F);
+  const size_t lds = (size_t)nbrt::RB * ((3 + 6 * L) | 1) * sizeof(float);
+  hipLaunchKernelGGL(nbrt::k_nbr_train_fwd, dim3((unsigned)ceil_div(rows, nbrt::RB)), dim3(nbrt::RB), lds, st, S,
+                     ray_pts, s_i, xyz, Rinv, sig, rgb_c, alpha_c, poc, L, eps, w_out, rgbd, alphad, feat_in, ldf);
+  const int pe4 = (3 + 6 * L + 3) & ~3;
+  const bool al = ldf % 4 == 0 && ((uintptr_t)feat_in % 16) == 0;
+  auto gather = [&](const int64_t* idx, const float* src, int W, int col0) {
+    const int vec = al && W % 4 == 0 && col0 % 4 == 0 && ((uintptr_t)src % 16) == 0;
+    const int64_t work = rows * (vec ? W / 4 : W);
+    hipLaunchKernelGGL(nbrt::k_gather_rows, dim3((unsigned)std::min<int64_t>(ceil_div(work, 256), 65536)), dim3(256), 0,
+                       st, rows, idx, src, W, feat_in, ldf, col0, vec);
+  };
+  if (F > 0) gather(s_i, canonical_feat, F, pe4);
+  if (P > 0) gather(nullptr, pose_emb, P, pe4 + F);
   return launch_status();
 }
 
@@ -281,18 +380,23 @@ extern "C" int apn_nbr_train_bwd(int64_t S, int64_t N, const float* ray_pts, con
                                  const float* d_alphad, const float* d_feat, int64_t ldd, int32_t F,
                                  const int64_t* rev_ptr, const int64_t* rev_edge, float* contrib, float* d_xyz,
                                  float* d_R, float* d_sig, float* d_c, float* d_a, float* d_featp, void* stream) {
-  if (S < 0 || N < 0 || L < 0 || L > 64 || !contrib) return APN_ERR_ARG;
+  if (S < 0 || N < 0 || L < 0 || L > 16 || !contrib) return APN_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
   const int64_t rows = S * 8;
   if (rows > 0)
-    hipLaunchKernelGGL(nbrt::k_nbr_train_bwd, dim3((unsigned)ceil_div(rows, 256)), dim3(256), 0, st, S, ray_pts, s_i,
-                       xyz, Rinv, sig, rgb_c, alpha_c, poc, L, eps, d_w, d_rgbd, d_alphad, d_feat, ldd, contrib);
+    hipLaunchKernelGGL(nbrt::k_nbr_train_bwd, dim3((unsigned)ceil_div(rows, nbrt::RB)), dim3(nbrt::RB),
+                       (size_t)nbrt::RB * ((3 + 6 * L) | 1) * sizeof(float), st, S, ray_pts, s_i, xyz, Rinv, sig, rgb_c,
+                       alpha_c, poc, L, eps, d_w, d_rgbd, d_alphad, d_feat, ldd, contrib);
   if (N > 0) {
     hipLaunchKernelGGL(nbrt::k_nbr_train_gather, dim3((unsigned)ceil_div(N, 256)), dim3(256), 0, st, N, rev_ptr,
                        rev_edge, contrib, d_xyz, d_R, d_sig, d_c, d_a);
-    if (d_featp && d_feat && F > 0)
-      hipLaunchKernelGGL(nbrt::k_feat_gather, dim3((unsigned)ceil_div(N, 4)), dim3(256), 0, st, N, rev_ptr, rev_edge,
-                         d_feat, ldd, 3 + 6 * L, F, d_featp);
+    if (d_featp && d_feat && F > 0) {
+      const int col0 = (3 + 6 * L + 3) & ~3;
+      const int vec = F % 4 == 0 && ldd % 4 == 0 && ((uintptr_t)d_feat % 16) == 0 && ((uintptr_t)d_featp % 16) == 0;
+      const int64_t work = N * (vec ? F / 4 : F);
+      hipLaunchKernelGGL(nbrt::k_feat_gather, dim3((unsigned)std::min<int64_t>(ceil_div(work, 256), 65536)), dim3(256), 0,
+                         st, N, rev_ptr, rev_edge, d_feat, ldd, col0, F, vec, d_featp);
+    }
   }
   return launch_status();
 }
@@ -311,5 +415,14 @@ extern "C" int apn_idw_sum_bwd(int64_t S, int32_t C, const float* w, const float
   if (S == 0) return APN_OK;
   hipLaunchKernelGGL(nbrt::k_idw_sum_bwd, dim3((unsigned)ceil_div(S, 4)), dim3(256), 0, (hipStream_t)stream, S, C, w,
                      out, dh, d_out, d_w);
+  return launch_status();
+}
+
+extern "C" int apn_cloud_bbox(const float* xyz, int64_t N, float* out6, int32_t* ord8, void* workspace, void* stream) {
+  if (N <= 0 || !xyz || !out6 || !workspace) return APN_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  const int nb = (int)std::min<int64_t>(ceil_div(N, 256), 1024);
+  hipLaunchKernelGGL(nbrt::k_bbox_part, dim3(nb), dim3(256), 0, st, N, xyz, (float*)workspace);
+  hipLaunchKernelGGL(nbrt::k_bbox_final, dim3(1), dim3(64), 0, st, nb, (const float*)workspace, out6, ord8);
   return launch_status();
 }

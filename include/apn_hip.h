@@ -424,9 +424,9 @@ int apn_gemm_f32_splitk(const float* A, const float* A2, const float* B, float* 
 /* The training forward's neighbour aggregation (temporalpoints.py:452-494 under autograd,
  * run.py:574-716): per MLP row (sample s, neighbour k = s_i[s,k]) the IDW weight w [S,8], the
  * direct blend rgb_d [S,3] / alpha_d [S] (459-470), and the feat_net input row
- * feat_in[8s+k] = [rel_c | sin(rel_c f) | cos(rel_c f) | canonical_feat[n] | pose_emb] (L = pos
- * frequencies poc[L], row stride ldf); sig = mean_min_distance * max(direct_eps, 0), rgb_c /
- * alpha_c the clipped canonical colours. */
+ * feat_in[8s+k] = [rel_c | sin(rel_c f) | cos(rel_c f) | 0 pad to a multiple of 4 | canonical_feat[n]
+ * | pose_emb] (L <= 16 pos frequencies poc[L], row stride ldf); sig = mean_min_distance *
+ * max(direct_eps, 0), rgb_c / alpha_c the clipped canonical colours. */
 int apn_nbr_train_fwd(int64_t S, const float* ray_pts, const int64_t* s_i, const float* xyz, const float* Rinv,
                       const float* canonical_feat, int32_t F, const float* pose_emb, int32_t P, const float* sig,
                       const float* rgb_c, const float* alpha_c, const float* poc, int32_t L, float eps, float* w_out,
@@ -446,6 +446,10 @@ int apn_nbr_train_bwd(int64_t S, int64_t N, const float* ray_pts, const int64_t*
 int apn_idw_sum_fwd(int64_t S, int32_t C, const float* w, const float* out, float* h, void* stream);
 int apn_idw_sum_bwd(int64_t S, int32_t C, const float* w, const float* out, const float* dh, float* d_out, float* d_w,
                     void* stream);
+/* Bounding box of a cloud xyz [N,3]: out6 = {min, max} (exact), ord8 (optional) = its
+ * order-preserving int32 encoding (the grid kernels' bbox_ord); workspace >= 1024 * 6 floats.
+ * (temporalpoints.py:423-427 min/max of the warped cloud.) */
+int apn_cloud_bbox(const float* xyz, int64_t N, float* out6, int32_t* ord8, void* workspace, void* stream);
 
 /* Utilities */
 size_t apn_scan_workspace_bytes(int64_t n);

@@ -89,7 +89,7 @@ def test_nbr_aggregate_vs_float64_autograd(dev, with_pose):
     rel_c posenc, feat_net input rows and the IDW sum, forward and backward) against the torch
     composition of temporalpoints.py:452-494 run in float64 under autograd, on random clouds with
     shared neighbours (every gradient is a sum over several rows per point)."""
-    from apn_amd.train import NbrAggregate, IdwSum
+    from apn_amd.train import NbrAggregate, IdwSum, feat_in_columns
     g = torch.Generator().manual_seed(5 + with_pose)
     N, S, F, P, C = 3000, 2500, 32, 7, 16
     xyz = torch.rand(N, 3, generator=g)
@@ -112,8 +112,10 @@ def test_nbr_aggregate_vs_float64_autograd(dev, with_pose):
         ts = [None if m is None else m.to(device, dtype).requires_grad_(True) for m in mats]
         w, rgbd, ad, fin = fn(ray_pts.to(device, dtype), s_i.to(device), ts[0], ts[1], ts[2], ts[3], ts[4], ts[5], ts[6],
                               poc.to(device, dtype), eps)
+        if fn is not _torch_aggregate:   # the padded column layout -> the reference's
+            fin = fin[:, feat_in_columns(len(poc), F, P if with_pose else 0, device)]
         out = fin @ proj.to(device, dtype)
-        h = IdwSum.apply(w, out) if fn is NbrAggregate.apply else (out.reshape(S, 8, -1) * w.unsqueeze(-1)).sum(1)
+        h = IdwSum.apply(w, out) if fn is not _torch_aggregate else (out.reshape(S, 8, -1) * w.unsqueeze(-1)).sum(1)
         loss = sum((a * b.to(device, dtype)).sum() for a, b in zip((w, rgbd, ad, h), grads_out))
         loss.backward()
         return [w, rgbd, ad, fin, h], [None if t is None else t.grad for t in ts]
@@ -129,3 +131,16 @@ def test_nbr_aggregate_vs_float64_autograd(dev, with_pose):
             assert a is None
             continue
         assert rel(a, r) <= max(1e-5, 3 * rel(t, r)), (i, rel(a, r), rel(t, r))
+
+
+@pytest.mark.parametrize("N", [1, 1000, 300_001])
+def test_cloud_bbox_equals_torch_min_max(dev, N):
+    """apn_cloud_bbox (the training forward's sampling bbox and grid bbox, temporalpoints.py:423-427)
+    equals torch's min / max exactly, and its ordered encoding equals ordered_bbox's."""
+    from apn_amd.train import cloud_bbox, cloud_min_max, ordered_bbox
+    g = torch.Generator().manual_seed(N)
+    xyz = (torch.randn(N, 3, generator=g) * torch.tensor([1.0, 0.2, 3.0]) - 0.5).to(dev)
+    mm, o = cloud_bbox(xyz)
+    lo, hi = cloud_min_max(xyz)
+    assert torch.equal(mm, torch.cat([lo, hi]))
+    assert torch.equal(o, ordered_bbox(xyz))
