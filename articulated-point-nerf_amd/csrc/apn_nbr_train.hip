@@ -289,17 +289,35 @@ __global__ __launch_bounds__(256) void k_bbox_part(int64_t N, const float* __res
   }
 }
 
-__global__ __launch_bounds__(64) void k_bbox_final(int nb, const float* __restrict__ part, float* __restrict__ out6,
-                                                   int* __restrict__ ord8) {
-  if (threadIdx.x >= 6) return;
-  const int j = threadIdx.x;
-  float v = part[j];
-  for (int b = 1; b < nb; ++b) v = j < 3 ? fminf(v, part[6 * b + j]) : fmaxf(v, part[6 * b + j]);
-  out6[j] = v;
-  if (ord8) {
-    const int i = __float_as_int(v);
-    ord8[j] = i >= 0 ? i : (i ^ 0x7fffffff);
-    if (j < 2) ord8[6 + j] = 0;
+__global__ __launch_bounds__(256) void k_bbox_final(int nb, const float* __restrict__ part, float* __restrict__ out6,
+                                                    int* __restrict__ ord8) {
+  __shared__ float sp[6][256];
+  float v[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) v[j] = j < 3 ? INFINITY : -INFINITY;
+  for (int b = threadIdx.x; b < nb; b += 256)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) v[j] = j < 3 ? fminf(v[j], part[6 * b + j]) : fmaxf(v[j], part[6 * b + j]);
+#pragma unroll
+  for (int j = 0; j < 6; ++j) sp[j][threadIdx.x] = v[j];
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o)
+#pragma unroll
+      for (int j = 0; j < 6; ++j)
+        sp[j][threadIdx.x] = j < 3 ? fminf(sp[j][threadIdx.x], sp[j][threadIdx.x + o])
+                                   : fmaxf(sp[j][threadIdx.x], sp[j][threadIdx.x + o]);
+    __syncthreads();
+  }
+  if (threadIdx.x < 6) {
+    const int j = threadIdx.x;
+    const float r = sp[j][0];
+    out6[j] = r;
+    if (ord8) {
+      const int i = __float_as_int(r);
+      ord8[j] = i >= 0 ? i : (i ^ 0x7fffffff);
+      if (j < 2) ord8[6 + j] = 0;
+    }
   }
 }
 
@@ -423,6 +441,6 @@ extern "C" int apn_cloud_bbox(const float* xyz, int64_t N, float* out6, int32_t*
   hipStream_t st = (hipStream_t)stream;
   const int nb = (int)std::min<int64_t>(ceil_div(N, 256), 1024);
   hipLaunchKernelGGL(nbrt::k_bbox_part, dim3(nb), dim3(256), 0, st, N, xyz, (float*)workspace);
-  hipLaunchKernelGGL(nbrt::k_bbox_final, dim3(1), dim3(64), 0, st, nb, (const float*)workspace, out6, ord8);
+  hipLaunchKernelGGL(nbrt::k_bbox_final, dim3(1), dim3(256), 0, st, nb, (const float*)workspace, out6, ord8);
   return launch_status();
 }
