@@ -83,6 +83,7 @@ SIGNATURES = {
     "apn_scan_workspace_bytes": (SZ, [I64]),
     "apn_scan_exclusive_i32": (C.c_int, [P, P, I64, P, P]),
     "apn_version": (C.c_char_p, []),
+    "apn_adam_multi": (C.c_int, [I32, P, P, P, P, P, P, P, P, P, P, P, P]),
     "apn_gemm_f32": (C.c_int, [P, P, P, P, P, I64, I64, I64, I64, I64, I64, I32, I32, F32, I32, F32, P]),
     "apn_gemm_f32_splitk_workspace_bytes": (SZ, [I64, I64, I32]),
     "apn_nbr_train_fwd": (C.c_int, [I64, P, P, P, P, P, I32, P, I32, P, P, P, P, I32, F32, P, P, P, P, I64, P]),

@@ -62,6 +62,30 @@ def adam_upd_with_perlr(param, grad, exp_avg, exp_avg_sq, perlr, step, beta1, be
     _bump(param, exp_avg, exp_avg_sq)
 
 
+MULTI_MAX = 24   # tensors per apn_adam_multi launch
+
+
+def adam_multi(batch):
+    """One apn_adam_multi launch over [(param, grad, exp_avg, exp_avg_sq, step, beta1, beta2, lr,
+    eps, masked)] (<= MULTI_MAX, contiguous fp32 device tensors): each tensor updated exactly as by
+    adam_upd / masked_adam_upd."""
+    import ctypes as C
+    n = len(batch)
+    if n == 0:
+        return
+    if n > MULTI_MAX:
+        raise ValueError(f"adam_multi: at most {MULTI_MAX} tensors per launch")
+    col = list(zip(*batch))
+    ptrs = lambda ts: (C.c_void_p * n)(*[t.data_ptr() for t in ts])
+    for t in col[1]:
+        L.require_cuda(t, what="adam_multi")
+    call("apn_adam_multi", n, ptrs(col[0]), ptrs(col[1]), ptrs(col[2]), ptrs(col[3]),
+         (C.c_int64 * n)(*[t.numel() for t in col[0]]), (C.c_int32 * n)(*[int(x) for x in col[4]]),
+         (C.c_float * n)(*col[5]), (C.c_float * n)(*col[6]), (C.c_float * n)(*col[7]), (C.c_float * n)(*col[8]),
+         (C.c_int32 * n)(*[int(x) for x in col[9]]), stream_ptr(col[0][0].device))
+    _bump(*col[0], *col[2], *col[3])
+
+
 def total_variation_add_grad(param, grad, wx, wy, wz, dense_mode):
     """total_variation_kernel.cu:13-67: grad += clamped neighbour differences of the 5-D grid
     param [1, C, I, J, K] (weights / 6; the reference weights the I direction with wz)."""
@@ -96,6 +120,7 @@ class MaskedAdam(torch.optim.Optimizer):
 
     @torch.no_grad()
     def step(self):
+        batch = []   # (param, grad, exp_avg, exp_avg_sq, step, beta1, beta2, lr, eps, masked): one launch
         for group in self.param_groups:
             lr = group['lr']
             beta1, beta2 = group['betas']
@@ -113,9 +138,15 @@ class MaskedAdam(torch.optim.Optimizer):
                 if self.per_lr is not None and param.shape == self.per_lr.shape:
                     adam_upd_with_perlr(param, param.grad, state['exp_avg'], state['exp_avg_sq'], self.per_lr,
                                         state['step'], beta1, beta2, lr, eps)
+                elif param.is_cuda and param.is_contiguous() and param.grad.is_contiguous() \
+                        and param.dtype == torch.float32 and param.grad.dtype == torch.float32:
+                    batch.append((param, param.grad, state['exp_avg'], state['exp_avg_sq'], state['step'], beta1,
+                                  beta2, lr, eps, bool(skip_zero_grad)))
                 elif skip_zero_grad:
                     masked_adam_upd(param, param.grad, state['exp_avg'], state['exp_avg_sq'], state['step'], beta1,
                                     beta2, lr, eps)
                 else:
                     adam_upd(param, param.grad, state['exp_avg'], state['exp_avg_sq'], state['step'], beta1, beta2,
                              lr, eps)
+        for i in range(0, len(batch), MULTI_MAX):
+            adam_multi(batch[i:i + MULTI_MAX])

@@ -435,7 +435,16 @@ class TemporalPoints(torch.nn.Module):
         return ((self.og_joint_distance.to(joint_distance.device) - joint_distance) ** 2).sum()
 
     def get_joint_chamfer_loss(self):
-        _, c2 = self.get_chamfer_loss(self.skeleton_pcd.to(self.joints.device), self.joints, c=None, get_raw=True)
+        dev = self.joints.device
+        sk = self.skeleton_pcd
+        if sk.device != dev:   # a device copy kept beside the (CPU) skeleton cloud: no per-step host copy
+            key = (str(dev), sk.data_ptr(), sk._version)
+            hit = self.__dict__.get("_skeleton_pcd_dev")
+            if hit is None or hit[0] != key:
+                hit = (key, sk.to(dev))
+                self.__dict__["_skeleton_pcd_dev"] = hit
+            sk = hit[1]
+        _, c2 = self.get_chamfer_loss(sk, self.joints, c=None, get_raw=True)
         return c2.sum()
 
     def _rho(self, x, c):

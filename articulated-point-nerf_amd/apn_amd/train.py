@@ -145,7 +145,9 @@ def reverse_index(idx: torch.Tensor, n_targets: int):
     flat = idx.reshape(-1)
     rev_edge = torch.argsort(flat, stable=True).contiguous()
     rev_ptr = torch.zeros(n_targets + 1, dtype=torch.int64, device=idx.device)
-    rev_ptr[1:] = torch.cumsum(torch.bincount(flat, minlength=n_targets), 0)
+    # counts by index_add (bincount reads its bound back to the host)
+    counts = torch.zeros(n_targets, dtype=torch.int64, device=idx.device).index_add_(0, flat, torch.ones_like(flat))
+    rev_ptr[1:] = torch.cumsum(counts, 0)
     return rev_ptr, rev_edge
 
 
@@ -575,13 +577,13 @@ def forward_train(model, t, render_depth=False, render_kwargs=None, query_radius
     lbsw = (weights[s_i, :] * w).sum(dim=1) if render_weights else None
     ray_id_d = ray_id
     thr = model.fast_color_thres
-    # pre-masks (611-627)
+    # pre-masks (611-627) as zeroed alphas instead of dropped samples (no host sync for the count):
+    # a zero alpha leaves the ray's transmittance and every other weight bit-identical, gets weight
+    # 0 and no gradient, as a dropped sample would
+    zero = alpha.new_zeros(())
     if thr > 0:
-        m = torch.where(alpha > thr)[0]
-        ray_id, step_id, alpha, rgbs = ray_id[m], step_id[m], alpha[m], rgbs[m]
-        lbsw = lbsw[m] if lbsw is not None else None
-        md = torch.where(alpha_direct > thr)[0]
-        ray_id_d, alpha_direct, rgbs_direct = ray_id_d[md], alpha_direct[md], rgbs_direct[md]
+        alpha = torch.where(alpha > thr, alpha, zero)
+        alpha_direct = torch.where(alpha_direct > thr, alpha_direct, zero)
 
     def a2w(a, rid):
         if a.numel() == 0:
@@ -589,13 +591,10 @@ def forward_train(model, t, render_depth=False, render_kwargs=None, query_radius
         return Alphas2Weights.apply(a.contiguous(), rid.contiguous(), R)
     weights_r, alphainv_last = a2w(alpha, ray_id)
     weights_d, alphainv_last_d = a2w(alpha_direct, ray_id_d)
-    # post-masks (633-651)
+    # post-masks (633-651), zeroed the same way: the ray sums add exact zeros
     if thr > 0:
-        m = torch.where(weights_r > thr)[0]
-        weights_r, ray_id, step_id, rgbs = weights_r[m], ray_id[m], step_id[m], rgbs[m]
-        lbsw = lbsw[m] if lbsw is not None else None
-        md = torch.where(weights_d > thr)[0]
-        weights_d, ray_id_d, rgbs_direct = weights_d[md], ray_id_d[md], rgbs_direct[md]
+        weights_r = torch.where(weights_r > thr, weights_r, zero)
+        weights_d = torch.where(weights_d > thr, weights_d, zero)
     # ray sums (653-677)
     rgb_marched = _ray_sum(weights_r.unsqueeze(-1) * rgbs, ray_id, R) + alphainv_last.unsqueeze(-1) * bg
     rgb_marched_d = _ray_sum(weights_d.unsqueeze(-1) * rgbs_direct, ray_id_d, R) + alphainv_last_d.unsqueeze(-1) * bg

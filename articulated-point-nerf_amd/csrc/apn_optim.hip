@@ -123,6 +123,58 @@ static int launch_adam(float* param, const float* grad, float* m, float* v, cons
 
 using namespace apn;
 
+// Multi-tensor form (MaskedAdam.step over every parameter tensor of a step in ONE launch): the
+// tensors' pointers, sizes and per-tensor step sizes travel as kernel arguments (up to
+// ADAM_MULTI_MAX tensors per launch); block b works on the tensor whose block range holds b, with
+// the same per-element update (adam_elem, the same step size) as apn_adam_upd /
+// apn_masked_adam_upd -- bit-identical to one launch per tensor.
+constexpr int ADAM_MULTI_MAX = 24;
+struct AdamMulti {
+  float* p[ADAM_MULTI_MAX];
+  const float* g[ADAM_MULTI_MAX];
+  float* m[ADAM_MULTI_MAX];
+  float* v[ADAM_MULTI_MAX];
+  int64_t n[ADAM_MULTI_MAX];
+  int block0[ADAM_MULTI_MAX + 1];   // first block of tensor i (block0[count] = grid)
+  float step_size[ADAM_MULTI_MAX], b1[ADAM_MULTI_MAX], b2[ADAM_MULTI_MAX], eps[ADAM_MULTI_MAX];
+  int masked[ADAM_MULTI_MAX];
+  int count;
+};
+
+__global__ __launch_bounds__(256) void k_adam_multi(AdamMulti a) {
+  int i = 0;
+  while (i + 1 < a.count && (int)blockIdx.x >= a.block0[i + 1]) ++i;   // wave-uniform
+  const int64_t t = (int64_t)(blockIdx.x - a.block0[i]) * 256 + threadIdx.x;
+  if (t >= a.n[i]) return;
+  if (a.masked[i] && a.g[i][t] == 0.f) return;
+  adam_elem(a.p[i][t], a.g[i][t], a.m[i][t], a.v[i][t], a.step_size[i], a.b1[i], a.b2[i], a.eps[i], 1.f);
+}
+
+extern "C" int apn_adam_multi(int32_t count, float* const* params, const float* const* grads, float* const* exp_avgs,
+                              float* const* exp_avg_sqs, const int64_t* numels, const int32_t* steps,
+                              const float* beta1, const float* beta2, const float* lrs, const float* eps,
+                              const int32_t* masked, void* stream) {
+  if (count < 0 || count > ADAM_MULTI_MAX) return APN_ERR_ARG;
+  AdamMulti a;
+  int blocks = 0;
+  a.count = count;
+  for (int i = 0; i < count; ++i) {
+    if (numels[i] < 0 || (numels[i] > 0 && (!params[i] || !grads[i] || !exp_avgs[i] || !exp_avg_sqs[i])))
+      return APN_ERR_ARG;
+    a.p[i] = params[i]; a.g[i] = grads[i]; a.m[i] = exp_avgs[i]; a.v[i] = exp_avg_sqs[i];
+    a.n[i] = numels[i];
+    a.block0[i] = blocks;
+    blocks += ceil_div(numels[i], 256);
+    a.step_size[i] = adam_step_size(steps[i], beta1[i], beta2[i], lrs[i]);
+    a.b1[i] = beta1[i]; a.b2[i] = beta2[i]; a.eps[i] = eps[i];
+    a.masked[i] = masked[i];
+  }
+  a.block0[count] = blocks;
+  if (blocks == 0) return APN_OK;
+  hipLaunchKernelGGL(k_adam_multi, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
+  return launch_status();
+}
+
 extern "C" int apn_adam_upd(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                             int32_t step, float beta1, float beta2, float lr, float eps, void* stream) {
   return launch_adam<0>(param, grad, exp_avg, exp_avg_sq, nullptr, n, step, beta1, beta2, lr, eps, stream);

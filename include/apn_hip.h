@@ -94,6 +94,13 @@ int apn_adam_upd_with_perlr(float* param, const float* grad, float* exp_avg, flo
 /* total_variation_add_grad (total_variation.cpp:16-20, total_variation_kernel.cu:13-67) on a
  * [1, C, sz_i, sz_j, sz_k] grid: grad += six clamped neighbour differences (weights / 6; the
  * reference weights the i direction with wz, wx is unused); dense_mode = 0 skips grad == 0. */
+/* adam_upd / masked_adam_upd over `count` (<= 24) tensors in one launch (MaskedAdam.step,
+ * lib/masked_adam.py:50-72): host arrays of device pointers, element counts, per-tensor step,
+ * betas, lr, eps and masked flag (1 = leave elements with grad == 0 untouched); each element
+ * updated exactly as by the single-tensor entry points. */
+int apn_adam_multi(int32_t count, float* const* params, const float* const* grads, float* const* exp_avgs,
+                   float* const* exp_avg_sqs, const int64_t* numels, const int32_t* steps, const float* beta1,
+                   const float* beta2, const float* lrs, const float* eps, const int32_t* masked, void* stream);
 int apn_total_variation_add_grad(const float* param, float* grad, float wx, float wy, float wz,
                                  int64_t sz_i, int64_t sz_j, int64_t sz_k, int64_t n,
                                  int32_t dense_mode, void* stream);

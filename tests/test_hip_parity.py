@@ -871,6 +871,34 @@ def test_masked_adam_optimizer(dev):
     assert np.array_equal(lin.detach().cpu().numpy(), pl)
 
 
+def test_masked_adam_multi_tensor_launch(dev):
+    """MaskedAdam.step batches every contiguous fp32 parameter of the step into apn_adam_multi
+    launches (24 tensors each): 30 tensors over three groups (plain, masked with zero grads, another
+    lr), sizes 1 .. 100 003, bit-exact against the oracle's per-tensor restatement over 3 steps."""
+    from apn_amd.optim import MaskedAdam
+    rng = np.random.default_rng(17)
+    sizes = [1, 3, 4, 5, 17, 256, 257, 1000, 100003, 64] * 3
+    ps = [torch.nn.Parameter(torch.from_numpy(rng.normal(size=n).astype(F32)).to(dev)) for n in sizes]
+    groups = [{"params": ps[0:10], "lr": 1e-2, "skip_zero_grad": False},
+              {"params": ps[10:20], "lr": 3e-3, "skip_zero_grad": True},
+              {"params": ps[20:30], "lr": 7e-4, "skip_zero_grad": False, "betas": (0.8, 0.95), "eps": 1e-6}]
+    opt = MaskedAdam(groups)
+    ref = [p.detach().cpu().numpy().copy() for p in ps]
+    st = [(np.zeros_like(x), np.zeros_like(x)) for x in ref]
+    hp = [(1e-2, False, 0.9, 0.99, 1e-8)] * 10 + [(3e-3, True, 0.9, 0.99, 1e-8)] * 10 + [(7e-4, False, 0.8, 0.95, 1e-6)] * 10
+    for step in range(1, 4):
+        for i, p in enumerate(ps):
+            g = rng.normal(size=sizes[i]).astype(F32)
+            if hp[i][1]:
+                g[::3] = 0
+            p.grad = torch.from_numpy(g).to(dev)
+            lr, masked, b1, b2, eps = hp[i]
+            O.adam_upd(ref[i], g, *st[i], step, b1, b2, lr, eps, masked=masked)
+        opt.step()
+    for p, r in zip(ps, ref):
+        assert np.array_equal(p.detach().cpu().numpy(), r)
+
+
 @pytest.mark.parametrize("k", [1, 8, 16])
 def test_knn_points_bit_exact(dev, k):
     """apn_knn_points (unbounded argKmin of the training losses) vs brute force: indices and
