@@ -67,13 +67,13 @@ __global__ __launch_bounds__(THREADS) void k_gemm_f32(Args p) {
   __shared__ __attribute__((aligned(16))) float Bs[BTile<NT>::LDS];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int li = lane & 15, kq = lane >> 4;
-  const int64_t m0 = (int64_t)blockIdx.x * BM, n0 = (int64_t)blockIdx.y * BN;
+  const int64_t n0 = (int64_t)blockIdx.y * BN;
   const int64_t kb = (int64_t)blockIdx.z * p.k_split, ke = min(p.K, kb + p.k_split);
   float* const C = p.C + (int64_t)blockIdx.z * p.M * p.ldc;
   const int64_t nreal = p.N;
   f32x4 ra[2], rb[2 * NT];
   f32x4 rs = {0.f, 0.f, 0.f, 0.f};   // trans_a row sums: this thread's 4 rows m0 + 4 (tid & 15) + j
-  auto load = [&](int64_t k0) {
+  auto load = [&](int64_t m0, int64_t k0) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {   // A: 512 slots
       const int f = tid + THREADS * i;
@@ -155,12 +155,55 @@ __global__ __launch_bounds__(THREADS) void k_gemm_f32(Args p) {
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int b = 0; b < NT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (kb < ke) load(kb);
-  for (int64_t k0 = kb; k0 < ke; k0 += BK) {
+  // Persistent over M tiles (grid.x may be smaller than the tile count): the (tile, K step)
+  // iterations run as one sequence, so the next tile's first operands load during this tile's last
+  // step (a 128-deep K is only 4 steps: per-tile load latency would otherwise stay exposed).
+  const int64_t n_mt = (p.M + BM - 1) / BM;
+  const int64_t nk = ke > kb ? (ke - kb + BK - 1) / BK : 0;
+  const int64_t my = n_mt > (int64_t)blockIdx.x ? (n_mt - 1 - (int64_t)blockIdx.x) / gridDim.x + 1 : 0;
+  auto tile_m0 = [&](int64_t j) { return ((int64_t)blockIdx.x + j * gridDim.x) * BM; };
+  auto epilogue = [&](int64_t m0) {
+    if (TA && p.row_sum && blockIdx.y == 0) {   // the 16 threads sharing rows (tid & 15), fixed order
+      __syncthreads();
+      *(f32x4*)(As + (tid >> 4) * 64 + 4 * (tid & 15)) = rs;
+      __syncthreads();
+      if (tid < BM && m0 + tid < p.M) {
+        float t = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t += As[r * 64 + tid];
+        p.row_sum[(int64_t)blockIdx.z * p.M + m0 + tid] = t;
+      }
+    }
+    // lane (li, kq) of tile (x, y) holds rows 4 kq .. 4 kq + 3, column li
+#pragma unroll
+    for (int y = 0; y < NT; ++y) {
+      const int64_t col = n0 + w * 16 * NT + y * 16 + li;
+      if (col >= p.N) continue;
+      const float bv = p.bias ? p.bias[col] : 0.f;
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int64_t row = m0 + x * 16 + 4 * kq + i;
+          if (row >= p.M) continue;
+          float v = acc[x][y][i];
+          if (p.bias) v = v + bv;
+          if (p.act) v = v > 0.f ? v : (p.slope_act == 0.f ? 0.f : v * p.slope_act);   // ReLU: +0
+          C[row * p.ldc + col] = v;
+        }
+    }
+  };
+  if (nk == 0) {   // empty K range: the epilogue of zero products
+    for (int64_t j = 0; j < my; ++j) epilogue(tile_m0(j));
+    return;
+  }
+  const int64_t total = my * nk;
+  if (total > 0) load(tile_m0(0), kb);
+  for (int64_t it = 0; it < total; ++it) {
     __syncthreads();   // the previous step's operand reads are done
     store();
     __syncthreads();
-    if (k0 + BK < ke) load(k0 + BK);
+    if (it + 1 < total) load(tile_m0((it + 1) / nk), kb + ((it + 1) % nk) * BK);
 #pragma unroll
     for (int s = 0; s < BK / 4; ++s) {
       const int k = 4 * s + kq;
@@ -177,35 +220,13 @@ __global__ __launch_bounds__(THREADS) void k_gemm_f32(Args p) {
 #pragma unroll
         for (int y = 0; y < NT; ++y) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[x], b[y], acc[x][y], 0, 0, 0);
     }
-  }
-  if (TA && p.row_sum && blockIdx.y == 0) {   // the 16 threads sharing rows (tid & 15), fixed order
-    __syncthreads();
-    *(f32x4*)(As + (tid >> 4) * 64 + 4 * (tid & 15)) = rs;
-    __syncthreads();
-    if (tid < BM && m0 + tid < p.M) {
-      float t = 0.f;
+    if (it % nk == nk - 1) {
+      epilogue(tile_m0(it / nk));
 #pragma unroll
-      for (int r = 0; r < 16; ++r) t += As[r * 64 + tid];
-      p.row_sum[(int64_t)blockIdx.z * p.M + m0 + tid] = t;
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < NT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-  }
-  // lane (li, kq) of tile (x, y) holds rows 4 kq .. 4 kq + 3, column li
-#pragma unroll
-  for (int y = 0; y < NT; ++y) {
-    const int64_t col = n0 + w * 16 * NT + y * 16 + li;
-    if (col >= p.N) continue;
-    const float bv = p.bias ? p.bias[col] : 0.f;
-#pragma unroll
-    for (int x = 0; x < 4; ++x)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int64_t row = m0 + x * 16 + 4 * kq + i;
-        if (row >= p.M) continue;
-        float v = acc[x][y][i];
-        if (p.bias) v = v + bv;
-        if (p.act) v = v > 0.f ? v : (p.slope_act == 0.f ? 0.f : v * p.slope_act);   // ReLU: +0
-        C[row * p.ldc + col] = v;
-      }
   }
 }
 
@@ -227,7 +248,11 @@ __global__ __launch_bounds__(256) void k_splitk_reduce(const float* __restrict__
 
 template <bool TA, bool TB, int NT>
 void launch(const Args& a, int splits, hipStream_t s) {
-  dim3 grid((unsigned)ceil_div(a.M, BM), (unsigned)ceil_div(a.N, BTile<NT>::BN), (unsigned)splits);
+  // one M tile per workgroup for split / row-sum launches; else at most the resident workgroups
+  // (4 per CU at 64 x 128 tiles, 2 at 64 x 192), each looping over its tiles
+  const int64_t n_mt = ceil_div(a.M, BM);
+  const int64_t cap = (splits > 1 || a.row_sum) ? n_mt : 256 * (NT == 2 ? 4 : 2);
+  dim3 grid((unsigned)std::min<int64_t>(n_mt, cap), (unsigned)ceil_div(a.N, BTile<NT>::BN), (unsigned)splits);
   hipLaunchKernelGGL((k_gemm_f32<TA, TB, NT>), grid, dim3(THREADS), 0, s, a);
 }
 
