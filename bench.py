@@ -561,9 +561,21 @@ def other_configs(dev, in_flight=3):
         log(f"[other configs] C5: {c5['value'] / 1e9:.2f} G points/s, LBS {c5['config']['lbs_kernel_ms']:.4f} ms")
     except Exception as e:
         out["C5"] = {"error": repr(e)}
+    try:   # the train_pcd step (tools/train_bench.py) at C2, 8192 rays
+        import importlib.util
+        spec = importlib.util.spec_from_file_location("train_bench", os.path.join(ROOT, "tools", "train_bench.py"))
+        tb = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(tb)
+        tr = tb.run(argparse.Namespace(config="C2", steps=20, warmup=5, n_rand=8192, no_cpu_baseline=True))
+        out["train_C2"] = {k: tr[k] for k in ("metric", "value", "unit", "ms_per_step", "stage_ms", "steps")}
+        log(f"[other configs] train C2: {tr['ms_per_step']:.2f} ms/step")
+    except Exception as e:
+        out["train_C2"] = {"error": repr(e)}
+    torch.cuda.empty_cache()
     out["note"] = ("one GPU each, after the headline run: C3/C4 = whole frames replayed as one HIP graph (10 timed), "
                    "MLP kernel ms from HIP events on 5 eager frames; C5 = 300 poses of the repose sweep graph, LBS "
-                   "kernel from a graph of 20 launches (bench.py --config C5 gives the full line)")
+                   "kernel from a graph of 20 launches (bench.py --config C5 gives the full line); train_C2 = 20 timed "
+                   "train_pcd steps (forward with autograd, all default losses, backward, MaskedAdam)")
     return out
 
 

@@ -44,7 +44,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n-rand", type=int, default=8192)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    args = ap.parse_args()
+    print(json.dumps(run(ap.parse_args())))
+
+
+def run(args):
+    """The timed train_pcd loop (see the module docstring); returns the result dict."""
     dev = torch.device("cuda")
     scene = S.make_scene(args.config)
     model = harness.build_model(scene, dev)
@@ -111,7 +115,7 @@ def main():
            "survivors_last_step": int(model.last_stats.get("survivors", -1))}
     if not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(model, scene, rk, target_rgb, args.n_rand, t)
-    print(json.dumps(out))
+    return out
 
 
 def cpu_baseline(model, scene, rk, target_rgb, n_rand, t):
