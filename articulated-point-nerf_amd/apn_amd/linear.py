@@ -16,7 +16,7 @@ import torch
 from ._lib import call, load, ptr, stream_ptr
 
 SPLIT_ROWS = 512     # rows per split of the weight-gradient product (at least)
-SPLIT_TILES = 1024   # aim: output tiles x splits of about this many workgroups (4 per CU)
+SPLIT_TILES = 512    # aim: output tiles x splits of about this many workgroups (more measured slower)
 
 
 def _padded_rows(w: torch.Tensor) -> torch.Tensor:
