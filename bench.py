@@ -566,7 +566,8 @@ def other_configs(dev, in_flight=3):
         spec = importlib.util.spec_from_file_location("train_bench", os.path.join(ROOT, "tools", "train_bench.py"))
         tb = importlib.util.module_from_spec(spec)
         spec.loader.exec_module(tb)
-        tr = tb.run(argparse.Namespace(config="C2", steps=20, warmup=5, n_rand=8192, no_cpu_baseline=True))
+        with torch.enable_grad():
+            tr = tb.run(argparse.Namespace(config="C2", steps=20, warmup=5, n_rand=8192, no_cpu_baseline=True))
         out["train_C2"] = {k: tr[k] for k in ("metric", "value", "unit", "ms_per_step", "stage_ms", "steps")}
         log(f"[other configs] train C2: {tr['ms_per_step']:.2f} ms/step")
     except Exception as e:
