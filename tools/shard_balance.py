@@ -46,8 +46,8 @@ def main():
 
     stages = {}
 
-    def timed(fn, reps):
-        for _ in range(2):
+    def timed(fn, reps, warm=2):
+        for _ in range(warm):
             fn()
         torch.cuda.synchronize(dev)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -97,7 +97,7 @@ def main():
         if split.startswith("ilv") or split.startswith("gilv"):
             graph = split.startswith("g")
             B = int(split[4:] if graph else split[3:])
-            rows = []
+            rows, fl_all = [], []
             for k in range(world):
                 if graph:   # the rank's frame as one graph replay (shard.capture_sharded, bench's step)
                     fk = {n: v for n, v in kw.items() if n not in ("render_kwargs", "render_depth", "render_weights")}
@@ -106,14 +106,24 @@ def main():
                     if extra:   # frames in flight: timed per frame (4 rounds of len(gsteps) frames per call)
                         gsteps = [gstep] + [model.capture_frame(t, rk, ray_shard=(k, world, B), workspace=w, **fk)
                                             for w in extra]
-                        fl_ms, _ = timed(lambda: in_flight(gsteps), args.reps)
+                        fl_ms, _ = timed(lambda: in_flight(gsteps), args.reps, warm=4)
                         print(f"   shard {k}: {args.in_flight} in flight {fl_ms / (4 * len(gsteps)):.3f} ms/frame")
+                        fl_all.append((k, gsteps))
                 else:
                     fn = lambda: model(t, ray_shard=(k, world, B), **kw)   # noqa: E731
                 ms, o = timed(fn, args.reps)
                 s = model.last_stats.resolved()
                 rows.append((ms, s.get("inbbox_samples", -1), s.get("kept_samples", -1), model.last_ray_count))
                 print(f"   shard {k}: {ms:.3f} ms, stages " + " ".join(f"{n} {v:.3f}" for n, v in stages.items()))
+            if fl_all:   # every shard's in-flight replay again, after all shards were captured (the first
+                # shard's first timing runs right after the previous world's graphs were dropped)
+                again = []
+                for k2, gs in fl_all:
+                    fl_ms, _ = timed(lambda: in_flight(gs), args.reps, warm=2)
+                    again.append(fl_ms / (4 * len(gs)))
+                print(f"   {args.in_flight} in flight, all shards re-timed: " + " ".join(f"{v:.3f}" for v in again)
+                      + f" | max {max(again):.3f} ms/frame")
+                fl_all.clear()
             mx = max(r[0] for r in rows)
             mean = sum(r[0] for r in rows) / world
             print(f"[{split}] world {world}: shard ms " + " ".join(f"{r[0]:.3f}" for r in rows)
