@@ -635,14 +635,22 @@ class TemporalPoints(torch.nn.Module):
                     raise RuntimeError("capture_frame: no sample capacity for this ray set (empty frame?)")
                 st.pop("graph", None)   # a re-capture: drop the old graph first (its retired buffers go with it)
                 step.graph = None
-                with _capture_guard():
-                    graph = torch.cuda.CUDAGraph()
-                    self._ws.hold(graph)          # the graph holds workspace addresses from here on
-                    self._ws_shared.hold(graph)   # (and the shared projection's)
-                    with torch.cuda.graph(graph, capture_error_mode=capture_error_mode):
-                        out = self._forward_render(t_in, *args)
-                        if out._info is not None:
-                            torch.bitwise_or(ovf, out._info[2:3], out=ovf)
+                # the captured frame is one chain: the kNN grid build stays on the frame's own stream
+                # (its side-stream branch made graphs of frames in flight land on shared hardware
+                # queues -- GPU_MAX_HW_QUEUES = 4 -- and serialise: shards of 8 in flight 1.08 or
+                # 1.28 ms per frame by capture, 1.01-1.04 ms as one chain; whole frames equal)
+                grid_branch, self.concurrent_grid = self.concurrent_grid, False
+                try:
+                    with _capture_guard():
+                        graph = torch.cuda.CUDAGraph()
+                        self._ws.hold(graph)          # the graph holds workspace addresses from here on
+                        self._ws_shared.hold(graph)   # (and the shared projection's)
+                        with torch.cuda.graph(graph, capture_error_mode=capture_error_mode):
+                            out = self._forward_render(t_in, *args)
+                            if out._info is not None:
+                                torch.bitwise_or(ovf, out._info[2:3], out=ovf)
+                finally:
+                    self.concurrent_grid = grid_branch
             st.update(graph=graph, static={k: dict.__getitem__(out, k) for k in dict.keys(out)}, info=out._info,
                       n_rays=out._n_rays, bg=out._bg, cap=self._capacity.get(cap_key), stale=False)
             step.graph = graph
