@@ -20,6 +20,14 @@
 // conflicting ds_write_b64 (SQ_LDS_BANK_CONFLICT).
 #include "apn_mlp_split.h"
 
+// The layers' operand reads are pinned ahead of the MFMAs that do not need them (sched_barrier):
+// left to the scheduler, each M-tile's activation reads sank below the previous M-tile's MFMAs into
+// the registers those had just read, so every 6-MFMA step waited on its LDS read behind an s_nop
+// hazard pad (685 pad states per wave-tile, 450 pinned): MLP 4.22 -> 3.94 ms per C2 frame.
+#ifndef APN_H4_PIN   // A/B builds: 0 leaves the activation / fragment reads to the scheduler
+#define APN_H4_PIN 1
+#endif
+
 namespace apn {
 namespace t128 {
 
@@ -161,7 +169,10 @@ __device__ __forceinline__ void layer_mfma(const char* __restrict__ X, rsrc_t rs
                                            h8 (&a)[2][2]) {
   const int lane = threadIdx.x & 63;
   const int li = lane & 15, g = lane >> 4;
-  h8 bh = *(const h8*)(X + act_off(li, g)), bl = *(const h8*)(X + act_off(li, g) + 256);
+  constexpr int NS = NQ * MT;   // (chunk, M-tile) steps
+  // activation fragments of step t: (chunk t / MT, M-tile t % MT)
+  auto act = [&](int t) { return X + act_off(16 * (t % MT) + li, 4 * (t / MT) + g); };
+  h8 bh = *(const h8*)act(0), bl = *(const h8*)(act(0) + 256);
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     h8 an[2][2];
@@ -176,16 +187,27 @@ __device__ __forceinline__ void layer_mfma(const char* __restrict__ X, rsrc_t rs
 #pragma unroll
         for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, vb, FBN + j * NQN * 2 + pt);
     }
+#if APN_H4_PIN
+    __builtin_amdgcn_sched_barrier(0);   // the next chunk's fragment loads issue here, before the MFMAs
+#endif
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
+      const int t = q * MT + mt;
       h8 nbh = bh, nbl = bl;
-      if (mt + 1 < MT || q + 1 < NQ) {
-        const char* p = X + act_off(16 * ((mt + 1) % MT) + li, 4 * (mt + 1 < MT ? q : q + 1) + g);
-        nbh = *(const h8*)p;
-        nbl = *(const h8*)(p + 256);
+      if (t + 1 < NS) {
+        nbh = *(const h8*)act(t + 1);
+        nbl = *(const h8*)(act(t + 1) + 256);
       }
+#if APN_H4_PIN
+      // the next M-tile's activation reads issue before this M-tile's MFMAs, into registers of their
+      // own: no MFMA-read -> LDS-write hazard pad (s_nop) and the LDS latency under 6 MFMAs
+      __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[mt][j] = mfma3(a[j][0], a[j][1], bh, bl, acc[mt][j]);
+#if APN_H4_PIN
+      __builtin_amdgcn_sched_barrier(0);
+#endif
       bh = nbh;
       bl = nbl;
     }
