@@ -73,7 +73,25 @@ __global__ __launch_bounds__(THREADS) void k_gemm_f32(Args p) {
   const int64_t nreal = p.N;
   f32x4 ra[2], rb[2 * NT];
   f32x4 rs = {0.f, 0.f, 0.f, 0.f};   // trans_a row sums: this thread's 4 rows m0 + 4 (tid & 15) + j
-  auto load = [&](int64_t m0, int64_t k0) {
+  // Interior tiles (every slot whole and in bounds: a workgroup-uniform test) load their operands
+  // with no branch around the loads, and the LeakyReLU-derivative mask and the row sums wait for
+  // store(): a load under a per-lane branch, or a value used at once, makes the compiler wait for
+  // it right there (the phi copy at the join reads it), which exposed every K step's load latency.
+  f32x4 ra2_0 = {0.f, 0.f, 0.f, 0.f}, ra2_1 = {0.f, 0.f, 0.f, 0.f};   // A2 slots of the interior path
+  bool a_late = false;
+  auto load = [&](int64_t m0, int64_t k0) __attribute__((always_inline)) {
+    a_late = p.vec_a && m0 + BM <= p.M && k0 + BK <= ke;
+    if (a_late) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int f = tid + THREADS * i;
+        const int64_t gk = TA ? k0 + (f >> 4) : k0 + 4 * (f & 7);
+        const int64_t gm = TA ? m0 + 4 * (f & 15) : m0 + (f >> 3);
+        const int64_t o = TA ? gk * p.lda + gm : gm * p.lda + gk;
+        ra[i] = *(const f32x4*)(p.A + o);
+        if (p.A2) (i ? ra2_1 : ra2_0) = *(const f32x4*)(p.A2 + o);
+      }
+    } else {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {   // A: 512 slots
       const int f = tid + THREADS * i;
@@ -103,6 +121,16 @@ __global__ __launch_bounds__(THREADS) void k_gemm_f32(Args p) {
       ra[i] = v;
       if (TA && p.row_sum) rs += v;
     }
+    }
+    if (p.vec_b && n0 + BN <= nreal && k0 + BK <= ke) {
+#pragma unroll
+      for (int i = 0; i < 2 * NT; ++i) {
+        const int f = tid + THREADS * i;
+        const int64_t gk = TB ? k0 + 4 * (f & 7) : k0 + f / (BN / 4);
+        const int64_t gn = TB ? n0 + (f >> 3) : n0 + 4 * (f % (BN / 4));
+        rb[i] = *(const f32x4*)(p.B + (TB ? gn * p.ldb + gk : gk * p.ldb + gn));
+      }
+    } else {
 #pragma unroll
     for (int i = 0; i < 2 * NT; ++i) {   // B: 512 NT slots
       const int f = tid + THREADS * i;
@@ -122,18 +150,26 @@ __global__ __launch_bounds__(THREADS) void k_gemm_f32(Args p) {
       }
       rb[i] = v;
     }
+    }
   };
-  auto store = [&]() {
+  auto store = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int f = tid + THREADS * i;
+      f32x4 v = ra[i];
+      if (a_late) {   // the interior path's deferred mask and row sums, in the order of the load path
+        const f32x4 u = i ? ra2_1 : ra2_0;
+        if (p.A2) v = f32x4{act_mask(v[0], u[0], p.slope_mask), act_mask(v[1], u[1], p.slope_mask),
+                            act_mask(v[2], u[2], p.slope_mask), act_mask(v[3], u[3], p.slope_mask)};
+        if (TA && p.row_sum) rs += v;
+      }
       if (TA) {
-        *(f32x4*)(As + (f >> 4) * SAM + 4 * (f & 15)) = ra[i];
+        *(f32x4*)(As + (f >> 4) * SAM + 4 * (f & 15)) = v;
       } else {
         float* d = As + (f >> 3) * SKM + 4 * (f & 7);
         typedef float f32x2 __attribute__((ext_vector_type(2)));
-        *(f32x2*)d = f32x2{ra[i][0], ra[i][1]};
-        *(f32x2*)(d + 2) = f32x2{ra[i][2], ra[i][3]};
+        *(f32x2*)d = f32x2{v[0], v[1]};
+        *(f32x2*)(d + 2) = f32x2{v[2], v[3]};
       }
     }
 #pragma unroll
