@@ -91,9 +91,13 @@ __global__ __launch_bounds__(256) void k_ert_pass(int64_t n_rays, int first, con
                                                   const int* __restrict__ end, const float4* __restrict__ out,
                                                   float thr, int use_mask, int* __restrict__ pos,
                                                   float* __restrict__ T, int* __restrict__ cnt, int B,
-                                                  int* __restrict__ list, int* __restrict__ count) {
+                                                  int* __restrict__ list, int* __restrict__ count,
+                                                  const int* __restrict__ prev_count) {
   __shared__ int s_wave[4];
   __shared__ int s_base;
+  // an empty previous pass leaves every ray with nothing listed, so this pass and every later one
+  // are empty too (their counts stay at the 0 they were filled with): the whole grid returns
+  if (prev_count && *prev_count == 0) return;
   const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
   int c = 0, p = 0;
   if (r < n_rays) {
@@ -218,7 +222,7 @@ int ert_run(const float4* s_pos, const int* s_ray, const int* s_nbr, int64_t max
   if (with_direct) APN_TRY(direct_blend(s_pos, s_nbr, max_samples, n_samples_dev, recA, recB, eps, out, s));
   for (int p = 0; p < ERT_PASSES; ++p) {
     hipLaunchKernelGGL(k_ert_pass, dim3(rb), dim3(256), 0, s, n_rays, p == 0 ? 1 : 0, beg, end, (const float4*)out,
-                       thr, use_mask, pos, T, cnt, ERT_PASS[p], list, sizes + p);
+                       thr, use_mask, pos, T, cnt, ERT_PASS[p], list, sizes + p, p == 0 ? nullptr : sizes + p - 1);
     if (events) APN_HIP_TRY(hipEventRecord((hipEvent_t)events[2 * p], s));
     APN_TRY(mlp(list, sizes + p));
     if (events) APN_HIP_TRY(hipEventRecord((hipEvent_t)events[2 * p + 1], s));
