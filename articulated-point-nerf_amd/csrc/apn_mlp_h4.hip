@@ -24,6 +24,9 @@
 // left to the scheduler, each M-tile's activation reads sank below the previous M-tile's MFMAs into
 // the registers those had just read, so every 6-MFMA step waited on its LDS read behind an s_nop
 // hazard pad (685 pad states per wave-tile, 450 pinned): MLP 4.22 -> 3.94 ms per C2 frame.
+#ifndef APN_H4_MERGED   // A/B builds: 0 launches the two weight-scale instantiations per pass
+#define APN_H4_MERGED 1
+#endif
 #ifndef APN_H4_PIN   // A/B builds: 0 leaves the activation / fragment reads to the scheduler
 #define APN_H4_PIN 1
 #endif
@@ -621,6 +624,36 @@ __global__ __launch_bounds__(MLP_THREADS, 2) void k_point_mlp_h4(
                     interval, out, X, sTo, sIdw, sRow, sOut, sV, sW, sPart);
 }
 
+// The early-ray-termination passes' kernel: both weight-scale modes in one launch, the mode read
+// from wbuf by each workgroup (one launch per pass instead of two; the registers are the larger
+// mode's, below the 256 of two waves per SIMD either way).
+__global__ __launch_bounds__(MLP_THREADS, 2) void k_point_mlp_h4_listed(
+    const float4* __restrict__ s_pos, const int* __restrict__ s_ray, const int* __restrict__ s_nbr,
+    const int* __restrict__ list, const int* __restrict__ n_samples_dev, const float4* __restrict__ recA, const float4* __restrict__ recB,
+    const float4* __restrict__ pproj, const float* __restrict__ viewdirs, const float* __restrict__ vemb_const,
+    const float* __restrict__ wbuf, float eps, float shift, float interval, float4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) char X[TR4 * XB];
+  __shared__ float sTo[TR4];
+  __shared__ float sIdw[TR4];
+  __shared__ float sRow[TR4 * RS];
+  __shared__ __attribute__((aligned(16))) float sOut[TS4 * 12];
+  __shared__ float sV[TS4 * 32];
+  __shared__ __attribute__((aligned(16))) float sW[SW_TOTAL];
+  __shared__ float sPart[4 * TS4 * 4];
+  __shared__ int s_mode;   // 0: unscaled weights, 1: scaled, 2: the range flag is set (skip)
+  if (threadIdx.x == 0)
+    s_mode = __builtin_nontemporal_load((const int*)(wbuf + OFF_FLAG)) != 0 ? 2 : (wbuf[OFF_SCALE + 6] != 0.f ? 1 : 0);
+  __syncthreads();
+  const int mode = s_mode;
+  if (mode == 2) return;
+  if (mode == 1)
+    mlp_tiles<true, false, true>(s_pos, s_ray, s_nbr, list, n_samples_dev, recA, recB, pproj, viewdirs, vemb_const, wbuf, eps,
+                                 shift, interval, out, X, sTo, sIdw, sRow, sOut, sV, sW, sPart);
+  else
+    mlp_tiles<false, false, true>(s_pos, s_ray, s_nbr, list, n_samples_dev, recA, recB, pproj, viewdirs, vemb_const, wbuf, eps,
+                                  shift, interval, out, X, sTo, sIdw, sRow, sOut, sV, sW, sPart);
+}
+
 }  // namespace t128
 
 void launch_point_mlp_h4(int blocks, bool timed, hipStream_t stream, const float4* s_pos, const int* s_ray, const int* s_nbr,
@@ -632,11 +665,13 @@ void launch_point_mlp_h4(int blocks, bool timed, hipStream_t stream, const float
                        recB, pproj, viewdirs, vemb_const, wbuf, eps, shift, interval, out);
   };
   const int nb_scaled = blocks < 256 * 8 ? blocks : 256 * 8;
-  if (list) {
-    // early-ray-termination passes (9 per frame): the scaled instantiation, which exits at once
-    // unless the weights needed scales, on 256 workgroups (an empty launch: ~3 us, not ~5)
+  if (list) {   // early-ray-termination passes (9 per frame): one launch, either weight-scale mode
+#if APN_H4_MERGED
+    go(t128::k_point_mlp_h4_listed, blocks);
+#else
     go(t128::k_point_mlp_h4<false, false, true>, blocks);
     go(t128::k_point_mlp_h4<true, false, true>, blocks < 256 ? blocks : 256);
+#endif
     return;
   }
 #ifdef APN_DEBUG_BUILD

@@ -12,9 +12,11 @@ import sys
 
 def main(summary, out, note, per_frame=9):
     d = json.load(open(summary))
-    name = next(k for k in d if "k_point_mlp_h4<false, false, true>" in k or "k_point_mlp_h4<false, false>" in k)
+    name = next(k for k in d if "k_point_mlp_h4_listed" in k or "k_point_mlp_h4<false, false, true>" in k
+                or "k_point_mlp_h4<false, false>" in k)
     e = d[name]
-    per_frame = int(per_frame) if "true>" in name else 1
+    listed = "listed" in name or "true>" in name   # one launch per early-ray-termination pass
+    per_frame = int(per_frame) if listed else 1
     res = {
         "kernel": name,
         "launches_per_frame": per_frame,
