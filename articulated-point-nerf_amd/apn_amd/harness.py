@@ -295,6 +295,11 @@ def _view_rays(i, HW, Ks, c2w, ndc, inverse_y, flip_x, flip_y, fixed_viewdirs, d
     return H, W, K, c2w, ro.reshape(-1, 3), rd.reshape(-1, 3), vd.reshape(-1, 3)
 
 
+# render_viewpoints' result stacks stay in pinned host memory up to this size (16 views at 800x800
+# take 287 MB); a longer sweep returns pageable arrays filled through the pipeline's pinned slots
+PINNED_STACK_BYTES = 1 << 30
+
+
 @torch.no_grad()
 def render_viewpoints(model, render_poses, HW, Ks, ndc, render_kwargs, gt_imgs=None, savedir=None, test_times=None,
                       render_factor=0, eval_psnr=False, eval_ssim=False, eval_lpips_alex=False,
@@ -340,7 +345,11 @@ def render_viewpoints(model, render_poses, HW, Ks, ndc, render_kwargs, gt_imgs=N
             # here (in the order _finish would: PNGs first), overlapped with the GPU's next frames
             nonlocal bones
             i, H, W, h = pending.pop(0)
-            r = h.result()   # the frame's images are already in the pinned stacks (DMA at submit)
+            if pinned:
+                r = h.result()   # the frame's images are already in the pinned stacks (DMA at submit)
+            else:   # pageable stacks: one host copy from the slot's pinned buffers
+                r = h.result(into={rgb_key: stack["rgb"][i], "depth": stack["depth"][i],
+                                   "weights": stack["weights"][i]})
             if "joints" in r:
                 b = _joint_record({"joints": r["joints"], "bones": model.bones if model.joints_to_keep is None
                                    else model.new_bones}, joints, i, HW, render_kwargs)
@@ -359,12 +368,19 @@ def render_viewpoints(model, render_poses, HW, Ks, ndc, render_kwargs, gt_imgs=N
                 pipe = cached_pipeline(model, t, rk, n=in_flight, render_depth=True, render_weights=True,
                                        poses=c2w[None], Ks=K[None], get_skeleton=True,
                                        readback=(rgb_key, "depth", "weights"))
-                # the returned image stacks, in pinned memory (torch's host cache reuses it from call to
-                # call): each frame's readback is a DMA straight into its slice, no host copy
+                # the returned image stacks: up to PINNED_STACK_BYTES in pinned memory (torch's host
+                # cache reuses it from call to call; each frame's readback is a DMA straight into its
+                # slice, no host copy), a longer sweep in pageable numpy arrays (the frame goes
+                # through its slot's pinned buffers, n_in_flight of them, and one host copy)
+                use_pinned = n_views * H * W * 7 * 4 <= PINNED_STACK_BYTES
                 for k, c in (("rgb", 3), ("depth", 1), ("weights", 3)):
-                    pinned[k] = torch.empty((n_views, H, W, c), dtype=torch.float32, pin_memory=True)
-                    stack[k] = pinned[k].numpy()
-            dest = {rgb_key: pinned["rgb"][i], "depth": pinned["depth"][i], "weights": pinned["weights"][i]}
+                    if use_pinned:
+                        pinned[k] = torch.empty((n_views, H, W, c), dtype=torch.float32, pin_memory=True)
+                        stack[k] = pinned[k].numpy()
+                    else:
+                        stack[k] = np.empty((n_views, H, W, c), dtype=np.float32)
+            dest = ({rgb_key: pinned["rgb"][i], "depth": pinned["depth"][i], "weights": pinned["weights"][i]}
+                    if pinned else None)
             pending.append((i, H, W, pipe.submit(t, (ro, rd, vd), c2w[None], K[None], dest=dest)))
             if len(pending) >= in_flight:
                 fetch()

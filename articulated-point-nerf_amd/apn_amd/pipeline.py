@@ -204,10 +204,19 @@ class FramePipeline:
                     if v.is_cuda:
                         v.record_stream(s)
                     slot["rk"][k].copy_(v, non_blocking=True)
+            # the caller's device inputs are read on this stream: record the use, so the caching
+            # allocator does not hand their blocks to the caller's next allocation before the copy
+            # has run (harness.render_viewpoints drops each view's c2w / K right after submit)
             if poses is not None and slot["poses"] is not None:
+                if poses.is_cuda:
+                    poses.record_stream(s)
                 slot["poses"].copy_(poses.reshape(slot["poses"].shape), non_blocking=True)
             if Ks is not None and slot["Ks"] is not None:
+                if Ks.is_cuda:
+                    Ks.record_stream(s)
                 slot["Ks"].copy_(Ks.reshape(slot["Ks"].shape), non_blocking=True)
+            if isinstance(t, torch.Tensor) and t.is_cuda:
+                t.record_stream(s)
             tt = torch.as_tensor(t, dtype=torch.float32, device=self.dev).reshape(-1)
             out = slot["step"](tt)
             if self.readback:
@@ -244,12 +253,27 @@ class FramePipeline:
 
 
 def capture_sharded_in_flight(model, t, render_kwargs, rank, world, group=None, n=3, **forward_kwargs):
-    """n capture_sharded steps of one model, each captured into its own per-frame workspace, for
-    shard.replay_in_flight (the ray-shard frames in flight of bench.py --gpus N)."""
+    """n capture_sharded steps of one model, each captured into its own per-frame workspace and
+    with its own input buffers (``step.inputs``: rays, and the camera pose / intrinsics when the
+    skeleton is projected), for shard.replay_in_flight (the ray-shard frames in flight of bench.py
+    --gpus N; a frame's view is copied into its step's inputs before the replay)."""
     from .shard import RAY_BLOCK, capture_sharded
     block = forward_kwargs.pop("block", RAY_BLOCK)
-    return [capture_sharded(model, t, render_kwargs, rank, world, group, block=block, workspace=Workspace(),
-                            **forward_kwargs) for _ in range(n)]
+    dev = model.canonical_feat.device
+    steps = []
+    for _ in range(n):
+        rk = dict(render_kwargs)
+        for k in ("rays_o", "rays_d", "viewdirs"):
+            rk[k] = render_kwargs[k].detach().to(dev, torch.float32).contiguous().clone()
+        fk = dict(forward_kwargs)
+        if fk.get("get_skeleton"):
+            fk["poses"] = fk["poses"].detach().to(dev, torch.float32).clone()
+            fk["Ks"] = fk["Ks"].detach().to(dev, torch.float32).clone()
+        st = capture_sharded(model, t, rk, rank, world, group, block=block, workspace=Workspace(), **fk)
+        st.inputs = {"rays": (rk["rays_o"], rk["rays_d"], rk["viewdirs"]), "poses": fk.get("poses"),
+                     "Ks": fk.get("Ks")}
+        steps.append(st)
+    return steps
 
 
 def _model_version(model):
@@ -259,21 +283,32 @@ def _model_version(model):
     return tuple((p.data_ptr(), p._version) for p in list(model.parameters()) + list(model.buffers()))
 
 
+def _render_settings(model):
+    """The model's plain (non-tensor) attributes a captured frame bakes in: compositing masks,
+    early ray termination, the kept joints, the density activation's shift and the IDW epsilon."""
+    keep = model.joints_to_keep
+    keep = tuple(keep.tolist()) if isinstance(keep, torch.Tensor) else (tuple(keep) if keep is not None else None)
+    tnv = model.tineuvox
+    return (float(model.fast_color_thres), bool(model.early_termination), keep,
+            float(getattr(tnv, "act_shift", 0.0)), float(getattr(tnv, "voxel_size_ratio", 1.0)), float(model._eps))
+
+
 def cached_pipeline(model, t, render_kwargs, n=3, **kw) -> FramePipeline:
     """The model's FramePipeline for this ray count and these render settings, captured on first
-    use and reused while the model's parameters are unchanged (harness.render_viewpoints calls it
-    once per viewpoint sweep). A pipeline whose model changed is dropped with its workspaces."""
+    use and reused while the model's parameters and plain render settings are unchanged
+    (harness.render_viewpoints calls it once per viewpoint sweep). A pipeline whose model changed is
+    dropped with its workspaces."""
     scal = tuple(sorted((k, v) for k, v in render_kwargs.items()
                         if isinstance(v, (int, float, bool, str)) or v is None))
     opts = tuple(sorted((k, v) for k, v in kw.items() if k not in ("poses", "Ks") and not isinstance(v, torch.Tensor)))
-    key = (len(render_kwargs["rays_o"]), n, scal, opts)
+    key = (len(render_kwargs["rays_o"]), n, scal, opts, _render_settings(model))
     ver = _model_version(model)
     cache = model.__dict__.setdefault("_pipelines", {})
     hit = cache.get(key)
     if hit is not None and hit[0] == ver:
         return hit[1]
-    for k in [k for k, v in cache.items() if v[0] != ver]:
-        del cache[k]
+    cache.clear()   # one pipeline per model: n per-frame workspaces are ~2 GB each at C2
+    torch.cuda.synchronize(model.canonical_feat.device)   # a dropped pipeline's frames may still run
     pipe = FramePipeline(model, t, render_kwargs, n=n, **kw)
     cache[key] = (_model_version(model), pipe)
     return pipe

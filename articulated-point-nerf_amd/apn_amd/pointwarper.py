@@ -168,7 +168,14 @@ class PointWarper(torch.nn.Module):
             self._tree_key = key
         return self._tree
 
-    def pose(self, joints, t=None, rot_params=None, global_t=None, time_poc=None, proj=None, sweep_index=None):
+    def pose_buffers(self, J, dev):
+        """Output buffers of one skeleton launch (``pose(out=...)``)."""
+        return {"thetas": torch.empty(J, device=dev), "bone_Ts": torch.empty(J, 4, 4, device=dev),
+                "T34": torch.empty(J, 12, device=dev), "gt": torch.empty(3, device=dev),
+                "joints_rel": torch.empty(J, 3, device=dev)}
+
+    def pose(self, joints, t=None, rot_params=None, global_t=None, time_poc=None, proj=None, sweep_index=None,
+             out=None):
         """Skeleton stage of forward (pointwarper.py:216-239) as one HIP launch
         (apn_skeleton_frame): returns bone_Ts [J,4,4], global_t [3] and joints_rel [J,3]; the
         bone rows [J,12] for apn_lbs_skin are kept in ``last_T34``. Sets prev_params /
@@ -180,18 +187,17 @@ class PointWarper(torch.nn.Module):
         (temporalpoints.py:578-583) runs in the launch too, left in ``last_joints2d`` [P,J,2]
         (None when not requested or beyond the kernel's limits: the caller projects in torch).
         ``sweep_index`` (device int32 [1]): rot_params is a pose sweep [P, J, rot_dim]; the launch
-        takes pose sweep_index % P and advances the index (TemporalPoints.capture_repose)."""
+        takes pose sweep_index % P and advances the index (TemporalPoints.capture_repose).
+        ``out`` (``pose_buffers``): write thetas / bone_Ts / T34 / global_t / joints_rel there
+        instead of fresh tensors (the pipelined repose sweep's double buffers)."""
         assert (t is None) ^ (rot_params is None)
         dev = joints.device
         L.require_cuda(joints, what="PointWarper.pose")
         J = joints.shape[0]
         pi, pjx, sib, rmask, prog = self._tree_buffers(dev)
         jts = joints.detach().float().contiguous()
-        thetas = torch.empty(J, device=dev)
-        bone_Ts = torch.empty(J, 4, 4, device=dev)
-        T34 = torch.empty(J, 12, device=dev)
-        gt = torch.empty(3, device=dev)
-        joints_rel = torch.empty(J, 3, device=dev)
+        o = out if out is not None else self.pose_buffers(J, dev)
+        thetas, bone_Ts, T34, gt, joints_rel = o["thetas"], o["bone_Ts"], o["T34"], o["gt"], o["joints_rel"]
         s = stream_ptr(dev)
         c2w = Km = j2d = None
         n_views = 0

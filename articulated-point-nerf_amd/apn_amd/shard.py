@@ -330,14 +330,17 @@ def capture_sharded(model, t, render_kwargs, rank: int, world: int, group=None, 
     return step
 
 
-def replay_in_flight(steps, ts, streams, comm, keep: bool = False) -> list:
+def replay_in_flight(steps, ts, streams, comm, keep: bool = False, views=None) -> list:
     """Ray-shard frames with len(steps) frames in flight (bench.py --in-flight): frame i (time
     ts[i]) replays steps[i % n]'s graph (capture_sharded steps of one model, each captured into a
     workspace of its own -- apn_amd.pipeline.capture_sharded_in_flight) on
     streams[i % n], and its tile all-gather (step.assemble) runs on the ONE collective stream
     ``comm`` in frame order, so every rank issues the same collectives in the same order. A
     stream's next replay waits (event) for the assembly of its previous frame, whose tile it
-    overwrites. Returns every assembled frame (``keep``) or the last one, in a list."""
+    overwrites. ``views[i]`` (objects with ``rays`` = (rays_o, rays_d, viewdirs), ``c2w``, ``K``;
+    synthetic.View): frame i's rays and camera, copied into the step's own inputs (``step.inputs``)
+    on its stream before the replay. Returns every assembled frame (``keep``) or the last one, in
+    a list."""
     n = len(steps)
     cur = torch.cuda.current_stream()
     ev = torch.cuda.Event()
@@ -351,6 +354,8 @@ def replay_in_flight(steps, ts, streams, comm, keep: bool = False) -> list:
         if i >= n:
             s.wait_event(done[i % n])   # frame i - n's tile has been packed and gathered
         with torch.cuda.stream(s):
+            if views is not None:
+                set_inputs(steps[i % n], views[i])
             o = steps[i % n].local(t)
         comm.wait_stream(s)
         with torch.cuda.stream(comm):
@@ -360,6 +365,20 @@ def replay_in_flight(steps, ts, streams, comm, keep: bool = False) -> list:
     for s in list(streams) + [comm]:
         cur.wait_stream(s)
     return frames
+
+
+def set_inputs(step, view):
+    """Copy a view's rays (and camera pose / intrinsics, when the step projects the skeleton) into
+    a capture_sharded_in_flight step's input buffers, on the current stream."""
+    inp = getattr(step, "inputs", None)
+    if inp is None:
+        raise RuntimeError("replay_in_flight(views=...): the steps need their own inputs "
+                           "(pipeline.capture_sharded_in_flight)")
+    for dst, src in zip(inp["rays"], view.rays):
+        dst.copy_(src.reshape(dst.shape), non_blocking=True)
+    if inp.get("poses") is not None:
+        inp["poses"].copy_(view.c2w.reshape(inp["poses"].shape), non_blocking=True)
+        inp["Ks"].copy_(view.K.reshape(inp["Ks"].shape), non_blocking=True)
 
 
 def _assemble(model, t, out, render_kwargs, rank, world, group, blocks, block, forward_kwargs, invalidate=None):

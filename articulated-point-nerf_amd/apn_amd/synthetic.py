@@ -340,6 +340,42 @@ def make_scene(name_or_cfg) -> Scene:
     return Scene(cfg, ctor, params, c2w, K, near, far, bg, inv_y)
 
 
+@dataclass
+class View:
+    """One frame of a render loop: its time (a [1] tensor on the device), camera-to-world pose,
+    intrinsics and rays (rays_o, rays_d, viewdirs), all resident on the device."""
+    t: torch.Tensor
+    c2w: torch.Tensor
+    K: torch.Tensor
+    rays: tuple
+
+
+def view_sweep(scene: Scene, n: int = 16, device="cpu") -> list:
+    """n distinct frames of the scene's render loop, as run.py:108-151 renders them: every frame
+    a new time and a new camera pose. View 0 is the scene's own frame (cfg.t, its camera); view i
+    orbits the camera by 360 i / n degrees about the scene's vertical axis at the same elevation
+    and distance (D-NeRF: pose_spherical(30 + 360 i / n, -30, 4); ZJU: the look-at eye at azimuth
+    40 + 360 i / n) and advances the time by 0.6 i / n (t stays in [0, 1))."""
+    cfg = scene.cfg
+    views = []
+    for i in range(n):
+        t = (cfg.t + 0.6 * i / n) % 1.0
+        if cfg.camera == "dnerf":
+            c2w = pose_spherical(30.0 + 360.0 * i / n, -30.0, 4.0)
+        elif cfg.camera == "zju":
+            az, el = math.radians(40.0 + 360.0 * i / n), math.radians(15)
+            c2w = look_at_opencv((2.6 * math.cos(az) * math.cos(el), 2.6 * math.sin(az) * math.cos(el),
+                                  2.6 * math.sin(el)))
+        else:
+            raise ValueError(cfg.camera)
+        if i == 0:
+            c2w, t = scene.c2w.clone(), cfg.t
+        c2w = c2w.to(device)
+        rays = get_rays(cfg.H, cfg.W, scene.K, c2w, inverse_y=scene.inverse_y)
+        views.append(View(torch.tensor([t], dtype=torch.float32, device=device), c2w, scene.K.to(device), rays))
+    return views
+
+
 def repose_sweep(J: int, steps: int = 30, seed: int = 0) -> torch.Tensor:
     """run.py:1364-1377: randn(J,4)*0.2 with row 0 zero, linear ramp of ``steps`` + reverse."""
     g = torch.Generator().manual_seed(seed)

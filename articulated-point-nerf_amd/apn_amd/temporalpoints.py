@@ -524,7 +524,7 @@ class TemporalPoints(torch.nn.Module):
         self._mark("lbs")
         return [xyz, joints_rel]
 
-    def capture_repose(self, rot_dim=4, sweep=None):
+    def capture_repose(self, rot_dim=4, sweep=None, pipelined=True):
         """The repose step (skeleton launch + fused LBS launch, run.py:1355-1396 sweeps it per pose)
         captured once in a HIP graph: returns ``step(rot_params) -> (xyz, joints_rel)``, which
         copies rot_params [J, rot_dim] into the graph's input and replays it -- no per-pose host
@@ -535,7 +535,16 @@ class TemporalPoints(torch.nn.Module):
         ``index % P`` from the sweep itself and advances a device index, so a step that is given
         the next row of the sweep (the sweep's order, as run.py walks it) is one graph launch with
         no input copy; another row sets the index first (one small fill), and rot_params that are
-        not a row of the sweep take the eager path."""
+        not a row of the sweep take the eager path.
+
+        ``pipelined`` (with a sweep): two poses in flight. The skeleton launch is one workgroup
+        (~16 us of latency) and the LBS waits for it; here step i's graph runs the LBS of pose i
+        from skeleton buffer k beside the skeleton of pose i + 1 into buffer 1 - k (a fork on a
+        side stream inside the graph), so in-order steps pay max(LBS, skeleton) instead of the
+        sum. A jump, the first step, or a sweep modified in place since the prefetch runs pose i's
+        skeleton first (a one-launch graph). joints_rel of a step stays valid for one more step."""
+        if sweep is not None and pipelined:
+            return self._capture_repose_pipelined(sweep)
         dev = self.canonical_pcd.device
         J = self.weights.shape[1]
         if sweep is not None:
@@ -584,6 +593,77 @@ class TemporalPoints(torch.nn.Module):
                 return xyz, joints_rel
 
         step.graph, step.inputs = graph, (rp if sweep is None else (sweep, idx))
+        return step
+
+    def _capture_repose_pipelined(self, sweep):
+        dev = self.canonical_pcd.device
+        J = self.weights.shape[1]
+        sweep = sweep.detach().to(dev, torch.float32).contiguous()
+        if sweep.dim() != 3 or sweep.shape[1] != J:
+            raise ValueError("capture_repose: sweep must be [P, J, rot_dim]")
+        P, rot_dim = sweep.shape[0], sweep.shape[2]
+        fw = self.forward_warp
+        idx = torch.zeros(1, dtype=torch.int32, device=dev)
+        bufs = [fw.pose_buffers(J, dev) for _ in range(2)]
+
+        def skel(k):
+            fw.pose(self.joints, rot_params=sweep, sweep_index=idx, out=bufs[k])
+
+        def lbs(k):
+            return self._lbs(bufs[k]["bone_Ts"], bufs[k]["gt"], records=False, T34=bufs[k]["T34"])[0]
+
+        with torch.no_grad():
+            cur = torch.cuda.current_stream(dev)
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):   # warm-up: caches, workspaces, packed buffers
+                for k in (0, 1):
+                    skel(k)
+                    lbs(k)
+            cur.wait_stream(side)
+            prologue, pair, xyz = [], [], []
+            with _capture_guard():
+                for k in (0, 1):
+                    g = torch.cuda.CUDAGraph()
+                    self._ws.hold(g)
+                    with torch.cuda.graph(g):
+                        skel(k)
+                    prologue.append(g)
+                for k in (0, 1):
+                    g = torch.cuda.CUDAGraph()
+                    self._ws.hold(g)
+                    with torch.cuda.graph(g):
+                        cap = torch.cuda.current_stream(dev)
+                        fork = torch.cuda.Stream(dev)
+                        fork.wait_stream(cap)
+                        with torch.cuda.stream(fork):   # the next pose's skeleton, beside this pose's LBS
+                            skel(1 - k)
+                        xyz.append(lbs(k))
+                        cap.wait_stream(fork)
+                    pair.append(g)
+        row = J * rot_dim * 4
+        base = sweep.data_ptr()
+        # k: the buffer holding the skeleton of pose `next` (None: nothing prefetched)
+        state = {"next": 0, "k": None, "ver": sweep._version}
+
+        def step(rot_params):
+            off = rot_params.data_ptr() - base
+            if (rot_params.device != sweep.device or not rot_params.is_contiguous() or off < 0 or off % row
+                    or off // row >= P or rot_params.numel() != J * rot_dim):
+                with torch.no_grad():
+                    return self.repose(rot_params)
+            i = off // row
+            k = state["k"]
+            if k is None or i != state["next"] or sweep._version != state["ver"]:
+                idx.fill_(i)
+                k = 0
+                prologue[0].replay()   # pose i's skeleton into buffer 0 (the index moves to i + 1)
+                state["ver"] = sweep._version
+            pair[k].replay()           # LBS of pose i from buffer k | skeleton of pose i + 1 into 1 - k
+            state["next"], state["k"] = (i + 1) % P, 1 - k
+            return xyz[k], bufs[k]["joints_rel"]
+
+        step.graph, step.inputs = pair, (sweep, idx)
         return step
 
     def capture_frame(self, t, render_kwargs, render_depth=True, render_weights=True, query_radius=0.01, poses=None,
@@ -655,7 +735,14 @@ class TemporalPoints(torch.nn.Module):
                       n_rays=out._n_rays, bg=out._bg, cap=self._capacity.get(cap_key), stale=False)
             step.graph = graph
 
+        cap_ws = workspace if workspace is not None else self._ws_eager
+
         def step(t):
+            if len(self.feat_net) == 6 and cap_ws.meta.get("pack_key") != self._mlp_weights_key():
+                # the MLP weights changed since this graph packed them: the shared projection P may
+                # already hold the new weights (an eager frame re-projected it), so replaying would
+                # mix two models -- capture again (the capture's warm-up repacks this workspace)
+                st["stale"] = True
             if st["stale"]:
                 # a replay overflowed the captured capacity; its re-render grew the capacity, so
                 # capture again (the old graph would overflow -- and re-render -- on every frame)
@@ -767,6 +854,14 @@ class TemporalPoints(torch.nn.Module):
             self.timing.setdefault("lbs_events", []).append((e0, e1))
         return xyz, wout, (recA, recB, bbox)
 
+    def _mlp_weights_key(self):
+        """Storage and in-place version of every tensor the packed MLP weights and the layer-1
+        projection P are derived from."""
+        layers = [self.feat_net[0], self.feat_net[2][0], self.feat_net[3][0], self.feat_net[4]]
+        params = [p for l in layers for p in (l.weight, l.bias)] + list(self.densitynet.parameters()) + \
+            list(self.rgbnet.parameters()) + [self.canonical_feat]
+        return tuple((p.data_ptr(), p._version) for p in params)
+
     def _packed_weights(self, pose_embedding, dev):
         """Packed MLP weights + the per-point layer-1 projection, cached on parameter versions
         (only the pose-embedding bias fold changes per frame)."""
@@ -774,9 +869,7 @@ class TemporalPoints(torch.nn.Module):
             raise NotImplementedError("the fused MLP kernel implements feat_depth=4 (the reference default)")
         from .ops import feat_project, fold_pose_bias, mlp_layout
         layers = [self.feat_net[0], self.feat_net[2][0], self.feat_net[3][0], self.feat_net[4]]
-        params = [p for l in layers for p in (l.weight, l.bias)] + list(self.densitynet.parameters()) + \
-            list(self.rgbnet.parameters()) + [self.canonical_feat]
-        key = tuple((p.data_ptr(), p._version) for p in params)
+        key = self._mlp_weights_key()
         # the packed buffer (0.5 MB) belongs to the frame's workspace: its b1 follows the frame's
         # pose embedding and its range flag the frame's MLP launch, so frames in flight each keep
         # their own; the projection P (N x 512 B) depends on the weights only and is shared
@@ -1118,7 +1211,7 @@ class TemporalPoints(torch.nn.Module):
         if self.timing is not None:
             e1.record()
             rows = self.last_mlp_rows.clone() if self.last_mlp_rows is not None else None
-            self.timing.setdefault("mlp_events", []).append((e0, e1, nsurv, rows))
+            self.timing.setdefault("mlp_events", []).append((e0, e1, nsurv.clone(), rows))
             self.timing["marks"].append(("mlp", e1))
         rx.switch("composite")
         # compositing

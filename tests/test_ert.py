@@ -6,8 +6,8 @@ and its compositing then stops each ray at the sample whose update takes T below
 path runs the MLP only on the samples the compositing reads (passes over the live rays' next
 samples) and the direct / weight-colour columns on every kept sample. The frame must be
 bit-identical to the one that runs the MLP on every kept sample -- on golden scenes, with and
-without the fast_color_thres masks, on a scene whose rays never terminate, and on the whole C2
-frame -- and the MLP must have skipped exactly the samples after each ray's break."""
+without the fast_color_thres masks, on a scene whose rays never terminate, and on the whole C2,
+C3 and C4 frames -- and the MLP must have skipped exactly the samples after each ray's break."""
 import numpy as np
 import pytest
 import torch
@@ -40,7 +40,36 @@ def _frame(model, t, rk, ert):
 
 def _breaks(alpha, s_ray, n_rays, thr):
     """Per kept sample: is it at or before its ray's break (the samples the compositing reads on the
-    Point-NeRF path), by the compositing's own arithmetic (float T updated in double)."""
+    Point-NeRF path), by the compositing's own arithmetic (float T updated in double). Vectorised over
+    rays (one numpy step per sample position along a ray), so the whole C4 frame takes seconds."""
+    a = alpha.astype(np.float32)
+    need = np.zeros(len(a), bool)
+    starts = np.searchsorted(s_ray, np.arange(n_rays))
+    ends = np.searchsorted(s_ray, np.arange(n_rays), side="right")
+    rays = np.nonzero(ends > starts)[0]
+    st, cnt = starts[rays], (ends - starts)[rays]
+    T = np.ones(len(rays), np.float32)
+    live = np.ones(len(rays), bool)
+    for j in range(int(cnt.max()) if len(rays) else 0):
+        act = live & (cnt > j)
+        if not act.any():
+            break
+        i = st[act] + j
+        need[i] = True
+        ai = a[i]
+        upd = (ai > np.float32(thr)) if thr > 0 else np.ones(len(i), bool)
+        Ta = T[act]
+        Tn = np.where(upd, (Ta.astype(np.float64) * (1.0 - ai.astype(np.float64))).astype(np.float32), Ta)
+        T[act] = Tn
+        brk = upd & (Tn.astype(np.float64) < 1e-3)
+        idx = np.nonzero(act)[0]
+        live[idx[brk]] = False
+    return need
+
+
+def _breaks_loop(alpha, s_ray, n_rays, thr):
+    """The same walk ray by ray, sample by sample (the compositing's loop as written); pins the
+    vectorised form above on the small scenes."""
     a = alpha.astype(np.float32)
     need = np.zeros(len(a), bool)
     starts = np.searchsorted(s_ray, np.arange(n_rays))
@@ -68,6 +97,8 @@ def _check(model, t, rk, thr):
     # the MLP's columns: identical on every sample the compositing reads, and the passes ran on
     # exactly those plus at most the rest of the pass in which the ray broke
     need = _breaks(f12[:, 3], f_ray.cpu().numpy(), len(rk["rays_o"]), thr)
+    if len(f12) < 200_000:
+        assert np.array_equal(need, _breaks_loop(f12[:, 3], f_ray.cpu().numpy(), len(rk["rays_o"]), thr))
     assert np.array_equal(f12[need, :4], e12[need, :4])
     n_rows = int(rows.sum())
     assert need.sum() <= n_rows <= len(f12)
@@ -104,14 +135,17 @@ def test_ert_without_masks_and_without_termination(dev):
     assert rows == kept == need
 
 
-def test_ert_full_c2_frame_bit_identical(dev):
+@pytest.mark.parametrize("config", ["C2", "C3", "C4"])
+def test_ert_full_frame_bit_identical(dev, config):
+    """Whole BASELINE frames: C2, C3 and C4 (inverse-y camera, pose embedding, the largest launch
+    and the only config with a sixth pass worth of rows past the fifth)."""
     from apn_amd import harness, synthetic as S
-    scene = S.make_scene("C2")
+    scene = S.make_scene(config)
     model = harness.build_model(scene, dev)
     rk = scene.render_kwargs(dev)
     t = torch.tensor([scene.cfg.t], device=dev)
     kept, need, rows, per = _check(model, t, rk, model.fast_color_thres)
-    print(f"C2: kept {kept}, read by the compositing {need} ({need / kept:.3f}), MLP rows {rows} "
+    print(f"{config}: kept {kept}, read by the compositing {need} ({need / kept:.3f}), MLP rows {rows} "
           f"({rows / kept:.3f}) per pass {per}")
     assert rows < kept
 

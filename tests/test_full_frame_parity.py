@@ -13,10 +13,12 @@ launch, ~20M in-bbox samples) -- over the WHOLE frame rather than a band:
   anisotropic-grid pass B, cost-ranked lanes);
 * ray shards of that frame (the "blocks" split at 4 and 8 ranks): every survivor of a shard
   equals the full frame's survivor of the same ray and step;
-* C2 end to end: EVERY ray of the frame -- all six output keys -- against the
-  oracle's forward (temporalpoints.py:540-712) on the GPU's warped cloud and rays, within 1e-5
-  unless the ray's oracle compositing sits on a discontinuity (oracle/flips.py, the rule of the
-  band tests in test_hip_parity.py)."""
+* end to end at C2, C3 and C4: EVERY ray of the frame -- all six
+  output keys -- against the oracle's forward (temporalpoints.py:540-712) on the GPU's warped cloud
+  and rays, within 1e-5 unless the ray's oracle compositing sits on a discontinuity
+  (oracle/flips.py, the rule of the band tests in test_hip_parity.py). C4 is the only config with
+  the ZJU inverse-y camera (tineuvox.py:675-703) and the pose embedding (temporalpoints.py:571-576),
+  and the largest launch (~5.6 M kept samples)."""
 import time
 
 import numpy as np
@@ -133,10 +135,10 @@ def test_ray_block_shard_knn_matches_full_frame(frame, world):
     assert np.array_equal(s_nbr, fr["s_nbr"][sel])
 
 
-@pytest.mark.parametrize("frame", ["C2"], indirect=True)
-def test_c2_every_ray_vs_oracle(frame):
-    """The whole C2 frame end to end: the oracle's forward over all 640k rays (in chunks of 50 image
-    rows; chunk invariance is the reference's own, and the bbox comes from the whole warped cloud)
+def test_every_ray_vs_oracle(frame):
+    """The whole frame end to end: the oracle's forward over all of its rays (640k at C2 / C3, 1M at
+    C4; in chunks of 50 image rows: chunk invariance is the reference's own, and the bbox comes
+    from the whole warped cloud)
     against the GPU frame, all six output keys, every ray within 1e-5 unless explained by a
     discontinuity of the reference's compositing (oracle/flips.py)."""
     from apn_amd import synthetic as S
@@ -180,6 +182,6 @@ def test_c2_every_ray_vs_oracle(frame):
             nb, w = assert_flips_explained(key, fr["out"][key][sel], ref[key].numpy(), orc.trace)
             n_bad[key] += nb
             worst[key] = max(worst[key], w)
-    print(f"C2 every ray: {R} rays, {kept} kept samples, oracle {time.perf_counter() - t0:.1f} s; rays over 1e-5 "
+    print(f"{fr['config']} every ray: {R} rays, {kept} kept samples, oracle {time.perf_counter() - t0:.1f} s; rays over 1e-5 "
           f"(all explained) {n_bad}; max error on rays off any discontinuity {worst}")
     assert kept == fr["ns"]

@@ -130,16 +130,18 @@ def test_captured_repose_graph_equals_eager(dev):
         assert torch.equal(xg, xe) and torch.equal(jg, je), k
 
 
-def test_captured_repose_sweep_graph(dev):
+@pytest.mark.parametrize("pipelined", [True, False])
+def test_captured_repose_sweep_graph(dev, pipelined):
     """capture_repose(sweep=poses): the graph reads its pose from the sweep through a device index
     it advances itself -- in-order steps, a jump (index reset), a wrap-around and rot_params that
-    are not a row of the sweep (eager fallback) all equal the eager repose bit for bit."""
+    are not a row of the sweep (eager fallback) all equal the eager repose bit for bit. Pipelined:
+    each step's graph also runs the next pose's skeleton beside its LBS (two poses in flight)."""
     from apn_amd import harness, synthetic as S
     scene = S.make_scene(S.SceneConfig("graph repose sweep", 30_000, 48, 0, 0))
     model = harness.build_model(scene, dev)
     poses = S.repose_sweep(48).to(dev).contiguous()
     P = poses.shape[0]
-    step = model.capture_repose(sweep=poses)
+    step = model.capture_repose(sweep=poses, pipelined=pipelined)
     order = [0, 1, 2, 3, 17, 18, P - 1, 0, 1, 5]
     for k in order:
         with torch.no_grad():
@@ -157,3 +159,28 @@ def test_captured_repose_sweep_graph(dev):
         xe, je = model.repose(poses[6])
     torch.cuda.synchronize()
     assert torch.equal(xg, xe) and torch.equal(jg, je)
+
+
+def test_pipelined_repose_sweep_modified_in_place(dev):
+    """The pipelined sweep prefetches pose i + 1's skeleton during step i; a sweep row changed in
+    place in between must not be rendered from the stale prefetch (the step re-runs the skeleton)."""
+    from apn_amd import harness, synthetic as S
+    scene = S.make_scene(S.SceneConfig("graph repose sweep inplace", 20_000, 24, 0, 0))
+    model = harness.build_model(scene, dev)
+    poses = S.repose_sweep(24).to(dev).contiguous()
+    step = model.capture_repose(sweep=poses)
+    for k in range(4):
+        step(poses[k])
+    with torch.no_grad():
+        poses[4].mul_(0.5)
+    xg, jg = (v.clone() for v in step(poses[4]))
+    with torch.no_grad():
+        xe, je = model.repose(poses[4])
+    torch.cuda.synchronize()
+    assert torch.equal(xg, xe) and torch.equal(jg, je)
+    for k in range(5, 9):   # and in order again afterwards
+        xg, jg = (v.clone() for v in step(poses[k]))
+        with torch.no_grad():
+            xe, je = model.repose(poses[k])
+        torch.cuda.synchronize()
+        assert torch.equal(xg, xe) and torch.equal(jg, je), k

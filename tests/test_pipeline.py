@@ -197,3 +197,68 @@ def test_render_viewpoints_in_flight_equals_serial(dev, tmp_path):
     assert next(iter(model._pipelines.values()))[1] is not pipe
     assert np.array_equal(d[0], e[0]) and not np.array_equal(d[0], b[0])
     del cached_pipeline
+
+
+def test_render_viewpoints_pageable_stacks_equal_pinned(dev, monkeypatch):
+    """A sweep whose result stacks exceed harness.PINNED_STACK_BYTES gets pageable numpy stacks
+    filled through the pipeline's pinned slots (no pinned allocation the size of the sweep): the
+    images are the same as with the pinned stacks."""
+    from apn_amd import harness as Hn
+    scene, model = _scene_model(dev)
+    rk = {k: v for k, v in scene.render_kwargs(dev).items() if k not in ("rays_o", "rays_d", "viewdirs")}
+    n = 7
+    poses = torch.stack([scene.c2w.float()] * n)
+    poses[:, 1, 3] += torch.linspace(0, 0.1, n)
+    HW = np.array([[scene.cfg.H, scene.cfg.W]] * n)
+    Ks = torch.stack([scene.K.float()] * n)
+    kw = dict(test_times=[scene.cfg.t + 0.03 * i for i in range(n)], verbose=False,
+              inverse_y=bool(rk.get("inverse_y", False)), in_flight=3)
+    a = Hn.render_viewpoints(model, poses, HW, Ks, False, dict(rk), **kw)
+    monkeypatch.setattr(Hn, "PINNED_STACK_BYTES", 0)
+    b = Hn.render_viewpoints(model, poses, HW, Ks, False, dict(rk), **kw)
+    for x, y in zip(a[:3], b[:3]):
+        assert x.shape == y.shape and np.array_equal(x, y)
+
+
+def test_held_pipeline_recaptures_after_weight_update(dev):
+    """A FramePipeline held across a weight update: an eager frame after the update
+    re-projects the shared layer-1 projection P with the new weights while the pipeline's
+    workspaces still hold the old packed weights; the next submit must capture again, not replay a
+    mix of the two models -- every later frame equals the eager frame of the updated model."""
+    from apn_amd.pipeline import FramePipeline
+    scene, model = _scene_model(dev)
+    rk = scene.render_kwargs(dev)
+    t = torch.tensor([scene.cfg.t], device=dev)
+    pipe = FramePipeline(model, t, rk, n=2, readback=("rgb_marched", "depth", "weights"))
+    old = pipe.submit(t).result()
+    with torch.no_grad():
+        model.feat_net[2][0].weight.mul_(1.02)
+        model.rgbnet.views_linears[0].bias.add_(0.05)
+    ref = _eager(model, t, rk)
+    got = [pipe.submit(t) for _ in range(3)]
+    for h in got:
+        r = h.result()
+        for k in ("rgb_marched", "depth", "weights"):
+            assert torch.equal(r[k], ref[k].cpu().reshape(r[k].shape)), k
+    assert not torch.equal(old["rgb_marched"], got[0].result()["rgb_marched"])
+
+
+def test_cached_pipeline_follows_render_settings(dev):
+    """cached_pipeline keys on the model's plain render settings too: changing
+    fast_color_thres between two sweeps captures a new pipeline instead of replaying the old one."""
+    from apn_amd.pipeline import cached_pipeline
+    scene, model = _scene_model(dev)
+    rk = scene.render_kwargs(dev)
+    t = torch.tensor([scene.cfg.t], device=dev)
+    p1 = cached_pipeline(model, t, rk, n=2, readback=("rgb_marched",))
+    assert cached_pipeline(model, t, rk, n=2, readback=("rgb_marched",)) is p1
+    thr = model.fast_color_thres
+    model.fast_color_thres = 0.2
+    try:
+        p2 = cached_pipeline(model, t, rk, n=2, readback=("rgb_marched",))
+        assert p2 is not p1
+        r = p2.submit(t).result()
+        ref = _eager(model, t, rk)
+        assert torch.equal(r["rgb_marched"], ref["rgb_marched"].cpu().reshape(r["rgb_marched"].shape))
+    finally:
+        model.fast_color_thres = thr
