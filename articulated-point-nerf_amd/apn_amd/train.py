@@ -20,6 +20,7 @@ What runs where:
 from __future__ import annotations
 
 import ctypes as C
+import gc
 
 import torch
 
@@ -368,9 +369,88 @@ def lbs_train(model, bone_Ts, global_t, identity_rules=None):
 
 # The warp stage of a training step -- skeleton (TransformNet, Rodrigues, masks, the kinematic
 # chain), fused LBS, pose embedding -- has the same shapes every step, so it runs as a captured
-# HIP graph pair (torch.cuda.make_graphed_callables: one forward replay, one backward replay)
-# instead of ~100 forward and ~250 backward launches from the host. Off: the eager composition.
+# HIP graph pair (graph_callable: one forward replay, one backward replay) instead of ~100 forward
+# and ~250 backward launches from the host. Off: the eager composition.
 GRAPH_WARP = True
+
+
+def graph_callable(module, sample, num_warmup=2):
+    """``module`` (forward(x) -> tuple of tensors) captured as a forward and a backward HIP graph
+    and wrapped in an autograd Function over (x, *module.parameters()): the role of
+    torch.cuda.make_graphed_callables, with the streams kept consistent for autograd.
+
+    Every parameter's AccumulateGrad node carries the stream it was created on, and a backward
+    that reaches it from another stream makes autograd synchronise -- and, inside a capture, ends
+    the capture when that stream is the default one (the core dump of round 5's capture probe).
+    make_graphed_callables warms up on one stream, captures on another, and keeps the captured
+    forward's autograd graph alive (its static outputs), so the parameters' nodes of the capture
+    stream stay alive and every later training backward on the default stream met them ("The
+    AccumulateGrad node's stream does not match ..."). Here: (1) unreachable graphs are collected
+    first and the caller has dropped its references to earlier steps' graphs, so no node of
+    another stream is alive; (2) warm-up and both captures run on ONE stream; (3) only detached
+    aliases of the static outputs are kept, so the captured forward's autograd graph -- and with
+    it the capture stream's AccumulateGrad nodes -- is freed before the first replay, and the
+    training step's own forward creates the nodes on its stream."""
+    dev = sample.device
+    params = tuple(module.parameters())
+    surface = (sample,) + params
+    req_in = [i for i, t in enumerate(surface) if t.requires_grad]
+    gc.collect()
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        for _ in range(num_warmup):
+            outs = tuple(module(sample))
+            req = [o for o in outs if o.requires_grad]
+            if req:
+                torch.autograd.grad(req, [surface[i] for i in req_in], [torch.empty_like(o) for o in req],
+                                    allow_unused=True)
+            del outs, req
+    torch.cuda.current_stream(dev).wait_stream(s)
+    torch.cuda.synchronize(dev)
+    static_in = sample.detach().clone()
+    pool = torch.cuda.graph_pool_handle()
+    fwd, bwd = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+    from .temporalpoints import _capture_guard
+    with _capture_guard():
+        with torch.cuda.graph(fwd, pool=pool, stream=s):
+            outs = tuple(module(static_in))
+        req_out = [i for i, o in enumerate(outs) if o.requires_grad]
+        static_gout = [torch.empty_like(outs[i]) for i in req_out]
+        with torch.cuda.graph(bwd, pool=pool, stream=s):
+            gin = torch.autograd.grad([outs[i] for i in req_out], [surface[i] for i in req_in], static_gout,
+                                      allow_unused=True)
+        static_out = tuple(o.detach() for o in outs)
+        static_gin = [None] * len(surface)
+        for i, g in zip(req_in, gin):
+            static_gin[i] = g.detach() if g is not None else None
+        del outs, gin
+    torch.cuda.current_stream(dev).wait_stream(s)
+
+    class _Graphed(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, *ps):
+            if x.data_ptr() != static_in.data_ptr():
+                static_in.copy_(x)
+            fwd.replay()
+            return tuple(o.detach() for o in static_out)
+
+        @staticmethod
+        @torch.autograd.function.once_differentiable
+        def backward(ctx, *grads):
+            for j, i in enumerate(req_out):
+                g = grads[i]
+                if g is None:
+                    static_gout[j].zero_()
+                elif g.data_ptr() != static_gout[j].data_ptr():
+                    static_gout[j].copy_(g)
+            bwd.replay()
+            return tuple(g.detach() if g is not None else None for g in static_gin)
+
+    def run(x):
+        return _Graphed.apply(x, *params)
+    run.graphs = (fwd, bwd)
+    return run
 
 
 class _WarpStage(torch.nn.Module):
@@ -426,7 +506,7 @@ def _graphed_warp(model, t_embed):
     stage = _WarpStage(model, identity_rules)
     stage.train(model.training)
     sample = t_embed.detach().clone()
-    graphed = torch.cuda.make_graphed_callables(stage, (sample,), num_warmup_iters=2, allow_unused_input=True)
+    graphed = graph_callable(stage, sample)
     model.__dict__["_warp_graph"] = (key, graphed)
     return graphed
 

@@ -10,7 +10,9 @@ import torch
 from golden_io import CASES, Golden
 from oracle import apn_oracle as O
 
-pytestmark = pytest.mark.gpu
+# a parameter's AccumulateGrad node reached from another stream is an error here (round 5: the
+# condition behind a captured-backward abort; apn_amd.train.graph_callable keeps the streams consistent)
+pytestmark = [pytest.mark.gpu, pytest.mark.filterwarnings("error:The AccumulateGrad node")]
 
 F32 = np.float32
 
@@ -969,7 +971,7 @@ def test_training_losses_vs_cpu(golden_model, dev):
     c2 = ((jt[:, None, :] - sk[torch.from_numpy(i2), :]) ** 2).sum(-1)
     ch = m.get_chamfer_loss(sk.to(dev), m.joints, c=0.03)
     ch_ref = m._rho(c1, 0.03).mean() + m._rho(c2, 0.03).mean()
-    assert abs(float(ch) - float(ch_ref)) < 1e-6
+    assert abs(float(ch.detach()) - float(ch_ref)) < 1e-6
     assert abs(float(m.get_joint_chamfer_loss()) - float(c2.sum())) < 1e-6
     assert float(m.get_joint_arap_loss()) >= 0 and torch.isfinite(m.get_weight_sparsity_loss())
 

@@ -6,7 +6,8 @@ and on later replays after optimizer updates, and the regularisers that read the
 import pytest
 import torch
 
-pytestmark = [pytest.mark.gpu, pytest.mark.autograd]
+# a parameter's AccumulateGrad node reached from another stream is an error (train.graph_callable)
+pytestmark = [pytest.mark.gpu, pytest.mark.autograd, pytest.mark.filterwarnings("error:The AccumulateGrad node")]
 
 
 @pytest.fixture(scope="module")
@@ -23,7 +24,7 @@ def _step(model, t, sub, target):
     loss = loss + 10.0 * model.get_neighbour_weight_tv_loss() + 0.2 * model.get_weight_sparsity_loss()
     loss.backward()
     grads = {k: p.grad.detach().clone() for k, p in model.named_parameters() if p.grad is not None}
-    return float(loss), out["t_hat_pcd"].detach().clone(), grads
+    return float(loss.detach()), out["t_hat_pcd"].detach().clone(), grads
 
 
 @pytest.mark.parametrize("name", ["C1", "G2"])

@@ -110,7 +110,7 @@ def run(args):
     ms = wall * 1e3 / args.steps
     out = {"metric": f"train_pcd iterations/s ({args.config}, N_rand={args.n_rand})", "value": 1e3 / ms,
            "unit": "it/s", "rays_per_s": args.n_rand * 1e3 / ms, "ms_per_step": ms, "stage_ms": stages,
-           "steps": args.steps, "warmup": args.warmup, "loss": float(loss), "dtype": "f32",
+           "steps": args.steps, "warmup": args.warmup, "loss": float(loss.detach()), "dtype": "f32",
            "data": "synthetic", "config": {"workload": scene.cfg.name, "n_rand": args.n_rand},
            "survivors_last_step": int(model.last_stats.get("survivors", -1))}
     if not args.no_cpu_baseline:
