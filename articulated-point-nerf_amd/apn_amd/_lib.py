@@ -52,6 +52,7 @@ SIGNATURES = {
     "apn_knn_points": (C.c_int, [P, I64, P, I64, I32, I32, P, P, P, P, P, P]),
     "apn_mlp_weight_layout": (C.c_int, [P]),
     "apn_mlp_split_weights": (C.c_int, [P, P]),
+    "apn_mlp_split_bias": (C.c_int, [P, P]),
     "apn_feat_project": (C.c_int, [P, I64, I32, P, P, P]),
     "apn_point_mlp": (C.c_int, [P, P, P, I64, P, P, P, P, I32, P, P, P, F32, F32, F32, I32, P, P]),
     "apn_point_mlp_ert_workspace_bytes": (SZ, [I64, I64]),
@@ -124,7 +125,10 @@ def load():
     except OSError as e:  # pragma: no cover
         _load_error = f"failed to load {LIB_PATH}: {e}"
         raise RuntimeError(_load_error)
+    ab_build = "APN_HIP_LIB" in os.environ   # an A/B build of an earlier revision (tools/)
     for name, (res, args) in SIGNATURES.items():
+        if ab_build and not hasattr(lib, name):
+            continue   # an entry point the earlier revision did not have (its callers skip it)
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

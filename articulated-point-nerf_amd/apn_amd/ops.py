@@ -305,6 +305,8 @@ def fold_pose_bias(l1, pose_embedding, buf):
     b1 = l1.bias.detach().float() + (w1[:, n_emb + n_feat:] @ pose_embedding.reshape(-1, 1).float()).reshape(-1)
     buf[lay["B1"]:lay["B1"] + b1.numel()].copy_(b1)
     buf[lay["FLAG"]:lay["FLAG"] + 1].view(torch.int32).zero_()
+    if hasattr(L.load(), "apn_mlp_split_bias"):   # (absent only from A/B builds of earlier revisions)
+        call("apn_mlp_split_bias", ptr(buf), stream_ptr(buf.device))   # b1 is also the bias column's weights
     return buf
 
 

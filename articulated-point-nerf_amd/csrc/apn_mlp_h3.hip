@@ -279,7 +279,8 @@ __device__ __forceinline__ void store_act(char* __restrict__ X, int ot0, const f
   for (int j = 0; j < 2; ++j) {
     const int o0 = 16 * (ot0 + j) + 4 * g;
     const f32x4 bb = bias ? *(const f32x4*)(bias + o0) : f32x4{0.f, 0.f, 0.f, 0.f};
-    const int c = o0 >> 3, sub = (g & 1) * 8;
+    // chunk 4w + g holds o-tile 2w's features 4g..4g+3 then o-tile 2w+1's (apn_mlp_layout.h act_k_of)
+    const int c = 2 * ot0 + g, sub = j * 8;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       const f32x4 a = acc[mt][j];
@@ -374,23 +375,8 @@ __device__ __forceinline__ void ws_gather_q(int nb, float4 q, const GatherRegs& 
       rw[2] = G.b0.x; rw[3] = G.b0.y; rw[4] = G.b0.z;
       rw[5] = G.b1.x; rw[6] = G.b1.y; rw[7] = G.b1.z;
     }
-    f32x4 sv0, sv1, cv0, cv1;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int aa = P + 4 * j;   // reference argument index a = 10 i + f (apn_mlp_layout.h pe_col_to_ref)
-      float sv, cv;
-      if (aa < 30) {
-#ifdef APN_H3_PROBE_NOPE   // timing probe only (wrong results): no posenc sin/cos
-        sv = rc[aa / 10] * (float)(1 << (aa % 10)); cv = sv * 0.5f;
-#else
-        sincos_pe(rc[aa / 10] * (float)(1 << (aa % 10)), sv, cv);
-#endif
-      } else {
-        sv = P == 2 ? rc[0] : rc[2];
-        cv = P == 2 ? rc[1] : 0.f;
-      }
-      if (j < 4) { sv0[j] = sv; cv0[j] = cv; } else { sv1[j - 4] = sv; cv1[j - 4] = cv; }
-    }
+    f32x4 sv0, sv1, cv0, cv1;   // arguments 8P .. 8P + 7 (apn_mlp_layout.h pe_col_to_ref)
+    pe_chunk<8 * P>(rc, sv0, sv1, cv0, cv1);
     h4 hs0, ls0, hs1, ls1, hc0, lc0, hc1, lc1;
     split4(sv0, hs0, ls0); split4(sv1, hs1, ls1);
     split4(cv0, hc0, lc0); split4(cv1, hc1, lc1);
@@ -614,7 +600,7 @@ __device__ __forceinline__ void mlp_tiles(
     if constexpr (PP || !kD2) layer_mfma<2, 4, 2, FR_W1E, FR_W2, PP || kBPF3>(X0, rs, vb, acc, a);
     else layer_mfma_d2<2, 4, 2, FR_W1E, FR_W2, false, true>(X0, rs, vb, acc, a, a1);
     if (!PP) __syncthreads();
-    store_act(X1, ot0, sW + SW_B1, acc, SCALED, SCALED ? sW[SW_DS + 0] : 1.f);
+    store_act(X1, ot0, nullptr, acc, SCALED, SCALED ? sW[SW_DS + 0] : 1.f);   // b1: the bias column
     __syncthreads();
     APN_PHASE(1)
     init_bias(acc, ot0, sW + SW_B2);
@@ -897,6 +883,7 @@ __global__ __launch_bounds__(256) void k_weight_scales(float* __restrict__ wbuf)
 #pragma unroll
   for (int m = 0; m < NG; ++m) red[m][tid] = 0.f;
   for (int i = tid; i < 128 * KE; i += 256) red[0][tid] = fmaxf(red[0][tid], fabsf(wbuf[OFF_W1E + i]));
+  if (tid < 128) red[0][tid] = fmaxf(red[0][tid], fabsf(wbuf[OFF_B1 + tid]));   // the bias column
   for (int i = tid; i < 128 * 128; i += 256) {
     red[1][tid] = fmaxf(red[1][tid], fabsf(wbuf[OFF_W2 + i]));
     red[2][tid] = fmaxf(red[2][tid], fabsf(wbuf[OFF_W3 + i]));
@@ -967,18 +954,34 @@ __global__ void k_split_weights(float* __restrict__ wbuf) {
     float w;
     if (mat == 0) {
       const int ref = pe_col_to_ref(k);
-      w = ref < 0 ? 0.f : wbuf[OFF_W1E + o * KE + ref];
+      w = ref == PE_BIAS ? wbuf[OFF_B1 + o] : (ref < 0 ? 0.f : wbuf[OFF_W1E + o * KE + ref]);
     } else if (mat == 4) {
       w = wbuf[OFF_WH + o * KV + k];
-    } else {
+    } else {   // hidden activations in the kernels' K order (apn_mlp_layout.h act_k_of)
       const int off = mat == 1 ? OFF_W2 : (mat == 2 ? OFF_W3 : OFF_W4);
-      w = wbuf[off + o * 128 + k];
+      w = wbuf[off + o * 128 + act_k_of(k)];
     }
     w *= (mat == 4 && k >= 128) ? sc_view : sc_mat;   // exact (powers of two)
     const _Float16 hi = (_Float16)w;
     dst[j] = hi;
     dst[FRAG_HALVES + j] = (_Float16)(w - (float)hi);
   }
+}
+
+// The bias column of W1E (apn_mlp_layout.h PE_BIAS, column 63 = k-chunk 1, lane group 3, half 7)
+// from the fp32 b1 -- after a per-frame pose-embedding fold of b1 (ops.fold_pose_bias). A value
+// beyond the fp16 range sets the range flag (the frame's MLP then runs on FP32 MFMA).
+__global__ void k_split_bias(float* __restrict__ wbuf) {
+  const int o = threadIdx.x;
+  if (o >= 128) return;
+  const float w = wbuf[OFF_B1 + o] * wbuf[OFF_SCALE + 0];
+  const int ot = o >> 4, lane = (o & 15) + 48;
+  const int fidx = (ot >> 1) * FR_WAVE + FR_W1E + ((ot & 1) * 2 + 1) * 2;
+  _Float16* dst = (_Float16*)(wbuf + OFF_H16) + (size_t)fidx * FRAG_HALVES + lane * 8 + 7;
+  const _Float16 hi = (_Float16)w;
+  dst[0] = hi;
+  dst[FRAG_HALVES] = (_Float16)(w - (float)hi);
+  if (!(fabsf(w) <= H3_RANGE)) *(int*)(wbuf + OFF_FLAG) = 1;
 }
 
 }  // namespace h3
@@ -1034,5 +1037,11 @@ extern "C" int apn_mlp_split_weights(float* wbuf, void* stream) {
   constexpr int n = 8 * 2 * 64 + 3 * 8 * 4 * 64 + 4 * 5 * 64;
   hipLaunchKernelGGL(h3::k_weight_scales, dim3(1), dim3(256), 0, (hipStream_t)stream, wbuf);
   hipLaunchKernelGGL(h3::k_split_weights, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, wbuf);
+  return launch_status();
+}
+
+extern "C" int apn_mlp_split_bias(float* wbuf, void* stream) {
+  if (!wbuf) return APN_ERR_ARG;
+  hipLaunchKernelGGL(h3::k_split_bias, dim3(1), dim3(128), 0, (hipStream_t)stream, wbuf);
   return launch_status();
 }

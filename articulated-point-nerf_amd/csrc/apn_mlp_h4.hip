@@ -50,15 +50,32 @@ constexpr int SW_B1 = 0, SW_B2 = 128, SW_B3 = 256, SW_B4 = 384, SW_WD = 512, SW_
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// Neighbour records of one gather row (loaded a segment ahead of their use).
+// Neighbour records of this thread's gather row. The posenc work of a tile is split by rows and
+// argument halves: thread t owns row r = t & 127 (sample r >> 3, neighbour r & 7) and half
+// h = t >> 7 (wave-uniform) of its arguments -- chunk pairs 2h, 2h + 1, i.e. arguments 16h ..
+// 16h + 15 (apn_mlp_layout.h pe_col_to_ref) -- so each row's records are read by two threads and
+// its rel_c computed twice (the 4-way quarter split before this read and computed them four times),
+// and consecutive frequencies of one coordinate meet in one thread (pe_chunk's double-angle steps).
 struct GatherRegs {
   float4 a0, a1, a2, a3, b0, b1;
-  float vv;
+  float v0, v1;   // viewdir components of the sample's view-embedding elements e, e + 1
 };
 
+// view-embedding element e (< 27) of poc_fre(viewdirs, 2^0..3) (tineuvox.py:872-878): its viewdir
+// component and frequency
+__device__ __forceinline__ int vemb_comp(int e) { return e < 3 ? e : ((e < 15 ? e - 3 : e - 15) >> 2); }
+__device__ __forceinline__ float vemb_val(int e, float vv) {
+  float sn_, cs_;
+  const int ee = e < 3 ? 0 : (e < 15 ? e - 3 : e - 15);
+  sincos_pe(vv * (float)(1 << (ee & 3)), sn_, cs_);
+  return e < 3 ? vv : (e < 15 ? sn_ : cs_);
+}
+
 // Loads are unconditional (clamped indices; invalid rows read row 0 and are discarded later): a
-// load under a divergent branch makes the compiler drain vmcnt(0) at the join.
-__device__ __forceinline__ void gather_load(int p, int k, int nb, int ray, GatherRegs& G,
+// load under a divergent branch makes the compiler drain vmcnt(0) at the join. recB (direct-blend
+// colours) only where the direct blend is computed here (not in the early-termination passes).
+template <bool DIRECT>
+__device__ __forceinline__ void gather_load(int h, int k, int nb, int ray, GatherRegs& G,
                                             const float4* __restrict__ recA, const float4* __restrict__ recB,
                                             const float* __restrict__ viewdirs, const float* __restrict__ vemb_const) {
   const size_t n = (size_t)max(nb, 0);
@@ -66,36 +83,52 @@ __device__ __forceinline__ void gather_load(int p, int k, int nb, int ray, Gathe
   G.a1 = recA[4 * n + 1];
   G.a2 = recA[4 * n + 2];
   G.a3 = recA[4 * n + 3];
-  G.b0 = recB[2 * n];
-  G.b1 = recB[2 * n + 1];
-  const int e = min(4 * k + p, 26);
-  const int ee = e < 3 ? 0 : (e < 15 ? e - 3 : e - 15);
-  G.vv = vemb_const ? 0.f : viewdirs[3 * (size_t)ray + (e < 3 ? e : ee >> 2)];
+  if (DIRECT) {
+    G.b0 = recB[2 * n];
+    G.b1 = recB[2 * n + 1];
+  }
+  const int e = 4 * k + 2 * h;
+  G.v0 = vemb_const ? 0.f : viewdirs[3 * (size_t)ray + vemb_comp(min(e, 26))];
+  G.v1 = vemb_const ? 0.f : viewdirs[3 * (size_t)ray + vemb_comp(min(e + 1, 26))];
 }
 
-// Row r = lane + 64 * HALF of the tile (sample r >> 3, neighbour r & 7); wave P computes quarter P
-// of the row's posenc columns (the reference's dim-major order, apn_mlp_layout.h pe_col_to_ref):
-// P is wave-uniform, so argument indices, frequencies and coordinate choices are compile-time
-// constants. Also writes the row's squared distance (sTo), the direct-blend terms (sRow) and the
-// sample's view-embedding element 4k + P (sV).
-template <int P, int HALF, bool DIRECT>
+// One chunk pair (arguments 8p .. 8p + 7) of row r: sines and cosines split into hi / lo halves and
+// stored as whole 16-B chunks at their swizzled positions.
+template <int PAIR>
+__device__ __forceinline__ void pe_store(char* __restrict__ xr, int r, const float (&rc)[3]) {
+  f32x4 sv0, sv1, cv0, cv1;
+  pe_chunk<8 * PAIR>(rc, sv0, sv1, cv0, cv1);
+  h4 hs0, ls0, hs1, ls1, hc0, lc0, hc1, lc1;
+  split4(sv0, hs0, ls0); split4(sv1, hs1, ls1);
+  split4(cv0, hc0, lc0); split4(cv1, hc1, lc1);
+  const int c_sin = (2 * PAIR) ^ (r & 15), c_cos = (2 * PAIR + 1) ^ (r & 15);
+  *(h8*)(xr + (c_sin << 4)) = __builtin_shufflevector(hs0, hs1, 0, 1, 2, 3, 4, 5, 6, 7);
+  *(h8*)(xr + (c_sin << 4) + 256) = __builtin_shufflevector(ls0, ls1, 0, 1, 2, 3, 4, 5, 6, 7);
+  *(h8*)(xr + (c_cos << 4)) = __builtin_shufflevector(hc0, hc1, 0, 1, 2, 3, 4, 5, 6, 7);
+  *(h8*)(xr + (c_cos << 4) + 256) = __builtin_shufflevector(lc0, lc1, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// Row r = t & 127 of the tile, argument half H (= wave >> 1, a compile-time constant): the posenc
+// chunk pairs 2H, 2H + 1, and -- half 0 -- the row's squared distance (sTo) or -- half 1 -- the
+// direct-blend terms (sRow); view-embedding elements 4k + 2H, 4k + 2H + 1 of the sample (sV).
+template <int H, bool DIRECT>
 __device__ __forceinline__ void gather_q(int nb, float4 q, const GatherRegs& G, char* __restrict__ PE,
                                          float* __restrict__ sTo, float* __restrict__ sRow, float* __restrict__ sV,
                                          const float* __restrict__ vemb_const) {
-  int r_ = (threadIdx.x & 63) + 64 * HALF;
+  int r_ = threadIdx.x & 127;
   asm volatile("" : "+v"(r_));   // per-lane LDS addresses recomputed per tile, not hoisted and spilled
   const int r = r_, s = r >> 3, k = r & 7;
   char* xr = PE + r * XB;
-  const int c_sin = (2 * P) ^ (r & 15), c_cos = (2 * P + 1) ^ (r & 15);
+  const int e = 4 * k + 2 * H;
   if (nb >= 0) {
     const float4 a0 = G.a0, a1 = G.a1, a2 = G.a2, a3 = G.a3;
     const float dx = q.x - a0.x, dy = q.y - a0.y, dz = q.z - a0.z;
     // rel_c = Rinv (x - p) (temporalpoints.py:454-458)
     const float rc[3] = {(a1.x * dx + a1.y * dy) + a1.z * dz, (a1.w * dx + a2.x * dy) + a2.y * dz,
                          (a2.z * dx + a2.w * dy) + a3.x * dz};
-    if constexpr (P == 0) {
+    if constexpr (H == 0) {
       sTo[r] = (dx * dx + dy * dy) + dz * dz;
-    } else if constexpr (P == 1 && DIRECT) {
+    } else if constexpr (DIRECT) {
       const float tn = (dx * dx + dy * dy) + dz * dz;
       float* rw = sRow + RS * r;
       rw[0] = expf(-(tn * tn) / a0.w);   // temporalpoints.py:461 (to_nn is already squared)
@@ -103,64 +136,43 @@ __device__ __forceinline__ void gather_q(int nb, float4 q, const GatherRegs& G, 
       rw[2] = G.b0.x; rw[3] = G.b0.y; rw[4] = G.b0.z;
       rw[5] = G.b1.x; rw[6] = G.b1.y; rw[7] = G.b1.z;
     }
-    f32x4 sv0, sv1, cv0, cv1;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int aa = P + 4 * j;   // reference argument index a = 10 i + f
-      float sv, cv;
-      if (aa < 30) {
-        sincos_pe(rc[aa / 10] * (float)(1 << (aa % 10)), sv, cv);
-      } else {
-        sv = P == 2 ? rc[0] : rc[2];
-        cv = P == 2 ? rc[1] : 0.f;
-      }
-      if (j < 4) { sv0[j] = sv; cv0[j] = cv; } else { sv1[j - 4] = sv; cv1[j - 4] = cv; }
+    pe_store<2 * H>(xr, r, rc);
+    pe_store<2 * H + 1>(xr, r, rc);
+    float v0 = 0.f, v1 = 0.f;
+    if (vemb_const) {
+      v0 = e < 27 ? vemb_const[e] : 0.f;
+      v1 = e + 1 < 27 ? vemb_const[e + 1] : 0.f;
+    } else {
+      if (e < 27) v0 = vemb_val(e, G.v0);
+      if (e + 1 < 27) v1 = vemb_val(e + 1, G.v1);
     }
-    h4 hs0, ls0, hs1, ls1, hc0, lc0, hc1, lc1;
-    split4(sv0, hs0, ls0); split4(sv1, hs1, ls1);
-    split4(cv0, hc0, lc0); split4(cv1, hc1, lc1);
-    *(h8*)(xr + (c_sin << 4)) = __builtin_shufflevector(hs0, hs1, 0, 1, 2, 3, 4, 5, 6, 7);
-    *(h8*)(xr + (c_sin << 4) + 256) = __builtin_shufflevector(ls0, ls1, 0, 1, 2, 3, 4, 5, 6, 7);
-    *(h8*)(xr + (c_cos << 4)) = __builtin_shufflevector(hc0, hc1, 0, 1, 2, 3, 4, 5, 6, 7);
-    *(h8*)(xr + (c_cos << 4) + 256) = __builtin_shufflevector(lc0, lc1, 0, 1, 2, 3, 4, 5, 6, 7);
-    const int e = 4 * k + P;   // view embedding element e of this sample (tineuvox.py:872-878)
-    float v = 0.f;
-    if (e < 27) {
-      if (vemb_const) {
-        v = vemb_const[e];
-      } else {
-        const int ee = e < 3 ? 0 : (e < 15 ? e - 3 : e - 15);
-        float sn_, cs_;
-        sincos_pe(G.vv * (float)(1 << (ee & 3)), sn_, cs_);
-        v = e < 3 ? G.vv : (e < 15 ? sn_ : cs_);
-      }
-    }
-    sV[s * 32 + e] = v;
+    sV[s * 32 + e] = v0;
+    sV[s * 32 + e + 1] = v1;
   } else {
     const h8 z = {0, 0, 0, 0, 0, 0, 0, 0};
-    *(h8*)(xr + (c_sin << 4)) = z;
-    *(h8*)(xr + (c_sin << 4) + 256) = z;
-    *(h8*)(xr + (c_cos << 4)) = z;
-    *(h8*)(xr + (c_cos << 4) + 256) = z;
-    sV[s * 32 + 4 * k + P] = 0.f;
-    if constexpr (P == 0) {
+#pragma unroll
+    for (int c = 4 * H; c < 4 * H + 4; ++c) {
+      *(h8*)(xr + ((c ^ (r & 15)) << 4)) = z;
+      *(h8*)(xr + ((c ^ (r & 15)) << 4) + 256) = z;
+    }
+    sV[s * 32 + e] = 0.f;
+    sV[s * 32 + e + 1] = 0.f;
+    if constexpr (H == 0) {
       sTo[r] = 1.f;
-    } else if constexpr (P == 1 && DIRECT) {
+    } else if constexpr (DIRECT) {
       for (int c = 0; c < 8; ++c) sRow[RS * r + c] = 0.f;
     }
   }
 }
 
-template <int HALF, bool DIRECT>
-__device__ __forceinline__ void gather(int p, int nb, float4 q, const GatherRegs& G, char* __restrict__ PE,
+template <bool DIRECT>
+__device__ __forceinline__ void gather(int h, int nb, float4 q, const GatherRegs& G, char* __restrict__ PE,
                                        float* __restrict__ sTo, float* __restrict__ sRow, float* __restrict__ sV,
                                        const float* __restrict__ vemb_const) {
-  switch (p) {
-    case 0: gather_q<0, HALF, DIRECT>(nb, q, G, PE, sTo, sRow, sV, vemb_const); break;
-    case 1: gather_q<1, HALF, DIRECT>(nb, q, G, PE, sTo, sRow, sV, vemb_const); break;
-    case 2: gather_q<2, HALF, DIRECT>(nb, q, G, PE, sTo, sRow, sV, vemb_const); break;
-    default: gather_q<3, HALF, DIRECT>(nb, q, G, PE, sTo, sRow, sV, vemb_const); break;
-  }
+  if (h == 0)
+    gather_q<0, DIRECT>(nb, q, G, PE, sTo, sRow, sV, vemb_const);
+  else
+    gather_q<1, DIRECT>(nb, q, G, PE, sTo, sRow, sV, vemb_const);
 }
 
 // acc[mt][j] += W[o-tile 2w+j] X^T over NQ chunks of 32 and the tile's 8 M-tiles. `a` carries chunk
@@ -224,35 +236,34 @@ __device__ __forceinline__ void layer_mfma(const char* __restrict__ X, rsrc_t rs
   }
 }
 
-// lrelu(acc [+ bias]) -> the next layer's input rows. Lane (li, g) of (mt, j) holds features
-// 16 (2w + j) + 4g + r of row 16 mt + li; lanes g and g ^ 1 swap halves (v_permlane16_swap) so the
-// even one writes the 16-B chunk's hi halves and the odd one its lo halves. `bias` (layer 1: the
-// unscaled b1 added as fma(acc, 2^-s, b)) or nullptr (layers 2-4: bias in the accumulator; scaled:
-// times 2^-s).
+// lrelu(acc [+ bias]) -> the next layer's input rows. Lane (li, g) of M-tile mt holds features
+// 16 (2w + j) + 4g + r (j = 0, 1; r = 0..3) of row 16 mt + li: its 8 values are stored as one 16-B
+// chunk of hi halves and one of lo halves, chunk 4w + g (the K order of apn_mlp_layout.h act_k_of,
+// which W2..W4's fragments follow) -- no cross-lane exchange. `bias` (layer 1: the unscaled b1
+// added as fma(acc, 2^-s, b)) or nullptr (layers 2-4: bias in the accumulator; scaled: times 2^-s).
 __device__ __forceinline__ void store_act(char* __restrict__ X, int ot0, const float* __restrict__ bias,
                                           const f32x4 (&acc)[MT][2], bool scaled, float dsc) {
   const int lane = threadIdx.x & 63;
   const int li = lane & 15, g = lane >> 4;
-  const int lo_off = (g & 1) * 256;
+  const int c = 2 * ot0 + g;
+  f32x4 bb[2];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int o0 = 16 * (ot0 + j) + 4 * g;
-    const f32x4 bb = bias ? *(const f32x4*)(bias + o0) : f32x4{0.f, 0.f, 0.f, 0.f};
-    const int c = 2 * (ot0 + j) + (g >> 1);   // the chunk holding features of lanes g & ~1, g | 1
+  for (int j = 0; j < 2; ++j)
+    bb[j] = bias ? *(const f32x4*)(bias + 16 * (ot0 + j) + 4 * g) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
+  for (int mt = 0; mt < MT; ++mt) {
+    h4 hi[2], lo[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
       const f32x4 a = acc[mt][j];
-      const f32x4 v = lrelu4(bias ? f32x4{fmaf(a[0], dsc, bb[0]), fmaf(a[1], dsc, bb[1]), fmaf(a[2], dsc, bb[2]),
-                                          fmaf(a[3], dsc, bb[3])}
+      const f32x4 v = lrelu4(bias ? f32x4{fmaf(a[0], dsc, bb[j][0]), fmaf(a[1], dsc, bb[j][1]),
+                                          fmaf(a[2], dsc, bb[j][2]), fmaf(a[3], dsc, bb[j][3])}
                                   : (scaled ? f32x4{a[0] * dsc, a[1] * dsc, a[2] * dsc, a[3] * dsc} : a));
-      h4 hi, lo;
-      split4(v, hi, lo);
-      const u32x2 hb = __builtin_bit_cast(u32x2, hi), lb = __builtin_bit_cast(u32x2, lo);
-      // even row of a 16-lane pair: {own hi, partner hi}; odd row: {partner lo, own lo}
-      const auto s0 = __builtin_amdgcn_permlane16_swap(hb[0], lb[0], false, false);
-      const auto s1 = __builtin_amdgcn_permlane16_swap(hb[1], lb[1], false, false);
-      *(u32x4*)(X + act_off(16 * mt + li, c) + lo_off) = u32x4{s0[0], s1[0], s0[1], s1[1]};
+      split4(v, hi[j], lo[j]);
     }
+    char* p = X + act_off(16 * mt + li, c);
+    *(h8*)p = __builtin_shufflevector(hi[0], hi[1], 0, 1, 2, 3, 4, 5, 6, 7);
+    *(h8*)(p + 256) = __builtin_shufflevector(lo[0], lo[1], 0, 1, 2, 3, 4, 5, 6, 7);
   }
 }
 
@@ -314,22 +325,22 @@ __device__ __forceinline__ void mlp_tiles(
   const int chunk = (ntiles + nx - 1) / nx;
   const int t_beg = xcd * chunk, t_end = min(ntiles, t_beg + chunk);
 
-  // next-tile prefetch (unconditional clamped loads): this thread's two gather rows (lane and
-  // lane + 64: neighbour lane & 7 of samples lane >> 3 and 8 + (lane >> 3)) and its 8 P rows
-  int pf_nb[2], pf_ray[2], pf_pn[MT];
-  bool pf_ok[2], pf_pok[MT];
-  float4 pf_q[2];
+  // next-tile prefetch (unconditional clamped loads): this thread's gather row (tid & 127:
+  // neighbour lane & 7 of sample (tid & 127) >> 3) and its 8 P rows
+  const int gh = wid >> 1;   // the thread's posenc argument half (wave-uniform)
+  int pf_nb, pf_ray, pf_pn[MT];
+  bool pf_ok, pf_pok[MT];
+  float4 pf_q;
   auto fetch = [&](int tl) {
     const int tc = min(tl, t_end - 1);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int gs = tc * TS4 + 8 * h + (lane >> 3);
+    {
+      const int gs = tc * TS4 + ((tid & 127) >> 3);
       const int gc = min(gs, nS - 1);
       const int si = LISTED ? list[gc] : gc;
-      pf_ok[h] = tl < t_end && gs < nS;
-      pf_nb[h] = s_nbr[(size_t)si * 8 + (lane & 7)];
-      pf_q[h] = s_pos[si];
-      pf_ray[h] = s_ray[si];
+      pf_ok = tl < t_end && gs < nS;
+      pf_nb = s_nbr[(size_t)si * 8 + (lane & 7)];
+      pf_q = s_pos[si];
+      pf_ray = s_ray[si];
     }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -365,19 +376,17 @@ __device__ __forceinline__ void mlp_tiles(
     if (TIMED) { tk = clock64(); ph[4] += 1; }
     // ------------------------------------------------ loads: the gather's records, then the next
     // tile's indices (vmcnt is in order: what is consumed first is issued first)
-    const int nb0 = pf_ok[0] ? pf_nb[0] : -1, nb1 = pf_ok[1] ? pf_nb[1] : -1;
-    const float4 q0 = pf_q[0], q1 = pf_q[1];
-    GatherRegs g0, g1;
-    gather_load(wid, lane & 7, nb0, pf_ray[0], g0, recA, recB, viewdirs, vemb_const);
-    gather_load(wid, lane & 7, nb1, pf_ray[1], g1, recA, recB, viewdirs, vemb_const);
+    const int nb0 = pf_ok ? pf_nb : -1;
+    const float4 q0 = pf_q;
+    GatherRegs g0;
+    gather_load<!LISTED>(gh, lane & 7, nb0, pf_ray, g0, recA, recB, viewdirs, vemb_const);
     int pn_tile[MT];
     bool pok_tile[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) { pn_tile[mt] = pf_pn[mt]; pok_tile[mt] = pf_pok[mt]; }
     fetch(tile + per_xcd);
     // ------------------------------------------------ gather + posenc + direct-blend terms
-    gather<0, !LISTED>(wid, nb0, q0, g0, X, sTo, sRow, sV, vemb_const);
-    gather<1, !LISTED>(wid, nb1, q1, g1, X, sTo, sRow, sV, vemb_const);
+    gather<!LISTED>(gh, nb0, q0, g0, X, sTo, sRow, sV, vemb_const);
     // layer-1 accumulators = P[nbr] (global -> VGPR), loaded after the gather's register peak
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -425,7 +434,7 @@ __device__ __forceinline__ void mlp_tiles(
     // ------------------------------------------------ feat_net: 4 x (Linear + LeakyReLU)
     layer_mfma<2, 4, 2, FR_W1E, FR_W2>(X, rs, vb, acc, a);
     __syncthreads();
-    store_act(X, ot0, sW + SW_B1, acc, SCALED, SCALED ? sW[SW_DS + 0] : 1.f);
+    store_act(X, ot0, nullptr, acc, SCALED, SCALED ? sW[SW_DS + 0] : 1.f);   // b1: the bias column
     __syncthreads();
     APN_PHASE(1)
     init_bias(acc, ot0, sW + SW_B2);

@@ -70,19 +70,33 @@ constexpr int W_TOTAL = OFF_SCALE + 8;
 constexpr float SCALE_LO = 0.03125f, SCALE_HI = 4096.f;   // unscaled range of max|w|
 constexpr int SCALE_TARGET_EXP = 13;                        // scaled: max|w 2^s| in [2^12, 2^13)
 
-// Column order of the positional encoding inside the fp16 kernel's layer-1 operand (64 columns):
-// gather thread p (4 per MLP row) owns columns 16p..16p+15 = sin(arg a_j), j = 0..7, then
-// cos(arg a_j), with a_j = p + 4 j the reference argument index a = 10 i + f (rel_c[i] * 2^f).
-// Slots whose a_j >= 30 carry rel_c: column 39 = rel_c[0], 47 = rel_c[1], 55 = rel_c[2], 63 = 0.
-// Returns the reference embedding index (poc_fre order: [x(3), sin(30), cos(30)]) or -1.
+// Column order of the positional encoding inside the fp16 kernels' layer-1 operand (64 columns,
+// 8 chunks of 8): chunk pair p (p = 0..3) holds the arguments a = 8p .. 8p+7 -- chunk 2p their
+// sines, chunk 2p+1 their cosines -- with a = 10 i + f the reference argument index (rel_c[i] * 2^f,
+// poc_fre's dim-major order). Consecutive frequencies of one coordinate are then neighbours, and
+// the gather computes every odd frequency from the even one below it by one double-angle step
+// (pe_chunk, apn_mlp_split.h). Slots a = 30, 31 carry rel_c: sin slot 30 = rel_c[0], cos slot 30 =
+// rel_c[1], sin slot 31 = rel_c[2]; cos slot 31 (column 63) is the constant 1 and its weights are
+// b1, so the MFMAs add layer 1's bias (no VALU add in the activation store).
+// Returns the reference embedding index (poc_fre order: [x(3), sin(30), cos(30)]) or PE_BIAS.
+constexpr int PE_BIAS = -2;
 __host__ __device__ constexpr int pe_col_to_ref(int c) {
-  const int p = c >> 4, j = c & 7, is_cos = (c >> 3) & 1;
-  const int a = p + 4 * j;
+  const int p = c >> 4, is_cos = (c >> 3) & 1, j = c & 7;
+  const int a = 8 * p + j;
   if (a < 30) return (is_cos ? 33 : 3) + a;
-  if (c == 39) return 0;
-  if (c == 47) return 1;
-  if (c == 55) return 2;
-  return -1;
+  if (a == 30) return is_cos ? 1 : 0;
+  return is_cos ? PE_BIAS : 2;
+}
+
+// K order of the fp16 kernels' hidden activations (the input of W2, W3, W4): position k of a
+// 32-wide K chunk q holds feature act_k_of(k). A lane of wave w holds, after its layer's MFMAs,
+// features 32w + 4g + r of o-tile 2w and 32w + 16 + 4g + r of o-tile 2w + 1 (r = 0..3, the
+// transposed product's C layout) of one row: stored together as chunk 4w + g -- a whole 16-B
+// chunk of hi halves and one of lo halves per lane, no cross-lane exchange -- so the weight
+// fragments of W2..W4 take their columns in that order (k_split_weights).
+__host__ __device__ constexpr int act_k_of(int k) {
+  const int q = k >> 5, g = (k >> 3) & 3, r = k & 7;
+  return 32 * q + (r < 4 ? 4 * g + r : 16 + 4 * g + r - 4);
 }
 
 // LeakyReLU(0.01): x >= 0 ? x : 0.01x == max(x, 0.01x) (the same rounded product; 2 VALU ops)

@@ -37,6 +37,42 @@ __device__ __forceinline__ void sincos_pe(float x, float& sn, float& cs) {
   cs = __uint_as_float(__float_as_uint(cc) ^ (((qb + 1u) << 30) & 0x80000000u));   // (q + 1) & 2: -cos
 }
 
+// sin / cos of the positional-encoding arguments a = A0 .. A0 + 7 of one MLP row (a = 10 i + f:
+// rel_c[i] * 2^f, tineuvox.py:872-878; apn_mlp_layout.h pe_col_to_ref): even frequencies (and the
+// chunk's first argument) by sincos_pe, each odd frequency from the one below it by one
+// double-angle step (sin 2x = 2 sin x cos x, cos 2x = 1 - 2 sin^2 x: 4 VALU instead of ~18; the
+// argument doubles exactly, 2^f being a power of two). Error budget (float64 over |rel_c| <= 0.3,
+// 2M draws): sincos_pe 9.2e-8 absolute, after one step 2.9e-7 (fp32 libm: 7e-8); the stage stays
+// within 1e-5 of the fp32 oracle and of float64 (tests/test_mlp_precision.py). Slots 30 / 31 carry
+// rel_c and the bias input 1 (see pe_col_to_ref).
+template <int A0>
+__device__ __forceinline__ void pe_chunk(const float (&rc)[3], f32x4& s0, f32x4& s1, f32x4& c0, f32x4& c1) {
+  float sv[8], cv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int a = A0 + j, i = a / 10, f = a % 10;
+    if (a < 30) {
+      if (j == 0 || (f & 1) == 0) {
+        sincos_pe(rc[i] * (float)(1 << f), sv[j], cv[j]);
+      } else {
+        const float s = sv[j - 1], c = cv[j - 1];
+        sv[j] = 2.f * (s * c);
+        cv[j] = fmaf(-2.f * s, s, 1.f);
+      }
+    } else if (a == 30) {
+      sv[j] = rc[0];
+      cv[j] = rc[1];
+    } else {
+      sv[j] = rc[2];
+      cv[j] = 1.f;   // the layer-1 bias column (apn_mlp_layout.h PE_BIAS)
+    }
+  }
+  s0 = f32x4{sv[0], sv[1], sv[2], sv[3]};
+  s1 = f32x4{sv[4], sv[5], sv[6], sv[7]};
+  c0 = f32x4{cv[0], cv[1], cv[2], cv[3]};
+  c1 = f32x4{cv[4], cv[5], cv[6], cv[7]};
+}
+
 // Byte offset of logical 16-B chunk c (8 halves, 0..15) of the hi part of activation row m.
 __device__ __forceinline__ int act_off(int m, int c) { return m * XB + ((c ^ (m & 15)) << 4); }
 // Byte offset of fp32 chunk c (4 floats, 0..31) of row m of the layer-4 output.

@@ -304,6 +304,12 @@ int apn_mlp_weight_layout(int32_t* offsets);
  * every change of the fp32 region and before apn_point_mlp with the default (split) kernel. */
 int apn_mlp_split_weights(float* wbuf, void* stream);
 
+/* Refresh only the layer-1 bias inside the fp16 fragment region (the split kernels take b1 as the
+ * weights of a constant-1 input column) from the fp32 b1 of wbuf -- after a per-frame fold of the
+ * pose embedding into b1 (temporalpoints.py:487-488). Sets the range flag if the scaled bias leaves
+ * the fp16 range. */
+int apn_mlp_split_bias(float* wbuf, void* stream);
+
 /* Per-point layer-1 feature projection proj [N,128] = canonical_feat [N,128] x W1F^T
  * (temporalpoints.py:483-491 reassociated: W1 [emb; feat] = W1e emb + W1f feat). Computed once
  * per model; feat_dim must be 128. */
