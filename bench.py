@@ -491,17 +491,19 @@ def replay_sharded(steps_in_flight, views, k, streams, comm):
 
 
 def viewpoint_rate(model, scene, dev, n_views=16, in_flight=3):
-    """harness.render_viewpoints (run.py:80-239) over n_views views at distinct times -- rays made
+    """harness.render_viewpoints (run.py:80-239) over n_views views (distinct times and camera poses,
+    synthetic.view_sweep) -- rays made
     on the device per view, n frames in flight on the model's FramePipeline, rgb / depth / weights
     read back to host numpy per view -- timed after one untimed sweep (the captures). The drop-in
     render loop's rate next to the timed loop's."""
     from apn_amd.tineuvox import get_rays_of_a_view  # noqa: F401  (the harness's ray maker)
     H, W = scene.cfg.H, scene.cfg.W
     rk = {k: v for k, v in scene.render_kwargs(dev).items() if k not in ("rays_o", "rays_d", "viewdirs")}
-    poses = scene.c2w[None].repeat(n_views, 1, 1)
+    sweep = S.view_sweep(scene, n_views, "cpu")   # the timed loop's views: new time and camera pose each
+    poses = torch.stack([v.c2w for v in sweep])
     HW = [[H, W]] * n_views
     Ks = scene.K[None].repeat(n_views, 1, 1)
-    times = [scene.cfg.t + 0.01 * i for i in range(n_views)]
+    times = [float(v.t) for v in sweep]
     kw = dict(test_times=times, verbose=False, inverse_y=bool(rk.get("inverse_y", False)), in_flight=in_flight)
     for _ in range(2):   # the first call captures the pipeline, the second warms the pinned stacks
         harness.render_viewpoints(model, poses, HW, Ks, False, dict(rk), **kw)
@@ -527,7 +529,7 @@ def viewpoint_rate(model, scene, dev, n_views=16, in_flight=3):
     return {"views": n_views, "distinct_times": n_views, "frames_in_flight": in_flight,
             "ms_per_frame": el / n_views * 1e3, "rays_per_s": n_views * H * W / el,
             "pipeline_readback_ms_per_frame": bare,
-            "note": "harness.render_viewpoints over views at distinct times, one model (apn_amd.pipeline."
+            "note": "harness.render_viewpoints over views at distinct times and camera poses, one model (apn_amd.pipeline."
                     "FramePipeline: per-frame workspaces, shared canonical tables / projection), per view: rays "
                     "on the device, frame submitted, rgb / depth / weights read back to host numpy; second call "
                     "timed (the first captures)"}
@@ -713,7 +715,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=None,
                     help="ranks (one per GPU); N > 1 without an outer launcher starts the N ranks itself; "
                          "under one it must equal WORLD_SIZE")
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=16)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C2")
     ap.add_argument("--views", type=int, default=16,
@@ -1069,12 +1071,12 @@ def main():
             knn = knn_report(model, S_last, stats.get("inbbox_samples"), stage_ms.get("knn", 0.0))
         except Exception as e:  # never lose the GPU line over a diagnostic
             log(f"knn work report failed: {e!r}")
-    views = None
+    vp = None
     if world == 1 and use_graph and not args.no_viewpoints:
         try:
-            views = viewpoint_rate(model, scene, dev, in_flight=args.in_flight)
-            log(f"[render_viewpoints] {views['ms_per_frame']:.3f} ms/frame over {views['views']} views "
-                f"({views['frames_in_flight']} in flight, host readback)")
+            vp = viewpoint_rate(model, scene, dev, in_flight=args.in_flight)
+            log(f"[render_viewpoints] {vp['ms_per_frame']:.3f} ms/frame over {vp['views']} views "
+                f"({vp['frames_in_flight']} in flight, host readback)")
         except Exception as e:  # never lose the GPU line over a diagnostic
             log(f"render_viewpoints leg failed: {e!r}")
     others = None
@@ -1149,7 +1151,7 @@ def main():
         "cpu_baseline": cpu,
         "psnr_vs_oracle": psnr,
         "same_cloud_vs_oracle": same,
-        **({"render_viewpoints": views} if views is not None else {}),
+        **({"render_viewpoints": vp} if vp is not None else {}),
         **({"other_configs": others} if others is not None else {}),
     }
     emit(line, args)
