@@ -36,6 +36,7 @@ SIGNATURES = {
     "apn_skeleton_pose": (C.c_int, [P, I32, P, I32, I32, P, I32, I32, P, P, I32, P, P, P, P, P, P, P, P, P, P, P]),
     "apn_skeleton_frame": (C.c_int, [P, P, I32, P, I32, I32, P, I32, I32, P, P, I32, P, P, P, P, P, P, P, P, P, P,
                                      P, P, I32, P, P, I32, P]),
+    "apn_skeleton_sweep": (C.c_int, [P, I32, I32, I32, P, P, I32, P, P, P, P, P, P, P, P, P, P]),
     "apn_bbox_unpack": (C.c_int, [P, F32, P, P]),
     "apn_gather_rays": (C.c_int, [P, P, P, P, I64, P, P, P, P]),
     "apn_inbbox_count": (C.c_int, [P, P, P, F32, F32, F32, I64, P, P, P]),

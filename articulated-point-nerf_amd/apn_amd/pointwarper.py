@@ -249,6 +249,19 @@ class PointWarper(torch.nn.Module):
         self.last_joints2d = j2d
         return bone_Ts, gt, joints_rel
 
+    def pose_sweep(self, joints, sweep, out):
+        """Every pose of a repose sweep [P, J, rot_dim] in one launch (apn_skeleton_sweep: one
+        workgroup per pose, each exactly as ``pose(rot_params=sweep[p])``) into ``out`` =
+        pose_buffers-shaped tensors with a leading P dimension."""
+        dev = joints.device
+        J = joints.shape[0]
+        P, rot_dim = sweep.shape[0], sweep.shape[2]
+        pi, pjx, sib, rmask, prog = self._tree_buffers(dev)
+        jts = joints.detach().float().contiguous()
+        call("apn_skeleton_sweep", ptr(sweep), P, rot_dim, J, ptr(jts), ptr(pi), pi.shape[1], ptr(pjx), ptr(sib),
+             ptr(rmask), ptr(out["thetas"]), ptr(out["bone_Ts"]), ptr(out["T34"]), ptr(out["gt"]),
+             ptr(out["joints_rel"]), ptr(prog), stream_ptr(dev))
+
     def pose_torch(self, joints, t=None, rot_params=None, global_t=None):
         """The skeleton stage as device torch ops (restatement of pointwarper.py:216-239 used to
         cross-check apn_skeleton_pose in the tests)."""

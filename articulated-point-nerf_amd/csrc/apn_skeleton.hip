@@ -77,6 +77,17 @@ __global__ __launch_bounds__(SK_THREADS) void k_skeleton_pose(
   __shared__ float sStk[SK_MAX_J][SK_STACK][16];
   const int tid = threadIdx.x;
   const bool tpath = rot_params == nullptr;
+  // batch mode (rot path, no index, sweep_len > 0): block b computes pose b of the sweep into
+  // output slot b (apn_skeleton_sweep: every pose of a repose sweep in one launch)
+  if (!tpath && !sweep_idx && sweep_len > 0) {
+    const size_t b = blockIdx.x;
+    rot_params += b * J * rot_dim;
+    thetas_out += b * J;
+    bone_T16 += b * J * 16;
+    bone_T34 += b * J * 12;
+    global_t_out += b * 3;
+    joints_rel_out += b * J * 3;
+  }
   // sweep mode (rot path): rot_params holds sweep_len poses; this launch takes pose *sweep_idx and
   // advances the index (a captured repose step then needs no per-pose input copy)
   const int sweep_i = sweep_idx ? *sweep_idx : 0;
@@ -315,6 +326,24 @@ extern "C" int apn_skeleton_frame(const float* t, const float* time_poc, int32_t
                      sibling_mask, rot_mask, params_out, thetas_out, bone_T16, bone_T34, global_t_out,
                      joints_rel_out, chain_prog, time_poc, n_freq, c2w, K, n_views, joints2d_out, sweep_index,
                      sweep_len);
+  return launch_status();
+}
+
+// Every pose of a repose sweep [n_poses, J, rot_dim] in one launch (one workgroup per pose, the
+// rot-param path of k_skeleton_pose); outputs are per-pose slices.
+extern "C" int apn_skeleton_sweep(const float* rot_params, int32_t n_poses, int32_t rot_dim, int32_t n_joints,
+                                  const float* joints, const int32_t* parent_indices, int32_t depth,
+                                  const int32_t* parent_joint_ex, const int32_t* sibling_mask, const int32_t* rot_mask,
+                                  float* thetas_out, float* bone_T16, float* bone_T34, float* global_t_out,
+                                  float* joints_rel_out, const int32_t* chain_prog, void* stream) {
+  if (n_poses <= 0 || !rot_params || (rot_dim != 3 && rot_dim != 4) || n_joints <= 0 || n_joints > SK_MAX_J ||
+      depth <= 0 || depth > SK_MAX_DEPTH || !joints || !parent_indices || !parent_joint_ex || !thetas_out ||
+      !bone_T16 || !bone_T34 || !global_t_out || !joints_rel_out)
+    return APN_ERR_ARG;
+  hipLaunchKernelGGL(k_skeleton_pose, dim3(n_poses), dim3(SK_THREADS), 0, (hipStream_t)stream, nullptr, 0, rot_params,
+                     rot_dim, n_joints, nullptr, 0, 0, joints, parent_indices, depth, parent_joint_ex, sibling_mask,
+                     rot_mask, nullptr, thetas_out, bone_T16, bone_T34, global_t_out, joints_rel_out, chain_prog,
+                     nullptr, 0, nullptr, nullptr, 0, nullptr, nullptr, n_poses);
   return launch_status();
 }
 

@@ -342,11 +342,11 @@ def lbs_sweep(args, rank, world, dev):
         torch.cuda.synchronize(dev)
         lbs_ms = e0.elapsed_time(e1) / (3 * n_lbs)
         del g_lbs
-    # throughput: every pose of the sweep through the captured repose step, the sweep's poses in
-    # their order: the graph reads pose i from the sweep through a device index it advances itself
-    # (no per-pose input copy) and runs pose i's LBS beside pose i + 1's one-workgroup skeleton
-    # launch (TemporalPoints.capture_repose(pipelined=True))
-    step = model.capture_repose(sweep=poses)
+    # throughput: every pose of the sweep through the captured repose step, in the sweep's order:
+    # each pass over the sweep starts with one launch computing every pose's skeleton, then one
+    # LBS graph per pose (TemporalPoints.capture_repose(batched=True))
+    mode = getattr(args, "repose_mode", "batched")
+    step = model.capture_repose(sweep=poses, batched=mode == "batched", pipelined=mode == "pipelined")
     for i in range(args.warmup):
         step(poses[i % len(poses)])
     if world > 1:
@@ -397,10 +397,10 @@ def lbs_sweep(args, rank, world, dev):
         "vs_baseline": None, "dtype": "fp32", "data": "synthetic (procedural 48-joint capsule cloud, repose sweep)",
         "config": {"workload": S.CONFIGS[args.config].name + f" ({args.config})", "points": N_total, "bones": J,
                    "points_per_rank": N, "poses_per_s": args.steps / elapsed,
-                   "step": ("two poses in flight: each step's HIP graph runs pose i's LBS beside pose i + 1's "
-                            "skeleton (a fork on a side stream inside the graph; double-buffered skeleton outputs), "
-                            "reading the sweep's next pose through a device index "
-                            "(TemporalPoints.capture_repose(sweep=..., pipelined=True))"),
+                   "step": ("one captured graph per pose: the LBS launch reading its pose's bone transforms; the "
+                            "skeleton stage of every pose of the sweep runs as ONE launch (one workgroup per pose) "
+                            "at the start of every pass over the sweep -- inside the timed loop, 5 passes of 60 "
+                            "poses here (TemporalPoints.capture_repose(sweep=..., batched=True))"),
                    "lbs_kernel_ms": lbs_ms,
                    "parallelism": f"points x{world} (no collective)" if world > 1 else "single"},
         "roofline": {"bound": "hbm", "kernel": "k_lbs_skin_mfma",
@@ -730,6 +730,10 @@ def main():
     ap.add_argument("--no-viewpoints", action="store_true",
                     help="skip the harness.render_viewpoints leg (8 views, frames in flight, host readback)")
     ap.add_argument("-o", "--out", default=None, help="also write the JSON line to this file")
+    ap.add_argument("--repose-mode", choices=["batched", "per_pose", "pipelined"], default="batched",
+                    help="C5: the captured repose step (TemporalPoints.capture_repose): batched = one skeleton "
+                         "launch per pass over the sweep + one LBS graph per pose; per_pose = skeleton + LBS per "
+                         "pose; pipelined = pose i's LBS beside pose i + 1's skeleton")
     ap.add_argument("--shard", choices=["frames", "rays"], default="rays",
                     help="N>1: 'rays' (default) = the ranks split one frame's rays and all-gather the tiles "
                          "over RCCL (strong scaling, SURVEY.md 8(e)); 'frames' = every rank renders its own "

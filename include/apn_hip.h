@@ -211,6 +211,16 @@ int apn_skeleton_frame(const float* t, const float* time_poc, int32_t n_freq, co
                        const float* c2w, const float* K, int32_t n_views, float* joints2d_out,
                        int32_t* sweep_index, int32_t sweep_len, void* stream);
 
+/* Every pose of a repose sweep (run.py:1355-1396) in one launch: rot_params [n_poses, J, rot_dim]
+ * -> per-pose thetas [n_poses, J], bone_T16 [n_poses, J, 16], bone_T34 [n_poses, J, 12], global_t
+ * [n_poses, 3] (zeros: the rot path), joints_rel [n_poses, J, 3]; each pose exactly as
+ * apn_skeleton_pose computes it (pointwarper.py:213-239, one workgroup per pose). */
+int apn_skeleton_sweep(const float* rot_params, int32_t n_poses, int32_t rot_dim, int32_t n_joints,
+                       const float* joints, const int32_t* parent_indices, int32_t depth,
+                       const int32_t* parent_joint_ex, const int32_t* sibling_mask, const int32_t* rot_mask,
+                       float* thetas_out, float* bone_T16, float* bone_T34, float* global_t_out,
+                       float* joints_rel_out, const int32_t* chain_prog, void* stream);
+
 /* Padded sampling bbox = bbox_ord -/+ query_radius (temporalpoints.py:424) as 6 floats. */
 int apn_bbox_unpack(const int32_t* bbox_ord, float query_radius, float* out6, void* stream);
 

@@ -130,18 +130,19 @@ def test_captured_repose_graph_equals_eager(dev):
         assert torch.equal(xg, xe) and torch.equal(jg, je), k
 
 
-@pytest.mark.parametrize("pipelined", [True, False])
-def test_captured_repose_sweep_graph(dev, pipelined):
-    """capture_repose(sweep=poses): the graph reads its pose from the sweep through a device index
-    it advances itself -- in-order steps, a jump (index reset), a wrap-around and rot_params that
-    are not a row of the sweep (eager fallback) all equal the eager repose bit for bit. Pipelined:
-    each step's graph also runs the next pose's skeleton beside its LBS (two poses in flight)."""
+@pytest.mark.parametrize("mode", ["batched", "pipelined", "per_pose"])
+def test_captured_repose_sweep_graph(dev, mode):
+    """capture_repose(sweep=poses) -- in-order steps, a jump, a wrap-around and rot_params that are
+    not a row of the sweep (eager fallback) all equal the eager repose bit for bit. batched (the
+    default): every pose's skeleton in one launch per pass over the sweep, one LBS graph per pose;
+    pipelined: each step's graph runs the next pose's skeleton beside its LBS; per_pose: one graph
+    reading its pose through a device index it advances itself."""
     from apn_amd import harness, synthetic as S
     scene = S.make_scene(S.SceneConfig("graph repose sweep", 30_000, 48, 0, 0))
     model = harness.build_model(scene, dev)
     poses = S.repose_sweep(48).to(dev).contiguous()
     P = poses.shape[0]
-    step = model.capture_repose(sweep=poses, pipelined=pipelined)
+    step = model.capture_repose(sweep=poses, batched=mode == "batched", pipelined=mode == "pipelined")
     order = [0, 1, 2, 3, 17, 18, P - 1, 0, 1, 5]
     for k in order:
         with torch.no_grad():
@@ -161,14 +162,16 @@ def test_captured_repose_sweep_graph(dev, pipelined):
     assert torch.equal(xg, xe) and torch.equal(jg, je)
 
 
-def test_pipelined_repose_sweep_modified_in_place(dev):
-    """The pipelined sweep prefetches pose i + 1's skeleton during step i; a sweep row changed in
-    place in between must not be rendered from the stale prefetch (the step re-runs the skeleton)."""
+@pytest.mark.parametrize("mode", ["batched", "pipelined"])
+def test_repose_sweep_modified_in_place(dev, mode):
+    """The batched sweep computes every pose's skeleton at the start of a pass, the pipelined one
+    pose i + 1's during step i; a sweep row changed in place in between must not be skinned from
+    the stale skeleton (the step runs the skeleton again)."""
     from apn_amd import harness, synthetic as S
     scene = S.make_scene(S.SceneConfig("graph repose sweep inplace", 20_000, 24, 0, 0))
     model = harness.build_model(scene, dev)
     poses = S.repose_sweep(24).to(dev).contiguous()
-    step = model.capture_repose(sweep=poses)
+    step = model.capture_repose(sweep=poses, batched=mode == "batched", pipelined=mode == "pipelined")
     for k in range(4):
         step(poses[k])
     with torch.no_grad():
