@@ -436,7 +436,7 @@ class TiNeuVox(nn.Module):
             weights, alpha, ray_id, step_id, rgb = weights[mask], alpha[mask], ray_id[mask], step_id[mask], rgb[mask]
         rgb_marched = ops.segment_coo_sum(weights.unsqueeze(-1) * rgb, ray_id, N)
         rgb_marched = rgb_marched + alphainv_last.unsqueeze(-1) * render_kwargs['bg']
-        n_samples = int(np.linalg.norm(np.array(self.world_size.cpu()) + 1) / render_kwargs['stepsize']) + 1
+        n_samples = int(np.linalg.norm(self.world_size.cpu().numpy() + 1) / render_kwargs["stepsize"]) + 1
         s = (step_id + 0.5) / n_samples
         ret.update({'alphainv_last': alphainv_last, 'weights': weights, 'rgb_marched': rgb_marched,
                     'raw_alpha': alpha, 'raw_rgb': rgb, 'ray_id': ray_id, 's': s, 'n_max': n_samples,

@@ -30,6 +30,12 @@
 #ifndef APN_H4_PIN   // A/B builds: 0 leaves the activation / fragment reads to the scheduler
 #define APN_H4_PIN 1
 #endif
+// The next tile's neighbour records are requested in this tile's epilogue (after the head's weight
+// fragments, which the head waits for first: vmcnt is in order), so the gather at the top of the
+// next tile finds them in registers instead of waiting a memory latency. 0: loaded at the top.
+#ifndef APN_H4_RECPF
+#define APN_H4_RECPF 1
+#endif
 
 namespace apn {
 namespace t128 {
@@ -354,6 +360,9 @@ __device__ __forceinline__ void mlp_tiles(
   };
   int tile = t_beg + blockIdx.x / nx;
   if (tile < t_end) fetch(tile);
+  GatherRegs gn;   // the records of the tile about to be gathered (APN_H4_RECPF)
+  if (APN_H4_RECPF && tile < t_end)
+    gather_load<!LISTED>(gh, lane & 7, pf_ok ? pf_nb : -1, pf_ray, gn, recA, recB, viewdirs, vemb_const);
   h8 a[2][2];   // carried A-fragment prefetch (chunk 0 of the next weight matrix)
 #pragma unroll
   for (int j = 0; j < 2; ++j)
@@ -379,7 +388,10 @@ __device__ __forceinline__ void mlp_tiles(
     const int nb0 = pf_ok ? pf_nb : -1;
     const float4 q0 = pf_q;
     GatherRegs g0;
-    gather_load<!LISTED>(gh, lane & 7, nb0, pf_ray, g0, recA, recB, viewdirs, vemb_const);
+    if (APN_H4_RECPF)
+      g0 = gn;
+    else
+      gather_load<!LISTED>(gh, lane & 7, nb0, pf_ray, g0, recA, recB, viewdirs, vemb_const);
     int pn_tile[MT];
     bool pok_tile[MT];
 #pragma unroll
@@ -464,6 +476,9 @@ __device__ __forceinline__ void mlp_tiles(
     for (int q = 1; q < KV / 32; ++q)
 #pragma unroll
       for (int pt = 0; pt < 2; ++pt) hfr[q - 1][pt] = frag(rs, vb, FR_WH + q * 2 + pt);
+    // the next tile's records (its indices came with this tile's fetch)
+    if (APN_H4_RECPF && tile + per_xcd < t_end)
+      gather_load<!LISTED>(gh, lane & 7, pf_ok ? pf_nb : -1, pf_ray, gn, recA, recB, viewdirs, vemb_const);
     __syncthreads();
     APN_PHASE(2)
     // ------------------------------------------------ IDW sum (temporalpoints.py:493-494) into
