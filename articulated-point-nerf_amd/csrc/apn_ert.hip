@@ -8,7 +8,11 @@
 // arithmetic (pre-mask alpha > thr, T in double, the same break test) retires the rays that
 // terminated; the next pass lists only the live rays' next samples. Every sample the compositing
 // reads has exactly the values a full MLP launch would give it (a sample's MLP rows do not depend
-// on the other rows of its tile), so apn_composite's output is bit-identical (tests/test_ert.py).
+// on the other rows of its tile), so apn_composite's output is bit-identical (tests/test_ert.py) --
+// unless the split kernel's fp16 range guard fires. Here only the samples the passes run can set
+// it; the all-samples launch also checks the samples past each ray's break. When the only
+// out-of-range value lies past a break, the all-samples frame is recomputed on FP32 MFMA and this
+// one keeps its fp16-split values: the two then differ in bits (both within the precision bar).
 //
 // The direct path (alpha_d, rgb_d, temporalpoints.py:459-470) and the weight-visualisation colour
 // (517-519) are cheap record blends; k_direct_blend computes them for every kept sample (the direct

@@ -30,11 +30,12 @@
 #ifndef APN_H4_PIN   // A/B builds: 0 leaves the activation / fragment reads to the scheduler
 #define APN_H4_PIN 1
 #endif
-// The next tile's neighbour records are requested in this tile's epilogue (after the head's weight
-// fragments, which the head waits for first: vmcnt is in order), so the gather at the top of the
-// next tile finds them in registers instead of waiting a memory latency. 0: loaded at the top.
+// A/B builds: 1 requests the next tile's neighbour records in this tile's epilogue (after the
+// head's weight fragments, which the head waits for first: vmcnt is in order), so the gather at the
+// top of the next tile finds them in registers. Measured slower (round 6, same box, interleaved:
+// MLP kernel 3.156-3.169 vs 3.084-3.092 ms per C2 frame; 227 vs 221 VGPRs): off.
 #ifndef APN_H4_RECPF
-#define APN_H4_RECPF 1
+#define APN_H4_RECPF 0
 #endif
 
 namespace apn {

@@ -5,7 +5,8 @@ and its compositing then stops each ray at the sample whose update takes T below
 (render_utils_kernel.cu:445-451); the {rgb, alpha} of later samples are never read. The render
 path runs the MLP only on the samples the compositing reads (passes over the live rays' next
 samples) and the direct / weight-colour columns on every kept sample. The frame must be
-bit-identical to the one that runs the MLP on every kept sample -- on golden scenes, with and
+bit-identical to the one that runs the MLP on every kept sample (while the fp16 range guard does
+not fire: its FP32 re-run is decided per path, csrc/apn_ert.hip) -- on golden scenes, with and
 without the fast_color_thres masks, on a scene whose rays never terminate, and on the whole C2,
 C3 and C4 frames -- and the MLP must have skipped exactly the samples after each ray's break."""
 import numpy as np

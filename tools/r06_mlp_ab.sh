@@ -3,12 +3,12 @@
 # default bench line and the C5 line on the product library.
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT || exit 1
 O=gpurun_out/r06m; mkdir -p $O
-NEW=${NEW:-"pk pkb"}
+NEW=${NEW:-"pkr"}
 PT="python -u -m pytest -q --timeout 600 --timeout-method thread -p no:cacheprovider -m gpu"
 [ -n "$SKIP_PARITY" ] || timeout -k 10 500 $PT tests/test_mlp_precision.py tests/test_ert.py "tests/test_hip_parity.py::test_mlp_stage_vs_oracle" "tests/test_full_frame_parity.py::test_every_ray_vs_oracle[C2]" -k "not C3 and not C4" -s > $O/parity.log 2>&1
 rc=$?; [ -n "$SKIP_PARITY" ] || grep -E "passed|failed|every ray" $O/parity.log | tail -5
 case $rc in 0) ;; *) echo "stop rc $rc"; grep -E "Error|assert" $O/parity.log | head -20; exit $rc;; esac
-for r in 1 2; do for v in base $NEW; do
+for r in 1 2; do for v in ${BASE:-base} $NEW; do
   APN_HIP_LIB=$PWD/ab/$v/libapn_hip.so timeout -k 10 200 python bench.py --steps 32 --warmup 3 --no-cpu-baseline --no-other-configs --no-viewpoints --no-full-mlp-leg -o $O/ab_${v}_$r.json 2>$O/ab_${v}_$r.err >/dev/null || { tail -20 $O/ab_${v}_$r.err; exit 1; }
   python -c "import json; d=json.load(open('$O/ab_${v}_$r.json')); s=d['stage_ms']; print('$v', 'mlp %.3f kernel %.3f frac %.3f knn %.3f frame %.3f serial %.3f sameview %.3f' % (s['mlp'], d['roofline']['avg_launch_ms'], d['roofline']['frac'], s['knn'], d['ms_per_step'], d['config'].get('serial_ms_per_step') or 0, d['config'].get('same_view_ms_per_step') or 0))"
 done; done
