@@ -721,7 +721,7 @@ def main():
     ap.add_argument("--views", type=int, default=16,
                     help="distinct frames the timed loop cycles through, each a new time and camera pose as in "
                          "the reference's render loop (synthetic.view_sweep); 1 = replay the scene's own frame")
-    ap.add_argument("--cpu-rows", type=int, default=16, help="image rows in the CPU-baseline sample")
+    ap.add_argument("--cpu-rows", type=int, default=48, help="image rows in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-other-configs", action="store_true",
                     help="skip the compact C3 / C4 / C5 measurements the default one-GPU C2 line carries")
