@@ -37,6 +37,12 @@
 #ifndef APN_H4_RECPF
 #define APN_H4_RECPF 0
 #endif
+// A/B builds: workgroups of the second dispatch round (blockIdx 256..511: the second workgroup on
+// each CU) start APN_H4_STAGGER x 127 x 64 cycles late, so the two workgroups of a CU -- whose
+// waves share each SIMD -- do not run their gather / epilogue phases at the same time.
+#ifndef APN_H4_STAGGER
+#define APN_H4_STAGGER 0
+#endif
 
 namespace apn {
 namespace t128 {
@@ -360,6 +366,8 @@ __device__ __forceinline__ void mlp_tiles(
     }
   };
   int tile = t_beg + blockIdx.x / nx;
+  if (APN_H4_STAGGER > 0 && ((blockIdx.x >> 8) & 1))
+    for (int i = 0; i < APN_H4_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
   if (tile < t_end) fetch(tile);
   GatherRegs gn;   // the records of the tile about to be gathered (APN_H4_RECPF)
   if (APN_H4_RECPF && tile < t_end)

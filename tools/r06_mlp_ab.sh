@@ -12,6 +12,7 @@ for r in 1 2; do for v in ${BASE:-base} $NEW; do
   APN_HIP_LIB=$PWD/ab/$v/libapn_hip.so timeout -k 10 200 python bench.py --steps 32 --warmup 3 --no-cpu-baseline --no-other-configs --no-viewpoints --no-full-mlp-leg -o $O/ab_${v}_$r.json 2>$O/ab_${v}_$r.err >/dev/null || { tail -20 $O/ab_${v}_$r.err; exit 1; }
   python -c "import json; d=json.load(open('$O/ab_${v}_$r.json')); s=d['stage_ms']; print('$v', 'mlp %.3f kernel %.3f frac %.3f knn %.3f frame %.3f serial %.3f sameview %.3f' % (s['mlp'], d['roofline']['avg_launch_ms'], d['roofline']['frac'], s['knn'], d['ms_per_step'], d['config'].get('serial_ms_per_step') or 0, d['config'].get('same_view_ms_per_step') or 0))"
 done; done
+[ -n "$SKIP_TAIL" ] && exit 0
 timeout -k 10 120 python bench.py --config C5 --steps 300 > $O/c5.json 2> $O/c5.err || { tail -20 $O/c5.err; exit 1; }
 python -c "import json; d=json.load(open('$O/c5.json')); print('C5', d['value']/1e9, 'Gpts/s', d['ms_per_step'], 'ms/pose, lbs', d['config']['lbs_kernel_ms'], d['roofline']['frac'])"
 timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
