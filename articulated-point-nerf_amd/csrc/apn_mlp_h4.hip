@@ -39,9 +39,16 @@
 #endif
 // A/B builds: workgroups of the second dispatch round (blockIdx 256..511: the second workgroup on
 // each CU) start APN_H4_STAGGER x 127 x 64 cycles late, so the two workgroups of a CU -- whose
-// waves share each SIMD -- do not run their gather / epilogue phases at the same time.
+// waves share each SIMD -- do not run their gather / epilogue phases at the same time. Measured
+// slower (round 6, same box: MLP kernel 3.08-3.11 -> 3.23-3.27 ms at 3, 3.40 ms at 6): off.
 #ifndef APN_H4_STAGGER
 #define APN_H4_STAGGER 0
+#endif
+// 1: the layer-1 P-row indices of the next tile come from LDS -- its gather rows' neighbour
+// indices, which the gather threads fetch anyway (row m's P row is row m's neighbour) -- instead of
+// 16 global loads (list + s_nbr per M-tile) and their address arithmetic per lane and tile.
+#ifndef APN_H4_LDSPN
+#define APN_H4_LDSPN 1
 #endif
 
 namespace apn {
@@ -71,18 +78,15 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // and consecutive frequencies of one coordinate meet in one thread (pe_chunk's double-angle steps).
 struct GatherRegs {
   float4 a0, a1, a2, a3, b0, b1;
-  float v0, v1;   // viewdir components of the sample's view-embedding elements e, e + 1
+  float v0;   // the viewdir component of this thread's view-embedding job (vemb_job)
 };
 
-// view-embedding element e (< 27) of poc_fre(viewdirs, 2^0..3) (tineuvox.py:872-878): its viewdir
-// component and frequency
-__device__ __forceinline__ int vemb_comp(int e) { return e < 3 ? e : ((e < 15 ? e - 3 : e - 15) >> 2); }
-__device__ __forceinline__ float vemb_val(int e, float vv) {
-  float sn_, cs_;
-  const int ee = e < 3 ? 0 : (e < 15 ? e - 3 : e - 15);
-  sincos_pe(vv * (float)(1 << (ee & 3)), sn_, cs_);
-  return e < 3 ? vv : (e < 15 ? sn_ : cs_);
-}
+// The view embedding poc_fre(viewdirs, 2^0..3) of a sample (tineuvox.py:872-878: [v (3),
+// sin(v_c 2^f) at 3 + 4c + f (12), cos(v_c 2^f) at 15 + 4c + f (12)]) is made by the sample's 16
+// gather threads, thread ts = 2k + h: ts < 12 computes one sincos (c = ts / 4, f = ts % 4) and
+// writes both its sine and its cosine slot; ts 12-14 copy the raw component ts - 12 and clear slot
+// 15 + ts; ts 15 clears slots 30, 31 (the head's K padding).
+__device__ __forceinline__ int vemb_comp(int ts) { return ts < 12 ? ts >> 2 : (ts < 15 ? ts - 12 : 0); }
 
 // Loads are unconditional (clamped indices; invalid rows read row 0 and are discarded later): a
 // load under a divergent branch makes the compiler drain vmcnt(0) at the join. recB (direct-blend
@@ -100,9 +104,7 @@ __device__ __forceinline__ void gather_load(int h, int k, int nb, int ray, Gathe
     G.b0 = recB[2 * n];
     G.b1 = recB[2 * n + 1];
   }
-  const int e = 4 * k + 2 * h;
-  G.v0 = vemb_const ? 0.f : viewdirs[3 * (size_t)ray + vemb_comp(min(e, 26))];
-  G.v1 = vemb_const ? 0.f : viewdirs[3 * (size_t)ray + vemb_comp(min(e + 1, 26))];
+  G.v0 = vemb_const ? 0.f : viewdirs[3 * (size_t)ray + vemb_comp(2 * k + h)];
 }
 
 // One chunk pair (arguments 8p .. 8p + 7) of row r: sines and cosines split into hi / lo halves and
@@ -123,7 +125,7 @@ __device__ __forceinline__ void pe_store(char* __restrict__ xr, int r, const flo
 
 // Row r = t & 127 of the tile, argument half H (= wave >> 1, a compile-time constant): the posenc
 // chunk pairs 2H, 2H + 1, and -- half 0 -- the row's squared distance (sTo) or -- half 1 -- the
-// direct-blend terms (sRow); view-embedding elements 4k + 2H, 4k + 2H + 1 of the sample (sV).
+// direct-blend terms (sRow); the sample's view-embedding job ts = 2k + H (sV).
 template <int H, bool DIRECT>
 __device__ __forceinline__ void gather_q(int nb, float4 q, const GatherRegs& G, char* __restrict__ PE,
                                          float* __restrict__ sTo, float* __restrict__ sRow, float* __restrict__ sV,
@@ -132,7 +134,8 @@ __device__ __forceinline__ void gather_q(int nb, float4 q, const GatherRegs& G, 
   asm volatile("" : "+v"(r_));   // per-lane LDS addresses recomputed per tile, not hoisted and spilled
   const int r = r_, s = r >> 3, k = r & 7;
   char* xr = PE + r * XB;
-  const int e = 4 * k + 2 * H;
+  const int ts = 2 * k + H;
+  float* const sv = sV + s * 32;
   if (nb >= 0) {
     const float4 a0 = G.a0, a1 = G.a1, a2 = G.a2, a3 = G.a3;
     const float dx = q.x - a0.x, dy = q.y - a0.y, dz = q.z - a0.z;
@@ -151,16 +154,24 @@ __device__ __forceinline__ void gather_q(int nb, float4 q, const GatherRegs& G, 
     }
     pe_store<2 * H>(xr, r, rc);
     pe_store<2 * H + 1>(xr, r, rc);
-    float v0 = 0.f, v1 = 0.f;
-    if (vemb_const) {
-      v0 = e < 27 ? vemb_const[e] : 0.f;
-      v1 = e + 1 < 27 ? vemb_const[e + 1] : 0.f;
+    if (ts < 12) {
+      const int c = ts >> 2, f = ts & 3;
+      float sn_, cs_;
+      if (vemb_const) {
+        sn_ = vemb_const[3 + 4 * c + f];
+        cs_ = vemb_const[15 + 4 * c + f];
+      } else {
+        sincos_pe(G.v0 * (float)(1 << f), sn_, cs_);
+      }
+      sv[3 + 4 * c + f] = sn_;
+      sv[15 + 4 * c + f] = cs_;
+    } else if (ts < 15) {
+      sv[ts - 12] = vemb_const ? vemb_const[ts - 12] : G.v0;
+      sv[15 + ts] = 0.f;
     } else {
-      if (e < 27) v0 = vemb_val(e, G.v0);
-      if (e + 1 < 27) v1 = vemb_val(e + 1, G.v1);
+      sv[30] = 0.f;
+      sv[31] = 0.f;
     }
-    sV[s * 32 + e] = v0;
-    sV[s * 32 + e + 1] = v1;
   } else {
     const h8 z = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
@@ -168,8 +179,8 @@ __device__ __forceinline__ void gather_q(int nb, float4 q, const GatherRegs& G, 
       *(h8*)(xr + ((c ^ (r & 15)) << 4)) = z;
       *(h8*)(xr + ((c ^ (r & 15)) << 4) + 256) = z;
     }
-    sV[s * 32 + e] = 0.f;
-    sV[s * 32 + e + 1] = 0.f;
+    sv[ts] = 0.f;        // the sample is past the launch's end: its 32 slots, two per thread
+    sv[ts + 16] = 0.f;
     if constexpr (H == 0) {
       sTo[r] = 1.f;
     } else if constexpr (DIRECT) {
@@ -304,7 +315,7 @@ __device__ __forceinline__ void mlp_tiles(
     const float4* __restrict__ pproj, const float* __restrict__ viewdirs, const float* __restrict__ vemb_const,
     const float* __restrict__ wbuf, float eps, float shift, float interval, float4* __restrict__ out,
     char* const X, float* const sTo, float* const sIdw, float* const sRow, float* const sOut, float* const sV,
-    float* const sW, float* const sPart) {
+    float* const sW, float* const sPart, int* const sNb) {
   const int nS = *n_samples_dev;
   const int ntiles = (nS + TS4 - 1) / TS4;
   const int tid = threadIdx.x;
@@ -355,20 +366,26 @@ __device__ __forceinline__ void mlp_tiles(
       pf_q = s_pos[si];
       pf_ray = s_ray[si];
     }
+    if (!APN_H4_LDSPN) {
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      const int m = 16 * mt + li;
-      pf_pok[mt] = tl < t_end && tc * TS4 + (m >> 3) < nS;
-      if (LISTED)
-        pf_pn[mt] = s_nbr[(size_t)list[min(tc * TS4 + (m >> 3), nS - 1)] * 8 + (m & 7)];
-      else
-        pf_pn[mt] = s_nbr[min((size_t)tc * TR4 + m, (size_t)nS * 8 - 1)];
+      for (int mt = 0; mt < MT; ++mt) {
+        const int m = 16 * mt + li;
+        pf_pok[mt] = tl < t_end && tc * TS4 + (m >> 3) < nS;
+        if (LISTED)
+          pf_pn[mt] = s_nbr[(size_t)list[min(tc * TS4 + (m >> 3), nS - 1)] * 8 + (m & 7)];
+        else
+          pf_pn[mt] = s_nbr[min((size_t)tc * TR4 + m, (size_t)nS * 8 - 1)];
+      }
     }
   };
   int tile = t_beg + blockIdx.x / nx;
   if (APN_H4_STAGGER > 0 && ((blockIdx.x >> 8) & 1))
     for (int i = 0; i < APN_H4_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
   if (tile < t_end) fetch(tile);
+  if (APN_H4_LDSPN) {   // the first tile's rows' neighbours (invalid rows: -1)
+    if (tid < TR4) sNb[tid] = pf_ok ? pf_nb : -1;
+    __syncthreads();
+  }
   GatherRegs gn;   // the records of the tile about to be gathered (APN_H4_RECPF)
   if (APN_H4_RECPF && tile < t_end)
     gather_load<!LISTED>(gh, lane & 7, pf_ok ? pf_nb : -1, pf_ray, gn, recA, recB, viewdirs, vemb_const);
@@ -404,7 +421,15 @@ __device__ __forceinline__ void mlp_tiles(
     int pn_tile[MT];
     bool pok_tile[MT];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) { pn_tile[mt] = pf_pn[mt]; pok_tile[mt] = pf_pok[mt]; }
+    for (int mt = 0; mt < MT; ++mt) {
+      if (APN_H4_LDSPN) {   // row 16 mt + li's neighbour = its P row (written last tile, barriers since)
+        pn_tile[mt] = sNb[16 * mt + li];
+        pok_tile[mt] = pn_tile[mt] >= 0;
+      } else {
+        pn_tile[mt] = pf_pn[mt];
+        pok_tile[mt] = pf_pok[mt];
+      }
+    }
     fetch(tile + per_xcd);
     // ------------------------------------------------ gather + posenc + direct-blend terms
     gather<!LISTED>(gh, nb0, q0, g0, X, sTo, sRow, sV, vemb_const);
@@ -470,6 +495,8 @@ __device__ __forceinline__ void mlp_tiles(
     __syncthreads();
     init_bias(acc, ot0, sW + SW_B4);
     layer_mfma<4, 5, 1, FR_W4, FR_WH>(X, rs, vb, acc, a);
+    // the next tile's gather rows' neighbours (fetched at this tile's top) for its P rows
+    if (APN_H4_LDSPN && tid < TR4) sNb[tid] = pf_ok ? pf_nb : -1;
     __syncthreads();
     // layer-4 output lrelu(acc) as fp32 rows (the IDW sum reads them)
 #pragma unroll
@@ -648,13 +675,14 @@ __global__ __launch_bounds__(MLP_THREADS, 2) void k_point_mlp_h4(
   __shared__ float sV[TS4 * 32];
   __shared__ __attribute__((aligned(16))) float sW[SW_TOTAL];
   __shared__ float sPart[4 * TS4 * 4];
+  __shared__ int sNb[TR4];
   __shared__ int s_skip;
   if (threadIdx.x == 0)
     s_skip = __builtin_nontemporal_load((const int*)(wbuf + OFF_FLAG)) != 0 || (wbuf[OFF_SCALE + 6] != 0.f) != SCALED;
   __syncthreads();
   if (s_skip) return;
   mlp_tiles<SCALED, TIMED, LISTED>(s_pos, s_ray, s_nbr, list, n_samples_dev, recA, recB, pproj, viewdirs, vemb_const, wbuf, eps, shift,
-                    interval, out, X, sTo, sIdw, sRow, sOut, sV, sW, sPart);
+                    interval, out, X, sTo, sIdw, sRow, sOut, sV, sW, sPart, sNb);
 }
 
 // The early-ray-termination passes' kernel: both weight-scale modes in one launch, the mode read
@@ -673,6 +701,7 @@ __global__ __launch_bounds__(MLP_THREADS, 2) void k_point_mlp_h4_listed(
   __shared__ float sV[TS4 * 32];
   __shared__ __attribute__((aligned(16))) float sW[SW_TOTAL];
   __shared__ float sPart[4 * TS4 * 4];
+  __shared__ int sNb[TR4];
   __shared__ int s_mode;   // 0: unscaled weights, 1: scaled, 2: the range flag is set (skip)
   if (threadIdx.x == 0)
     s_mode = __builtin_nontemporal_load((const int*)(wbuf + OFF_FLAG)) != 0 ? 2 : (wbuf[OFF_SCALE + 6] != 0.f ? 1 : 0);
@@ -681,10 +710,10 @@ __global__ __launch_bounds__(MLP_THREADS, 2) void k_point_mlp_h4_listed(
   if (mode == 2) return;
   if (mode == 1)
     mlp_tiles<true, false, true>(s_pos, s_ray, s_nbr, list, n_samples_dev, recA, recB, pproj, viewdirs, vemb_const, wbuf, eps,
-                                 shift, interval, out, X, sTo, sIdw, sRow, sOut, sV, sW, sPart);
+                                 shift, interval, out, X, sTo, sIdw, sRow, sOut, sV, sW, sPart, sNb);
   else
     mlp_tiles<false, false, true>(s_pos, s_ray, s_nbr, list, n_samples_dev, recA, recB, pproj, viewdirs, vemb_const, wbuf, eps,
-                                  shift, interval, out, X, sTo, sIdw, sRow, sOut, sV, sW, sPart);
+                                  shift, interval, out, X, sTo, sIdw, sRow, sOut, sV, sW, sPart, sNb);
 }
 
 }  // namespace t128
