@@ -973,7 +973,7 @@ def test_training_losses_vs_cpu(golden_model, dev):
     ch_ref = m._rho(c1, 0.03).mean() + m._rho(c2, 0.03).mean()
     assert abs(float(ch.detach()) - float(ch_ref)) < 1e-6
     assert abs(float(m.get_joint_chamfer_loss().detach()) - float(c2.sum())) < 1e-6
-    assert float(m.get_joint_arap_loss()) >= 0 and torch.isfinite(m.get_weight_sparsity_loss())
+    assert float(m.get_joint_arap_loss().detach()) >= 0 and torch.isfinite(m.get_weight_sparsity_loss())
 
 
 def test_batch_chamfer_loss_2d(golden_model, dev):
