@@ -50,6 +50,19 @@
 #ifndef APN_H4_LDSPN
 #define APN_H4_LDSPN 1
 #endif
+// 1: weight fragments two K-chunks ahead of their MFMAs (a second carried register set, across the
+// layer boundaries and the head) instead of one: 194 -> 210 VGPRs (still 2 waves per SIMD). Same box,
+// interleaved (round 6): MLP kernel 3.048 / 3.009 -> 3.003 / 2.984 ms per C2 frame, parity green.
+#ifndef APN_H4_PF2
+#define APN_H4_PF2 1
+#endif
+// 1: wave priority 1 while a wave runs a layer's MFMAs, 0 elsewhere (s_setprio): of the two waves of
+// a SIMD (one per workgroup), the one in its MFMA phase issues first and the other's gather /
+// epilogue VALU fills the cycles an MFMA leaves free. Same box, against two-deep fragments alone:
+// 2.946 / 2.931 -> 2.902 / 2.928 ms (frame in flight equal, one at a time 5.85 -> 5.81 ms).
+#ifndef APN_H4_PRIO
+#define APN_H4_PRIO 1
+#endif
 
 namespace apn {
 namespace t128 {
@@ -205,29 +218,32 @@ __device__ __forceinline__ void gather(int h, int nb, float4 q, const GatherRegs
 // activation (B) fragments roll one M-tile ahead of their 6 MFMAs.
 template <int NQ, int NQN, int NTN, int FB, int FBN>
 __device__ __forceinline__ void layer_mfma(const char* __restrict__ X, rsrc_t rs, int vb, f32x4 (&acc)[MT][2],
-                                           h8 (&a)[2][2]) {
+                                           h8 (&a)[2][2], h8 (&a1)[2][2]) {
   const int lane = threadIdx.x & 63;
   const int li = lane & 15, g = lane >> 4;
   constexpr int NS = NQ * MT;   // (chunk, M-tile) steps
+  constexpr int AHEAD = APN_H4_PF2 ? 2 : 1;   // K-chunks between a fragment load and its MFMAs
   // activation fragments of step t: (chunk t / MT, M-tile t % MT)
   auto act = [&](int t) { return X + act_off(16 * (t % MT) + li, 4 * (t / MT) + g); };
   h8 bh = *(const h8*)act(0), bl = *(const h8*)(act(0) + 256);
+  if (APN_H4_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     h8 an[2][2];
-    if (q + 1 < NQ) {
+    const int qn = q + AHEAD;   // the chunk whose fragments are requested now
+    if (qn < NQ) {
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, vb, FB + (j * NQ + q + 1) * 2 + pt);
-    } else {
+        for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, vb, FB + (j * NQ + qn) * 2 + pt);
+    } else {   // the next matrix's chunk qn - NQ
 #pragma unroll
       for (int j = 0; j < NTN; ++j)
 #pragma unroll
-        for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, vb, FBN + j * NQN * 2 + pt);
+        for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, vb, FBN + (j * NQN + qn - NQ) * 2 + pt);
     }
 #if APN_H4_PIN
-    __builtin_amdgcn_sched_barrier(0);   // the next chunk's fragment loads issue here, before the MFMAs
+    __builtin_amdgcn_sched_barrier(0);   // the fragment loads issue here, before the MFMAs
 #endif
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -250,14 +266,18 @@ __device__ __forceinline__ void layer_mfma(const char* __restrict__ X, rsrc_t rs
       bh = nbh;
       bl = nbl;
     }
-    if (q + 1 < NQ) {
+    // rotate the carried sets: a <- a1 <- an (AHEAD 1: a <- an)
+    const int nt_next = (q + 1 < NQ) ? 2 : NTN;   // o-tiles of the chunk a now receives
 #pragma unroll
-      for (int j = 0; j < 2; ++j) { a[j][0] = an[j][0]; a[j][1] = an[j][1]; }
-    } else {
-#pragma unroll
-      for (int j = 0; j < NTN; ++j) { a[j][0] = an[j][0]; a[j][1] = an[j][1]; }
+    for (int j = 0; j < 2; ++j) {
+      if (j < nt_next) {
+        if (APN_H4_PF2) { a[j][0] = a1[j][0]; a[j][1] = a1[j][1]; }
+        else { a[j][0] = an[j][0]; a[j][1] = an[j][1]; }
+      }
+      if (APN_H4_PF2 && j < (qn < NQ ? 2 : NTN)) { a1[j][0] = an[j][0]; a1[j][1] = an[j][1]; }
     }
   }
+  if (APN_H4_PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
 // lrelu(acc [+ bias]) -> the next layer's input rows. Lane (li, g) of M-tile mt holds features
@@ -389,11 +409,14 @@ __device__ __forceinline__ void mlp_tiles(
   GatherRegs gn;   // the records of the tile about to be gathered (APN_H4_RECPF)
   if (APN_H4_RECPF && tile < t_end)
     gather_load<!LISTED>(gh, lane & 7, pf_ok ? pf_nb : -1, pf_ray, gn, recA, recB, viewdirs, vemb_const);
-  h8 a[2][2];   // carried A-fragment prefetch (chunk 0 of the next weight matrix)
+  h8 a[2][2], a1[2][2];   // carried A-fragment prefetch (chunks 0 [, 1] of the next weight matrix)
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int pt = 0; pt < 2; ++pt) a[j][pt] = frag(rs, vb, FR_W1E + j * 4 + pt);
+    for (int pt = 0; pt < 2; ++pt) {
+      a[j][pt] = frag(rs, vb, FR_W1E + j * 4 + pt);
+      a1[j][pt] = APN_H4_PF2 ? frag(rs, vb, FR_W1E + j * 4 + 2 + pt) : a[j][pt];
+    }
   f32x4 acc[MT][2];
   bool pok[MT];
   int prev_s0 = -1;
@@ -478,23 +501,23 @@ __device__ __forceinline__ void mlp_tiles(
           if (!pok[mt]) acc[mt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
     // ------------------------------------------------ feat_net: 4 x (Linear + LeakyReLU)
-    layer_mfma<2, 4, 2, FR_W1E, FR_W2>(X, rs, vb, acc, a);
+    layer_mfma<2, 4, 2, FR_W1E, FR_W2>(X, rs, vb, acc, a, a1);
     __syncthreads();
     store_act(X, ot0, nullptr, acc, SCALED, SCALED ? sW[SW_DS + 0] : 1.f);   // b1: the bias column
     __syncthreads();
     APN_PHASE(1)
     init_bias(acc, ot0, sW + SW_B2);
-    layer_mfma<4, 4, 2, FR_W2, FR_W3>(X, rs, vb, acc, a);
+    layer_mfma<4, 4, 2, FR_W2, FR_W3>(X, rs, vb, acc, a, a1);
     __syncthreads();
     store_act(X, ot0, nullptr, acc, SCALED, SCALED ? sW[SW_DS + 1] : 1.f);
     __syncthreads();
     init_bias(acc, ot0, sW + SW_B3);
-    layer_mfma<4, 4, 2, FR_W3, FR_W4>(X, rs, vb, acc, a);
+    layer_mfma<4, 4, 2, FR_W3, FR_W4>(X, rs, vb, acc, a, a1);
     __syncthreads();
     store_act(X, ot0, nullptr, acc, SCALED, SCALED ? sW[SW_DS + 2] : 1.f);
     __syncthreads();
     init_bias(acc, ot0, sW + SW_B4);
-    layer_mfma<4, 5, 1, FR_W4, FR_WH>(X, rs, vb, acc, a);
+    layer_mfma<4, 5, 1, FR_W4, FR_WH>(X, rs, vb, acc, a, a1);
     // the next tile's gather rows' neighbours (fetched at this tile's top) for its P rows
     if (APN_H4_LDSPN && tid < TR4) sNb[tid] = pf_ok ? pf_nb : -1;
     __syncthreads();
@@ -511,7 +534,8 @@ __device__ __forceinline__ void mlp_tiles(
 #pragma unroll
     for (int q = 1; q < KV / 32; ++q)
 #pragma unroll
-      for (int pt = 0; pt < 2; ++pt) hfr[q - 1][pt] = frag(rs, vb, FR_WH + q * 2 + pt);
+      for (int pt = 0; pt < 2; ++pt)   // (chunk 1 came with layer 4 too when two-deep: not reloaded)
+        hfr[q - 1][pt] = (APN_H4_PF2 && q == 1) ? a1[0][pt] : frag(rs, vb, FR_WH + q * 2 + pt);
     // the next tile's records (its indices came with this tile's fetch)
     if (APN_H4_RECPF && tile + per_xcd < t_end)
       gather_load<!LISTED>(gh, lane & 7, pf_ok ? pf_nb : -1, pf_ray, gn, recA, recB, viewdirs, vemb_const);
@@ -604,10 +628,14 @@ __device__ __forceinline__ void mlp_tiles(
       f32x4 ah = *(const f32x4*)(sW + SW_BH + o0);   // views_linears.0 (folded) bias
       const char* hr = X + li * HB;                   // B column li = sample li (16 real columns)
       h8 an[2][2];   // the next tile's W1E chunk 0 (carried across the gather)
+      h8 an1[2][2];   // and chunk 1 (two-deep)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, vb, FR_W1E + j * 4 + pt);
+        for (int pt = 0; pt < 2; ++pt) {
+          an[j][pt] = frag(rs, vb, FR_W1E + j * 4 + pt);
+          an1[j][pt] = APN_H4_PF2 ? frag(rs, vb, FR_W1E + j * 4 + 2 + pt) : an[j][pt];
+        }
 #pragma unroll
       for (int q = 0; q < KV / 32; ++q) {
         const h8 bh = *(const h8*)(hr + 16 * (4 * q + g));
@@ -615,7 +643,10 @@ __device__ __forceinline__ void mlp_tiles(
         ah = q == 0 ? mfma3(a[0][0], a[0][1], bh, bl, ah) : mfma3(hfr[q - 1][0], hfr[q - 1][1], bh, bl, ah);
       }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) { a[j][0] = an[j][0]; a[j][1] = an[j][1]; }
+      for (int j = 0; j < 2; ++j) {
+        a[j][0] = an[j][0]; a[j][1] = an[j][1];
+        a1[j][0] = an1[j][0]; a1[j][1] = an1[j][1];
+      }
       // lane (li = sample, g): head features o = 16 wid + 4 g + r
       float pc[3] = {0.f, 0.f, 0.f};
 #pragma unroll
