@@ -63,6 +63,13 @@
 #ifndef APN_H4_PRIO
 #define APN_H4_PRIO 1
 #endif
+// 1: layer 1's P rows requested before the gather instead of after it (their latency under the
+// gather's VALU, the accumulators live through it; 210 -> 215 VGPRs, no spill). Same box, against
+// PF2 + PRIO: MLP kernel 2.907 / 2.877 -> 2.859 / 2.856 ms per C2 frame (frac 0.57); phase split
+// (debug build, full MLP) layer 1 14.9 -> 13.7 %, gather 17.6 -> 18.5 %, tile 41.8k -> 41.5k cycles.
+#ifndef APN_H4_PEARLY
+#define APN_H4_PEARLY 1
+#endif
 
 namespace apn {
 namespace t128 {
@@ -454,18 +461,26 @@ __device__ __forceinline__ void mlp_tiles(
       }
     }
     fetch(tile + per_xcd);
+    // layer-1 accumulators = P[nbr] (global -> VGPR): before the gather (PEARLY), or after the
+    // gather's register peak
+    auto load_p = [&]() {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        pok[mt] = pok_tile[mt];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const float4 v = pproj[(size_t)max(pn_tile[mt], 0) * (FEAT / 4) + 4 * (ot0 + j) + g];
+          acc[mt][j] = f32x4{v.x, v.y, v.z, v.w};
+        }
+      }
+    };
+    if (APN_H4_PEARLY) {
+      load_p();
+      __builtin_amdgcn_sched_barrier(0);   // issued here, not sunk into the gather
+    }
     // ------------------------------------------------ gather + posenc + direct-blend terms
     gather<!LISTED>(gh, nb0, q0, g0, X, sTo, sRow, sV, vemb_const);
-    // layer-1 accumulators = P[nbr] (global -> VGPR), loaded after the gather's register peak
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      pok[mt] = pok_tile[mt];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const float4 v = pproj[(size_t)max(pn_tile[mt], 0) * (FEAT / 4) + 4 * (ot0 + j) + g];
-        acc[mt][j] = f32x4{v.x, v.y, v.z, v.w};
-      }
-    }
+    if (!APN_H4_PEARLY) load_p();
     if (SCALED) {
       const float sc1 = sW[SW_SC];
 #pragma unroll
