@@ -62,6 +62,8 @@ __global__ __launch_bounds__(256) void k_direct_blend(const float4* __restrict__
       w[k] = __builtin_amdgcn_rcpf(to[k] + eps);   // v_rcp_f32, as the MLP kernel's IDW weights
       sum += w[k];
     }
+    if (APN_H4_IDWG)   // the MLP kernel's shuffle-tree order (apn_mlp_layout.h)
+      sum = ((w[0] + w[1]) + (w[2] + w[3])) + ((w[4] + w[5]) + (w[6] + w[7]));
     const float inv = __builtin_amdgcn_rcpf(sum);
 #pragma unroll
     for (int k = 0; k < 8; ++k) sumd += dw[k];

@@ -70,6 +70,26 @@
 #ifndef APN_H4_PEARLY
 #define APN_H4_PEARLY 1
 #endif
+// APN_H4_IDWG (apn_mlp_layout.h): the IDW weights made in the gather.
+// 1: head-input row s written inside the X rows that its own wave's IDW sum read (wave w sums
+// samples 4w .. 4w + 3 over rows 32w .. 32w + 31, 16 KB), so no barrier between the IDW reads and
+// the head-row writes (a wave's LDS accesses stay in program order); rows 832 B apart and shifted
+// 16 B per wave so the head's 16 B-column reads (one row per lane) hit 16 distinct bank groups.
+// Measured equal to slightly slower (round 6, same box, parity green: 2.981 / 2.948 -> 2.985 /
+// 3.003 ms per C2 frame): the barrier's cost is the waves' skew there, which is small. Off.
+#ifndef APN_H4_HEADW
+#define APN_H4_HEADW 0
+#endif
+// 1 (early-termination passes' kernel): the next tile's posenc -- rel_c, the 16 sin / cos
+// arguments, their hi / lo split -- computed inside this tile's layer-4 MFMA stream (its VALU
+// scheduled into the MFMAs' issue gaps by sched_group_barrier instead of the phase-pinning fences)
+// and held in 33 VGPRs until the next tile's gather stores them; the next tile's records are
+// requested at the start of layer 3. Needs two-deep fragments off (255 VGPRs). Measured slower
+// (round 6, same box, parity green: MLP kernel 2.883 / 2.888 -> 2.967 / 2.979 ms per C2 frame; the
+// interleave itself compiled as asked, one VALU per MFMA gap): off.
+#ifndef APN_H4_PEFILL
+#define APN_H4_PEFILL 0
+#endif
 
 namespace apn {
 namespace t128 {
@@ -81,8 +101,13 @@ constexpr int TR4 = TS4 * 8;       // MLP rows per tile
 constexpr int MT = TR4 / 16;       // 16-row M-tiles
 constexpr int HB = 800;            // bytes per head-input row: hi 160 | lo 160 | pad (800/4 = 8 mod 64)
 constexpr int HLO = 320;           // lo offset inside a head-input row
+// byte offset of head-input row s (APN_H4_HEADW: inside wave s / 4's IDW rows)
+__device__ __forceinline__ int head_row(int s) {
+  return APN_H4_HEADW ? (s >> 2) * (32 * XB) + (s & 3) * 832 + (s >> 2) * 16 : s * HB;
+}
 constexpr int RS = 9;              // floats per row of sRow (8 used; odd stride: conflict-free columns)
 static_assert(TS4 * HB <= TR4 * XB, "head rows alias the activation buffer");
+static_assert(3 * 832 + 3 * 16 + HB <= 32 * XB, "a wave's head rows stay inside its IDW rows");
 
 constexpr int SW_B1 = 0, SW_B2 = 128, SW_B3 = 256, SW_B4 = 384, SW_WD = 512, SW_BD = 640, SW_BH = 644,
               SW_WV2 = 708, SW_BV2 = 900, SW_SC = 904, SW_DS = 912, SW_HSC = 921, SW_TOTAL = 924;
@@ -127,6 +152,44 @@ __device__ __forceinline__ void gather_load(int h, int k, int nb, int ray, Gathe
   G.v0 = vemb_const ? 0.f : viewdirs[3 * (size_t)ray + vemb_comp(2 * k + h)];
 }
 
+// A row's posenc chunks 4H .. 4H + 3 (chunk pairs 2H, 2H + 1: sin, cos) as hi / lo halves, and its
+// squared distance, made ahead of the gather that stores them (APN_H4_PEFILL).
+struct PeRegs {
+  h8 hi[4], lo[4];
+  float tn;
+};
+
+__device__ __forceinline__ void rel_c_of(float4 q, const GatherRegs& G, float (&rc)[3], float& tn) {
+  const float4 a0 = G.a0, a1 = G.a1, a2 = G.a2, a3 = G.a3;
+  const float dx = q.x - a0.x, dy = q.y - a0.y, dz = q.z - a0.z;
+  // rel_c = Rinv (x - p) (temporalpoints.py:454-458)
+  rc[0] = (a1.x * dx + a1.y * dy) + a1.z * dz;
+  rc[1] = (a1.w * dx + a2.x * dy) + a2.y * dz;
+  rc[2] = (a2.z * dx + a2.w * dy) + a3.x * dz;
+  tn = (dx * dx + dy * dy) + dz * dz;
+}
+
+template <int H>
+__device__ __forceinline__ void pe_compute(float4 q, const GatherRegs& G, PeRegs& P) {
+  float rc[3];
+  rel_c_of(q, G, rc, P.tn);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    f32x4 sv0, sv1, cv0, cv1;
+    if (u == 0)
+      pe_chunk<16 * H>(rc, sv0, sv1, cv0, cv1);
+    else
+      pe_chunk<16 * H + 8>(rc, sv0, sv1, cv0, cv1);
+    h4 hs0, ls0, hs1, ls1, hc0, lc0, hc1, lc1;
+    split4(sv0, hs0, ls0); split4(sv1, hs1, ls1);
+    split4(cv0, hc0, lc0); split4(cv1, hc1, lc1);
+    P.hi[2 * u] = __builtin_shufflevector(hs0, hs1, 0, 1, 2, 3, 4, 5, 6, 7);
+    P.lo[2 * u] = __builtin_shufflevector(ls0, ls1, 0, 1, 2, 3, 4, 5, 6, 7);
+    P.hi[2 * u + 1] = __builtin_shufflevector(hc0, hc1, 0, 1, 2, 3, 4, 5, 6, 7);
+    P.lo[2 * u + 1] = __builtin_shufflevector(lc0, lc1, 0, 1, 2, 3, 4, 5, 6, 7);
+  }
+}
+
 // One chunk pair (arguments 8p .. 8p + 7) of row r: sines and cosines split into hi / lo halves and
 // stored as whole 16-B chunks at their swizzled positions.
 template <int PAIR>
@@ -146,34 +209,47 @@ __device__ __forceinline__ void pe_store(char* __restrict__ xr, int r, const flo
 // Row r = t & 127 of the tile, argument half H (= wave >> 1, a compile-time constant): the posenc
 // chunk pairs 2H, 2H + 1, and -- half 0 -- the row's squared distance (sTo) or -- half 1 -- the
 // direct-blend terms (sRow); the sample's view-embedding job ts = 2k + H (sV).
-template <int H, bool DIRECT>
+template <int H, bool DIRECT, bool FILL>
 __device__ __forceinline__ void gather_q(int nb, float4 q, const GatherRegs& G, char* __restrict__ PE,
                                          float* __restrict__ sTo, float* __restrict__ sRow, float* __restrict__ sV,
-                                         const float* __restrict__ vemb_const) {
+                                         const float* __restrict__ vemb_const, float* __restrict__ sIdw, float eps,
+                                         const PeRegs& P) {
   int r_ = threadIdx.x & 127;
   asm volatile("" : "+v"(r_));   // per-lane LDS addresses recomputed per tile, not hoisted and spilled
   const int r = r_, s = r >> 3, k = r & 7;
   char* xr = PE + r * XB;
   const int ts = 2 * k + H;
   float* const sv = sV + s * 32;
+  float tn0 = 1.f;   // the row's squared distance (rows past the launch's end: 1)
   if (nb >= 0) {
-    const float4 a0 = G.a0, a1 = G.a1, a2 = G.a2, a3 = G.a3;
-    const float dx = q.x - a0.x, dy = q.y - a0.y, dz = q.z - a0.z;
-    // rel_c = Rinv (x - p) (temporalpoints.py:454-458)
-    const float rc[3] = {(a1.x * dx + a1.y * dy) + a1.z * dz, (a1.w * dx + a2.x * dy) + a2.y * dz,
-                         (a2.z * dx + a2.w * dy) + a3.x * dz};
-    if constexpr (H == 0) {
-      sTo[r] = (dx * dx + dy * dy) + dz * dz;
-    } else if constexpr (DIRECT) {
-      const float tn = (dx * dx + dy * dy) + dz * dz;
-      float* rw = sRow + RS * r;
-      rw[0] = expf(-(tn * tn) / a0.w);   // temporalpoints.py:461 (to_nn is already squared)
-      rw[1] = a3.y;
-      rw[2] = G.b0.x; rw[3] = G.b0.y; rw[4] = G.b0.z;
-      rw[5] = G.b1.x; rw[6] = G.b1.y; rw[7] = G.b1.z;
+    if constexpr (FILL) {   // the posenc made during the previous tile's layer 4
+      static_assert(!DIRECT, "the fill path serves the early-termination passes");
+      if constexpr (H == 0) {
+        tn0 = P.tn;
+        if (!APN_H4_IDWG) sTo[r] = tn0;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int c = (4 * H + u) ^ (r & 15);
+        *(h8*)(xr + (c << 4)) = P.hi[u];
+        *(h8*)(xr + (c << 4) + 256) = P.lo[u];
+      }
+    } else {
+      float rc[3], tn;
+      rel_c_of(q, G, rc, tn);
+      if constexpr (H == 0) {
+        tn0 = tn;
+        if (!APN_H4_IDWG) sTo[r] = tn0;
+      } else if constexpr (DIRECT) {
+        float* rw = sRow + RS * r;
+        rw[0] = expf(-(tn * tn) / G.a0.w);   // temporalpoints.py:461 (to_nn is already squared)
+        rw[1] = G.a3.y;
+        rw[2] = G.b0.x; rw[3] = G.b0.y; rw[4] = G.b0.z;
+        rw[5] = G.b1.x; rw[6] = G.b1.y; rw[7] = G.b1.z;
+      }
+      pe_store<2 * H>(xr, r, rc);
+      pe_store<2 * H + 1>(xr, r, rc);
     }
-    pe_store<2 * H>(xr, r, rc);
-    pe_store<2 * H + 1>(xr, r, rc);
     if (ts < 12) {
       const int c = ts >> 2, f = ts & 3;
       float sn_, cs_;
@@ -202,30 +278,44 @@ __device__ __forceinline__ void gather_q(int nb, float4 q, const GatherRegs& G, 
     sv[ts] = 0.f;        // the sample is past the launch's end: its 32 slots, two per thread
     sv[ts + 16] = 0.f;
     if constexpr (H == 0) {
-      sTo[r] = 1.f;
+      if (!APN_H4_IDWG) sTo[r] = 1.f;
     } else if constexpr (DIRECT) {
       for (int c = 0; c < 8; ++c) sRow[RS * r + c] = 0.f;
     }
   }
+  if constexpr (H == 0 && APN_H4_IDWG) {   // outside the branch: every lane takes part in the shuffles
+    const float w = __builtin_amdgcn_rcpf(tn0 + eps);   // v_rcp_f32 (1 ulp)
+    float sum = w + __shfl_xor(w, 1, 64);
+    sum += __shfl_xor(sum, 2, 64);
+    sum += __shfl_xor(sum, 4, 64);
+    sIdw[r] = w * __builtin_amdgcn_rcpf(sum);
+  }
 }
 
-template <bool DIRECT>
+template <bool DIRECT, bool FILL>
 __device__ __forceinline__ void gather(int h, int nb, float4 q, const GatherRegs& G, char* __restrict__ PE,
                                        float* __restrict__ sTo, float* __restrict__ sRow, float* __restrict__ sV,
-                                       const float* __restrict__ vemb_const) {
+                                       const float* __restrict__ vemb_const, float* __restrict__ sIdw, float eps,
+                                       const PeRegs& P) {
   if (h == 0)
-    gather_q<0, DIRECT>(nb, q, G, PE, sTo, sRow, sV, vemb_const);
+    gather_q<0, DIRECT, FILL>(nb, q, G, PE, sTo, sRow, sV, vemb_const, sIdw, eps, P);
   else
-    gather_q<1, DIRECT>(nb, q, G, PE, sTo, sRow, sV, vemb_const);
+    gather_q<1, DIRECT, FILL>(nb, q, G, PE, sTo, sRow, sV, vemb_const, sIdw, eps, P);
 }
 
 // acc[mt][j] += W[o-tile 2w+j] X^T over NQ chunks of 32 and the tile's 8 M-tiles. `a` carries chunk
 // 0 of this matrix's fragments (block FB) in and chunk 0 of the next matrix (block FBN, NQN chunks,
 // NTN o-tiles) out: each chunk's fragments are requested a whole chunk (48 MFMAs) before use. The
 // activation (B) fragments roll one M-tile ahead of their 6 MFMAs.
-template <int NQ, int NQN, int NTN, int FB, int FBN>
+struct NoFill {
+  __device__ void operator()() const {}
+};
+
+// FILL: `fill` (VALU work of its own) runs inside the layer's scheduling region and is spread over
+// the MFMA issue gaps (sched_group_barrier) in place of the phase-pinning fences.
+template <int NQ, int NQN, int NTN, int FB, int FBN, bool FILL = false, class F = NoFill>
 __device__ __forceinline__ void layer_mfma(const char* __restrict__ X, rsrc_t rs, int vb, f32x4 (&acc)[MT][2],
-                                           h8 (&a)[2][2], h8 (&a1)[2][2]) {
+                                           h8 (&a)[2][2], h8 (&a1)[2][2], F fill = F()) {
   const int lane = threadIdx.x & 63;
   const int li = lane & 15, g = lane >> 4;
   constexpr int NS = NQ * MT;   // (chunk, M-tile) steps
@@ -234,6 +324,7 @@ __device__ __forceinline__ void layer_mfma(const char* __restrict__ X, rsrc_t rs
   auto act = [&](int t) { return X + act_off(16 * (t % MT) + li, 4 * (t / MT) + g); };
   h8 bh = *(const h8*)act(0), bl = *(const h8*)(act(0) + 256);
   if (APN_H4_PRIO) __builtin_amdgcn_s_setprio(1);
+  fill();
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     h8 an[2][2];
@@ -250,6 +341,7 @@ __device__ __forceinline__ void layer_mfma(const char* __restrict__ X, rsrc_t rs
         for (int pt = 0; pt < 2; ++pt) an[j][pt] = frag(rs, vb, FBN + (j * NQN + qn - NQ) * 2 + pt);
     }
 #if APN_H4_PIN
+    if (!FILL)
     __builtin_amdgcn_sched_barrier(0);   // the fragment loads issue here, before the MFMAs
 #endif
 #pragma unroll
@@ -263,12 +355,12 @@ __device__ __forceinline__ void layer_mfma(const char* __restrict__ X, rsrc_t rs
 #if APN_H4_PIN
       // the next M-tile's activation reads issue before this M-tile's MFMAs, into registers of their
       // own: no MFMA-read -> LDS-write hazard pad (s_nop) and the LDS latency under 6 MFMAs
-      __builtin_amdgcn_sched_barrier(0);
+      if (!FILL) __builtin_amdgcn_sched_barrier(0);
 #endif
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[mt][j] = mfma3(a[j][0], a[j][1], bh, bl, acc[mt][j]);
 #if APN_H4_PIN
-      __builtin_amdgcn_sched_barrier(0);
+      if (!FILL) __builtin_amdgcn_sched_barrier(0);
 #endif
       bh = nbh;
       bl = nbl;
@@ -282,6 +374,19 @@ __device__ __forceinline__ void layer_mfma(const char* __restrict__ X, rsrc_t rs
         else { a[j][0] = an[j][0]; a[j][1] = an[j][1]; }
       }
       if (APN_H4_PF2 && j < (qn < NQ ? 2 : NTN)) { a1[j][0] = an[j][0]; a1[j][1] = an[j][1]; }
+    }
+  }
+  if (FILL) {
+    // the region's other VALU (the next tile's posenc, pe_compute) one instruction per MFMA issue
+    // gap, each step's two activation reads ahead of its MFMAs
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // DS read
+#pragma unroll
+      for (int m = 0; m < 6; ++m) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);   // VALU
+      }
     }
   }
   if (APN_H4_PRIO) __builtin_amdgcn_s_setprio(0);
@@ -416,6 +521,16 @@ __device__ __forceinline__ void mlp_tiles(
   GatherRegs gn;   // the records of the tile about to be gathered (APN_H4_RECPF)
   if (APN_H4_RECPF && tile < t_end)
     gather_load<!LISTED>(gh, lane & 7, pf_ok ? pf_nb : -1, pf_ray, gn, recA, recB, viewdirs, vemb_const);
+  constexpr bool FILL = APN_H4_PEFILL && LISTED;
+  GatherRegs gx;   // FILL: the next tile's records, then its posenc (made during layer 4)
+  PeRegs pe;
+  if (FILL && tile < t_end) {   // the first tile's posenc
+    gather_load<false>(gh, lane & 7, pf_ok ? pf_nb : -1, pf_ray, gx, recA, recB, viewdirs, vemb_const);
+    if (gh == 0)
+      pe_compute<0>(pf_q, gx, pe);
+    else
+      pe_compute<1>(pf_q, gx, pe);
+  }
   h8 a[2][2], a1[2][2];   // carried A-fragment prefetch (chunks 0 [, 1] of the next weight matrix)
 #pragma unroll
   for (int j = 0; j < 2; ++j)
@@ -444,7 +559,9 @@ __device__ __forceinline__ void mlp_tiles(
     const int nb0 = pf_ok ? pf_nb : -1;
     const float4 q0 = pf_q;
     GatherRegs g0;
-    if (APN_H4_RECPF)
+    if (FILL)
+      g0 = gx;   // its view component (the posenc is in pe)
+    else if (APN_H4_RECPF)
       g0 = gn;
     else
       gather_load<!LISTED>(gh, lane & 7, nb0, pf_ray, g0, recA, recB, viewdirs, vemb_const);
@@ -479,7 +596,7 @@ __device__ __forceinline__ void mlp_tiles(
       __builtin_amdgcn_sched_barrier(0);   // issued here, not sunk into the gather
     }
     // ------------------------------------------------ gather + posenc + direct-blend terms
-    gather<!LISTED>(gh, nb0, q0, g0, X, sTo, sRow, sV, vemb_const);
+    gather<!LISTED, FILL>(gh, nb0, q0, g0, X, sTo, sRow, sV, vemb_const, sIdw, eps, pe);
     if (!APN_H4_PEARLY) load_p();
     if (SCALED) {
       const float sc1 = sW[SW_SC];
@@ -497,7 +614,7 @@ __device__ __forceinline__ void mlp_tiles(
     } else if (prev_s0 >= 0 && tid < TS4 * 3 && prev_s0 + tid / 3 < nS) {
       out[(size_t)prev_s0 * 3 + tid] = *(const float4*)(sOut + 4 * tid);
     }
-    if (tid < TS4) {  // IDW weights (temporalpoints.py:473-475)
+    if (!APN_H4_IDWG && tid < TS4) {  // IDW weights (temporalpoints.py:473-475)
       float w[8], sum = 0.f;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -527,12 +644,21 @@ __device__ __forceinline__ void mlp_tiles(
     store_act(X, ot0, nullptr, acc, SCALED, SCALED ? sW[SW_DS + 1] : 1.f);
     __syncthreads();
     init_bias(acc, ot0, sW + SW_B3);
+    if (FILL)   // the next tile's records (its indices came with this tile's fetch) for layer 4's fill
+      gather_load<false>(gh, lane & 7, pf_ok ? pf_nb : -1, pf_ray, gx, recA, recB, viewdirs, vemb_const);
     layer_mfma<4, 4, 2, FR_W3, FR_W4>(X, rs, vb, acc, a, a1);
     __syncthreads();
     store_act(X, ot0, nullptr, acc, SCALED, SCALED ? sW[SW_DS + 2] : 1.f);
     __syncthreads();
     init_bias(acc, ot0, sW + SW_B4);
-    layer_mfma<4, 5, 1, FR_W4, FR_WH>(X, rs, vb, acc, a, a1);
+    if (FILL) {   // layer 4 with the next tile's posenc in its MFMA gaps (one copy per argument half)
+      if (gh == 0)
+        layer_mfma<4, 5, 1, FR_W4, FR_WH, true>(X, rs, vb, acc, a, a1, [&]() { pe_compute<0>(pf_q, gx, pe); });
+      else
+        layer_mfma<4, 5, 1, FR_W4, FR_WH, true>(X, rs, vb, acc, a, a1, [&]() { pe_compute<1>(pf_q, gx, pe); });
+    } else {
+      layer_mfma<4, 5, 1, FR_W4, FR_WH>(X, rs, vb, acc, a, a1);
+    }
     // the next tile's gather rows' neighbours (fetched at this tile's top) for its P rows
     if (APN_H4_LDSPN && tid < TR4) sNb[tid] = pf_ok ? pf_nb : -1;
     __syncthreads();
@@ -616,10 +742,10 @@ __device__ __forceinline__ void mlp_tiles(
       const int slot = qn == 0 ? 7 : (qn < 4 ? 3 + qn : (qn < 7 ? 4 + qn : 11));
       sOut[12 * s + slot] = acc1;
     }
-    __syncthreads();   // every IDW read of X is done: the head rows may overwrite it
+    if (!APN_H4_HEADW) __syncthreads();   // every IDW read of X is done: the head rows may overwrite it
     {
       // head input row s: [h (128) | view embedding (27) | 0] as hi/lo halves (rows alias X)
-      char* hr = X + s_ * HB;
+      char* hr = X + head_row(s_);
       h4 hi0, lo0, hi1, lo1;
       split4(h0, hi0, lo0);
       split4(h1, hi1, lo1);
@@ -641,7 +767,7 @@ __device__ __forceinline__ void mlp_tiles(
     {
       const int o0 = 16 * wid + 4 * g;
       f32x4 ah = *(const f32x4*)(sW + SW_BH + o0);   // views_linears.0 (folded) bias
-      const char* hr = X + li * HB;                   // B column li = sample li (16 real columns)
+      const char* hr = X + head_row(li);              // B column li = sample li (16 real columns)
       h8 an[2][2];   // the next tile's W1E chunk 0 (carried across the gather)
       h8 an1[2][2];   // and chunk 1 (two-deep)
 #pragma unroll

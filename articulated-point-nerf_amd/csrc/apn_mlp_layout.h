@@ -117,6 +117,18 @@ void launch_point_mlp_h4(int blocks, bool timed, hipStream_t stream, const float
 // Early ray termination (apn_ert.hip): the MLP in ERT_PASSES passes over the live rays' next
 // kept samples; ``MlpPass(list, n_list_dev)`` launches the MLP on one pass's sample list.
 constexpr int ERT_PASSES = 9;
+// 1: the MLP kernel's IDW weights (temporalpoints.py:473-475) made in its gather by the 128 threads
+// that compute the rows' squared distances (the sample's 8 rows are 8 consecutive lanes: a 3-step
+// xor-shuffle sum) instead of by 16 threads of wave 0 at the top of layer 1 (8 dependent LDS reads
+// and adds per thread while the other waves run layer 1). The 8-term sum becomes the pairwise tree
+// ((w0 + w1) + (w2 + w3)) + ((w4 + w5) + (w6 + w7)), which k_direct_blend (apn_ert.hip) then
+// follows too, so the early-termination frame stays bit-identical to the full one. Measured slower
+// (round 6, same box, parity green: MLP kernel 2.960 / 2.969 -> 2.995 / 3.005 ms per C2 frame; the
+// two gather waves of half 0 carry the shuffles alone): off.
+#ifndef APN_H4_IDWG
+#define APN_H4_IDWG 0
+#endif
+
 #ifndef APN_ERT_MLP_BLOCKS
 #define APN_ERT_MLP_BLOCKS 2048
 #endif
