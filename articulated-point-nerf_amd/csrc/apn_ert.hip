@@ -39,13 +39,15 @@ __global__ __launch_bounds__(256) void k_direct_blend(const float4* __restrict__
     for (int k = 0; k < 8; ++k) {
       const int nb = nbs[k];
       const size_t m = (size_t)max(nb, 0);
-      const float4 a0 = recA[4 * m], a3 = recA[4 * m + 3], b0 = recB[2 * m], b1 = recB[2 * m + 1];
+      // 3 of the point's 6 float4s: b0.w carries alpha (apn_lbs.hip record layout), so recA's
+      // last float4 is not read
+      const float4 a0 = recA[4 * m], b0 = recB[2 * m], b1 = recB[2 * m + 1];
       if (nb >= 0) {
         const float dx = q.x - a0.x, dy = q.y - a0.y, dz = q.z - a0.z;
         const float tn = (dx * dx + dy * dy) + dz * dz;
         to[k] = tn;
         dw[k] = expf(-(tn * tn) / a0.w);   // temporalpoints.py:461 (to_nn is already squared)
-        al[k] = a3.y;
+        al[k] = b0.w;
         cd[k] = make_float3(b0.x, b0.y, b0.z);
         cw[k] = make_float3(b1.x, b1.y, b1.z);
       } else {

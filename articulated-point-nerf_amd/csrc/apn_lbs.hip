@@ -9,7 +9,8 @@
 //   bbox of x'             temporalpoints.py:424       atomic min/max on order-preserving ints
 // and writes the per-point records the kNN / MLP stages gather:
 //   recA[n] = {x', y', z', den, Rinv(9, row-major), clip(alpha,0,1), 0, 0}   (64 B)
-//   recB[n] = {clip(rgb,0,1), 0, pcol, 0}                                     (32 B)
+//   recB[n] = {clip(rgb,0,1), clip(alpha,0,1), pcol, 0}                      (32 B)
+// (alpha twice: the direct blend reads recA's first and recB's two float4s, not recA[3])
 // HBM-bound: per point it reads 12 + 4J + 4 + 12 + 4 bytes and writes 12 + 4J + 96 bytes.
 #include "apn_common.h"
 #include "apn_mlp_split.h"   // split4 (the hi/lo fp16 split of the 3-term MFMA)
@@ -68,7 +69,7 @@ __device__ __forceinline__ void lbs_finish(int64_t n, const float (&G)[12], floa
     const float r = fminf(fmaxf(rgb_c[3 * n], 0.f), 1.f);
     const float g = fminf(fmaxf(rgb_c[3 * n + 1], 0.f), 1.f);
     const float b = fminf(fmaxf(rgb_c[3 * n + 2], 0.f), 1.f);
-    recB[2 * n + 0] = make_float4(r, g, b, 0.f);
+    recB[2 * n + 0] = make_float4(r, g, b, ac);
     recB[2 * n + 1] = make_float4((float)pc0, (float)pc1, (float)pc2, 0.f);
   }  // recA
 }

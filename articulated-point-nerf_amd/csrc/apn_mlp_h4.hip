@@ -450,6 +450,15 @@ __device__ __forceinline__ void mlp_tiles(
     float* const sW, float* const sPart, int* const sNb) {
   const int nS = *n_samples_dev;
   const int ntiles = (nS + TS4 - 1) / TS4;
+  // XCD-aware tile order: XCD x = block % 8 walks a contiguous tile range, so neighbouring samples
+  // (which share neighbour points) gather through the same L2
+  const int nx = (gridDim.x % 8 == 0) ? 8 : 1;
+  const int xcd = blockIdx.x % nx, per_xcd = gridDim.x / nx;
+  const int chunk = (ntiles + nx - 1) / nx;
+  const int t_beg = xcd * chunk, t_end = min(ntiles, t_beg + chunk);
+  // a workgroup without tiles (an early-termination pass that found no live rays, or more
+  // workgroups than tiles) leaves before staging the weights (workgroup-uniform: no barrier yet)
+  if (t_beg + (int)blockIdx.x / nx >= t_end) return;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, g = lane >> 4;
@@ -474,12 +483,6 @@ __device__ __forceinline__ void mlp_tiles(
   if (tid < 3) sW[SW_BV2 + tid] = wbuf[OFF_BV2 + tid];
   if (tid == 0) sW[SW_BD] = wbuf[OFF_BD];
   if (SCALED) __syncthreads();
-  // XCD-aware tile order: XCD x = block % 8 walks a contiguous tile range, so neighbouring samples
-  // (which share neighbour points) gather through the same L2
-  const int nx = (gridDim.x % 8 == 0) ? 8 : 1;
-  const int xcd = blockIdx.x % nx, per_xcd = gridDim.x / nx;
-  const int chunk = (ntiles + nx - 1) / nx;
-  const int t_beg = xcd * chunk, t_end = min(ntiles, t_beg + chunk);
 
   // next-tile prefetch (unconditional clamped loads): this thread's gather row (tid & 127:
   // neighbour lane & 7 of sample (tid & 127) >> 3) and its 8 P rows

@@ -738,10 +738,12 @@ def main():
                     help="N>1: 'rays' (default) = the ranks split one frame's rays and all-gather the tiles "
                          "over RCCL (strong scaling, SURVEY.md 8(e)); 'frames' = every rank renders its own "
                          "frame (weak scaling, no data-path collective)")
-    ap.add_argument("--in-flight", type=int, choices=[1, 2, 3, 4], default=3,
+    ap.add_argument("--in-flight", type=int, choices=[1, 2, 3, 4], default=None,
                     help="frames in flight: one model's frame captured into n workspaces, frame i on stream i %% n "
                          "(ray shards: the all-gathers in frame order on one collective stream); 1 = one "
-                         "after another")
+                         "after another. Default 3, and 4 for ray shards over >= 4 ranks (a shard of 8 at C2: "
+                         "0.945 vs 0.985 ms per frame in flight, shards of 2 / 4 equal, 6 slower; "
+                         "profiles/r06_shard_inflight.log)")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                     help="replay the frame as one HIP graph (TemporalPoints.capture_frame; with --shard rays "
                          "each rank's blocks, shard.capture_sharded); auto = on unless the ranks use the "
@@ -750,6 +752,8 @@ def main():
     torch.set_grad_enabled(False)   # a render benchmark: the reference renders under no_grad (run.py:80, 241)
 
     world = check_world(args.gpus, os.environ)
+    if args.in_flight is None:
+        args.in_flight = 4 if (world >= 4 and args.shard == "rays") else 3
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one process per GPU; APN_DIST_BACKEND=gloo rehearses N>1 with several ranks on one card

@@ -160,7 +160,7 @@ int apn_weight_sparsity_loss_backward(const float* w, int64_t n, float eps, cons
  *   bone_T34 [J,12]: rows 0..2 of each bone 4x4; merge_rules [J] int32 or NULL (identity);
  *   joint_colors [J,3] or NULL; weights_out [N,J] or NULL;
  *   recA16 [N,16] = {x,y,z, 2*(mmd*max(eps_n,0))^2+1e-12, Rinv(9), clip(alpha), 0,0};
- *   recB8 [N,8] = {clip(rgb), 0, sum_j col_j w_j, 0}; bbox_ord [6] ordered-int min/max of the
+ *   recB8 [N,8] = {clip(rgb), clip(alpha), sum_j col_j w_j, 0}; bbox_ord [6] ordered-int min/max of the
  *   skinned cloud or NULL; workspace: apn_lbs_workspace_bytes(n_points) (needed with bbox_ord). */
 size_t apn_lbs_workspace_bytes(int64_t n_points);
 int apn_lbs_skin(const float* canonical_pcd, const float* raw_weights, int64_t n_points,

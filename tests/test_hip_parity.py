@@ -367,7 +367,7 @@ def _records(orc, t_hat, colors):
     recA[:, :3] = torch.as_tensor(t_hat); recA[:, 3] = den; recA[:, 4:13] = Rinv
     recA[:, 13] = orc.alpha_c.clip(0, 1)
     recB = torch.zeros(N, 8)
-    recB[:, :3] = orc.rgb_c.clip(0, 1)
+    recB[:, :3] = orc.rgb_c.clip(0, 1); recB[:, 3] = orc.alpha_c.clip(0, 1)
     recB[:, 4:7] = (orc.trace["weights"].double() @ colors.double()).float()
     return recA, recB
 
@@ -562,6 +562,8 @@ def test_lbs_records_vs_oracle(golden_model, dev):
     recA = m._ws.bufs["recA"][:N * 16].reshape(N, 16).cpu()
     Rinv = torch.inverse(G)[:, :3, :3].reshape(-1, 9)
     assert (recA[:, 4:13] - Rinv).abs().max() < 1e-5
+    recB = m._ws.bufs["recB"][:N * 8].reshape(N, 8).cpu()   # alpha in both (the direct blend reads recB's)
+    assert torch.equal(recB[:, 3], recA[:, 13]) and torch.equal(recB[:, 7], torch.zeros(N))
     assert (m._last_weights.cpu() - orc.get_weights()).abs().max() < 1e-6
     assert (out["joints"].cpu() - g.t("out_joints")).abs().max() < 1e-3
 
