@@ -95,18 +95,32 @@ __global__ __launch_bounds__(256) void k_direct_blend(const float4* __restrict__
 // (the list's order between blocks varies from run to run; a sample's MLP result does not depend
 // on its tile-mates, so the frame does not), and the pass size accumulates in *count -- the MLP
 // launch's device count.
+// APN_ERT_RAYLIST: pass 0 walks every ray and lists the rays it gave samples to (rl_out, *n_rl_out);
+// every later pass walks only the previous pass's listed rays (rl_in) -- the rays still live --
+// instead of all n_rays, and lists its own (the same block scan: one atomic per block for each).
+#ifndef APN_ERT_RAYLIST
+#define APN_ERT_RAYLIST 1
+#endif
 __global__ __launch_bounds__(256) void k_ert_pass(int64_t n_rays, int first, const int* __restrict__ beg,
                                                   const int* __restrict__ end, const float4* __restrict__ out,
                                                   float thr, int use_mask, int* __restrict__ pos,
                                                   float* __restrict__ T, int* __restrict__ cnt, int B,
                                                   int* __restrict__ list, int* __restrict__ count,
-                                                  const int* __restrict__ prev_count) {
+                                                  const int* __restrict__ prev_count, const int* __restrict__ rl_in,
+                                                  const int* __restrict__ n_rl_in, int* __restrict__ rl_out,
+                                                  int* __restrict__ n_rl_out) {
   __shared__ int s_wave[4];
-  __shared__ int s_base;
+  __shared__ int s_base, s_rbase;
   // an empty previous pass leaves every ray with nothing listed, so this pass and every later one
   // are empty too (their counts stay at the 0 they were filled with): the whole grid returns
   if (prev_count && *prev_count == 0) return;
-  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  int64_t r = i;
+  if (APN_ERT_RAYLIST && !first) {   // the rays the previous pass listed
+    const int n_live = *n_rl_in;
+    if ((int64_t)blockIdx.x * 256 >= n_live) return;   // workgroup-uniform
+    r = i < n_live ? rl_in[i] : n_rays;
+  }
   int c = 0, p = 0;
   if (r < n_rays) {
     const int e = end[r];
@@ -138,7 +152,7 @@ __global__ __launch_bounds__(256) void k_ert_pass(int64_t n_rays, int first, con
     pos[r] = p;
     cnt[r] = c;
   }
-  // block-wide exclusive scan of c
+  // block-wide exclusive scans of c and (APN_ERT_RAYLIST, by ballot) of the live flag c > 0
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   int inc = c;
 #pragma unroll
@@ -146,18 +160,30 @@ __global__ __launch_bounds__(256) void k_ert_pass(int64_t n_rays, int first, con
     const int v = __shfl_up(inc, o, 64);
     if (lane >= o) inc += v;
   }
-  if (lane == 63) s_wave[wid] = inc;
+  const unsigned long long live = APN_ERT_RAYLIST ? __ballot(c > 0) : 0ull;
+  __shared__ int s_live[4];
+  if (lane == 63) {
+    s_wave[wid] = inc;
+    s_live[wid] = __popcll(live);
+  }
   __syncthreads();
-  int wbase = 0, tot = 0;
+  int wbase = 0, tot = 0, lbase = 0, ltot = 0;
 #pragma unroll
   for (int w = 0; w < 4; ++w) {
     wbase += w < wid ? s_wave[w] : 0;
     tot += s_wave[w];
+    lbase += w < wid ? s_live[w] : 0;
+    ltot += s_live[w];
   }
-  if (threadIdx.x == 0) s_base = tot > 0 ? atomicAdd(count, tot) : 0;
+  if (threadIdx.x == 0) {
+    s_base = tot > 0 ? atomicAdd(count, tot) : 0;
+    if (APN_ERT_RAYLIST) s_rbase = ltot > 0 ? atomicAdd(n_rl_out, ltot) : 0;
+  }
   __syncthreads();
   const int o = s_base + wbase + inc - c;
   for (int j = 0; j < c; ++j) list[o + j] = p + j;
+  if (APN_ERT_RAYLIST && c > 0)
+    rl_out[s_rbase + lbase + __popcll(live & ((1ull << lane) - 1ull))] = (int)r;
 }
 
 __global__ void k_ray_bounds_ert(const int* __restrict__ s_ray, const int* __restrict__ n_dev, int* __restrict__ beg,
@@ -178,7 +204,8 @@ int direct_blend(const float4* s_pos, const int* s_nbr, int64_t max_samples, con
 }
 
 // workspace: beg, end, pos, cnt [n_rays] i32, T [n_rays] f32, the passes' list sizes
-// [ERT_PASSES] i32, list [max_samples] i32
+// [ERT_PASSES] i32, list [max_samples] i32, two live-ray lists [n_rays] i32 and their sizes
+// [ERT_PASSES] i32
 static size_t ert_ws_layout(int64_t max_samples, int64_t n_rays, size_t* off) {
   size_t o = 0;
   auto take = [&](size_t bytes) {
@@ -193,11 +220,14 @@ static size_t ert_ws_layout(int64_t max_samples, int64_t n_rays, size_t* off) {
   off[4] = take(4 * (size_t)n_rays);        // T
   off[5] = take(4 * (size_t)ERT_PASSES);    // pass sizes
   off[6] = take(4 * (size_t)max_samples);   // list
+  off[7] = take(4 * (size_t)n_rays);        // live rays, even passes' output
+  off[8] = take(4 * (size_t)n_rays);        // live rays, odd passes' output
+  off[9] = take(4 * (size_t)ERT_PASSES);    // live-ray list sizes
   return o;
 }
 
 size_t ert_workspace_bytes(int64_t max_samples, int64_t n_rays) {
-  size_t off[7];
+  size_t off[10];
   return ert_ws_layout(max_samples, n_rays, off);
 }
 
@@ -208,7 +238,7 @@ static const int ERT_PASS[ERT_PASSES] = {2, 2, 2, 2, 2, 2, 4, 8, 1 << 30};
 int ert_run(const float4* s_pos, const int* s_ray, const int* s_nbr, int64_t max_samples, const int* n_samples_dev,
             int64_t n_rays, const float4* recA, const float4* recB, float eps, float thr, float4* out, void* ws,
             int with_direct, int* stats, void* const* events, hipStream_t s, const MlpPass& mlp) {
-  size_t off[7];
+  size_t off[10];
   ert_ws_layout(max_samples, n_rays, off);
   char* w = (char*)ws;
   int* beg = (int*)(w + off[0]);
@@ -218,11 +248,14 @@ int ert_run(const float4* s_pos, const int* s_ray, const int* s_nbr, int64_t max
   float* T = (float*)(w + off[4]);
   int* sizes = (int*)(w + off[5]);
   int* list = (int*)(w + off[6]);
+  int* rl[2] = {(int*)(w + off[7]), (int*)(w + off[8])};
+  int* rl_n = (int*)(w + off[9]);
   const int rb = ceil_div(n_rays, 256);
   const int use_mask = thr > 0.f ? 1 : 0;
   APN_TRY(fill_i32(beg, 0, n_rays, s));   // rays without kept samples: beg = end = 0
   APN_TRY(fill_i32(end, 0, n_rays, s));
   APN_TRY(fill_i32(sizes, 0, ERT_PASSES, s));
+  if (APN_ERT_RAYLIST) APN_TRY(fill_i32(rl_n, 0, ERT_PASSES, s));
   hipLaunchKernelGGL(k_ray_bounds_ert, dim3(ceil_div(max_samples, 256)), dim3(256), 0, s, s_ray, n_samples_dev, beg,
                      end);
   // direct path + weight colour of every kept sample (read up to the direct path's own break);
@@ -230,7 +263,8 @@ int ert_run(const float4* s_pos, const int* s_ray, const int* s_nbr, int64_t max
   if (with_direct) APN_TRY(direct_blend(s_pos, s_nbr, max_samples, n_samples_dev, recA, recB, eps, out, s));
   for (int p = 0; p < ERT_PASSES; ++p) {
     hipLaunchKernelGGL(k_ert_pass, dim3(rb), dim3(256), 0, s, n_rays, p == 0 ? 1 : 0, beg, end, (const float4*)out,
-                       thr, use_mask, pos, T, cnt, ERT_PASS[p], list, sizes + p, p == 0 ? nullptr : sizes + p - 1);
+                       thr, use_mask, pos, T, cnt, ERT_PASS[p], list, sizes + p, p == 0 ? nullptr : sizes + p - 1,
+                       (const int*)rl[(p + 1) & 1], p == 0 ? nullptr : rl_n + p - 1, rl[p & 1], rl_n + p);
     if (events) APN_HIP_TRY(hipEventRecord((hipEvent_t)events[2 * p], s));
     APN_TRY(mlp(list, sizes + p));
     if (events) APN_HIP_TRY(hipEventRecord((hipEvent_t)events[2 * p + 1], s));

@@ -5,7 +5,7 @@ cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT || exit 1
 O=gpurun_out/r06m; mkdir -p $O
 NEW=${NEW:-"pkr"}
 PT="python -u -m pytest -q --timeout 600 --timeout-method thread -p no:cacheprovider -m gpu"
-[ -n "$SKIP_PARITY" ] || ${PARITY_NEW:+env APN_HIP_LIB=$PWD/ab/$NEW/libapn_hip.so} timeout -k 10 500 $PT tests/test_mlp_precision.py tests/test_ert.py "tests/test_hip_parity.py::test_mlp_stage_vs_oracle" "tests/test_full_frame_parity.py::test_every_ray_vs_oracle[C2]" -k "not C3 and not C4" -s > $O/parity.log 2>&1
+[ -n "$SKIP_PARITY" ] || ${PARITY_NEW:+env APN_HIP_LIB=$PWD/ab/${NEW%% *}/libapn_hip.so} timeout -k 10 500 $PT tests/test_mlp_precision.py tests/test_ert.py "tests/test_hip_parity.py::test_mlp_stage_vs_oracle" "tests/test_full_frame_parity.py::test_every_ray_vs_oracle[C2]" -k "not C3 and not C4" -s > $O/parity.log 2>&1
 rc=$?; [ -n "$SKIP_PARITY" ] || grep -E "passed|failed|every ray" $O/parity.log | tail -5
 case $rc in 0) ;; *) echo "stop rc $rc"; grep -E "Error|assert" $O/parity.log | head -20; exit $rc;; esac
 for r in 1 2; do for v in ${BASE:-base} $NEW; do
