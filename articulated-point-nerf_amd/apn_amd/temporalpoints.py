@@ -524,7 +524,7 @@ class TemporalPoints(torch.nn.Module):
         self._mark("lbs")
         return [xyz, joints_rel]
 
-    def capture_repose(self, rot_dim=4, sweep=None, batched=True, pipelined=False):
+    def capture_repose(self, rot_dim=4, sweep=None, batched=True, pipelined=False, in_flight=1):
         """The repose step (skeleton launch + fused LBS launch, run.py:1355-1396 sweeps it per pose)
         captured once in a HIP graph: returns ``step(rot_params) -> (xyz, joints_rel)``, which
         copies rot_params [J, rot_dim] into the graph's input and replays it -- no per-pose host
@@ -545,10 +545,15 @@ class TemporalPoints(torch.nn.Module):
         one-workgroup skeleton launch (~10 us of latency plus a dependent launch) leaves the per-pose
         critical path. Every step still skins its pose in full; within a pass each pose's skeleton
         is computed once, as in the per-pose path.
+        ``in_flight`` (batched only) = n > 1: poses in flight, pose i on ``step.streams[i % n]``
+        into its own output slot ``step.outputs[i % n]`` (so the next pose's LBS starts while this
+        one drains, instead of after a graph-launch gap); the returned xyz is then ready on that
+        stream only: a consumer waits on it (``torch.cuda.current_stream().wait_stream(...)``) and
+        has it until step i + n.
         ``pipelined`` (with a sweep, measured and not kept: 0.066 vs 0.052 ms per pose at C5):
         step i's graph runs pose i's LBS beside pose i + 1's skeleton on a forked side stream."""
         if sweep is not None and batched:
-            return self._capture_repose_batched(sweep)
+            return self._capture_repose_batched(sweep, in_flight=in_flight)
         if sweep is not None and pipelined:
             return self._capture_repose_pipelined(sweep)
         dev = self.canonical_pcd.device
@@ -601,7 +606,7 @@ class TemporalPoints(torch.nn.Module):
         step.graph, step.inputs = graph, (rp if sweep is None else (sweep, idx))
         return step
 
-    def _capture_repose_batched(self, sweep):
+    def _capture_repose_batched(self, sweep, in_flight=1):
         dev = self.canonical_pcd.device
         N, J = self.weights.shape
         sweep = sweep.detach().to(dev, torch.float32).contiguous()
@@ -612,10 +617,11 @@ class TemporalPoints(torch.nn.Module):
         bufs = {"thetas": torch.empty(P, J, device=dev), "bone_Ts": torch.empty(P, J, 4, 4, device=dev),
                 "T34": torch.empty(P, J, 12, device=dev), "gt": torch.empty(P, 3, device=dev),
                 "joints_rel": torch.empty(P, J, 3, device=dev)}
-        xyz = torch.empty(N, 3, device=dev)
+        n_fl = max(1, int(in_flight))
+        outs = [torch.empty(N, 3, device=dev) for _ in range(n_fl)]   # pose i -> outs[i % n_fl]
 
         def lbs(i):
-            self._lbs(bufs["bone_Ts"][i], bufs["gt"][i], records=False, T34=bufs["T34"][i], out=xyz)
+            self._lbs(bufs["bone_Ts"][i], bufs["gt"][i], records=False, T34=bufs["T34"][i], out=outs[i % n_fl])
 
         with torch.no_grad():
             cur = torch.cuda.current_stream(dev)
@@ -640,21 +646,40 @@ class TemporalPoints(torch.nn.Module):
         row = J * rot_dim * 4
         base = sweep.data_ptr()
         state = {"ver": None}   # the sweep version the skeleton batch was computed from
+        streams = [torch.cuda.Stream(dev) for _ in range(n_fl)] if n_fl > 1 else None
 
         def step(rot_params):
             off = rot_params.data_ptr() - base
             if (rot_params.device != sweep.device or not rot_params.is_contiguous() or off < 0 or off % row
                     or off // row >= P or rot_params.numel() != J * rot_dim):
+                if streams:   # the eager path runs on the caller's stream, after the poses in flight
+                    for t in streams:
+                        torch.cuda.current_stream(dev).wait_stream(t)
                 with torch.no_grad():
                     return self.repose(rot_params)
             i = off // row
+            if streams is None:
+                if i == 0 or state["ver"] != sweep._version:
+                    g_skel.replay()   # every pose's skeleton (a new pass over the sweep, or the sweep changed)
+                    state["ver"] = sweep._version
+                graphs[i].replay()
+                return outs[0], bufs["joints_rel"][i]
+            cur = torch.cuda.current_stream(dev)
             if i == 0 or state["ver"] != sweep._version:
-                g_skel.replay()   # every pose's skeleton (a new pass over the sweep, or the sweep changed)
+                # the skeleton batch is rewritten: after every pose in flight has read it, and after
+                # the caller's writes to the sweep; every slot's next pose after it
+                for t in streams:
+                    cur.wait_stream(t)
+                g_skel.replay()
                 state["ver"] = sweep._version
-            graphs[i].replay()
-            return xyz, bufs["joints_rel"][i]
+                for t in streams:
+                    t.wait_stream(cur)
+            with torch.cuda.stream(streams[i % n_fl]):
+                graphs[i].replay()
+            return outs[i % n_fl], bufs["joints_rel"][i]
 
         step.graph, step.inputs = graphs, (sweep,)
+        step.streams, step.outputs = streams, outs
         return step
 
     def _capture_repose_pipelined(self, sweep):

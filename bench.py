@@ -346,7 +346,9 @@ def lbs_sweep(args, rank, world, dev):
     # each pass over the sweep starts with one launch computing every pose's skeleton, then one
     # LBS graph per pose (TemporalPoints.capture_repose(batched=True))
     mode = getattr(args, "repose_mode", "batched")
-    step = model.capture_repose(sweep=poses, batched=mode == "batched", pipelined=mode == "pipelined")
+    n_fl = getattr(args, "repose_in_flight", 1) if mode == "batched" else 1
+    step = model.capture_repose(sweep=poses, batched=mode == "batched", pipelined=mode == "pipelined",
+                                in_flight=n_fl)
     for i in range(args.warmup):
         step(poses[i % len(poses)])
     if world > 1:
@@ -401,7 +403,7 @@ def lbs_sweep(args, rank, world, dev):
                             "skeleton stage of every pose of the sweep runs as ONE launch (one workgroup per pose) "
                             "at the start of every pass over the sweep -- inside the timed loop, 5 passes of 60 "
                             "poses here (TemporalPoints.capture_repose(sweep=..., batched=True))"),
-                   "lbs_kernel_ms": lbs_ms,
+                   "lbs_kernel_ms": lbs_ms, "poses_in_flight": n_fl,
                    "parallelism": f"points x{world} (no collective)" if world > 1 else "single"},
         "roofline": {"bound": "hbm", "kernel": "k_lbs_skin_mfma",
                      "achieved": b_alg / (lbs_ms * 1e-3) / 1e9 if lbs_ms > 0 else 0.0,
@@ -734,6 +736,8 @@ def main():
                     help="C5: the captured repose step (TemporalPoints.capture_repose): batched = one skeleton "
                          "launch per pass over the sweep + one LBS graph per pose; per_pose = skeleton + LBS per "
                          "pose; pipelined = pose i's LBS beside pose i + 1's skeleton")
+    ap.add_argument("--repose-in-flight", type=int, choices=[1, 2, 3], default=1,
+                    help="C5, batched: poses in flight (pose i on stream i %% n into output slot i %% n)")
     ap.add_argument("--shard", choices=["frames", "rays"], default="rays",
                     help="N>1: 'rays' (default) = the ranks split one frame's rays and all-gather the tiles "
                          "over RCCL (strong scaling, SURVEY.md 8(e)); 'frames' = every rank renders its own "

@@ -961,7 +961,7 @@ def test_training_losses_vs_cpu(golden_model, dev):
     assert warped.grad is not None and torch.isfinite(warped.grad).all()
     lw = m._last_weights.detach().cpu()
     tv_ref = torch.abs(lw[:, None, :] - lw[nn_ref, :]).mean()
-    assert abs(float(m.get_neighbour_weight_tv_loss()) - float(tv_ref)) < 1e-6
+    assert abs(float(m.get_neighbour_weight_tv_loss().detach()) - float(tv_ref)) < 1e-6
     jt = m.joints.detach().cpu()
     # a skeleton cloud along the bones (the golden models were built without one)
     sk = torch.cat([jt[p][None] + torch.linspace(0, 1, 7)[:, None] * (jt[c] - jt[p])[None]
@@ -992,7 +992,7 @@ def test_batch_chamfer_loss_2d(golden_model, dev):
             d2, _ = O.knn_kmin(np.pad(x[bi], ((0, 0), (0, 1))), np.pad(y[bi], ((0, 0), (0, 1))), 1, use_tree=False)
             tot.append(d2[:, 0].astype(np.float64))
         ref += np.concatenate(tot).mean()
-    assert abs(float(loss) - ref) < 1e-5
+    assert abs(float(loss.detach()) - ref) < 1e-5
 
 
 @pytest.mark.parametrize("config", ["C1", "C2", "C3", "C4"])
@@ -1234,7 +1234,7 @@ def _train_grad_check(g, m, dev):
             print("\nXYZDIFF", float((out["t_hat_pcd"].detach().cpu() - orc.trace["t_hat_pcd"]).abs().max()),
                   float((out["t_hat_pcd"].detach().cpu() != orc.trace["t_hat_pcd"]).float().mean()))
         lref = torch.nn.functional.mse_loss(ro["rgb_marched"], target)
-        assert abs(float(loss) - float(lref)) < 1e-6
+        assert abs(float(loss.detach()) - float(lref.detach())) < 1e-6
         lref.backward()
         grads[blend] = {k: p.grad for k, p in params.items()}
         if blend == "sum":

@@ -130,19 +130,33 @@ def test_captured_repose_graph_equals_eager(dev):
         assert torch.equal(xg, xe) and torch.equal(jg, je), k
 
 
-@pytest.mark.parametrize("mode", ["batched", "pipelined", "per_pose"])
+def _capture(model, poses, mode):
+    """capture_repose in a test mode; batched2 = batched with two poses in flight."""
+    return model.capture_repose(sweep=poses, batched=mode in ("batched", "batched2"), pipelined=mode == "pipelined",
+                                in_flight=2 if mode == "batched2" else 1)
+
+
+def _ready(step, k, res):
+    """The step's outputs for pose k on the caller's stream (poses in flight: wait on pose k's stream)."""
+    if getattr(step, "streams", None):
+        torch.cuda.current_stream().wait_stream(step.streams[k % len(step.streams)])
+    return res
+
+
+@pytest.mark.parametrize("mode", ["batched", "batched2", "pipelined", "per_pose"])
 def test_captured_repose_sweep_graph(dev, mode):
     """capture_repose(sweep=poses) -- in-order steps, a jump, a wrap-around and rot_params that are
     not a row of the sweep (eager fallback) all equal the eager repose bit for bit. batched (the
     default): every pose's skeleton in one launch per pass over the sweep, one LBS graph per pose;
     pipelined: each step's graph runs the next pose's skeleton beside its LBS; per_pose: one graph
-    reading its pose through a device index it advances itself."""
+    reading its pose through a device index it advances itself; batched2: batched with two poses in
+    flight (pose k on stream k % 2 into output slot k % 2)."""
     from apn_amd import harness, synthetic as S
     scene = S.make_scene(S.SceneConfig("graph repose sweep", 30_000, 48, 0, 0))
     model = harness.build_model(scene, dev)
     poses = S.repose_sweep(48).to(dev).contiguous()
     P = poses.shape[0]
-    step = model.capture_repose(sweep=poses, batched=mode == "batched", pipelined=mode == "pipelined")
+    step = _capture(model, poses, mode)
     order = [0, 1, 2, 3, 17, 18, P - 1, 0, 1, 5]
     for k in order:
         with torch.no_grad():
@@ -162,7 +176,7 @@ def test_captured_repose_sweep_graph(dev, mode):
     assert torch.equal(xg, xe) and torch.equal(jg, je)
 
 
-@pytest.mark.parametrize("mode", ["batched", "pipelined"])
+@pytest.mark.parametrize("mode", ["batched", "batched2", "pipelined"])
 def test_repose_sweep_modified_in_place(dev, mode):
     """The batched sweep computes every pose's skeleton at the start of a pass, the pipelined one
     pose i + 1's during step i; a sweep row changed in place in between must not be skinned from
@@ -171,18 +185,18 @@ def test_repose_sweep_modified_in_place(dev, mode):
     scene = S.make_scene(S.SceneConfig("graph repose sweep inplace", 20_000, 24, 0, 0))
     model = harness.build_model(scene, dev)
     poses = S.repose_sweep(24).to(dev).contiguous()
-    step = model.capture_repose(sweep=poses, batched=mode == "batched", pipelined=mode == "pipelined")
+    step = _capture(model, poses, mode)
     for k in range(4):
         step(poses[k])
     with torch.no_grad():
         poses[4].mul_(0.5)
-    xg, jg = (v.clone() for v in step(poses[4]))
+    xg, jg = (v.clone() for v in _ready(step, 4, step(poses[4])))
     with torch.no_grad():
         xe, je = model.repose(poses[4])
     torch.cuda.synchronize()
     assert torch.equal(xg, xe) and torch.equal(jg, je)
     for k in range(5, 9):   # and in order again afterwards
-        xg, jg = (v.clone() for v in step(poses[k]))
+        xg, jg = (v.clone() for v in _ready(step, k, step(poses[k])))
         with torch.no_grad():
             xe, je = model.repose(poses[k])
         torch.cuda.synchronize()
