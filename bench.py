@@ -346,7 +346,7 @@ def lbs_sweep(args, rank, world, dev):
     # each pass over the sweep starts with one launch computing every pose's skeleton, then one
     # LBS graph per pose (TemporalPoints.capture_repose(batched=True))
     mode = getattr(args, "repose_mode", "batched")
-    n_fl = getattr(args, "repose_in_flight", 1) if mode == "batched" else 1
+    n_fl = getattr(args, "repose_in_flight", 4) if mode == "batched" else 1
     step = model.capture_repose(sweep=poses, batched=mode == "batched", pipelined=mode == "pipelined",
                                 in_flight=n_fl)
     for i in range(args.warmup):
@@ -402,7 +402,9 @@ def lbs_sweep(args, rank, world, dev):
                    "step": ("one captured graph per pose: the LBS launch reading its pose's bone transforms; the "
                             "skeleton stage of every pose of the sweep runs as ONE launch (one workgroup per pose) "
                             "at the start of every pass over the sweep -- inside the timed loop, 5 passes of 60 "
-                            "poses here (TemporalPoints.capture_repose(sweep=..., batched=True))"),
+                            "poses here (TemporalPoints.capture_repose(sweep=..., batched=True, in_flight=n)); with "
+                            "n = poses_in_flight > 1, pose i's graph runs on stream i % n into its own output slot "
+                            "(every pose still skinned in full, each output kept until pose i + n)"),
                    "lbs_kernel_ms": lbs_ms, "poses_in_flight": n_fl,
                    "parallelism": f"points x{world} (no collective)" if world > 1 else "single"},
         "roofline": {"bound": "hbm", "kernel": "k_lbs_skin_mfma",
@@ -607,7 +609,7 @@ def other_configs(dev, in_flight=3):
             out[cfg] = {"error": repr(e)}
         torch.cuda.empty_cache()
     try:
-        a = argparse.Namespace(config="C5", steps=300, warmup=3, no_cpu_baseline=True)
+        a = argparse.Namespace(config="C5", steps=300, warmup=3, no_cpu_baseline=True, repose_in_flight=4)
         c5 = lbs_sweep(a, 0, 1, dev)
         out["C5"] = {"workload": c5["config"]["workload"], "value": c5["value"], "unit": c5["unit"],
                      "ms_per_step": c5["ms_per_step"], "steps": a.steps, "lbs_kernel_ms": c5["config"]["lbs_kernel_ms"],
@@ -736,8 +738,10 @@ def main():
                     help="C5: the captured repose step (TemporalPoints.capture_repose): batched = one skeleton "
                          "launch per pass over the sweep + one LBS graph per pose; per_pose = skeleton + LBS per "
                          "pose; pipelined = pose i's LBS beside pose i + 1's skeleton")
-    ap.add_argument("--repose-in-flight", type=int, choices=[1, 2, 3], default=1,
-                    help="C5, batched: poses in flight (pose i on stream i %% n into output slot i %% n)")
+    ap.add_argument("--repose-in-flight", type=int, choices=[1, 2, 3, 4], default=4,
+                    help="C5, batched: poses in flight (pose i on stream i %% n into output slot i %% n, "
+                         "TemporalPoints.capture_repose(in_flight=n)); same box: 1: 0.0400-0.0403 ms per pose, "
+                         "2: 0.0412-0.0414, 3: 0.0345-0.0363, 4: 0.0340 (profiles/r06_c5_inflight.log)")
     ap.add_argument("--shard", choices=["frames", "rays"], default="rays",
                     help="N>1: 'rays' (default) = the ranks split one frame's rays and all-gather the tiles "
                          "over RCCL (strong scaling, SURVEY.md 8(e)); 'frames' = every rank renders its own "

@@ -131,9 +131,9 @@ def test_captured_repose_graph_equals_eager(dev):
 
 
 def _capture(model, poses, mode):
-    """capture_repose in a test mode; batched2 = batched with two poses in flight."""
-    return model.capture_repose(sweep=poses, batched=mode in ("batched", "batched2"), pipelined=mode == "pipelined",
-                                in_flight=2 if mode == "batched2" else 1)
+    """capture_repose in a test mode; batchedN = batched with N poses in flight."""
+    return model.capture_repose(sweep=poses, batched=mode.startswith("batched"), pipelined=mode == "pipelined",
+                                in_flight=int(mode[7:]) if mode[7:].isdigit() else 1)
 
 
 def _ready(step, k, res):
@@ -143,7 +143,7 @@ def _ready(step, k, res):
     return res
 
 
-@pytest.mark.parametrize("mode", ["batched", "batched2", "pipelined", "per_pose"])
+@pytest.mark.parametrize("mode", ["batched", "batched2", "batched3", "pipelined", "per_pose"])
 def test_captured_repose_sweep_graph(dev, mode):
     """capture_repose(sweep=poses) -- in-order steps, a jump, a wrap-around and rot_params that are
     not a row of the sweep (eager fallback) all equal the eager repose bit for bit. batched (the
@@ -176,7 +176,7 @@ def test_captured_repose_sweep_graph(dev, mode):
     assert torch.equal(xg, xe) and torch.equal(jg, je)
 
 
-@pytest.mark.parametrize("mode", ["batched", "batched2", "pipelined"])
+@pytest.mark.parametrize("mode", ["batched", "batched2", "batched3", "pipelined"])
 def test_repose_sweep_modified_in_place(dev, mode):
     """The batched sweep computes every pose's skeleton at the start of a pass, the pipelined one
     pose i + 1's during step i; a sweep row changed in place in between must not be skinned from
