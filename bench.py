@@ -19,7 +19,7 @@ has every rank render its own frame instead (weak scaling, no data-path collecti
 (LBS-only) shards the points N/W per rank with no collective (strong scaling). The timing is
 barrier + synchronize bracketed and the max over ranks (all-reduce MAX of the elapsed time).
 
-Frames in flight (``--in-flight``, default 3): a frame's stages run in sequence (the kNN needs the
+Frames in flight (``--in-flight``, default 4): a frame's stages run in sequence (the kNN needs the
 warped cloud, the MLP the kNN's survivors), so one frame leaves the chip under-used while its kNN
 and small stages run. With n frames in flight ONE TemporalPoints replays its frame, captured n
 times into n per-frame workspaces (apn_amd.pipeline.FramePipeline; the canonical tables and the
@@ -749,9 +749,9 @@ def main():
     ap.add_argument("--in-flight", type=int, choices=[1, 2, 3, 4], default=None,
                     help="frames in flight: one model's frame captured into n workspaces, frame i on stream i %% n "
                          "(ray shards: the all-gathers in frame order on one collective stream); 1 = one "
-                         "after another. Default 3, and 4 for ray shards over >= 4 ranks (a shard of 8 at C2: "
-                         "0.945 vs 0.985 ms per frame in flight, shards of 2 / 4 equal, 6 slower; "
-                         "profiles/r06_shard_inflight.log)")
+                         "after another. Default 4 (C2, same box, 3 rounds: 4.96-5.07 vs 5.05-5.17 ms per frame at "
+                         "3, profiles/r06_frame_inflight.log; a ray shard of 8: 0.945 vs 0.985 ms, shards of 2 / 4 "
+                         "equal, 6 slower, profiles/r06_shard_inflight.log)")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                     help="replay the frame as one HIP graph (TemporalPoints.capture_frame; with --shard rays "
                          "each rank's blocks, shard.capture_sharded); auto = on unless the ranks use the "
@@ -761,7 +761,7 @@ def main():
 
     world = check_world(args.gpus, os.environ)
     if args.in_flight is None:
-        args.in_flight = 4 if (world >= 4 and args.shard == "rays") else 3
+        args.in_flight = 4
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one process per GPU; APN_DIST_BACKEND=gloo rehearses N>1 with several ranks on one card
