@@ -9,15 +9,15 @@
 // MFMAs instead of 24 -- its L2 latency hides behind one chunk of MFMAs. The head's 16-wide MFMA
 // B tile holds 16 real samples (no padding). Cost: 2 workgroups (8 waves) per CU instead of 3.
 //
-// Layout per workgroup (LDS, 77 KB): one activation buffer X of 128 rows x [hi 128 | lo 128] fp16
+// Layout per workgroup (LDS, 74.6 KB): one activation buffer X of 128 rows x [hi 128 | lo 128] fp16
 // (512 B rows, 16-B chunks XOR-swizzled by row: conflict-free ds_read_b128 operand reads), reused
 // in place by every layer (a barrier between the last read and the first write), then for the
 // layer-4 output as fp32 rows, then -- after the IDW sums are in registers -- for the 16 head-input
-// rows. Activations are written as whole 16-B chunks: a lane holds 4 consecutive features of a
-// row (the transposed product's C layout), v_permlane16_swap pairs it with the lane holding the
-// next 4 (rows g, g ^ 1 of the lane's 16-lane groups), and the even lane writes the chunk's 8 hi
-// halves, the odd lane its 8 lo halves: one conflict-free ds_write_b128 instead of two 2-way
-// conflicting ds_write_b64 (SQ_LDS_BANK_CONFLICT).
+// rows. Activations are written as whole 16-B chunks with no cross-lane exchange: a lane holds 4
+// features of each of its wave's two o-tiles for one row (the transposed product's C layout) and
+// writes those 8 values as one hi and one lo chunk; W2-W4's fragments take their K columns in that
+// order (apn_mlp_layout.h act_k_of). (Rounds 4-5 paired lanes with v_permlane16_swap for the same
+// conflict-free ds_write_b128s.)
 #include "apn_mlp_split.h"
 
 // The layers' operand reads are pinned ahead of the MFMAs that do not need them (sched_barrier):
