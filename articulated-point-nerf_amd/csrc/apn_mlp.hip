@@ -24,6 +24,8 @@
 // 16-byte load feeds 4 MFMAs.
 #include "apn_mlp_layout.h"
 
+#include <algorithm>
+
 namespace apn {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -633,7 +635,12 @@ extern "C" int apn_point_mlp_ert(const float* s_pos4, const int32_t* s_ray, cons
   // a pass's size is known on the device only: a grid of ERT_MLP_BLOCKS workgroups (grid-stride
   // over the pass's tiles) instead of one per tile, so the passes that find few or no live rays
   // cost a few microseconds, not the dispatch of 16k workgroups that exit at once
-  const int blocks = (int)(ntiles < ERT_MLP_BLOCKS ? ntiles : ERT_MLP_BLOCKS);
+  // sized by the launch's capacity: ~1/64 of its tiles, between 512 (2 per CU) and ERT_MLP_BLOCKS,
+  // a multiple of 8 (the XCD-aware tile order): a ray shard's passes hold ~2k tiles, and at 2048
+  // workgroups most of them staged the weights for one tile (shard of 8, same box, 4 in flight:
+  // 0.909 / 0.925 ms at 512 vs 0.928 / 0.928 at 2048; the full frame keeps 2048)
+  const int64_t want = std::max<int64_t>(512, std::min<int64_t>(ERT_MLP_BLOCKS, ntiles / 64)) & ~int64_t(7);
+  const int blocks = (int)(ntiles < want ? ntiles : want);
   MlpPass pass = [&](const int* list, const int* n_list) {
     launch_point_mlp_h4(blocks, false, s, (const float4*)s_pos4, s_ray, s_nbr, n_list, (const float4*)recA16,
                         (const float4*)recB8, (const float4*)feat_proj, viewdirs, vemb_const, wbuf, eps, act_shift,
