@@ -1499,6 +1499,14 @@ __global__ __launch_bounds__(ORDER_THREADS) void k_order_blocks(const int* __res
 #else
 #define APN_KNN_PASS_B_ATTR __attribute__((amdgpu_waves_per_eu(PTS > 4 ? 4 : 8, 8)))
 #endif
+// Wave priority of the scanning passes (A/B builds; 0 = the default). With frames in flight the
+// passes share SIMDs with the neighbour MLP of other frames, whose waves hold priority 1 through
+// their MFMA streams (apn_mlp_h4.hip APN_H4_PRIO); a kNN wave issues rarely, on its dependent
+// loads' return. Priority 2 / 3 measured equal (round 6, C2, 4 frames in flight, same box:
+// 4.978 / 4.958 and 5.017 / 4.943 vs 4.957 / 4.976 ms per frame): off.
+#ifndef APN_KNN_PRIO
+#define APN_KNN_PRIO 0
+#endif
 #ifndef APN_KNN_A_PTS
 #define APN_KNN_A_PTS 4
 #endif
@@ -1529,6 +1537,7 @@ __global__ __launch_bounds__(KNN_THREADS) void k_knn_pass_a8(
     const int* __restrict__ u4, int* __restrict__ flag, int* __restrict__ t_nbr, int* __restrict__ hard,
     int* __restrict__ n_hard, int* __restrict__ hard_r, int* __restrict__ n_hard_r, const AGrid* __restrict__ agp,
     const int* __restrict__ cell_start2, const float4* __restrict__ sorted2, const int* __restrict__ perm) {
+  if (APN_KNN_PRIO) __builtin_amdgcn_s_setprio(APN_KNN_PRIO);
   const int nc = *n_cand_dev;
   const int base = (perm ? perm[blockIdx.x] : (int)blockIdx.x) * KNN_THREADS;
   int c = base + threadIdx.x;
@@ -1949,6 +1958,7 @@ __global__ __launch_bounds__(KNN_THREADS) APN_KNN_PASS_B_ATTR void k_knn_pass_b9
     const AGrid* __restrict__ agp, const int* __restrict__ cell_start2, const float4* __restrict__ sorted2,
     int* __restrict__ flag, int* __restrict__ t_nbr, const int* __restrict__ perm, const int* __restrict__ ccell,
     const int* __restrict__ u1, const int* __restrict__ u2) {
+  if (APN_KNN_PRIO) __builtin_amdgcn_s_setprio(APN_KNN_PRIO);
   const int base = (perm ? perm[blockIdx.x] : (int)blockIdx.x) * KNN_THREADS;
   const int n1 = *n_hard, n2 = hard2 ? *n_hard2 : 0;
   int i = base + threadIdx.x;
