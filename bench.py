@@ -746,7 +746,7 @@ def main():
                     help="N>1: 'rays' (default) = the ranks split one frame's rays and all-gather the tiles "
                          "over RCCL (strong scaling, SURVEY.md 8(e)); 'frames' = every rank renders its own "
                          "frame (weak scaling, no data-path collective)")
-    ap.add_argument("--in-flight", type=int, choices=[1, 2, 3, 4], default=None,
+    ap.add_argument("--in-flight", type=int, choices=[1, 2, 3, 4, 5, 6], default=None,
                     help="frames in flight: one model's frame captured into n workspaces, frame i on stream i %% n "
                          "(ray shards: the all-gathers in frame order on one collective stream); 1 = one "
                          "after another. Default 4 (C2, same box, 3 rounds: 4.96-5.07 vs 5.05-5.17 ms per frame at "
