@@ -304,7 +304,7 @@ PINNED_STACK_BYTES = 1 << 30
 def render_viewpoints(model, render_poses, HW, Ks, ndc, render_kwargs, gt_imgs=None, savedir=None, test_times=None,
                       render_factor=0, eval_psnr=False, eval_ssim=False, eval_lpips_alex=False,
                       eval_lpips_vgg=False, inverse_y=False, flip_x=False, flip_y=False, batch_size=4096 * 2,
-                      verbose=True, render_pcd_direct=False, render_flow=False, fixed_viewdirs=None, in_flight=3):
+                      verbose=True, render_pcd_direct=False, render_flow=False, fixed_viewdirs=None, in_flight=4):
     """run.py:80-239: every view's rays (tineuvox.get_rays_of_a_view), the model at that view's
     time, rgb / depth / weight-visualisation images, optional PSNR / SSIM against gt_imgs, PNGs
     in savedir, the skeleton drawn on the weight images. Returns (rgbs, depths, weights, flows).

@@ -117,7 +117,7 @@ class FramePipeline:
     frames are read on the device through ``FrameHandle.device()`` or not at all, as bench.py's
     timed loop does)."""
 
-    def __init__(self, model, t, render_kwargs, n=3, render_depth=True, render_weights=True, query_radius=0.01,
+    def __init__(self, model, t, render_kwargs, n=4, render_depth=True, render_weights=True, query_radius=0.01,
                  poses=None, Ks=None, get_skeleton=False, readback=READBACK):
         if n < 1:
             raise ValueError("FramePipeline: n >= 1")
@@ -252,7 +252,7 @@ class FramePipeline:
             yield h.result()
 
 
-def capture_sharded_in_flight(model, t, render_kwargs, rank, world, group=None, n=3, **forward_kwargs):
+def capture_sharded_in_flight(model, t, render_kwargs, rank, world, group=None, n=4, **forward_kwargs):
     """n capture_sharded steps of one model, each captured into its own per-frame workspace and
     with its own input buffers (``step.inputs``: rays, and the camera pose / intrinsics when the
     skeleton is projected), for shard.replay_in_flight (the ray-shard frames in flight of bench.py
@@ -293,7 +293,7 @@ def _render_settings(model):
             float(getattr(tnv, "act_shift", 0.0)), float(getattr(tnv, "voxel_size_ratio", 1.0)), float(model._eps))
 
 
-def cached_pipeline(model, t, render_kwargs, n=3, **kw) -> FramePipeline:
+def cached_pipeline(model, t, render_kwargs, n=4, **kw) -> FramePipeline:
     """The model's FramePipeline for this ray count and these render settings, captured on first
     use and reused while the model's parameters and plain render settings are unchanged
     (harness.render_viewpoints calls it once per viewpoint sweep). A pipeline whose model changed is
