@@ -157,7 +157,7 @@ def test_gemm_linear_vs_float64(M, K, N, slope):
     refs = {"y": y64, "x": gd @ w64, "w": gd.t() @ x64, "b": gd.sum(0)}
     for name, a in (("y", y), ("x", ps[0].grad), ("w", ps[1].grad), ("b", ps[2].grad)):
         r = refs[name]
-        err = float((a.double() - r).abs().max() / r.abs().max().clamp_min(1e-30))
+        err = float((a.detach().double() - r.detach()).abs().max() / r.detach().abs().max().clamp_min(1e-30))
         assert err < 2e-6, (name, err)
 
 

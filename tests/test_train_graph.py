@@ -54,8 +54,8 @@ def test_graphed_warp_stage_equals_eager(dev, name):
         assert abs(le - lg) <= 1e-6 * max(1.0, abs(le)), (it, le, lg)
         assert set(ge) == set(gg), set(ge) ^ set(gg)
         for k in ge:
-            scale = float(ge[k].abs().max().clamp_min(1e-30))
-            err = float((ge[k] - gg[k]).abs().max()) / scale
+            scale = float(ge[k].detach().abs().max().clamp_min(1e-30))
+            err = float((ge[k] - gg[k]).detach().abs().max()) / scale
             assert err < 1e-4, (it, k, err)
         assert "forward_warp.transform_net.net.0.weight" in gg
         with torch.no_grad():   # an optimizer-like in-place update: the graph reads the new values
@@ -124,7 +124,7 @@ def test_nbr_aggregate_vs_float64_autograd(dev, with_pose):
     outs, grads = run(NbrAggregate.apply, torch.float32, dev)
     routs, rgrads = run(_torch_aggregate, torch.float64, dev)
     touts, tgrads = run(_torch_aggregate, torch.float32, dev)   # fp32 conditioning floor (2^9 posenc)
-    rel = lambda a, r: float((a.double() - r).abs().max() / r.abs().max())
+    rel = lambda a, r: float((a.detach().double() - r.detach()).abs().max() / r.detach().abs().max())
     for i, (a, t, r) in enumerate(zip(outs, touts, routs)):
         assert rel(a, r) <= max(1e-5, 3 * rel(t, r)), (i, rel(a, r), rel(t, r))
     for i, (a, t, r) in enumerate(zip(grads, tgrads, rgrads)):
