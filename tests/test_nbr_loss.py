@@ -192,7 +192,7 @@ def test_weight_sparsity_loss_vs_float64(n, J):
     wd = w.to(dev).requires_grad_(True)
     loss = SparsityLoss.apply(wd, eps)
     (0.2 * loss).backward()
-    assert abs(float(loss.detach()) - float(ref)) <= 2e-6 * max(1.0, abs(float(ref)))
+    assert abs(float(loss.detach()) - float(ref.detach())) <= 2e-6 * max(1.0, abs(float(ref.detach())))
     err = (wd.grad.cpu().double() - w64.grad).abs() / w64.grad.abs().clamp_min(0.2 / w.numel())
     assert float(err.max()) < 1e-5, float(err.max())
 
