@@ -21,6 +21,12 @@
 
 namespace apn {
 
+// 1: the XCD-aware sample order below. Measured no better (round 6, same box, parity green: MLP
+// stage minus the pass kernels 0.402 / 0.402 -> 0.417 / 0.413 ms per C2 frame): off.
+#ifndef APN_DIRECT_XCD
+#define APN_DIRECT_XCD 0
+#endif
+
 // out12 columns 4..11 = {r_d, g_d, b_d, alpha_d, wr, wg, wb, 0} of sample i, the arithmetic of the
 // fused MLP kernel's gather (apn_mlp_h4.hip gather_q: squared distance, direct weight) and its
 // epilogue (IDW weights, sequential sums over the 8 neighbours in order).
@@ -29,7 +35,16 @@ __global__ __launch_bounds__(256) void k_direct_blend(const float4* __restrict__
                                                       const float4* __restrict__ recB, float eps,
                                                       float4* __restrict__ out) {
   const int n = *n_dev;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+  // XCD-aware sample order: workgroup b runs on XCD b % 8, so each XCD walks one contiguous eighth
+  // of the samples -- neighbouring samples share neighbour points, and their records then meet in
+  // that XCD's L2 instead of being fetched by all eight (PMC: L2 hit 0.79, 0.63 GB of HBM per
+  // launch against ~0.25 GB of samples and records, round 6)
+  const int nx = APN_DIRECT_XCD && (gridDim.x % 8 == 0) ? 8 : 1;
+  const int xcd = blockIdx.x % nx, per_xcd = gridDim.x / nx;
+  const int chunk = (n + nx - 1) / nx;
+  const int i_end = min(n, (xcd + 1) * chunk);
+  for (int i = xcd * chunk + (int)(blockIdx.x / nx) * (int)blockDim.x + (int)threadIdx.x; i < i_end;
+       i += per_xcd * (int)blockDim.x) {
     const float4 q = s_pos[i];
     const int4 nb0 = ((const int4*)s_nbr)[2 * (size_t)i], nb1 = ((const int4*)s_nbr)[2 * (size_t)i + 1];
     const int nbs[8] = {nb0.x, nb0.y, nb0.z, nb0.w, nb1.x, nb1.y, nb1.z, nb1.w};
